@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: env steps/sec (whole node) + episode return, 2x128 MLP Q-net.
+
+BASELINE.json config 2/3: a 2-layer 128-hidden MLP Q-network in bf16, online
+Q-learning (select -> env step -> TD update -> Adam) over ``--envs`` vectorised
+Buy/Sell/Hold trading envs per GPU on synthetic random-walk price series
+(6,047 days each, like the reference's MSFT file) with random-init weights;
+one process per GPU, gradients all-reduced every step with RCCL.
+
+Single GPU:   python bench.py --steps 200 --warmup 20
+N GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+                  --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Every timed step is a full learner step (all envs act, every env's TD error
+is back-propagated, the optimizer updates all parameters); nothing is skipped.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env steps/sec (whole node) + episode return, 2x128 MLP Q-net at 1/2/4/8 MI355X"
+REFERENCE_FLOOR = 58.0  # derived minimum throughput of the reference app; not a published number
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 65536)),
+                    help="vectorised envs per GPU")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        group = dist.group.WORLD
+
+    import build as _build  # in-tree native build (no-op when up to date)
+
+    if rank == 0 or world == 1:
+        _build.build_all()
+    if world > 1:
+        torch.distributed.barrier()
+
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    cfg.engine.envs_per_rank = args.envs
+    eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
+    eng.sync_params_from(0)
+
+    use_graph = (world == 1) and not args.no_graph
+    if use_graph:
+        eng.capture_graph(warmup=2)
+    for _ in range(args.warmup):
+        eng.step()
+    eng.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    # start-of-window portfolio (episode return is measured over the timed window)
+    pf0 = eng.current_portfolios().double().clone()
+    prof = None
+    if args.trace:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        prof.export_chrome_trace(args.trace)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    pf1 = eng.current_portfolios().double()
+    # per-env return over the window (episode resets inside the window are rare: 5,846-step episodes)
+    ret = torch.stack([(pf1 - pf0).sum(), torch.tensor(float(eng.E), dtype=torch.float64, device=dev)])
+    stats = eng.stat_acc.clone() if eng.backend == "native" else eng.stats.to(dev)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ret)
+        dist.all_reduce(stats)
+    el = float(elapsed[0])
+    total_steps = eng.E * world * args.steps
+    value = total_steps / el
+    if rank == 0:
+        st = stats.cpu().tolist()
+        n_trans = eng.E * world * (args.warmup + args.steps + (2 if use_graph else 0))
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env_steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (per-env geometric random-walk price series, 6047 days; random-init weights)",
+            "config": {
+                "model": "2x128 MLP Q-net (203->128->128->3), online DQN, Adam",
+                "global_batch": eng.E * world,
+                "seq_len": cfg.model.history,
+                "parallelism": f"dp{world}",
+                "envs_per_gpu": eng.E,
+                "hip_graph": use_graph,
+            },
+            "episode_return_mean": round(float(ret[0] / ret[1]), 4),
+            "episode_return_window_steps": args.steps,
+            "mean_reward_per_step": st[0] / max(n_trans, 1),
+            "mean_td_loss": st[1] / max(n_trans, 1),
+            "vs_reference_floor": round(value / REFERENCE_FLOOR, 1),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""In-tree native build for sharetrade.
+
+Produces (next to the Python package, so they travel with the repo snapshot):
+
+* ``sharetrade/_native/libsharetrade_hip.so`` — every HIP/CDNA4 kernel, built
+  with ``hipcc --offload-arch=gfx950`` (C ABI, loaded with ctypes; no torch
+  headers, so a full rebuild takes seconds);
+* ``sharetrade/_native/libsharetrade_rt.so`` — the host-side C++ runtime
+  (journal / snapshot store / checkpoint writer), built with g++.
+
+Usage: ``python build.py [--force] [-j N]``.  Rebuilds only when a source is
+newer than the library.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(ROOT, "csrc")
+OUT = os.path.join(ROOT, "sharetrade", "_native")
+OBJ = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("SHARETRADE_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+             "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter"]
+
+HIP_LIB = os.path.join(OUT, "libsharetrade_hip.so")
+RT_LIB = os.path.join(OUT, "libsharetrade_rt.so")
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout)
+        raise RuntimeError(f"build step failed: {cmd[0]} {cmd[-1]}")
+    return r.stdout
+
+
+def build_hip(force: bool = False, jobs: int = 8) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "*.h")))
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(OUT, exist_ok=True)
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            todo.append((s, o))
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(lambda so: _run([HIPCC] + HIP_FLAGS + ["-c", so[0], "-o", so[1]]), todo))
+    if force or todo or _newer(HIP_LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_LIB] + objs)
+    return HIP_LIB
+
+
+def build_rt(force: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.h")))
+    if not srcs:
+        return ""
+    os.makedirs(OUT, exist_ok=True)
+    if force or _newer(RT_LIB, srcs + hdrs):
+        _run(["g++"] + CXX_FLAGS + ["-shared", "-o", RT_LIB] + srcs + ["-lpthread"])
+    return RT_LIB
+
+
+def build_all(force: bool = False, jobs: int = 8):
+    libs = [build_hip(force, jobs)]
+    rt = build_rt(force)
+    if rt:
+        libs.append(rt)
+    return libs
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
+    a = ap.parse_args()
+    for lib in build_all(a.force, a.j):
+        print(lib)

@@ -1,0 +1,49 @@
+// Synthetic price-bank generation directly in HBM.
+//
+// The reference "fetches" a single bundled MSFT series (SharePriceGetter.scala:83-102);
+// the engine keeps one price series per env resident in HBM ([E, T] fp32,
+// ~1.6 GB for 65,536 envs x 6,047 days) and reads state windows from it in place.
+// One wave generates one series: Philox normals (Box-Muller) for 64 days at a
+// time, a wave-level inclusive scan of the log-returns, coalesced 256-B stores.
+#include "common.h"
+
+namespace st {
+
+__global__ void __launch_bounds__(256) random_walk_kernel(float* __restrict__ out, int E, int T, float start_price,
+                                                          float vol, float drift, uint32_t key0, uint32_t key1) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= E) return;
+  float carry = 0.f;  // log-price at the last day of the previous block
+  float* row = out + (size_t)wave * T;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    uint32_t c0 = (uint32_t)wave, c1 = (uint32_t)t, c2 = 0x5EEDu, c3 = 2u;
+    philox4x32(c0, c1, c2, c3, key0, key1);
+    const float u1 = ((float)(c0 >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+    const float u2 = u24(c1);
+    float z = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+    float inc = (t == 0 || t >= T) ? 0.f : vol * z + drift;
+    // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float n = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += n;
+    }
+    const float lp = carry + inc;
+    if (t < T) row[t] = start_price * expf(lp);
+    carry = __shfl(lp, 63, 64);
+  }
+}
+
+}  // namespace st
+
+extern "C" hipError_t st_random_walk(float* out, int E, int T, float start_price, float vol, float drift,
+                                     uint32_t key0, uint32_t key1, hipStream_t stream) {
+  const int threads = 256;
+  const long waves = E;
+  const int grid = (int)((waves * 64 + threads - 1) / threads);
+  hipLaunchKernelGGL(st::random_walk_kernel, dim3(grid), dim3(threads), 0, stream, out, E, T, start_price, vol,
+                     drift, key0, key1);
+  return hipGetLastError();
+}

@@ -1,0 +1,277 @@
+"""Typed configuration for the sharetrade engine.
+
+The reference hard-codes every algorithmic knob as a Scala constant and keeps
+runtime settings in HOCON (`src/main/resources/application.conf:1-25`,
+`src/test/resources/application.conf:1-11`).  Here every knob lives in one
+dataclass tree with the reference values as the ``reference_compat`` preset
+(SURVEY.md §5.6):
+
+=====================  ==========================  =====================================
+knob                   reference value             cite
+=====================  ==========================  =====================================
+actions / order        Buy, Sell, Hold             QDecisionPolicyActor.scala:17
+input dim              203 = 201 prices + 2        QDecisionPolicyActor.scala:18
+epsilon (max exploit)  0.9                         QDecisionPolicyActor.scala:19
+exploit ramp           min(eps, step/1000)         QDecisionPolicyActor.scala:58
+gamma                  0.001                       QDecisionPolicyActor.scala:20
+hidden                 [200] + ReLU on output      QDecisionPolicyActor.scala:22,47
+init                   W~N(0,1), biases 0.1 const  QDecisionPolicyActor.scala:41-46
+optimizer              AdaGrad(0.01)               QDecisionPolicyActor.scala:50
+snapshot interval      500 updates                 QDecisionPolicyActor.scala:74
+rollout workers        10                          TrainerRouterActor.scala:36
+backoff                3 s / 60 s / 0.2            TrainerRouterActor.scala:46-51
+ask timeouts           20 s app, 10 s router/child ShareTradeHelper.scala:18; ...:42; ...:28
+poll                   201 x 5 s, Await 10 s       ShareTradeHelper.scala:32-33,45
+budget / shares        2400.0 / 0                  ShareTradeHelper.scala:20-21
+progress log every     200 steps                   TrainerChildActor.scala:108
+=====================  ==========================  =====================================
+
+Configs load from JSON or TOML files and accept ``a.b.c=value`` CLI overrides.
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence
+
+ACTIONS = ("Buy", "Sell", "Hold")  # index order 0,1,2 (QDecisionPolicyActor.scala:17)
+
+
+@dataclass
+class ModelConfig:
+    """Q-network architecture (an MLP over the 203-feature trading state)."""
+
+    history: int = 201              # prices per state window (QDecisionPolicyActor.scala:18)
+    hidden: List[int] = field(default_factory=lambda: [200])
+    n_actions: int = 3
+    output_relu: bool = True        # quirk Q3 (QDecisionPolicyActor.scala:47)
+    train_bias: bool = False        # quirk Q4: tf.constant biases (QDecisionPolicyActor.scala:42,46)
+    bias_init: float = 0.1
+    init_std: float = 1.0           # tf.RandomNormalInitializer() default N(0,1)
+    init: str = "normal"            # "normal" (reference) | "he" (scaled, for deep nets)
+
+    @property
+    def input_dim(self) -> int:
+        return self.history + 2
+
+
+@dataclass
+class AgentConfig:
+    """Q-learning hyper-parameters."""
+
+    epsilon: float = 0.9            # max exploit probability
+    ramp: float = 1000.0            # exploit prob = min(epsilon, step / ramp)
+    gamma: float = 0.001
+    optimizer: str = "adagrad"      # adagrad | adam | sgd
+    lr: float = 0.01
+    adagrad_init_acc: float = 0.1   # TF default initial accumulator (SURVEY §5.6 knob)
+    adam_betas: Sequence[float] = (0.9, 0.999)
+    adam_eps: float = 1e-8
+    # "compat": TD target written at argmax(q_next) (quirk Q2, QDecisionPolicyActor.scala:69-71)
+    # "action": TD target written at the taken action (the intended semantics)
+    target_slot: str = "compat"
+    loss_reduction: str = "sum"     # "sum" over the batch (reference, B=1) | "mean"
+    snapshot_interval: int = 500    # QDecisionPolicyActor.scala:74
+    seed: int = 1234
+
+
+@dataclass
+class EnvConfig:
+    """Trading environment."""
+
+    budget: float = 2400.0          # ShareTradeHelper.scala:20
+    shares: int = 0                 # ShareTradeHelper.scala:21
+    # quirk Q1: decisions use the constructor budget/shares (TrainerChildActor.scala:120-122)
+    compat_decisions: bool = True
+    # feature normalisation of the state row: "raw" (reference) | "relative"
+    features: str = "raw"
+    progress_every: int = 200       # TrainerChildActor.scala:108
+
+
+@dataclass
+class DataConfig:
+    source: str = "csv"             # csv | linear | random_walk
+    ticker: str = "MSFT"
+    start: str = "1992-01-01"
+    end: str = "2015-01-01"
+    filter_range: bool = False      # quirk Q10: reference ignores the date range
+    csv_path: Optional[str] = None  # default: bundled MSFT series
+    length: int = 6047              # synthetic series length
+    start_price: float = 50.0
+    volatility: float = 0.02
+    seed: int = 7
+
+
+@dataclass
+class RouterConfig:
+    n_workers: int = 10             # TrainerRouterActor.scala:36
+    backoff_min_s: float = 3.0      # TrainerRouterActor.scala:48
+    backoff_max_s: float = 60.0     # TrainerRouterActor.scala:49
+    backoff_jitter: float = 0.2     # TrainerRouterActor.scala:50
+    ask_timeout_s: float = 10.0     # TrainerRouterActor.scala:42, TrainerChildActor.scala:28
+    app_ask_timeout_s: float = 20.0  # ShareTradeHelper.scala:18
+    poll_interval_s: float = 5.0    # ShareTradeHelper.scala:33
+    poll_rounds: int = 201          # ShareTradeHelper.scala:32
+    await_s: float = 10.0           # ShareTradeHelper.scala:45
+    reply_result: bool = True       # quirk Q9 fixed: GetAvg/GetStd reply Result(x)
+    redispatch_on_restart: bool = True  # quirk Q14 fixed
+
+
+@dataclass
+class PersistConfig:
+    """Akka persistence settings (application.conf:5-18)."""
+
+    journal_plugin: str = "file"    # file (native C++ journal) | inmemory (test profile)
+    journal_dir: str = "target/my/journal"
+    snapshot_dir: str = "target/my/snapshots"
+    persist_before_reply: bool = False  # quirk Q11: reference replies before persisting
+    merge_on_recovery: bool = True      # quirk Q10 fixed: merge tickers on recovery
+
+
+@dataclass
+class EngineConfig:
+    """GPU vectorized engine (data plane)."""
+
+    device: str = "auto"            # auto | cuda | cpu
+    envs_per_rank: int = 10
+    dtype: str = "bf16"             # bf16 (MFMA fused step) | fp32 (exact path)
+    chunk: int = 32                 # envs per LDS chunk inside the fused step kernel
+    graph: bool = True              # capture the step in a HIP graph
+    backend: str = "auto"           # auto | native | torch
+
+
+@dataclass
+class LogConfig:
+    loglevel: str = "INFO"          # application.conf:3
+    test_listener: bool = False     # src/test/resources/application.conf:5
+
+
+@dataclass
+class Config:
+    model: ModelConfig = field(default_factory=ModelConfig)
+    agent: AgentConfig = field(default_factory=AgentConfig)
+    env: EnvConfig = field(default_factory=EnvConfig)
+    data: DataConfig = field(default_factory=DataConfig)
+    router: RouterConfig = field(default_factory=RouterConfig)
+    persist: PersistConfig = field(default_factory=PersistConfig)
+    engine: EngineConfig = field(default_factory=EngineConfig)
+    log: LogConfig = field(default_factory=LogConfig)
+
+    # ------------------------------------------------------------------ io
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict(), indent=2, sort_keys=True)
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "Config":
+        cfg = cls()
+        _merge(cfg, d)
+        return cfg
+
+    @classmethod
+    def load(cls, path: str, preset: str = "reference_compat") -> "Config":
+        cfg = preset_config(preset)
+        with open(path, "rb") as f:
+            raw = f.read()
+        if path.endswith(".toml"):
+            import tomli
+
+            d = tomli.loads(raw.decode())
+        else:
+            d = json.loads(raw.decode())
+        _merge(cfg, d)
+        return cfg
+
+    def override(self, items: Sequence[str]) -> "Config":
+        """Apply ``section.key=value`` overrides (values parsed as JSON when possible)."""
+        for it in items:
+            if "=" not in it:
+                raise ValueError(f"override must be key=value: {it!r}")
+            key, val = it.split("=", 1)
+            try:
+                v: Any = json.loads(val)
+            except json.JSONDecodeError:
+                v = val
+            node: Any = self
+            parts = key.split(".")
+            for p in parts[:-1]:
+                node = getattr(node, p)
+            if not hasattr(node, parts[-1]):
+                raise KeyError(f"unknown config key {key}")
+            setattr(node, parts[-1], v)
+        return self
+
+    def clone(self) -> "Config":
+        return copy.deepcopy(self)
+
+
+def _merge(obj: Any, d: Dict[str, Any]) -> None:
+    for k, v in d.items():
+        if not hasattr(obj, k):
+            raise KeyError(f"unknown config key {k}")
+        cur = getattr(obj, k)
+        if dataclasses.is_dataclass(cur) and isinstance(v, dict):
+            _merge(cur, v)
+        else:
+            setattr(obj, k, v)
+
+
+def preset_config(name: str = "reference_compat") -> Config:
+    """Named presets.
+
+    * ``reference_compat`` — the reference's constants and quirks.
+    * ``intended`` — same network but with the quirks fixed (default semantics).
+    * ``flagship`` — BASELINE.json config 2/3: 2x128 MLP, bf16 fused step,
+      normalised features, correct env/TD semantics, Adam.
+    * ``test`` — the test profile (src/test/resources/application.conf): in-memory
+      journal, DEBUG log level, test event listener.
+    """
+    cfg = Config()
+    if name == "reference_compat":
+        cfg.engine.dtype = "fp32"
+        return cfg
+    if name == "intended":
+        cfg.engine.dtype = "fp32"
+        cfg.env.compat_decisions = False
+        cfg.agent.target_slot = "action"
+        cfg.model.output_relu = False
+        cfg.model.train_bias = True
+        return cfg
+    if name == "flagship":
+        cfg.model.hidden = [128, 128]
+        cfg.model.output_relu = False
+        cfg.model.train_bias = True
+        cfg.model.init = "he"
+        cfg.env.compat_decisions = False
+        cfg.env.features = "relative"
+        cfg.agent.target_slot = "action"
+        cfg.agent.optimizer = "adam"
+        cfg.agent.lr = 1e-3
+        cfg.agent.loss_reduction = "mean"
+        cfg.agent.gamma = 0.99
+        cfg.data.source = "random_walk"
+        cfg.engine.dtype = "bf16"
+        cfg.engine.envs_per_rank = 65536
+        return cfg
+    if name == "test":
+        cfg.engine.dtype = "fp32"
+        cfg.persist.journal_plugin = "inmemory"
+        cfg.log.loglevel = "DEBUG"
+        cfg.log.test_listener = True
+        return cfg
+    raise KeyError(f"unknown preset {name}")
+
+
+REFERENCE_CSV = "/root/reference/src/main/resources/MSFT-stock-prices-revised.txt"
+
+
+def default_csv_path() -> str:
+    """Location of the MSFT price file the reference bundles as a classpath resource
+    (`SharePriceGetter.scala:90`).  The file is read in place (it is data the
+    reference ships, not re-distributed here); ``SHARETRADE_MSFT_CSV`` overrides."""
+    return os.environ.get("SHARETRADE_MSFT_CSV", REFERENCE_CSV)

@@ -1,0 +1,121 @@
+"""ctypes bindings to the in-tree HIP kernel library (``libsharetrade_hip.so``).
+
+The kernels are plain C-ABI entry points (``csrc/*.hip``); tensors are
+allocated by PyTorch's caching allocator and passed by device pointer, and
+every launch goes onto PyTorch's *current* HIP stream, so the calls compose
+with ``torch.cuda.graph`` capture and with RCCL collectives on the same stream.
+
+If the library is missing while a GPU is present, :func:`lib` raises — the
+engine never silently falls back to a non-native path on a GPU box.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(_HERE), "_native")
+HIP_LIB_PATH = os.path.join(LIB_DIR, "libsharetrade_hip.so")
+
+_lib: Optional[C.CDLL] = None
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class QStepParams(C.Structure):
+    _fields_ = [
+        ("prices", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
+        ("pos", C.c_void_p), ("episodes", C.c_void_p), ("last_final", C.c_void_p), ("ret_sum", C.c_void_p),
+        ("wq", C.c_void_p), ("wf", C.c_void_p), ("slab", C.c_void_p), ("stats", C.c_void_p),
+        ("actions_out", C.c_void_p), ("rewards_out", C.c_void_p), ("ctrl", C.c_void_p),
+        ("T", C.c_int), ("E", C.c_int), ("H", C.c_int), ("P", C.c_int),
+        ("off_w0", C.c_int), ("off_w1", C.c_int), ("off_b1", C.c_int), ("off_w2", C.c_int), ("off_b2", C.c_int),
+        ("eps", C.c_float), ("inv_ramp", C.c_float), ("gamma", C.c_float), ("loss_coef", C.c_float),
+        ("b0", C.c_float), ("inv_b0", C.c_float),
+        ("s0", C.c_int), ("compat_env", C.c_int), ("target_compat", C.c_int), ("output_relu", C.c_int),
+        ("feat_mode", C.c_int),
+        ("key0", C.c_uint32), ("key1", C.c_uint32),
+        ("env_offset", C.c_int),
+    ]
+
+
+class OptimParams(C.Structure):
+    _fields_ = [
+        ("params", C.c_void_p), ("params_bf", C.c_void_p), ("mask", C.c_void_p), ("s1", C.c_void_p),
+        ("s2", C.c_void_p), ("slab", C.c_void_p), ("grad", C.c_void_p), ("ctrl", C.c_void_p),
+        ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int),
+        ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
+    ]
+
+
+def available() -> bool:
+    return os.path.exists(HIP_LIB_PATH)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(HIP_LIB_PATH):
+        raise NativeUnavailable(
+            f"{HIP_LIB_PATH} not built: run `python build.py` (hipcc --offload-arch=gfx950)")
+    L = C.CDLL(HIP_LIB_PATH)
+    L.st_qstep_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_qstep_launch.restype = C.c_int
+    L.st_qstep_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.st_qstep_lds_bytes.restype = C.c_int
+    L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
+    L.st_reduce_optim.restype = C.c_int
+    L.st_advance.argtypes = [C.c_void_p, C.c_void_p]
+    L.st_advance.restype = C.c_int
+    L.st_to_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.st_to_bf16.restype = C.c_int
+    L.st_random_walk.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_uint32,
+                                 C.c_uint32, C.c_void_p]
+    L.st_random_walk.restype = C.c_int
+    _bind_optional(L)
+    _lib = L
+    return L
+
+
+def _bind_optional(L: C.CDLL) -> None:
+    """Entry points of the fp32 small-batch path (csrc/mlp_f32.hip)."""
+    if hasattr(L, "st_mlp_fwd_f32"):
+        L.st_mlp_fwd_f32.restype = C.c_int
+        L.st_td_update_f32.restype = C.c_int
+
+
+def check(err: int, what: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"HIP error {err} in {what}")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def qstep_supported(inp: int, h1p: int, h2p: int) -> bool:
+    if not available():
+        return False
+    return lib().st_qstep_lds_bytes(inp, h1p, h2p) > 0
+
+
+def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float, key0: int, key1: int) -> None:
+    E, T = out.shape
+    check(lib().st_random_walk(ptr(out), E, T, start_price, vol, drift, key0 & 0xFFFFFFFF, key1 & 0xFFFFFFFF,
+                               stream_handle()), "st_random_walk")
+
+
+def to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
+    check(lib().st_to_bf16(ptr(src), ptr(dst), src.numel(), stream_handle()), "st_to_bf16")

@@ -1,0 +1,331 @@
+"""VectorEngine — the data plane: E vectorised trading envs + the Q-learner on one GPU.
+
+This replaces the reference's hot path — 10 ``TrainerChildActor`` rollout
+workers each doing two blocking asks per step (``SelectionAction``,
+``UpdateQ``) against ONE ``QDecisionPolicyActor`` mailbox
+(`TrainerChildActor.scala:82-103`, `QDecisionPolicyActor.scala:54-77`) — with
+two kernel launches per step for every env on the GPU:
+
+1. ``qstep_fused`` (csrc/qstep_fused.hip): select + env step + TD target +
+   backward for all envs, per-workgroup gradient slabs;
+2. ``reduce_optim`` (csrc/optim.hip): slab reduction + optimizer + bf16 refresh.
+
+With ``world_size > 1`` (one process per GPU, RCCL over xGMI) the reduction
+is split: reduce -> ``all_reduce(SUM)`` of ONE flat fp32 gradient bucket ->
+update; the loss is pre-scaled by ``1/(E*world)`` so SUM is the global mean.
+This is the synchronous-DP analogue of the reference's Hogwild-style shared
+learner.
+
+``backend="torch"`` runs the same step through the plain-PyTorch oracle
+(`sharetrade.env.trading.engine_step_ref`) — used on CPU (tests, gloo DP
+rehearsal) and as the numerics reference; it is never chosen silently on a GPU.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..config import Config
+from ..env import trading as tr
+from ..models import qnet as qn
+from ..ops import native
+from ..utils import rng
+
+NSTAT = 8
+STAT_NAMES = ("reward_sum", "loss_sum", "explore", "episodes_done", "final_sum", "final_sq", "qslot_sum", "_")
+OPT_KIND = {"sgd": 0, "adagrad": 1, "adam": 2}
+
+
+def resolve_device(spec: str) -> torch.device:
+    if spec == "auto":
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    return torch.device(spec)
+
+
+def make_price_bank(cfg: Config, E: int, device: torch.device, seed: int = 0) -> torch.Tensor:
+    """[E, T] fp32 price bank resident on ``device``."""
+    d = cfg.data
+    if d.source == "random_walk":
+        if device.type == "cuda":
+            out = torch.empty(E, d.length, dtype=torch.float32, device=device)
+            k0, k1 = rng.key_for(d.seed + 7919 * seed)
+            native.random_walk(out, d.start_price, d.volatility, 0.0, int(k0), int(k1))
+            return out
+        arr = tr_random_walk(E, d.length, d.start_price, d.volatility, d.seed + 7919 * seed)
+        return torch.from_numpy(arr).to(device)
+    from ..data import prices as pr
+
+    src = pr.make_source(d)
+    q = src.query(d.ticker, pr.to_date(d.start), pr.to_date(d.end))
+    _, series = pr.sorted_series(q)
+    row = torch.tensor(series, dtype=torch.float32)
+    return row[None, :].expand(E, -1).contiguous().to(device)
+
+
+def tr_random_walk(E: int, T: int, start: float, vol: float, seed: int) -> np.ndarray:
+    from ..data.prices import random_walk
+
+    return random_walk(T, start, vol, seed, n_series=E).astype(np.float32)
+
+
+class VectorEngine:
+    """E envs + learner on one device; optionally one rank of a DP group."""
+
+    def __init__(self, cfg: Config, prices: Optional[torch.Tensor] = None, device: Optional[torch.device] = None,
+                 rank: int = 0, world_size: int = 1, group=None, envs: Optional[int] = None,
+                 backend: Optional[str] = None, params: Optional[torch.Tensor] = None):
+        self.cfg = cfg
+        self.device = device if device is not None else resolve_device(cfg.engine.device)
+        self.rank, self.world_size, self.group = rank, world_size, group
+        self.E = int(envs if envs is not None else cfg.engine.envs_per_rank)
+        self.layout = qn.QNetLayout.from_config(cfg.model)
+        self.H = cfg.model.history
+        be = backend or cfg.engine.backend
+        if be == "auto":
+            be = "native" if self.device.type == "cuda" else "torch"
+        self.backend = be
+        L = self.layout
+        if be == "native":
+            if self.device.type != "cuda":
+                raise ValueError("native backend needs a GPU device")
+            if L.n_layers != 3 or not native.qstep_supported(L.pdims[0], L.pdims[1], L.pdims[2]):
+                raise NotImplementedError(f"no fused bf16 step kernel for padded dims {L.pdims}")
+            if self.E % 32:
+                raise ValueError("native engine needs envs_per_rank % 32 == 0")
+            if self.H + 3 > L.in_p - 16:
+                raise ValueError("history too long for the fused kernel's input padding")
+        # ------------------------------------------------------------ data
+        self.prices = prices.to(self.device, torch.float32).contiguous() if prices is not None else \
+            make_price_bank(cfg, self.E, self.device, seed=rank)
+        if self.prices.shape[0] != self.E:
+            raise ValueError(f"price bank has {self.prices.shape[0]} rows, expected {self.E}")
+        self.T = int(self.prices.shape[1])
+        if self.T <= self.H + 1:
+            # TrainerChildActor.scala:69-70
+            raise ValueError("Stock price count should be more than Tensorflow input nodes")
+        # ------------------------------------------------------------ params / optimizer
+        m, a = cfg.model, cfg.agent
+        p0 = params.clone().float() if params is not None else qn.init_params(L, m, seed=a.seed)
+        self.params = p0.to(self.device)
+        self.mask = L.trainable_mask(m.train_bias).to(self.device)
+        self.opt = qn.OptimState(a.optimizer, L.numel, a.adagrad_init_acc, device=self.device)
+        self.state = tr.EnvState.create(self.E, cfg.env.budget, cfg.env.shares, device=self.device)
+        self.env_offset = rank * self.E
+        self.step_count = 0
+        self.key0, self.key1 = rng.key_for(a.seed, rank)
+        total = self.E * world_size
+        self.loss_coef = 2.0 / total if a.loss_reduction == "mean" else 2.0
+        self.stats = torch.zeros(NSTAT, dtype=torch.float64)
+        self._graph = None
+        self._last_actions: Optional[torch.Tensor] = None
+        if be == "native":
+            self._init_native()
+
+    # ---------------------------------------------------------------- native buffers
+    def _init_native(self):
+        dev = self.device
+        L = self.layout
+        self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
+        native.to_bf16(self.params, self.params_bf)
+        props = torch.cuda.get_device_properties(dev)
+        self.grid = max(1, min(props.multi_processor_count, self.E // 32))
+        self.slab = torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev)
+        self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)
+        self.stat_acc = torch.zeros(NSTAT, dtype=torch.float64, device=dev)
+        self.grad = torch.zeros(L.numel, dtype=torch.float32, device=dev)
+        self.ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.actions_out = torch.zeros(self.E, dtype=torch.int32, device=dev)
+        self.rewards_out = torch.zeros(self.E, dtype=torch.float32, device=dev)
+        self._build_structs()
+
+    def _build_structs(self):
+        cfg, L, st = self.cfg, self.layout, self.state
+        seg = L.segments
+        q = native.QStepParams()
+        q.prices, q.budget, q.shares, q.value = (native.ptr(self.prices), native.ptr(st.budget),
+                                                 native.ptr(st.shares), native.ptr(st.value))
+        q.pos, q.episodes, q.last_final, q.ret_sum = (native.ptr(st.pos), native.ptr(st.episodes),
+                                                      native.ptr(st.last_final), native.ptr(st.ret_sum))
+        q.wq, q.wf = native.ptr(self.params_bf), native.ptr(self.params)
+        q.slab, q.stats = native.ptr(self.slab), native.ptr(self.stat_slab)
+        q.actions_out, q.rewards_out = native.ptr(self.actions_out), native.ptr(self.rewards_out)
+        q.ctrl = native.ptr(self.ctrl)
+        q.T, q.E, q.H, q.P = self.T, self.E, self.H, L.numel
+        q.off_w0, q.off_w1, q.off_b1 = seg["W0"].offset, seg["W1"].offset, seg["b1"].offset
+        q.off_w2, q.off_b2 = seg["W2"].offset, seg["b2"].offset
+        q.eps = cfg.agent.epsilon
+        q.inv_ramp = float(np.float32(1.0 / cfg.agent.ramp))
+        q.gamma = cfg.agent.gamma
+        q.loss_coef = self.loss_coef
+        q.b0 = cfg.env.budget
+        q.inv_b0 = float(np.float32(1.0 / cfg.env.budget))
+        q.s0 = cfg.env.shares
+        q.compat_env = int(cfg.env.compat_decisions)
+        q.target_compat = int(cfg.agent.target_slot == "compat")
+        q.output_relu = int(cfg.model.output_relu)
+        q.feat_mode = tr.FEATURES[cfg.env.features]
+        q.key0, q.key1 = int(self.key0), int(self.key1)
+        q.env_offset = self.env_offset
+        self._qp = q
+        a = cfg.agent
+        o = native.OptimParams()
+        o.params, o.params_bf, o.mask = native.ptr(self.params), native.ptr(self.params_bf), native.ptr(self.mask)
+        o.s1 = native.ptr(self.opt.s1) if self.opt.s1.numel() else None
+        o.s2 = native.ptr(self.opt.s2) if self.opt.s2.numel() else None
+        o.slab, o.grad, o.ctrl = native.ptr(self.slab), native.ptr(self.grad), native.ptr(self.ctrl)
+        o.G, o.P, o.kind = self.grid, L.numel, OPT_KIND[a.optimizer]
+        o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+        self._op = o
+
+    # ---------------------------------------------------------------- stepping
+    def _native_step(self):
+        L = native.lib()
+        sh = native.stream_handle()
+        native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],
+                                       self.layout.pdims[2], self.grid, sh), "qstep")
+        if self.world_size > 1:
+            self._op.mode = 1
+            native.check(L.st_reduce_optim(self._op, sh), "reduce")
+            torch.distributed.all_reduce(self.grad, group=self.group)
+            self._op.mode = 2
+            native.check(L.st_reduce_optim(self._op, sh), "update")
+        else:
+            self._op.mode = 0
+            native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
+        self.stat_acc += self.stat_slab.sum(0, dtype=torch.float64)
+
+    def native_grad(self) -> torch.Tensor:
+        """Test hook: run the fused step kernel + slab reduction only (no optimizer
+        update); returns the reduced gradient.  Advances the env state."""
+        L = native.lib()
+        sh = native.stream_handle()
+        native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],
+                                       self.layout.pdims[2], self.grid, sh), "qstep")
+        self._op.mode = 1
+        native.check(L.st_reduce_optim(self._op, sh), "reduce")
+        self.step_count += 1
+        return self.grad
+
+    def _torch_step(self):
+        cfg = self.cfg
+        ns, grad, info = tr.engine_step_ref(
+            self.prices, self.state, self.params, self.layout, history=self.H, feature_mode=cfg.env.features,
+            budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
+            target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
+            epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=self.rank,
+            step=self.step_count, loss_coef=self.loss_coef, env_offset=self.env_offset,
+            emulate_bf16=(cfg.engine.dtype == "bf16"))
+        if self.world_size > 1:
+            torch.distributed.all_reduce(grad, group=self.group)
+        qn.optimizer_step_ref(self.params, grad, self.opt, self.mask, cfg.agent.lr, cfg.agent.adam_betas,
+                              cfg.agent.adam_eps)
+        done = ns.episodes > self.state.episodes
+        fin = torch.where(done, ns.last_final, torch.zeros_like(ns.last_final)).double()
+        self.stats += torch.tensor([
+            float(info["reward"].double().sum()), float(info["loss"]), float((~info["exploit"]).sum()),
+            float(done.sum()), float(fin.sum()), float((fin * fin).sum()),
+            float(info["q"].gather(1, info["slot"][:, None]).double().sum()), 0.0], dtype=torch.float64)
+        self.state = ns
+        self._last_actions = info["actions"]
+        self.grad_last = grad
+
+    def step(self) -> None:
+        if self.backend == "native":
+            if self._graph is not None:
+                self._graph.replay()
+            else:
+                self._native_step()
+        else:
+            self._torch_step()
+        self.step_count += 1
+
+    def run(self, n: int) -> None:
+        for _ in range(n):
+            self.step()
+
+    def capture_graph(self, warmup: int = 2) -> bool:
+        """Capture one native step in a HIP graph (single-rank only)."""
+        if self.backend != "native" or self.world_size > 1:
+            return False
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._native_step()
+                self.step_count += 1
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._native_step()
+        self._graph = g
+        return True
+
+    # ---------------------------------------------------------------- metrics
+    def stats_dict(self) -> Dict[str, float]:
+        acc = self.stat_acc.cpu() if self.backend == "native" else self.stats
+        out = {k: float(v) for k, v in zip(STAT_NAMES, acc.tolist()) if not k.startswith("_")}
+        return out
+
+    def actions(self) -> torch.Tensor:
+        return self.actions_out if self.backend == "native" else self._last_actions
+
+    def final_portfolios(self) -> torch.Tensor:
+        """Final portfolio of the last completed episode per env (NaN if none)."""
+        return self.state.last_final
+
+    def current_portfolios(self) -> torch.Tensor:
+        st = self.state
+        return st.budget + st.shares.float() * st.value
+
+    def portfolio_summary(self) -> Dict[str, float]:
+        """Mean / population std over envs (TrainerRouterActor.scala:148-151)."""
+        fin = self.final_portfolios()
+        ok = ~torch.isnan(fin)
+        vals = fin[ok].double() if bool(ok.any()) else self.current_portfolios().double()
+        mean = float(vals.mean())
+        std = float(((vals - mean) ** 2).mean().sqrt())
+        return {"mean": mean, "std": std, "n": int(vals.numel()),
+                "return_mean": mean - self.cfg.env.budget}
+
+    # ---------------------------------------------------------------- state
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        d = {"params": self.params, "opt_s1": self.opt.s1, "opt_s2": self.opt.s2,
+             "opt_t": torch.tensor([self.opt.t], dtype=torch.int64),
+             "step": torch.tensor([self.step_count], dtype=torch.int64)}
+        for k, v in self.state.as_dict().items():
+            d["env_" + k] = v
+        return {k: v.detach().cpu().clone() for k, v in d.items()}
+
+    def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
+        self.params.copy_(d["params"].to(self.device))
+        if self.opt.s1.numel():
+            self.opt.s1.copy_(d["opt_s1"].to(self.device))
+        if self.opt.s2.numel():
+            self.opt.s2.copy_(d["opt_s2"].to(self.device))
+        self.opt.t = int(d["opt_t"][0])
+        self.step_count = int(d["step"][0])
+        for k in self.state.as_dict():
+            getattr(self.state, k).copy_(d["env_" + k].to(self.device))
+        if self.backend == "native":
+            native.to_bf16(self.params, self.params_bf)
+            self.ctrl.fill_(self.step_count)
+
+    def sync_params_from(self, src_rank: int = 0) -> None:
+        """Broadcast parameters + optimizer state (DP start / elastic re-join)."""
+        if self.world_size <= 1:
+            return
+        import torch.distributed as dist
+
+        for t in (self.params, self.opt.s1, self.opt.s2):
+            if t.numel():
+                dist.broadcast(t, src_rank, group=self.group)
+        if self.backend == "native":
+            native.to_bf16(self.params, self.params_bf)
+
+    def synchronize(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

@@ -1,0 +1,180 @@
+"""Numerics of the fused HIP engine step vs the plain-PyTorch fp32 oracle.
+
+The oracle (`sharetrade.env.trading.engine_step_ref`) rounds to bf16 at the same
+points as the kernel (``emulate_bf16=True``); accumulation order differs, so
+gradients are compared with a relative-norm tolerance while env transitions
+(fp32, no FMA contraction on either side) must match exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(compat=False):
+    from sharetrade.config import preset_config
+
+    cfg = preset_config("flagship")
+    if compat:
+        cfg.env.compat_decisions = True
+        cfg.agent.target_slot = "compat"
+        cfg.model.output_relu = True
+    return cfg
+
+
+def _prices(E, T=400, seed=3):
+    from sharetrade.data.prices import random_walk
+
+    return torch.from_numpy(random_walk(T, 50.0, 0.02, seed, n_series=E).astype(np.float32))
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.parametrize("compat", [False, True])
+@pytest.mark.parametrize("E", [32, 96, 256])
+def test_qstep_matches_oracle(native_built, compat, E):
+    from sharetrade.env import trading as tr
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg(compat)
+    cfg.agent.epsilon = 0.5
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    # advance positions so the epsilon ramp and shares are non-trivial
+    st0 = eng.state.clone()
+    st0.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 3 % 150)
+    st0.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
+    st0.value.copy_(prices[:, 0].to(dev))
+    for k in st0.as_dict():
+        getattr(eng.state, k).copy_(getattr(st0, k))
+    eng.ctrl.fill_(5)
+    params = eng.params.detach().cpu().clone()
+    grad = eng.native_grad().detach().cpu().clone()
+    torch.cuda.synchronize()
+    acts = eng.actions_out.cpu().clone()
+    rew = eng.rewards_out.cpu().clone()
+
+    # unforced oracle: the actions must agree except on near-ties of q
+    ns_ref, g_ref0, info0 = tr.engine_step_ref(
+        prices, st0.to("cpu"), params, eng.layout, history=cfg.model.history, feature_mode=cfg.env.features,
+        budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
+        target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
+        epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
+        loss_coef=eng.loss_coef, emulate_bf16=True)
+    mism = (info0["actions"].cpu() != acts).float().mean().item()
+    assert mism <= 0.05, f"action mismatch rate {mism}"
+
+    ns, g_ref, info = tr.engine_step_ref(
+        prices, st0.to("cpu"), params, eng.layout, history=cfg.model.history, feature_mode=cfg.env.features,
+        budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
+        target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
+        epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
+        loss_coef=eng.loss_coef, emulate_bf16=True, forced_actions=acts)
+    assert torch.equal(info["reward"], rew)
+    for k in ("budget", "shares", "value", "pos", "episodes"):
+        assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), k
+    # gradient vs oracle (bf16 activations, fp32 accumulation)
+    L = eng.layout
+    for l in range(L.n_layers):
+        gw, rw = L.w(grad, l), L.w(g_ref, l)
+        assert _rel(gw, rw) < 3e-2, (l, _rel(gw, rw))
+        if l > 0:
+            assert _rel(L.b(grad, l), L.b(g_ref, l)) < 3e-2
+    # and vs the pure fp32 oracle (no bf16 emulation): looser
+    _, g32, _ = tr.engine_step_ref(
+        prices, st0.to("cpu"), params, eng.layout, history=cfg.model.history, feature_mode=cfg.env.features,
+        budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
+        target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
+        epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
+        loss_coef=eng.loss_coef, emulate_bf16=False, forced_actions=acts)
+    assert _rel(grad, g32) < 0.1
+
+
+@pytest.mark.parametrize("opt", ["adam", "adagrad", "sgd"])
+def test_optimizer_step_matches_reference(native_built, opt):
+    from sharetrade.models import qnet as qn
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg()
+    cfg.agent.optimizer = opt
+    cfg.agent.lr = 1e-2
+    E = 64
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    p0 = eng.params.detach().cpu().clone()
+    st = qn.OptimState(opt, eng.layout.numel, cfg.agent.adagrad_init_acc)
+    for it in range(3):
+        grad = eng.native_grad().detach().cpu().clone()
+        # apply the native update only (mode 2 on the already-reduced grad)
+        eng._op.mode = 2
+        from sharetrade.ops import native
+
+        native.check(native.lib().st_reduce_optim(eng._op, native.stream_handle()), "update")
+        torch.cuda.synchronize()
+        qn.optimizer_step_ref(p0, grad, st, eng.mask.cpu(), cfg.agent.lr, cfg.agent.adam_betas, cfg.agent.adam_eps)
+        got = eng.params.detach().cpu()
+        assert torch.allclose(got, p0, rtol=1e-5, atol=1e-6), (opt, it, float((got - p0).abs().max()))
+        assert torch.equal(eng.params_bf.float().cpu(), got.to(torch.bfloat16).float())
+
+
+def test_random_walk_kernel(native_built):
+    from sharetrade.ops import native
+
+    E, T = 256, 3000
+    out = torch.empty(E, T, device="cuda")
+    native.random_walk(out, 50.0, 0.02, 0.0, 123, 456)
+    torch.cuda.synchronize()
+    p = out.double().cpu()
+    assert torch.isfinite(p).all() and (p > 0).all()
+    assert torch.allclose(p[:, 0], torch.full((E,), 50.0, dtype=torch.float64), rtol=1e-6)
+    r = torch.log(p[:, 1:] / p[:, :-1])
+    assert abs(float(r.mean())) < 2e-3
+    assert abs(float(r.std()) - 0.02) < 1e-3
+    # rows differ, and the generator is deterministic
+    assert not torch.equal(p[0], p[1])
+    out2 = torch.empty_like(out)
+    native.random_walk(out2, 50.0, 0.02, 0.0, 123, 456)
+    assert torch.equal(out, out2)
+
+
+def test_graph_replay_matches_eager(native_built):
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg()
+    E = 128
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    a = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    b = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    b.capture_graph(warmup=2)   # runs 2 eager steps + captures (no replay yet)
+    a.run(2)
+    for _ in range(5):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.state.budget, b.state.budget)
+    assert torch.equal(a.state.pos, b.state.pos)
+    assert int(a.ctrl[0]) == int(b.ctrl[0]) == 7
+
+
+def test_compat_env_rewards_zero(native_built):
+    """Quirk Q1 on the GPU path: decisions from constructor budget/shares => reward 0."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg(compat=True)
+    cfg.env.features = "raw"
+    E = 64
+    eng = VectorEngine(cfg, prices=_prices(E, T=260), device=torch.device("cuda", 0), envs=E)
+    eng.run(70)  # > one episode (T - H = 59 steps)
+    torch.cuda.synchronize()
+    s = eng.stats_dict()
+    assert s["reward_sum"] == 0.0
+    assert s["episodes_done"] == E
+    fin = eng.final_portfolios().cpu()
+    assert torch.all(fin == cfg.env.budget)
