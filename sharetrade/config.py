@@ -68,7 +68,7 @@ class AgentConfig:
     optimizer: str = "adagrad"      # adagrad | adam | sgd
     lr: float = 0.01
     adagrad_init_acc: float = 0.1   # TF default initial accumulator (SURVEY §5.6 knob)
-    adam_betas: Sequence[float] = (0.9, 0.999)
+    adam_betas: List[float] = field(default_factory=lambda: [0.9, 0.999])
     adam_eps: float = 1e-8
     # "compat": TD target written at argmax(q_next) (quirk Q2, QDecisionPolicyActor.scala:69-71)
     # "action": TD target written at the taken action (the intended semantics)

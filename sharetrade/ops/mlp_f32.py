@@ -1,0 +1,239 @@
+"""Host side of the exact-fp32 kernels (`csrc/mlp_f32.hip`).
+
+* :class:`F32Learner` — the GPU backend of :class:`~sharetrade.policy.learner.QLearner`
+  (the ``QDecisionPolicyActor`` path): ``forward`` = 1 launch,
+  ``td_update`` = 2 launches (rows kernel + grad/optimizer kernel).
+* :class:`F32EngineStep` — the fp32 step of :class:`~sharetrade.trainer.engine.VectorEngine`
+  for networks the fused bf16 kernel does not cover (the reference's
+  203->200->3 compat net): env step + TD + backward in the rows kernel, then the
+  grad/optimizer kernel, then a counter advance — graph-capturable.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..models import qnet as qn
+from . import native
+
+F_MAXL = 6
+OPT_KIND = {"sgd": 0, "adagrad": 1, "adam": 2}
+
+
+class F32Net(C.Structure):
+    _fields_ = [
+        ("L", C.c_int), ("pd", C.c_int * (F_MAXL + 1)), ("dims", C.c_int * (F_MAXL + 1)),
+        ("off_w", C.c_int * F_MAXL), ("off_b", C.c_int * F_MAXL), ("act_off", C.c_int * F_MAXL),
+        ("dz_off", C.c_int * F_MAXL), ("act_stride", C.c_int), ("dz_stride", C.c_int),
+        ("bias_col", C.c_int), ("input_dim", C.c_int), ("output_relu", C.c_int), ("P", C.c_int),
+    ]
+
+
+class F32Rows(C.Structure):
+    _fields_ = [
+        ("params", C.c_void_p), ("x", C.c_void_p), ("xn", C.c_void_p), ("reward", C.c_void_p),
+        ("action", C.c_void_p), ("q_out", C.c_void_p), ("qn_out", C.c_void_p), ("acts", C.c_void_p),
+        ("dz", C.c_void_p), ("loss", C.c_void_p), ("B", C.c_int), ("mode", C.c_int),
+        ("gamma", C.c_float), ("coef", C.c_float),
+        ("prices", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
+        ("pos", C.c_void_p), ("episodes", C.c_void_p), ("last_final", C.c_void_p), ("ret_sum", C.c_void_p),
+        ("actions_out", C.c_void_p), ("rewards_out", C.c_void_p), ("ctrl", C.c_void_p),
+        ("T", C.c_int), ("H", C.c_int), ("compat_env", C.c_int), ("target_compat", C.c_int),
+        ("feat_mode", C.c_int), ("s0", C.c_int), ("env_offset", C.c_int),
+        ("eps", C.c_float), ("inv_ramp", C.c_float), ("b0", C.c_float), ("inv_b0", C.c_float),
+        ("key0", C.c_uint32), ("key1", C.c_uint32),
+    ]
+
+
+class F32Optim(C.Structure):
+    _fields_ = [
+        ("params", C.c_void_p), ("mask", C.c_void_p), ("s1", C.c_void_p), ("s2", C.c_void_p),
+        ("acts", C.c_void_p), ("dz", C.c_void_p), ("ctrl", C.c_void_p), ("grad", C.c_void_p), ("B", C.c_int),
+        ("kind", C.c_int), ("t", C.c_int), ("mode", C.c_int), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+        ("scale", C.c_float),
+    ]
+
+
+def _bind():
+    L = native.lib()
+    if not getattr(L, "_f32_bound", False):
+        L.st_f32_rows.argtypes = [C.POINTER(F32Net), C.POINTER(F32Rows), C.c_void_p]
+        L.st_f32_rows.restype = C.c_int
+        L.st_f32_grad_optim.argtypes = [C.POINTER(F32Net), C.POINTER(F32Optim), C.c_void_p]
+        L.st_f32_grad_optim.restype = C.c_int
+        L.st_f32_advance.argtypes = [C.c_void_p, C.c_void_p]
+        L.st_f32_advance.restype = C.c_int
+        L.st_f32_lds_bytes.argtypes = [C.POINTER(F32Net)]
+        L.st_f32_lds_bytes.restype = C.c_int
+        L._f32_bound = True
+    return L
+
+
+def make_net(layout: qn.QNetLayout, output_relu: bool) -> F32Net:
+    if layout.n_layers > F_MAXL:
+        raise NotImplementedError(f"fp32 kernels support up to {F_MAXL} layers")
+    if max(layout.pdims) > 1024:
+        raise NotImplementedError("fp32 kernels support padded widths up to 1024")
+    n = F32Net()
+    n.L = layout.n_layers
+    for l, d in enumerate(layout.pdims):
+        n.pd[l] = d
+        n.dims[l] = layout.dims[l]
+    ao = dz = 0
+    for l in range(layout.n_layers):
+        n.off_w[l] = layout.segments[f"W{l}"].offset
+        n.off_b[l] = layout.segments[f"b{l}"].offset if l > 0 else -1
+        n.act_off[l] = ao
+        ao += layout.pdims[l]
+        n.dz_off[l] = dz
+        dz += layout.pdims[l + 1]
+    n.act_stride, n.dz_stride = ao, dz
+    n.bias_col, n.input_dim, n.output_relu, n.P = layout.bias_col, layout.input_dim, int(output_relu), layout.numel
+    return n
+
+
+class _Scratch:
+    """Per-batch-size work buffers (activations, dz, q, loss)."""
+
+    def __init__(self, net: F32Net, B: int, device):
+        f = dict(dtype=torch.float32, device=device)
+        self.B = B
+        self.acts = torch.zeros(B, net.act_stride, **f)
+        self.dz = torch.zeros(B, net.dz_stride, **f)
+        self.q = torch.zeros(B, 16, **f)
+        self.qn = torch.zeros(B, 16, **f)
+        self.loss = torch.zeros(B, **f)
+
+
+class F32Learner:
+    def __init__(self, learner):
+        self.l = learner
+        self.layout: qn.QNetLayout = learner.layout
+        self.net = make_net(self.layout, learner.cfg.model.output_relu)
+        self.L = _bind()
+        self._scratch = {}
+
+    def _s(self, B: int) -> _Scratch:
+        s = self._scratch.get(B)
+        if s is None:
+            s = self._scratch[B] = _Scratch(self.net, B, self.l.device)
+        return s
+
+    def sync_from_learner(self) -> None:
+        pass  # the learner's tensors are used in place
+
+    def _pad(self, x: torch.Tensor) -> torch.Tensor:
+        return qn.pad_input(self.layout, x.to(self.l.device, torch.float32)).contiguous()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B = x.shape[0]
+        s = self._s(B)
+        xp = self._pad(x)
+        r = F32Rows()
+        r.params, r.x, r.q_out, r.B, r.mode = self.l.params.data_ptr(), xp.data_ptr(), s.q.data_ptr(), B, 0
+        native.check(self.L.st_f32_rows(self.net, r, native.stream_handle()), "st_f32_rows(fwd)")
+        return s.q.clone()
+
+    def td_update(self, x, r_, xn, act: Optional[torch.Tensor], coef: float) -> float:
+        B = x.shape[0]
+        s = self._s(B)
+        xp, xnp = self._pad(x), self._pad(xn)
+        rew = r_.to(self.l.device, torch.float32).contiguous()
+        acti = act.to(self.l.device, torch.int32).contiguous() if act is not None else None
+        a = self.l.cfg.agent
+        r = F32Rows()
+        r.params, r.x, r.xn, r.reward = self.l.params.data_ptr(), xp.data_ptr(), xnp.data_ptr(), rew.data_ptr()
+        r.action = acti.data_ptr() if acti is not None else None
+        r.q_out, r.qn_out, r.acts, r.dz, r.loss = (s.q.data_ptr(), s.qn.data_ptr(), s.acts.data_ptr(),
+                                                   s.dz.data_ptr(), s.loss.data_ptr())
+        r.B, r.mode, r.gamma, r.coef = B, 1, float(a.gamma), float(coef)
+        sh = native.stream_handle()
+        native.check(self.L.st_f32_rows(self.net, r, sh), "st_f32_rows(td)")
+        opt = self.l.opt
+        opt.t += 1
+        o = F32Optim()
+        o.params, o.mask = self.l.params.data_ptr(), self.l.mask.data_ptr()
+        o.s1 = opt.s1.data_ptr() if opt.s1.numel() else None
+        o.s2 = opt.s2.data_ptr() if opt.s2.numel() else None
+        o.acts, o.dz, o.ctrl, o.B, o.kind, o.t = s.acts.data_ptr(), s.dz.data_ptr(), None, B, OPT_KIND[opt.kind], opt.t
+        o.mode, o.grad = 0, None
+        o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+        native.check(self.L.st_f32_grad_optim(self.net, o, sh), "st_f32_grad_optim")
+        return float(s.loss.sum())
+
+
+class F32EngineStep:
+    """fp32 engine step for :class:`VectorEngine` (see module docstring)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        cfg = eng.cfg
+        self.layout = eng.layout
+        self.net = make_net(self.layout, cfg.model.output_relu)
+        self.L = _bind()
+        E = eng.E
+        self.s = _Scratch(self.net, E, eng.device)
+        st = eng.state
+        r = F32Rows()
+        r.params = eng.params.data_ptr()
+        r.q_out, r.qn_out, r.acts, r.dz, r.loss = (self.s.q.data_ptr(), None, self.s.acts.data_ptr(),
+                                                   self.s.dz.data_ptr(), self.s.loss.data_ptr())
+        r.B, r.mode, r.gamma, r.coef = E, 2, float(cfg.agent.gamma), float(eng.loss_coef)
+        r.prices = eng.prices.data_ptr()
+        r.budget, r.shares, r.value, r.pos = (st.budget.data_ptr(), st.shares.data_ptr(), st.value.data_ptr(),
+                                              st.pos.data_ptr())
+        r.episodes, r.last_final, r.ret_sum = st.episodes.data_ptr(), st.last_final.data_ptr(), st.ret_sum.data_ptr()
+        r.actions_out, r.rewards_out, r.ctrl = (eng.actions_out.data_ptr(), eng.rewards_out.data_ptr(),
+                                                eng.ctrl.data_ptr())
+        r.T, r.H = eng.T, eng.H
+        r.compat_env = int(cfg.env.compat_decisions)
+        r.target_compat = int(cfg.agent.target_slot == "compat")
+        from ..env.trading import FEATURES
+
+        r.feat_mode = FEATURES[cfg.env.features]
+        r.s0, r.env_offset = int(cfg.env.shares), int(eng.env_offset)
+        r.eps = float(cfg.agent.epsilon)
+        r.inv_ramp = float(np.float32(1.0 / cfg.agent.ramp))
+        r.b0 = float(cfg.env.budget)
+        r.inv_b0 = float(np.float32(1.0 / cfg.env.budget))
+        r.key0, r.key1 = int(eng.key0), int(eng.key1)
+        self.rows = r
+        a = cfg.agent
+        o = F32Optim()
+        opt = eng.opt
+        o.params, o.mask = eng.params.data_ptr(), eng.mask.data_ptr()
+        o.s1 = opt.s1.data_ptr() if opt.s1.numel() else None
+        o.s2 = opt.s2.data_ptr() if opt.s2.numel() else None
+        o.acts, o.dz, o.ctrl, o.B, o.kind = self.s.acts.data_ptr(), self.s.dz.data_ptr(), eng.ctrl.data_ptr(), E, \
+            OPT_KIND[opt.kind]
+        o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+        self.optim = o
+
+    def grad_only(self) -> None:
+        sh = native.stream_handle()
+        native.check(self.L.st_f32_rows(self.net, self.rows, sh), "st_f32_rows(engine)")
+
+    def grad(self, out: torch.Tensor) -> torch.Tensor:
+        """Rows kernel + local gradient into ``out`` (no update)."""
+        sh = native.stream_handle()
+        native.check(self.L.st_f32_rows(self.net, self.rows, sh), "st_f32_rows(engine)")
+        self.optim.mode, self.optim.grad = 1, out.data_ptr()
+        native.check(self.L.st_f32_grad_optim(self.net, self.optim, sh), "st_f32_grad(engine)")
+        return out
+
+    def step(self, grad_buf: Optional[torch.Tensor] = None, allreduce=None) -> None:
+        """One engine step.  With ``allreduce`` (DP): local grad -> allreduce(grad_buf) -> update."""
+        sh = native.stream_handle()
+        if allreduce is None:
+            native.check(self.L.st_f32_rows(self.net, self.rows, sh), "st_f32_rows(engine)")
+            self.optim.mode, self.optim.grad = 0, None
+            native.check(self.L.st_f32_grad_optim(self.net, self.optim, sh), "st_f32_grad_optim")
+        else:
+            self.grad(grad_buf)
+            allreduce(grad_buf)
+            self.optim.mode, self.optim.grad = 2, grad_buf.data_ptr()
+            native.check(self.L.st_f32_grad_optim(self.net, self.optim, sh), "st_f32_update(engine)")
+        native.check(self.L.st_f32_advance(self.eng.ctrl.data_ptr(), sh), "st_f32_advance")

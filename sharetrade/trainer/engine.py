@@ -89,15 +89,19 @@ class VectorEngine:
             be = "native" if self.device.type == "cuda" else "torch"
         self.backend = be
         L = self.layout
+        self.kernel = None
         if be == "native":
             if self.device.type != "cuda":
                 raise ValueError("native backend needs a GPU device")
-            if L.n_layers != 3 or not native.qstep_supported(L.pdims[0], L.pdims[1], L.pdims[2]):
-                raise NotImplementedError(f"no fused bf16 step kernel for padded dims {L.pdims}")
-            if self.E % 32:
-                raise ValueError("native engine needs envs_per_rank % 32 == 0")
-            if self.H + 3 > L.in_p - 16:
-                raise ValueError("history too long for the fused kernel's input padding")
+            fused_ok = (cfg.engine.dtype == "bf16" and L.n_layers == 3 and self.E % 32 == 0
+                        and self.H + 3 <= L.in_p - 16
+                        and native.qstep_supported(L.pdims[0], L.pdims[1], L.pdims[2]))
+            if cfg.engine.dtype == "bf16" and not fused_ok:
+                raise NotImplementedError(
+                    f"no fused bf16 step kernel for padded dims {L.pdims} / E={self.E} (use engine.dtype=fp32)")
+            # bf16: the fused MFMA step kernel (csrc/qstep_fused.hip);
+            # fp32: the exact-fp32 row kernels (csrc/mlp_f32.hip) — any MLP up to 6 layers x 1024
+            self.kernel = "bf16_fused" if fused_ok else "fp32_rows"
         # ------------------------------------------------------------ data
         self.prices = prices.to(self.device, torch.float32).contiguous() if prices is not None else \
             make_price_bank(cfg, self.E, self.device, seed=rank)
@@ -129,17 +133,22 @@ class VectorEngine:
     def _init_native(self):
         dev = self.device
         L = self.layout
+        self.ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.actions_out = torch.zeros(self.E, dtype=torch.int32, device=dev)
+        self.rewards_out = torch.zeros(self.E, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(L.numel, dtype=torch.float32, device=dev)
+        self.stat_acc = torch.zeros(NSTAT, dtype=torch.float64, device=dev)
+        if self.kernel == "fp32_rows":
+            from ..ops.mlp_f32 import F32EngineStep
+
+            self._f32 = F32EngineStep(self)
+            return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
         self.grid = max(1, min(props.multi_processor_count, self.E // 32))
         self.slab = torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev)
         self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)
-        self.stat_acc = torch.zeros(NSTAT, dtype=torch.float64, device=dev)
-        self.grad = torch.zeros(L.numel, dtype=torch.float32, device=dev)
-        self.ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.actions_out = torch.zeros(self.E, dtype=torch.int32, device=dev)
-        self.rewards_out = torch.zeros(self.E, dtype=torch.float32, device=dev)
         self._build_structs()
 
     def _build_structs(self):
@@ -183,6 +192,13 @@ class VectorEngine:
 
     # ---------------------------------------------------------------- stepping
     def _native_step(self):
+        if self.kernel == "fp32_rows":
+            ar = None
+            if self.world_size > 1:
+                ar = lambda g: torch.distributed.all_reduce(g, group=self.group)  # noqa: E731
+            self._f32.step(self.grad, ar)
+            self._f32_stats()
+            return
         L = native.lib()
         sh = native.stream_handle()
         native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],
@@ -198,9 +214,19 @@ class VectorEngine:
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
         self.stat_acc += self.stat_slab.sum(0, dtype=torch.float64)
 
+    def _f32_stats(self) -> None:
+        r = self.rewards_out.double()
+        self.stat_acc[0] += r.sum()
+        self.stat_acc[1] += self._f32.s.loss.double().sum()
+
     def native_grad(self) -> torch.Tensor:
         """Test hook: run the fused step kernel + slab reduction only (no optimizer
         update); returns the reduced gradient.  Advances the env state."""
+        if self.kernel == "fp32_rows":
+            self._f32.grad(self.grad)
+            self._f32_stats()
+            self.step_count += 1
+            return self.grad
         L = native.lib()
         sh = native.stream_handle()
         native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],

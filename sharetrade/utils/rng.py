@@ -74,6 +74,17 @@ class PhiloxStream:
         self.seed, self.rank, self.stream = seed, rank, stream
         self.counter = 0
 
+    def next_blocks(self, n: int) -> np.ndarray:
+        """``n`` independent draws of 4 uniforms (one Philox counter each) -> [n, 4];
+        a batch of ``n`` consumes exactly the counters ``n`` single draws would."""
+        k0, k1 = key_for(self.seed, self.rank)
+        c = np.arange(self.counter, self.counter + n, dtype=np.uint64)
+        r = philox4x32((c & np.uint64(0xFFFFFFFF)).astype(np.uint32), (c >> np.uint64(32)).astype(np.uint32),
+                       np.zeros(n, np.uint32), np.full(n, self.stream, np.uint32),
+                       np.full(n, k0, np.uint32), np.full(n, k1, np.uint32))
+        self.counter += n
+        return np.stack([u24(v) for v in r], axis=1)
+
     def next_uniforms(self, n: int = 2) -> np.ndarray:
         out = []
         while len(out) < n:

@@ -1,0 +1,76 @@
+"""End-to-end ShareTradeHelper runs (CPU): price service -> router -> workers -> learner."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from sharetrade.config import default_csv_path, preset_config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HAVE_CSV = os.path.exists(default_csv_path())
+
+
+def _cfg(max_ok=True):
+    cfg = preset_config("test")
+    cfg.router.poll_interval_s = 0.1
+    cfg.env.progress_every = 0
+    return cfg
+
+
+@pytest.mark.skipif(not HAVE_CSV, reason="reference MSFT csv not present")
+@pytest.mark.parametrize("engine", ["actors", "vector"])
+def test_compat_run_reproduces_reference_avg_std(engine):
+    """Reference semantics (quirk Q1): every worker ends at its initial budget -> 2400.0 / 0.0."""
+    from sharetrade.app import run
+
+    res = run(_cfg(), engine=engine, device="cpu", max_prices=260, quiet=True)
+    assert res["completed"] == 1.0
+    assert res["avg"] == 2400.0 and res["std"] == 0.0
+
+
+@pytest.mark.skipif(not HAVE_CSV, reason="reference MSFT csv not present")
+def test_intended_semantics_trade():
+    from sharetrade.app import run
+
+    cfg = preset_config("intended")
+    cfg.persist.journal_plugin = "inmemory"
+    cfg.router.poll_interval_s = 0.1
+    cfg.env.progress_every = 0
+    cfg.agent.ramp = 10.0
+    res = run(cfg, engine="vector", device="cpu", max_prices=320, quiet=True)
+    assert res["completed"] == 1.0
+    assert res["avg"] != 2400.0        # the fixed env actually trades
+
+
+def test_cli_config_and_engine():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "sharetrade", "config", "--preset", "flagship",
+                          "--set", "model.hidden=[64,64]"], capture_output=True, text=True, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr
+    cfg = json.loads(out.stdout)
+    assert cfg["model"]["hidden"] == [64, 64] and cfg["agent"]["optimizer"] == "adam"
+    out = subprocess.run([sys.executable, "-m", "sharetrade", "engine", "--preset", "intended", "--steps", "3",
+                          "--envs", "4", "--device", "cpu", "--set", "data.source=random_walk",
+                          "--set", "data.length=300"], capture_output=True, text=True, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["backend"] == "torch" and res["envs"] == 4
+
+
+def test_config_file_roundtrip(tmp_path):
+    from sharetrade.config import Config
+
+    cfg = preset_config("flagship")
+    p = tmp_path / "c.json"
+    p.write_text(cfg.to_json())
+    back = Config.load(str(p), "reference_compat")
+    assert back.to_dict() == cfg.to_dict()
+    t = tmp_path / "c.toml"
+    t.write_text('[agent]\noptimizer = "sgd"\nlr = 0.5\n[model]\nhidden = [32]\n')
+    c2 = Config.load(str(t))
+    assert c2.agent.optimizer == "sgd" and c2.agent.lr == 0.5 and c2.model.hidden == [32]
+    with pytest.raises(KeyError):
+        cfg.override(["agent.nope=1"])

@@ -1,0 +1,127 @@
+"""Exact-fp32 HIP kernels (csrc/mlp_f32.hip) vs the plain-PyTorch fp32 oracle."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.fixture
+def dev(native_built):
+    return torch.device("cuda", 0)
+
+
+def _states(B, seed=0, raw=True):
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(15, 180, (B, 203)).astype(np.float32)
+    if raw:
+        x[:, 201] = rng.uniform(500, 2400, B)
+        x[:, 202] = rng.integers(0, 5, B)
+    return torch.from_numpy(x)
+
+
+@pytest.mark.parametrize("preset", ["reference_compat", "intended", "flagship"])
+def test_forward_matches_oracle(dev, preset):
+    from sharetrade.config import preset_config
+    from sharetrade.models import qnet as qn
+    from sharetrade.policy.learner import QLearner
+
+    cfg = preset_config(preset)
+    ln = QLearner(cfg, device=dev)
+    assert ln.backend == "native"
+    x = _states(9, raw=preset != "flagship")
+    got = ln.q_values(x).cpu()
+    ref, _, _ = qn.forward(ln.params.cpu(), ln.layout, x, cfg.model.output_relu)
+    assert torch.allclose(got, ref[:, :3], rtol=2e-5, atol=1e-3 * float(ref.abs().max() + 1)), (got, ref[:, :3])
+
+
+@pytest.mark.parametrize("opt", ["adagrad", "adam", "sgd"])
+@pytest.mark.parametrize("slot", ["compat", "action"])
+@pytest.mark.parametrize("B", [1, 5])
+def test_td_update_matches_oracle(dev, opt, slot, B):
+    from sharetrade.config import preset_config
+    from sharetrade.policy.learner import QLearner
+
+    cfg = preset_config("intended" if slot == "action" else "reference_compat")
+    cfg.agent.optimizer = opt
+    cfg.agent.lr = 1e-3
+    cfg.agent.target_slot = slot
+    gpu = QLearner(cfg, device=dev)
+    cpu = QLearner(cfg, device=torch.device("cpu"))
+    assert torch.equal(gpu.params.cpu(), cpu.params)
+    for it in range(3):
+        x, xn = _states(B, 10 + it), _states(B, 20 + it)
+        r = np.linspace(-3, 3, B).astype(np.float32)
+        acts = np.arange(B) % 3 if slot == "action" else None
+        lg = gpu.update(x, r, xn, acts)
+        lc = cpu.update(x, r, xn, acts)
+        assert abs(lg - lc) <= 1e-4 * max(1.0, abs(lc)), (lg, lc)
+        assert _rel(gpu.params.cpu(), cpu.params) < 1e-5, _rel(gpu.params.cpu(), cpu.params)
+        if cpu.opt.s1.numel():
+            assert _rel(gpu.opt.s1.cpu(), cpu.opt.s1) < 1e-4
+
+
+def test_policy_actor_on_gpu_uses_native_learner(dev):
+    from sharetrade import protocol as P
+    from sharetrade.actors.runtime import ActorSystem
+    from sharetrade.config import preset_config
+    from sharetrade.policy.actor import QDecisionPolicyActor
+
+    s = ActorSystem("gpu")
+    try:
+        pol = s.actor_of(QDecisionPolicyActor.props(preset_config("test"), device=dev))
+        st = list(range(55, 256)) + [1000, 0]
+        nx = list(range(55, 256)) + [940, 1]
+        assert pol.ask(P.UpdateQ(st, 10.0, nx), 10).result(20) is P.Updated
+        assert isinstance(pol.ask(P.SelectionAction(st, 0), 10).result(20), P.Action)
+        actor = pol._cell.actor
+        assert actor.learner.backend == "native"
+    finally:
+        s.terminate()
+
+
+@pytest.mark.parametrize("preset", ["reference_compat", "intended"])
+def test_fp32_engine_matches_torch_engine(dev, preset):
+    """The fp32 engine step (rows kernel + grad/optim) vs the oracle engine for 6 steps."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config(preset)
+    cfg.engine.dtype = "fp32"
+    cfg.agent.epsilon = 0.5
+    cfg.agent.ramp = 4.0          # exploit early so argmax paths are exercised
+    E, T = 10, 260
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 5, n_series=E).astype(np.float32))
+    g = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    c = VectorEngine(cfg, prices=prices, device=torch.device("cpu"), envs=E, backend="torch")
+    assert g.kernel == "fp32_rows"
+    for _ in range(6):
+        g.step()
+        c.step()
+        torch.cuda.synchronize()
+        for k in ("budget", "shares", "pos"):
+            assert torch.equal(getattr(g.state, k).cpu(), getattr(c.state, k)), k
+        assert _rel(g.params.cpu(), c.params) < 1e-5
+
+
+def test_fp32_engine_compat_reproduces_reference_portfolio(dev):
+    """Quirk Q1 on the GPU fp32 path: reward 0 at every step, final portfolio = budget."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("reference_compat")
+    E, T = 10, 320
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 9, n_series=1).astype(np.float32)).expand(E, -1)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    eng.capture_graph(warmup=1) if hasattr(eng, "capture_graph") else None
+    eng.run(T - 201 - 1)
+    torch.cuda.synchronize()
+    assert float(eng.stat_acc[0]) == 0.0
+    fin = eng.final_portfolios().cpu()
+    assert torch.all(fin == 2400.0), fin

@@ -1,0 +1,358 @@
+"""Ports of the reference's ScalaTest specs, with the §4.3 intents:
+
+* QDecisionPolicyActorSpec.scala   -> TestPolicyActor
+* TrainerChildActorSpec.scala      -> TestTrainerChild
+* TrainerRouterActorSpec.scala     -> TestTrainerRouter (fake `train` returning 10.0)
+* SharePriceGetterSpec.scala       -> TestSharePriceGetter (synthetic linear source)
+"""
+import datetime as dt
+import random
+import time
+
+import numpy as np
+import pytest
+
+from sharetrade import protocol as P
+from sharetrade.actors.routing import GetRoutees, Routees
+from sharetrade.actors.runtime import ActorSystem, PoisonPill, Props
+from sharetrade.actors.testkit import EventFilter, TestActorRef, TestKit, TestProbe, await_assert
+from sharetrade.config import preset_config
+from sharetrade.data.getter import SharePriceGetter
+from sharetrade.data.prices import LinearPriceSource
+from sharetrade.errors import IllegalArgumentException
+from sharetrade.persist.journal import InMemoryJournal, InMemorySnapshotStore
+from sharetrade.policy.actor import QDecisionPolicyActor
+from sharetrade.trainer.child import TrainerChildActor
+from sharetrade.trainer.router import TrainerRouterActor
+
+
+@pytest.fixture
+def system():
+    s = ActorSystem("spec", loglevel="DEBUG")
+    yield s
+    s.terminate()
+
+
+@pytest.fixture
+def kit(system):
+    return TestKit(system)
+
+
+def _cfg():
+    cfg = preset_config("test")
+    return cfg
+
+
+# ====================================================================== QDecisionPolicyActorSpec
+STATE = list(range(55, 256)) + [1000, 0]          # 203 values (QDecisionPolicyActorSpec.scala:16)
+NEXT_STATE = list(range(55, 256)) + [940, 1]
+WRONG = list(range(55, 100)) + [1000, 0]
+
+
+class TestPolicyActor:
+    def setup_method(self):
+        InMemoryJournal.clear()        # InMemoryCleanup trait (QDecisionPolicyActorSpec.scala:75-87)
+        InMemorySnapshotStore.clear()
+
+    def test_state_lists_have_203_values(self):
+        assert len(STATE) == 203 and len(NEXT_STATE) == 203
+
+    def test_return_action_in_initial_stage(self, system, kit):
+        pol = system.actor_of(QDecisionPolicyActor.props(_cfg()))
+        kit.tell(pol, P.SelectionAction(np.array([STATE], np.float32), 0))
+        kit.expect_msg_type(P.Action)
+
+    def test_update_q_replies_updated(self, system, kit):
+        # the spec expects no reply, but the worker depends on `Updated`
+        pol = system.actor_of(QDecisionPolicyActor.props(_cfg()))
+        kit.tell(pol, P.UpdateQ(np.array([STATE], np.float32), 10, np.array([NEXT_STATE], np.float32)))
+        kit.expect_msg(P.Updated)
+        kit.expect_no_message()
+
+    def test_action_after_update(self, system, kit):
+        pol = system.actor_of(QDecisionPolicyActor.props(_cfg()))
+        kit.tell(pol, P.UpdateQ(STATE, 10, NEXT_STATE))
+        kit.expect_msg(P.Updated)
+        kit.tell(pol, P.SelectionAction(STATE, 0))
+        kit.expect_msg_type(P.Action)
+
+    def test_selection_wrong_shape_throws(self, system, kit):
+        pol = system.actor_of(QDecisionPolicyActor.props(_cfg()))
+        with EventFilter(system, IllegalArgumentException, occurrences=1).intercept():
+            kit.tell(pol, P.SelectionAction(WRONG, 0))
+
+    def test_update_wrong_shape_throws(self, system, kit):
+        pol = system.actor_of(QDecisionPolicyActor.props(_cfg()))
+        with EventFilter(system, IllegalArgumentException, occurrences=1).intercept():
+            kit.tell(pol, P.UpdateQ(STATE, 10, WRONG))
+
+    def test_exploit_ramp_greedy_after_1000_steps(self, system, kit):
+        """step >= 1000 * eps => exploit with prob 0.9; the greedy action is argmax q."""
+        cfg = _cfg()
+        cfg.agent.epsilon = 1.0
+        pol_actor = QDecisionPolicyActor(cfg)
+        q = pol_actor.learner.q_values(np.array([STATE], np.float32))[0]
+        greedy = int(q.argmax())
+        acts = pol_actor.learner.select(np.array([STATE] * 64, np.float32), 5000)
+        assert (acts == greedy).all()
+
+    def test_batched_selections_match_serial(self, system):
+        """Mailbox micro-batching is invisible: same actions as one-at-a-time."""
+        cfg = _cfg()
+        a = system.actor_of(QDecisionPolicyActor.props(cfg, batch_selections=True))
+        b = system.actor_of(QDecisionPolicyActor.props(cfg, batch_selections=False))
+        rng = np.random.default_rng(0)
+        states = [rng.uniform(10, 100, 203).astype(np.float32) for _ in range(40)]
+        fa = [a.ask(P.SelectionAction(s, 900 + i), 5) for i, s in enumerate(states)]
+        fb = [b.ask(P.SelectionAction(s, 900 + i), 5) for i, s in enumerate(states)]
+        assert [f.result(10) for f in fa] == [f.result(10) for f in fb]
+
+
+# ====================================================================== TrainerChildActorSpec
+def _stock(n_from, n_to, name="my-share"):
+    base = dt.date(2001, 7, 10)
+    return P.StockDataResponse(name, P.TreeMap((base + dt.timedelta(days=i), float(i)) for i in range(n_from, n_to)))
+
+
+class TestTrainerChild:
+    def test_too_few_prices_throws(self, system, kit):
+        probe = TestProbe(system)
+        trainer = system.actor_of(TrainerChildActor.props(probe.ref, 2000, 0, _cfg()), "trainer-actor-test")
+        with EventFilter(system, IllegalArgumentException, occurrences=1).intercept():
+            kit.tell(trainer, P.Train(_stock(55, 100)))
+
+    def test_initial_get_portfolio_not_computed(self, system, kit):
+        probe = TestProbe(system)
+        trainer = system.actor_of(TrainerChildActor.props(probe.ref, 2000, 0, _cfg()), "trainer-actor-test")
+        kit.tell(trainer, P.GetPortfolio)
+        kit.expect_msg(P.NotComputed)
+
+    def _normal_trained_case(self, system, kit):
+        stock = _stock(55, 257)                      # 202 prices -> exactly one step
+        assert stock.size >= 202
+        parent = TestProbe(system)
+        policy = TestProbe(system)
+        trainer = TestActorRef(system, TrainerChildActor.props(policy.ref, 2000, 0, _cfg()), parent.ref,
+                               "ChildActor")
+        kit.tell(trainer, P.Train(stock))
+        sa = policy.expect_msg_type(P.SelectionAction)   # mocking
+        assert np.asarray(sa.current_state).shape == (1, 203)
+        policy.reply(P.Sell)
+        upd = policy.expect_msg_type(P.UpdateQ)          # the probe must answer UpdateQ
+        assert upd.reward == 0.0                         # Sell with 0 shares -> Hold, portfolio unchanged
+        policy.reply(P.Updated)
+        parent.expect_msg(P.Trained)
+        kit.tell(trainer, P.GetPortfolio)
+        td = kit.expect_msg_type(P.TrainedData)
+        assert td.portfolio == 2000.0
+        return trainer, parent
+
+    def test_train_reports_trained(self, system, kit):
+        self._normal_trained_case(system, kit)
+
+    def test_initialise_rolls_back(self, system, kit):
+        trainer, parent = self._normal_trained_case(system, kit)
+        kit.tell(trainer, P.Initialise)
+        parent.expect_msg(P.Initialised)
+        kit.tell(trainer, P.GetPortfolio)
+        kit.expect_msg(P.NotComputed)
+
+    def test_already_trained_ignores_train(self, system, kit):
+        trainer, parent = self._normal_trained_case(system, kit)
+        kit.tell(trainer, P.Train(_stock(55, 257)))
+        kit.tell(trainer, P.GetPortfolio)
+        kit.expect_msg_type(P.TrainedData)
+        parent.expect_no_message()
+
+
+# ====================================================================== TrainerRouterActorSpec
+class FakeTrainer(TrainerChildActor):
+    """`override def train` of TrainerRouterActorSpec.scala:146-151: sleep U[0,500) ms, return 10.0."""
+
+    def train(self, stock_data):
+        def run():
+            time.sleep(random.random() * 0.5)
+            return 10.0
+        return self.context.system.blocking_future(run)
+
+
+def _router(system, policy, cfg=None):
+    cfg = cfg or _cfg()
+    child = Props(FakeTrainer, policy.ref, 2000, 0, cfg)
+    return system.actor_of(TrainerRouterActor.props(policy.ref, 2000, 0, cfg, child_trainer_props=child),
+                           "trainer-router-test-actor")
+
+
+def _routees(kit, router) -> Routees:
+    kit.tell(router, GetRoutees)
+    return kit.expect_msg_type(Routees)
+
+
+def _result(v):
+    return v.double if isinstance(v, P.Result) else v
+
+
+class TestTrainerRouter:
+    def test_probe_sanity(self, system):
+        probe = TestProbe(system)
+        f = probe.ref.ask(P.SelectionAction(STATE, 0), 1)
+        probe.expect_msg_type(P.SelectionAction)
+        probe.reply(P.Sell)
+        assert f.result(1) is P.Sell
+
+    def test_creates_10_children(self, system, kit):
+        r = _router(system, TestProbe(system))
+        assert _routees(kit, r).size == 10
+
+    def test_initial_stage_replies(self, system, kit):
+        r = _router(system, TestProbe(system))
+        kit.tell(r, P.GetStd)
+        kit.expect_msg(P.NoTrainingDataReceived)
+        kit.tell(r, P.GetAvg)
+        kit.expect_msg(P.NoTrainingDataReceived)
+        kit.tell(r, P.StartTraining)
+        kit.expect_no_message()                    # stashed
+
+    def test_training_stage_not_computed(self, system, kit):
+        r = _router(system, TestProbe(system))
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        kit.tell(r, P.GetAvg)
+        kit.expect_msg(P.NotComputed)
+        kit.tell(r, P.GetStd)
+        kit.expect_msg(P.NotComputed)
+
+    def test_avg_std_after_all_trained(self, system, kit):
+        r = _router(system, TestProbe(system))
+        assert _routees(kit, r).size == 10
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        kit.tell(r, P.StartTraining)
+        await_assert(lambda: _assert(_routees(kit, r).size == 0), 20, 0.1)
+        kit.tell(r, P.GetAvg)
+        assert _result(kit.receive_one()) == 10.0
+        kit.tell(r, P.GetStd)
+        assert _result(kit.receive_one()) == 0.0
+
+    def test_avg_std_while_partially_trained(self, system, kit):
+        r = _router(system, TestProbe(system))
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        kit.tell(r, P.StartTraining)
+        await_assert(lambda: _assert(0 < _routees(kit, r).size < 10), 3, 0.001)
+        kit.tell(r, P.GetAvg)
+        assert _result(kit.receive_one()) == 10.0
+        kit.tell(r, P.GetStd)
+        assert _result(kit.receive_one()) == 0.0
+
+    def _kill_third(self, kit, r):
+        def attempt():
+            rs = _routees(kit, r)
+            assert len(rs) > 3
+            third = rs[3]
+            third.send(PoisonPill, kit.ref)
+            return third
+        return await_assert(attempt, 5, 0.01)
+
+    def _third_replaced(self, kit, r, third):
+        def check():
+            rs = _routees(kit, r)
+            assert third not in list(rs)
+            assert rs.size == 10
+        await_assert(check, 5, 0.01)
+
+    def test_dead_child_replaced_in_data_stage(self, system, kit):
+        r = _router(system, TestProbe(system))
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        third = self._kill_third(kit, r)
+        self._third_replaced(kit, r, third)
+        kit.tell(r, P.GetAvg)
+        kit.expect_msg(P.NotComputed)
+
+    def test_dead_child_replaced_during_training(self, system, kit):
+        r = _router(system, TestProbe(system))
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        kit.tell(r, P.StartTraining)
+        third = self._kill_third(kit, r)
+        self._third_replaced(kit, r, third)
+
+        def avg10():
+            kit.tell(r, P.GetAvg)
+            assert _result(kit.receive_one()) == 10.0
+        await_assert(avg10, 5, 0.01)
+
+    def test_replacement_is_retrained_and_run_completes(self, system, kit):
+        """Quirk Q14 fixed: the replacement worker gets `Train`, so the run still completes."""
+        r = _router(system, TestProbe(system))
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        kit.tell(r, P.StartTraining)
+        self._kill_third(kit, r)
+
+        def done():
+            kit.tell(r, P.IsEverythingDone)
+            assert kit.receive_one() is P.Completed
+        await_assert(done, 10, 0.05)
+
+    def test_async_training_data(self, system, kit):
+        r = _router(system, TestProbe(system))
+        from sharetrade.actors.runtime import pipe_to
+
+        def later():
+            time.sleep(0.5)
+            return P.SendTrainingData(_stock(55, 255))
+        pipe_to(system.future(later), r)
+        kit.tell(r, P.StartTraining)
+
+        def done():
+            kit.tell(r, P.IsEverythingDone)
+            assert kit.receive_one() is P.Completed
+        await_assert(done, 10, 0.01)
+
+    def test_reference_reply_is_bare_double(self, system, kit):
+        cfg = _cfg()
+        cfg.router.reply_result = False            # quirk Q9
+        r = _router(system, TestProbe(system), cfg)
+        kit.tell(r, P.SendTrainingData(_stock(55, 255)))
+        kit.tell(r, P.StartTraining)
+        await_assert(lambda: _assert(_routees(kit, r).size == 0), 20, 0.1)
+        kit.tell(r, P.GetAvg)
+        v = kit.receive_one()
+        assert isinstance(v, float) and v == 10.0
+
+
+def _assert(c):
+    assert c
+
+
+# ====================================================================== SharePriceGetterSpec
+class TestSharePriceGetter:
+    def setup_method(self):
+        InMemoryJournal.clear()
+        InMemorySnapshotStore.clear()
+
+    def _getter(self, system):
+        return system.actor_of(SharePriceGetter.props(LinearPriceSource(), _cfg()))
+
+    def test_lloy_10_to_13(self, system, kit):
+        g = self._getter(system)
+        kit.tell(g, P.RequestStockPrice("lloy", dt.date(2001, 7, 10), dt.date(2001, 7, 13)))
+        kit.expect_msg(P.StockDataResponse("lloy", P.TreeMap({
+            dt.date(2001, 7, 10): 0.0, dt.date(2001, 7, 11): 10.0, dt.date(2001, 7, 12): 20.0,
+            dt.date(2001, 7, 13): 30.0})))
+
+    def test_lloy_10_to_15(self, system, kit):
+        g = self._getter(system)
+        kit.tell(g, P.RequestStockPrice("lloy", dt.date(2001, 7, 10), dt.date(2001, 7, 15)))
+        m = kit.expect_msg_type(P.StockDataResponse)
+        assert list(m.share_prices.values()) == [0.0, 10.0, 20.0, 30.0, 40.0, 50.0]
+        assert list(m.share_prices.keys()) == [dt.date(2001, 7, d) for d in range(10, 16)]
+
+    def test_capita_is_persisted_and_recovered(self, system, kit):
+        g = self._getter(system)
+        kit.tell(g, P.RequestStockPrice("capita", dt.date(2002, 7, 10), dt.date(2002, 7, 11)))
+        kit.expect_msg(P.StockDataResponse("capita", P.TreeMap({dt.date(2002, 7, 10): 0.0,
+                                                                dt.date(2002, 7, 11): 10.0})))
+        await_assert(lambda: _assert(InMemoryJournal().highest_sequence_nr("Share-price-getter") == 1), 2, 0.01)
+        # a fresh incarnation recovers the persisted event
+        g2 = SharePriceGetter(LinearPriceSource(), _cfg())
+        g2.context = g._cell.context        # logging only
+        g2.recover()
+        assert g2.recovered_events == 1
+        assert g2.stored()["capita"] == {dt.date(2002, 7, 10): 0.0, dt.date(2002, 7, 11): 10.0}
