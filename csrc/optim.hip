@@ -24,7 +24,10 @@ struct OptimParams {
   const float* slab;       // [G][P] partial gradients (fused reduce) or null
   float* grad;             // [P] gradient in (if slab null) / out (reduce-only)
   unsigned long long* ctrl;
+  const float* stats;      // [G][nstat] per-workgroup step statistics (or null)
+  double* stat_acc;        // [nstat] running fp64 totals
   int G, P, kind, mode;    // mode: 0 = reduce+update, 1 = reduce only, 2 = update only
+  int nstat;
   float lr, beta1, beta2, eps, scale;
 };
 
@@ -36,10 +39,16 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
   const int tid = threadIdx.x, rg = tid >> 6, c = tid & 63;
   const int col4 = blockIdx.x * 64 + c;  // float4 column index
   const int P4 = p.P >> 2;
+  if (p.mode != 2 && p.stats && blockIdx.x == gridDim.x - 1 && tid < p.nstat) {
+    double acc = 0.0;  // step statistics folded into this pass (no extra launches)
+    for (int r = 0; r < p.G; ++r) acc += (double)p.stats[r * p.nstat + tid];
+    p.stat_acc[tid] += acc;
+  }
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
   if (p.mode != 2) {
     if (col4 < P4) {
       const float4* s = reinterpret_cast<const float4*>(p.slab) + col4;
+#pragma unroll 8
       for (int r = rg; r < p.G; r += RG) {
         const float4 v = s[(size_t)r * P4];
         g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;

@@ -287,27 +287,58 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
         st_qslot = 0.f;
 
   const int nchunks = p.E / C;
+  constexpr int RPW = C / 4;  // rows (envs) per wave in the gather
+
+  // ---------------------------------------------------------------- software-pipelined gather
+  // Global traffic of a chunk is a dependent chain (pos -> price window), so it is
+  // issued ahead: the env state of chunk i+1 is loaded while chunk i is processed
+  // (lanes 0..RPW-1 of each wave own one row each), and chunk i+1's price windows
+  // are issued right after chunk i's gather, landing during chunk i's MFMA phases.
+  int eA_pos = 0, eA_sh = 0, eA_ep = 0, eB_pos = 0, eB_sh = 0, eB_ep = 0;
+  float eA_b = 0.f, eA_val = 0.f, eA_rs = 0.f, eB_b = 0.f, eB_val = 0.f, eB_rs = 0.f;
+  float w[RPW][4];
+#define ST_LOAD_ENV(CH, POS, B, SH, VAL, RS, EP)                           \
+  if ((CH) < nchunks && lane < RPW) {                                      \
+    const int e_ = (CH) * C + wave * RPW + lane;                           \
+    POS = p.pos[e_]; B = p.budget[e_]; SH = p.shares[e_];                  \
+    VAL = p.value[e_]; RS = p.ret_sum[e_]; EP = p.episodes[e_];            \
+  }
+#define ST_LOAD_PRICES(CH, POS)                                            \
+  if ((CH) < nchunks) {                                                    \
+    _Pragma("unroll") for (int rr = 0; rr < RPW; ++rr) {                   \
+      const int ps_ = __shfl(POS, rr, 64);                                 \
+      const float* pr_ = p.prices + (size_t)((CH) * C + wave * RPW + rr) * p.T + ps_; \
+      _Pragma("unroll") for (int c = 0; c < 4; ++c) {                      \
+        const int k_ = c * 64 + lane;                                      \
+        w[rr][c] = (k_ <= H) ? pr_[k_] : 0.f;                              \
+      }                                                                    \
+    }                                                                      \
+  }
+  ST_LOAD_ENV(blockIdx.x, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
+  ST_LOAD_PRICES(blockIdx.x, eA_pos)
+  ST_LOAD_ENV(blockIdx.x + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
   __syncthreads();
 
   for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     const int ebase = chunk * C;
-    // ------------------------------------------------------------ P0: gather windows
-    for (int rr = 0; rr < C / 4; ++rr) {
-      const int r = wave * (C / 4) + rr;
-      const int e = ebase + r;
-      const int ps = p.pos[e];
-      const float b = p.budget[e];
-      const int s = p.shares[e];
-      const float* pr = p.prices + (size_t)e * p.T + ps;
-      float w[4];
+    // ------------------------------------------------------------ P0: gather windows (from registers)
+    if (lane < RPW) {
+      const int r = wave * RPW + lane;
+      sEnv[r * 8 + 0] = eA_b;
+      sEnv[r * 8 + 1] = eA_val;
+      sEnv[r * 8 + 5] = eA_rs;
+      sEnvI[r * 4 + 0] = eA_pos;
+      sEnvI[r * 4 + 1] = eA_sh;
+      sEnvI[r * 4 + 3] = eA_ep;
+    }
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int k = c * 64 + lane;
-        w[c] = (k <= H) ? pr[k] : 0.f;
-      }
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int r = wave * RPW + rr;
+      const float b = __shfl(eA_b, rr, 64);
+      const int s = __shfl(eA_sh, rr, 64);
       const int kl = H - 1, kn = H;
-      const float srcl = (kl >> 6) == 0 ? w[0] : (kl >> 6) == 1 ? w[1] : (kl >> 6) == 2 ? w[2] : w[3];
-      const float srcn = (kn >> 6) == 0 ? w[0] : (kn >> 6) == 1 ? w[1] : (kn >> 6) == 2 ? w[2] : w[3];
+      const float srcl = (kl >> 6) == 0 ? w[rr][0] : (kl >> 6) == 1 ? w[rr][1] : (kl >> 6) == 2 ? w[rr][2] : w[rr][3];
+      const float srcn = (kn >> 6) == 0 ? w[rr][0] : (kn >> 6) == 1 ? w[rr][1] : (kn >> 6) == 2 ? w[rr][2] : w[rr][3];
       const float last = __shfl(srcl, kl & 63, 64);
       const float vnew = __shfl(srcn, kn & 63, 64);
       const float inv = __fdiv_rn(1.0f, last), invn = __fdiv_rn(1.0f, vnew);
@@ -316,8 +347,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int k = c * 64 + lane;
-        if (k < H) xr[k] = f2bf(feat_price(w[c], inv, p.feat_mode));
-        if (k >= 1 && k <= H) xn[k - 1] = f2bf(feat_price(w[c], invn, p.feat_mode));
+        if (k < H) xr[k] = f2bf(feat_price(w[rr][c], inv, p.feat_mode));
+        if (k >= 1 && k <= H) xn[k - 1] = f2bf(feat_price(w[rr][c], invn, p.feat_mode));
       }
       for (int k = H + lane; k < INP; k += 64) {
         float v = 0.f;
@@ -327,13 +358,14 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
         xr[k] = f2bf(v);
         if (k >= H + 3) xn[k] = 0;
       }
-      if (lane == 0) {
-        sEnv[r * 8 + 0] = b;
-        sEnv[r * 8 + 1] = p.value[e];
-        sEnv[r * 8 + 2] = vnew;
-        sEnvI[r * 4 + 0] = ps;
-        sEnvI[r * 4 + 1] = s;
-      }
+      if (lane == 0) sEnv[r * 8 + 2] = vnew;
+    }
+    // next chunk's price windows (its env state arrived during this chunk's predecessor)
+    {
+      const int nxt = chunk + gridDim.x;
+      ST_LOAD_PRICES(nxt, eB_pos)
+      eA_pos = eB_pos; eA_b = eB_b; eA_sh = eB_sh; eA_val = eB_val; eA_rs = eB_rs; eA_ep = eB_ep;
+      ST_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
     }
     __syncthreads();
     // ------------------------------------------------------------ P1-P3: forward Q(x)
@@ -417,11 +449,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       const float b2 = sEnv[r * 8 + 3], vnew = sEnv[r * 8 + 2];
       const int s2 = sEnvI[r * 4 + 1];
       const int np = sEnvI[r * 4 + 0] + 1;
-      const float rs = p.ret_sum[e] + rew;
+      const float rs = sEnv[r * 8 + 5] + rew;
       if (np >= p.T - H) {
         const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
         p.last_final[e] = fin;
-        p.episodes[e] = p.episodes[e] + 1;
+        p.episodes[e] = sEnvI[r * 4 + 3] + 1;
         p.budget[e] = p.b0;
         p.shares[e] = p.s0;
         p.value[e] = 0.f;

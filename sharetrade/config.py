@@ -141,6 +141,8 @@ class EngineConfig:
     chunk: int = 32                 # envs per LDS chunk inside the fused step kernel
     graph: bool = True              # capture the step in a HIP graph
     backend: str = "auto"           # auto | native | torch
+    bucket_mb: float = 4.0          # DP gradient all-reduce bucket (one call below this size)
+    grad_compress: str = ""         # "" | "bf16" (wire format of the DP all-reduce)
 
 
 @dataclass

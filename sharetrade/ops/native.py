@@ -48,7 +48,8 @@ class OptimParams(C.Structure):
     _fields_ = [
         ("params", C.c_void_p), ("params_bf", C.c_void_p), ("mask", C.c_void_p), ("s1", C.c_void_p),
         ("s2", C.c_void_p), ("slab", C.c_void_p), ("grad", C.c_void_p), ("ctrl", C.c_void_p),
-        ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int),
+        ("stats", C.c_void_p), ("stat_acc", C.c_void_p),
+        ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int), ("nstat", C.c_int),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
     ]
 

@@ -120,10 +120,19 @@ class VectorEngine:
         self.state = tr.EnvState.create(self.E, cfg.env.budget, cfg.env.shares, device=self.device)
         self.env_offset = rank * self.E
         self.step_count = 0
-        self.key0, self.key1 = rng.key_for(a.seed, rank)
+        # one key for the whole job: draws are indexed by the GLOBAL env id (env_offset + e), so a
+        # DP run draws exactly what a single process holding all envs would
+        self.key0, self.key1 = rng.key_for(a.seed, 0)
         total = self.E * world_size
         self.loss_coef = 2.0 / total if a.loss_reduction == "mean" else 2.0
         self.stats = torch.zeros(NSTAT, dtype=torch.float64)
+        self._sync = None
+        if world_size > 1:
+            from ..parallel.dist import DistContext, GradSync
+
+            ctx = DistContext(rank, world_size, 0, "dist", self.device, group)
+            self._sync = GradSync(ctx, L.numel, bucket_mb=cfg.engine.bucket_mb,
+                                  compress=cfg.engine.grad_compress or None)
         self._graph = None
         self._last_actions: Optional[torch.Tensor] = None
         if be == "native":
@@ -187,6 +196,7 @@ class VectorEngine:
         o.s2 = native.ptr(self.opt.s2) if self.opt.s2.numel() else None
         o.slab, o.grad, o.ctrl = native.ptr(self.slab), native.ptr(self.grad), native.ptr(self.ctrl)
         o.G, o.P, o.kind = self.grid, L.numel, OPT_KIND[a.optimizer]
+        o.stats, o.stat_acc, o.nstat = native.ptr(self.stat_slab), native.ptr(self.stat_acc), NSTAT
         o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
         self._op = o
 
@@ -195,7 +205,7 @@ class VectorEngine:
         if self.kernel == "fp32_rows":
             ar = None
             if self.world_size > 1:
-                ar = lambda g: torch.distributed.all_reduce(g, group=self.group)  # noqa: E731
+                ar = self._sync.all_reduce
             self._f32.step(self.grad, ar)
             self._f32_stats()
             return
@@ -206,13 +216,12 @@ class VectorEngine:
         if self.world_size > 1:
             self._op.mode = 1
             native.check(L.st_reduce_optim(self._op, sh), "reduce")
-            torch.distributed.all_reduce(self.grad, group=self.group)
+            self._sync.all_reduce(self.grad)
             self._op.mode = 2
             native.check(L.st_reduce_optim(self._op, sh), "update")
         else:
             self._op.mode = 0
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
-        self.stat_acc += self.stat_slab.sum(0, dtype=torch.float64)
 
     def _f32_stats(self) -> None:
         r = self.rewards_out.double()
@@ -242,11 +251,11 @@ class VectorEngine:
             self.prices, self.state, self.params, self.layout, history=self.H, feature_mode=cfg.env.features,
             budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
             target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
-            epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=self.rank,
+            epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0,
             step=self.step_count, loss_coef=self.loss_coef, env_offset=self.env_offset,
             emulate_bf16=(cfg.engine.dtype == "bf16"))
         if self.world_size > 1:
-            torch.distributed.all_reduce(grad, group=self.group)
+            self._sync.all_reduce(grad)
         qn.optimizer_step_ref(self.params, grad, self.opt, self.mask, cfg.agent.lr, cfg.agent.adam_betas,
                               cfg.agent.adam_eps)
         done = ns.episodes > self.state.episodes

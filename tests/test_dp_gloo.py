@@ -1,0 +1,103 @@
+"""Multi-process data parallelism on CPU (gloo): the same code path the MI355X
+node runs over RCCL, world_size 2 and 4.
+
+Sync-DP equivalence: N ranks holding E envs each must produce exactly the
+parameters of one process holding all N*E envs (global env ids index the RNG,
+the loss is pre-scaled by the global batch, gradients are all-reduced)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(opt="adam"):
+    from sharetrade.config import preset_config
+
+    cfg = preset_config("flagship")
+    cfg.engine.dtype = "fp32"
+    cfg.agent.optimizer = opt
+    cfg.agent.epsilon = 0.6
+    cfg.agent.ramp = 5.0
+    cfg.model.hidden = [32, 32]
+    return cfg
+
+
+def _prices(n, T=260):
+    from sharetrade.data.prices import random_walk
+
+    return torch.from_numpy(random_walk(T, 50.0, 0.02, 11, n_series=n).astype(np.float32))
+
+
+def _worker(rank, world, port, E, steps, out_dir, opt, compress):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from sharetrade.parallel import dist as D
+    from sharetrade.trainer.engine import VectorEngine
+
+    ctx = D.init(backend="gloo", device="cpu")
+    cfg = _cfg(opt)
+    cfg.engine.grad_compress = compress
+    cfg.engine.bucket_mb = 0.01 if compress == "" else 4.0   # force several buckets in the fp32 case
+    bank = _prices(E * world)[rank * E:(rank + 1) * E]
+    eng = VectorEngine(cfg, prices=bank, device=torch.device("cpu"), rank=rank, world_size=world, group=ctx.group,
+                       envs=E, backend="torch")
+    if rank != 0:
+        eng.params.add_(1.0)          # broadcast must overwrite this
+    eng.sync_params_from(0)
+    eng.run(steps)
+    summ = D.global_mean_std(ctx, eng.current_portfolios())
+    gathered = D.all_gather_values(ctx, eng.current_portfolios())
+    torch.save({"params": eng.params, "summary": summ, "gathered": gathered,
+                "done": D.all_done(ctx, True)}, os.path.join(out_dir, f"r{rank}.pt"))
+    D.shutdown(ctx)
+
+
+def _run_dp(world, E, steps, opt="adam", compress=""):
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, port, E, steps, d, opt, compress), nprocs=world, join=True,
+                           start_method="spawn")
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sync_dp_equals_single_process(world):
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, steps = 3, 6
+    res = _run_dp(world, E, steps)
+    for r in res[1:]:
+        assert torch.equal(r["params"], res[0]["params"])        # replicas stay identical
+    single = VectorEngine(_cfg(), prices=_prices(E * world), device=torch.device("cpu"), envs=E * world,
+                          backend="torch")
+    single.run(steps)
+    rel = float((res[0]["params"] - single.params).norm() / single.params.norm())
+    assert rel < 1e-5, rel
+    # cross-rank aggregation == single-process aggregation
+    pf = single.current_portfolios().double()
+    s = res[0]["summary"]
+    assert s["n"] == E * world
+    assert abs(s["mean"] - float(pf.mean())) < 1e-6 * abs(float(pf.mean()))
+    assert torch.allclose(res[0]["gathered"].double(), pf, rtol=1e-6)
+    assert res[0]["done"] is True
+
+
+def test_dp_bf16_wire_compression_stays_close():
+    res = _run_dp(2, 3, 4, opt="sgd", compress="bf16")
+    assert torch.equal(res[0]["params"], res[1]["params"])
+    res32 = _run_dp(2, 3, 4, opt="sgd", compress="")
+    rel = float((res[0]["params"] - res32[0]["params"]).norm() / res32[0]["params"].norm())
+    assert rel < 1e-2

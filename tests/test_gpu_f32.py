@@ -48,13 +48,13 @@ def test_td_update_matches_oracle(dev, opt, slot, B):
 
     cfg = preset_config("intended" if slot == "action" else "reference_compat")
     cfg.agent.optimizer = opt
-    cfg.agent.lr = 1e-3
+    cfg.agent.lr = 1e-3 if opt != "sgd" else 1e-5
     cfg.agent.target_slot = slot
     gpu = QLearner(cfg, device=dev)
     cpu = QLearner(cfg, device=torch.device("cpu"))
     assert torch.equal(gpu.params.cpu(), cpu.params)
     for it in range(3):
-        x, xn = _states(B, 10 + it), _states(B, 20 + it)
+        x, xn = _states(B, 10 + it) / 100.0, _states(B, 20 + it) / 100.0
         r = np.linspace(-3, 3, B).astype(np.float32)
         acts = np.arange(B) % 3 if slot == "action" else None
         lg = gpu.update(x, r, xn, acts)
