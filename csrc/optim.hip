@@ -32,17 +32,28 @@ struct OptimParams {
 };
 
 constexpr int RT = 256;   // threads per workgroup
-constexpr int RG = 4;     // row groups per workgroup (RT / 64 float4 columns)
+constexpr int CW = 16;    // float4 columns per workgroup (256 B of every slab row)
+constexpr int RG = RT / CW;  // row groups per workgroup: 16 independent partial sums per column
 
 __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
-  __shared__ float4 part[RG][64];
-  const int tid = threadIdx.x, rg = tid >> 6, c = tid & 63;
-  const int col4 = blockIdx.x * 64 + c;  // float4 column index
+  __shared__ float4 part[RG][CW];
+  const int tid = threadIdx.x, rg = tid / CW, c = tid % CW;
+  const int col4 = blockIdx.x * CW + c;  // float4 column index
   const int P4 = p.P >> 2;
-  if (p.mode != 2 && p.stats && blockIdx.x == gridDim.x - 1 && tid < p.nstat) {
-    double acc = 0.0;  // step statistics folded into this pass (no extra launches)
-    for (int r = 0; r < p.G; ++r) acc += (double)p.stats[r * p.nstat + tid];
-    p.stat_acc[tid] += acc;
+  if (p.mode != 2 && p.stats && blockIdx.x == gridDim.x - 1) {
+    // step statistics folded into this pass (no extra launches): 32 row groups x 8 stats
+    __shared__ double sred[RT / 8][8];
+    const int j = tid & 7, grp = tid >> 3;
+    double acc = 0.0;
+    if (j < p.nstat)
+      for (int r = grp; r < p.G; r += RT / 8) acc += (double)p.stats[r * p.nstat + j];
+    sred[grp][j] = acc;
+    __syncthreads();
+    if (tid < p.nstat) {
+      double t = 0.0;
+      for (int k = 0; k < RT / 8; ++k) t += sred[k][tid];
+      p.stat_acc[tid] += t;
+    }
   }
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
   if (p.mode != 2) {
@@ -131,7 +142,7 @@ __global__ void to_bf16_kernel(const float* __restrict__ in, bf16_t* __restrict_
 
 extern "C" hipError_t st_reduce_optim(const st::OptimParams* p, hipStream_t stream) {
   const int P4 = p->P >> 2;
-  const int grid = (P4 + 63) / 64;
+  const int grid = (P4 + st::CW - 1) / st::CW;   // ~740 workgroups for the 2x128 net: fills 256 CUs
   hipLaunchKernelGGL(st::reduce_optim_kernel, dim3(grid), dim3(st::RT), 0, stream, *p);
   return hipGetLastError();
 }

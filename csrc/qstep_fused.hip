@@ -58,6 +58,7 @@ struct QStepParams {
   int s0, compat_env, target_compat, output_relu, feat_mode;
   uint32_t key0, key1;
   int env_offset;
+  unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][8]) or null
 };
 
 template <int INP, int H1P, int H2P>
@@ -287,7 +288,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
         st_qslot = 0.f;
 
   const int nchunks = p.E / C;
-  constexpr int RPW = C / 4;  // rows (envs) per wave in the gather
+  constexpr int RPW = C / 4;
+  int iter = 0;
+#define ST_STAMP(I) \
+  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[iter * 8 + (I)] = __builtin_amdgcn_s_memtime();  // rows (envs) per wave in the gather
 
   // ---------------------------------------------------------------- software-pipelined gather
   // Global traffic of a chunk is a dependent chain (pos -> price window), so it is
@@ -320,6 +324,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
   __syncthreads();
 
   for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    ST_STAMP(0);
     const int ebase = chunk * C;
     // ------------------------------------------------------------ P0: gather windows (from registers)
     if (lane < RPW) {
@@ -368,6 +373,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       ST_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
     }
     __syncthreads();
+    ST_STAMP(1);
     // ------------------------------------------------------------ P1-P3: forward Q(x)
     fwd_hidden<INP, G::SX, G::SX, G::SH1, MT1>(sW0, sX, sH1, nullptr, wave * 16 * MT1, l16, g4);
     __syncthreads();
@@ -375,6 +381,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
     __syncthreads();
     if (wave < 2) fwd_out<H2P, G::SH2, G::SH2>(sW2, sH2, sQ, sB2, p.output_relu, wave, l16, g4);
     __syncthreads();
+    ST_STAMP(2);
     // ------------------------------------------------------------ P4: epsilon-greedy + env step
     if (wave == 0 && lane < C) {
       const int r = lane, e = ebase + r;
@@ -416,6 +423,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       if (p.rewards_out) p.rewards_out[e] = rew;
     }
     __syncthreads();
+    ST_STAMP(3);
     // ------------------------------------------------------------ P5-P7: forward Q(x')
     fwd_hidden<INP, G::SX, G::SX, G::SH1, MT1>(sW0, sR0, sR1, nullptr, wave * 16 * MT1, l16, g4);
     __syncthreads();
@@ -423,6 +431,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
     __syncthreads();
     if (wave < 2) fwd_out<H2P, G::SH2, G::SH2>(sW2, sR0, sQN, sB2, p.output_relu, wave, l16, g4);
     __syncthreads();
+    ST_STAMP(4);
     // ------------------------------------------------------------ P8: TD target, dQ, state write-back
     if (wave == 0 && lane < C) {
       const int r = lane, e = ebase + r;
@@ -471,11 +480,13 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       }
     }
     __syncthreads();
+    ST_STAMP(5);
     // ------------------------------------------------------------ P9-P10: backward (data)
     bwd_data<OUTP, G::SH2, SQ, G::SH2, G::SH2, MT2>(sW2, sDQ, sH2, sR0, wave * 16 * MT2, l16, g4);
     __syncthreads();
     bwd_data<H2P, G::SH1, G::SH2, G::SH1, G::SH1, MT1>(sW1, sR0, sH1, sR1, wave * 16 * MT1, l16, g4);
     __syncthreads();
+    ST_STAMP(6);
     // ------------------------------------------------------------ P11: weight gradients (sum over envs)
     {
       // dW0^T[h1][in] += dZ1^T . X
@@ -509,6 +520,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       if (wave == 0) gB2 = mfma32(aq, ones, gB2);
     }
     __syncthreads();
+    ST_STAMP(7);
+    ++iter;
   }
 
   // ---------------------------------------------------------------- gradient slab write-out

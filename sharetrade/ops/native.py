@@ -41,6 +41,7 @@ class QStepParams(C.Structure):
         ("feat_mode", C.c_int),
         ("key0", C.c_uint32), ("key1", C.c_uint32),
         ("env_offset", C.c_int),
+        ("stamps", C.c_void_p),
     ]
 
 

@@ -169,16 +169,26 @@ class TestTrainerChild:
 class FakeTrainer(TrainerChildActor):
     """`override def train` of TrainerRouterActorSpec.scala:146-151: sleep U[0,500) ms, return 10.0."""
 
+    MIN_S = 0.0
+
     def train(self, stock_data):
+        lo = self.MIN_S
+
         def run():
-            time.sleep(random.random() * 0.5)
+            time.sleep(lo + random.random() * 0.5)
             return 10.0
         return self.context.system.blocking_future(run)
 
 
-def _router(system, policy, cfg=None):
+class SlowFakeTrainer(FakeTrainer):
+    # the fault-injection specs check "10 routees" while training runs; the reference
+    # relies on no worker finishing within the first few ms — make that deterministic
+    MIN_S = 0.4
+
+
+def _router(system, policy, cfg=None, trainer=FakeTrainer):
     cfg = cfg or _cfg()
-    child = Props(FakeTrainer, policy.ref, 2000, 0, cfg)
+    child = Props(trainer, policy.ref, 2000, 0, cfg)
     return system.actor_of(TrainerRouterActor.props(policy.ref, 2000, 0, cfg, child_trainer_props=child),
                            "trainer-router-test-actor")
 
@@ -267,7 +277,7 @@ class TestTrainerRouter:
         kit.expect_msg(P.NotComputed)
 
     def test_dead_child_replaced_during_training(self, system, kit):
-        r = _router(system, TestProbe(system))
+        r = _router(system, TestProbe(system), trainer=SlowFakeTrainer)
         kit.tell(r, P.SendTrainingData(_stock(55, 255)))
         kit.tell(r, P.StartTraining)
         third = self._kill_third(kit, r)
