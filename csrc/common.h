@@ -16,8 +16,12 @@ ST_DEV bf16_t f2bf(float x) {
   return __builtin_bit_cast(bf16_t, h);
 }
 ST_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 (RNE) for two values
 ST_DEV uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // ----------------------------------------------------------------- LDS fragment loads

@@ -31,13 +31,16 @@
 namespace st {
 
 constexpr int C = 32;       // envs per chunk
-constexpr int NT = 256;     // threads per workgroup
+constexpr int NT = 512;     // threads per workgroup: 8 waves = 2 per SIMD (latency hiding for the
+                            // instruction-bound gather / env phases; see profiles/)
+constexpr int NW = NT / 64;
 constexpr int OUTP = 16;    // padded action dimension
 constexpr int SQ = OUTP + 8;
 constexpr int NSTAT = 8;
 
 struct QStepParams {
   const float* prices;      // [E, T] env-major
+  const float* prices4;     // [4][E][T4] shifted replicas (series.hip: replicate4)
   float* budget;
   int* shares;
   float* value;
@@ -52,22 +55,26 @@ struct QStepParams {
   int* actions_out;         // [E] or null
   float* rewards_out;       // [E] or null
   unsigned long long* ctrl;   // ctrl[0] = step index (read), ctrl[1] = step+1 (written by block 0)
-  int T, E, H, P;
+  int T, E, H, P, T4;
   int off_w0, off_w1, off_b1, off_w2, off_b2;
   float eps, inv_ramp, gamma, loss_coef, b0, inv_b0;
   int s0, compat_env, target_compat, output_relu, feat_mode;
   uint32_t key0, key1;
   int env_offset;
-  unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][8]) or null
+  unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][16]) or null
 };
 
 template <int INP, int H1P, int H2P>
 struct Geo {
-  static constexpr int SX = INP + 8, SH1 = H1P + 8, SH2 = H2P + 8;
+  // weight images: +8 bf16 row padding; activation images (the hot MFMA B-operand row
+  // reads): +16, which makes the 16x16x32 fragment reads bank-conflict-free (stride search
+  // in tools/, transposed reads stay 2-way either way)
+  static constexpr int SW0 = INP + 8, SW1 = H1P + 8, SW2 = H2P + 8;
+  static constexpr int SX = INP + 16, SH1 = H1P + 16, SH2 = H2P + 16;
   static constexpr int oW0 = 0;
-  static constexpr int oW1 = oW0 + H1P * SX;
-  static constexpr int oW2 = oW1 + H2P * SH1;
-  static constexpr int oX = oW2 + OUTP * SH2;
+  static constexpr int oW1 = oW0 + H1P * SW0;
+  static constexpr int oW2 = oW1 + H2P * SW1;
+  static constexpr int oX = oW2 + OUTP * SW2;
   static constexpr int oH1 = oX + C * SX;
   static constexpr int oH2 = oH1 + C * SH1;
   static constexpr int oR0 = oH2 + C * SH2;          // X' / H2' / dZ2
@@ -84,9 +91,9 @@ struct Geo {
   static constexpr int fB2 = fB1 + H2P * 4;          // b2 [16]
   static constexpr int BYTES = fB2 + OUTP * 4;
   static_assert(BYTES <= 163840, "LDS budget exceeded");
-  static_assert(INP % 32 == 0 && H1P % 64 == 0 && H2P % 64 == 0, "padding");
-  static constexpr int MT1 = H1P / 64;   // h1 m-tiles per wave
-  static constexpr int MT2 = H2P / 64;   // h2 m-tiles per wave
+  static_assert(INP % 32 == 0 && H1P % (16 * NW) == 0 && H2P % (16 * NW) == 0, "padding");
+  static constexpr int MT1 = H1P / (16 * NW);   // h1 m-tiles per wave
+  static constexpr int MT2 = H2P / (16 * NW);   // h2 m-tiles per wave
   static constexpr int NT0 = INP / 16 - 1;  // in-col tiles of dW0 (last tile is pure padding)
   static constexpr int NT1 = H1P / 16;
 };
@@ -105,6 +112,11 @@ ST_DEV s8v frag_tr(const bf16_t* img, int S, int k0, int c0, int l16, int g4) {
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
+}
+
+// value of lane+1 (lane 63 gets 0): DPP wave_shl:1 — one VALU op instead of a ds_bpermute
+ST_DEV float dpp_next_lane(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
 }
 
 ST_DEV float feat_price(float w, float inv, int mode) {
@@ -214,8 +226,8 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
   }
 }
 
-template <int INP, int H1P, int H2P>
-__global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
+template <int INP, int H1P, int H2P, int FEAT>
+__global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
   using G = Geo<INP, H1P, H2P>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* sbf = reinterpret_cast<bf16_t*>(smem);
@@ -244,17 +256,17 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
     const bf16_t* w0 = p.wq + p.off_w0;
     for (int i = tid; i < H1P * INP / 8; i += NT) {
       const int r = i / (INP / 8), c = (i % (INP / 8)) * 8;
-      *reinterpret_cast<uint4*>(sW0 + r * G::SX + c) = *reinterpret_cast<const uint4*>(w0 + r * INP + c);
+      *reinterpret_cast<uint4*>(sW0 + r * G::SW0 + c) = *reinterpret_cast<const uint4*>(w0 + r * INP + c);
     }
     const bf16_t* w1 = p.wq + p.off_w1;
     for (int i = tid; i < H2P * H1P / 8; i += NT) {
       const int r = i / (H1P / 8), c = (i % (H1P / 8)) * 8;
-      *reinterpret_cast<uint4*>(sW1 + r * G::SH1 + c) = *reinterpret_cast<const uint4*>(w1 + r * H1P + c);
+      *reinterpret_cast<uint4*>(sW1 + r * G::SW1 + c) = *reinterpret_cast<const uint4*>(w1 + r * H1P + c);
     }
     const bf16_t* w2 = p.wq + p.off_w2;
     for (int i = tid; i < OUTP * H2P / 8; i += NT) {
       const int r = i / (H2P / 8), c = (i % (H2P / 8)) * 8;
-      *reinterpret_cast<uint4*>(sW2 + r * G::SH2 + c) = *reinterpret_cast<const uint4*>(w2 + r * H2P + c);
+      *reinterpret_cast<uint4*>(sW2 + r * G::SW2 + c) = *reinterpret_cast<const uint4*>(w2 + r * H2P + c);
     }
     for (int i = tid; i < H2P; i += NT) sB1[i] = p.wf[p.off_b1 + i];
     if (tid < OUTP) sB2[tid] = p.wf[p.off_b2 + tid];
@@ -288,10 +300,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
         st_qslot = 0.f;
 
   const int nchunks = p.E / C;
-  constexpr int RPW = C / 4;
+  constexpr int RPW = C / NW;
   int iter = 0;
 #define ST_STAMP(I) \
-  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[iter * 8 + (I)] = __builtin_amdgcn_s_memtime();  // rows (envs) per wave in the gather
+  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[iter * 16 + (I)] = __builtin_amdgcn_s_memtime();  // rows (envs) per wave in the gather
 
   // ---------------------------------------------------------------- software-pipelined gather
   // Global traffic of a chunk is a dependent chain (pos -> price window), so it is
@@ -300,22 +312,30 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
   // are issued right after chunk i's gather, landing during chunk i's MFMA phases.
   int eA_pos = 0, eA_sh = 0, eA_ep = 0, eB_pos = 0, eB_sh = 0, eB_ep = 0;
   float eA_b = 0.f, eA_val = 0.f, eA_rs = 0.f, eB_b = 0.f, eB_val = 0.f, eB_rs = 0.f;
-  float w[RPW][4];
+  float4 w[RPW];              // lane L: prices[ps + 4L .. ps + 4L + 3] of each of the wave's rows
+  float wl = 0.f, wv = 0.f;   // lane rr < RPW: prices[pos + H - 1] and prices[pos + H] of row rr
 #define ST_LOAD_ENV(CH, POS, B, SH, VAL, RS, EP)                           \
   if ((CH) < nchunks && lane < RPW) {                                      \
     const int e_ = (CH) * C + wave * RPW + lane;                           \
     POS = p.pos[e_]; B = p.budget[e_]; SH = p.shares[e_];                  \
     VAL = p.value[e_]; RS = p.ret_sum[e_]; EP = p.episodes[e_];            \
   }
+// One dwordx4 per lane per row: the window [ps, ps+H] is a run of aligned float4s in the
+// shifted replica ps & 3 of the bank (1 KiB contiguous per wave-instruction, no realignment).
 #define ST_LOAD_PRICES(CH, POS)                                            \
   if ((CH) < nchunks) {                                                    \
     _Pragma("unroll") for (int rr = 0; rr < RPW; ++rr) {                   \
-      const int ps_ = __shfl(POS, rr, 64);                                 \
-      const float* pr_ = p.prices + (size_t)((CH) * C + wave * RPW + rr) * p.T + ps_; \
-      _Pragma("unroll") for (int c = 0; c < 4; ++c) {                      \
-        const int k_ = c * 64 + lane;                                      \
-        w[rr][c] = (k_ <= H) ? pr_[k_] : 0.f;                              \
-      }                                                                    \
+      const int ps_ = __builtin_amdgcn_readlane(POS, rr);                  \
+      const int sh_ = ps_ & 3;                                             \
+      const int e_ = (CH) * C + wave * RPW + rr;                           \
+      const float4* pr_ = reinterpret_cast<const float4*>(                 \
+          p.prices4 + ((size_t)sh_ * p.E + e_) * p.T4 + (ps_ - sh_));      \
+      if (lane < INP / 4) w[rr] = pr_[lane];                               \
+    }                                                                      \
+    if (lane < RPW) {                                                      \
+      const float* pl_ = p.prices + (size_t)((CH) * C + wave * RPW + lane) * p.T + (POS) + H; \
+      wl = pl_[-1];                                                        \
+      wv = pl_[0];                                                         \
     }                                                                      \
   }
   ST_LOAD_ENV(blockIdx.x, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
@@ -325,6 +345,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
 
   for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     ST_STAMP(0);
+    if (p.stamps != nullptr) {  // debug only: split P0 into (wait for prefetched data) + (work)
+      __builtin_amdgcn_s_waitcnt(0);
+      ST_STAMP(8);
+    }
     const int ebase = chunk * C;
     // ------------------------------------------------------------ P0: gather windows (from registers)
     if (lane < RPW) {
@@ -336,35 +360,46 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       sEnvI[r * 4 + 1] = eA_sh;
       sEnvI[r * 4 + 3] = eA_ep;
     }
+    // per-row scalars: lane rr < RPW computes row rr's (1/last, 1/vnew, budget & shares features)
+    float r_inv = 0.f, r_invn = 0.f, r_fb = 0.f, r_fs = 0.f;
+    if (lane < RPW) {
+      r_inv = __fdiv_rn(1.0f, wl);
+      r_invn = __fdiv_rn(1.0f, wv);
+      r_fb = feat_budget(eA_b, p.inv_b0, FEAT);
+      r_fs = feat_shares(eA_sh, wl, p.inv_b0, FEAT);
+    }
+    // lane L owns window columns k = 4L..4L+3: branch-free features, one 8-byte LDS store per row
+    // for x and one for x' (x'[k] = f(prices[k+1]) takes its 4th value from lane L+1)
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr) {
       const int r = wave * RPW + rr;
-      const float b = __shfl(eA_b, rr, 64);
-      const int s = __shfl(eA_sh, rr, 64);
-      const int kl = H - 1, kn = H;
-      const float srcl = (kl >> 6) == 0 ? w[rr][0] : (kl >> 6) == 1 ? w[rr][1] : (kl >> 6) == 2 ? w[rr][2] : w[rr][3];
-      const float srcn = (kn >> 6) == 0 ? w[rr][0] : (kn >> 6) == 1 ? w[rr][1] : (kn >> 6) == 2 ? w[rr][2] : w[rr][3];
-      const float last = __shfl(srcl, kl & 63, 64);
-      const float vnew = __shfl(srcn, kn & 63, 64);
-      const float inv = __fdiv_rn(1.0f, last), invn = __fdiv_rn(1.0f, vnew);
-      bf16_t* xr = sX + r * G::SX;
-      bf16_t* xn = sR0 + r * G::SX;
+      const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_inv), rr));
+      const float invn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_invn), rr));
+      const float fb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_fb), rr));
+      const float fs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_fs), rr));
+      const float vnew = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), rr));
+      // prices[ps + 4L + t], t = 0..4 (t = 4 from lane L+1 via DPP)
+      const float win[5] = {w[rr].x, w[rr].y, w[rr].z, w[rr].w, dpp_next_lane(w[rr].x)};
+      float xv[4], xnv[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int k = c * 64 + lane;
-        if (k < H) xr[k] = f2bf(feat_price(w[rr][c], inv, p.feat_mode));
-        if (k >= 1 && k <= H) xn[k - 1] = f2bf(feat_price(w[rr][c], invn, p.feat_mode));
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * lane + j;
+        // every candidate is materialised first (empty asm pins it) so that the
+        // per-lane choice is a v_cndmask, not a divergent branch around 2 VALU ops
+        float fp = feat_price(win[j], inv, FEAT);
+        float fpn = feat_price(win[j + 1], invn, FEAT);
+        float sp = (k == H) ? fb : (k == H + 1) ? fs : (k == H + 2) ? 1.0f : 0.f;
+        asm volatile("" : "+v"(fp), "+v"(fpn), "+v"(sp));
+        xv[j] = (k < H) ? fp : sp;
+        xnv[j] = (k < H) ? fpn : 0.f;
       }
-      for (int k = H + lane; k < INP; k += 64) {
-        float v = 0.f;
-        if (k == H) v = feat_budget(b, p.inv_b0, p.feat_mode);
-        else if (k == H + 1) v = feat_shares(s, last, p.inv_b0, p.feat_mode);
-        else if (k == H + 2) v = 1.0f;
-        xr[k] = f2bf(v);
-        if (k >= H + 3) xn[k] = 0;
+      if (lane < INP / 4) {
+        lds_st4(sX + r * G::SX + 4 * lane, xv[0], xv[1], xv[2], xv[3]);
+        lds_st4(sR0 + r * G::SX + 4 * lane, xnv[0], xnv[1], xnv[2], xnv[3]);
       }
       if (lane == 0) sEnv[r * 8 + 2] = vnew;
     }
+    ST_STAMP(9);
     // next chunk's price windows (its env state arrived during this chunk's predecessor)
     {
       const int nxt = chunk + gridDim.x;
@@ -372,14 +407,15 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       eA_pos = eB_pos; eA_b = eB_b; eA_sh = eB_sh; eA_val = eB_val; eA_rs = eB_rs; eA_ep = eB_ep;
       ST_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
     }
+    ST_STAMP(10);
     __syncthreads();
     ST_STAMP(1);
     // ------------------------------------------------------------ P1-P3: forward Q(x)
-    fwd_hidden<INP, G::SX, G::SX, G::SH1, MT1>(sW0, sX, sH1, nullptr, wave * 16 * MT1, l16, g4);
+    fwd_hidden<INP, G::SW0, G::SX, G::SH1, MT1>(sW0, sX, sH1, nullptr, wave * 16 * MT1, l16, g4);
     __syncthreads();
-    fwd_hidden<H1P, G::SH1, G::SH1, G::SH2, MT2>(sW1, sH1, sH2, sB1, wave * 16 * MT2, l16, g4);
+    fwd_hidden<H1P, G::SW1, G::SH1, G::SH2, MT2>(sW1, sH1, sH2, sB1, wave * 16 * MT2, l16, g4);
     __syncthreads();
-    if (wave < 2) fwd_out<H2P, G::SH2, G::SH2>(sW2, sH2, sQ, sB2, p.output_relu, wave, l16, g4);
+    if (wave < 2) fwd_out<H2P, G::SW2, G::SH2>(sW2, sH2, sQ, sB2, p.output_relu, wave, l16, g4);
     __syncthreads();
     ST_STAMP(2);
     // ------------------------------------------------------------ P4: epsilon-greedy + env step
@@ -415,8 +451,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
       sEnvI[r * 4 + 1] = s2;
       sEnvI[r * 4 + 2] = a;
       bf16_t* xn = sR0 + r * G::SX;
-      xn[H] = f2bf(feat_budget(b2, p.inv_b0, p.feat_mode));
-      xn[H + 1] = f2bf(feat_shares(s2, vnew, p.inv_b0, p.feat_mode));
+      xn[H] = f2bf(feat_budget(b2, p.inv_b0, FEAT));
+      xn[H + 1] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
       xn[H + 2] = f2bf(1.0f);
       st_explore += exploit ? 0.f : 1.f;
       if (p.actions_out) p.actions_out[e] = a;
@@ -425,11 +461,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
     __syncthreads();
     ST_STAMP(3);
     // ------------------------------------------------------------ P5-P7: forward Q(x')
-    fwd_hidden<INP, G::SX, G::SX, G::SH1, MT1>(sW0, sR0, sR1, nullptr, wave * 16 * MT1, l16, g4);
+    fwd_hidden<INP, G::SW0, G::SX, G::SH1, MT1>(sW0, sR0, sR1, nullptr, wave * 16 * MT1, l16, g4);
     __syncthreads();
-    fwd_hidden<H1P, G::SH1, G::SH1, G::SH2, MT2>(sW1, sR1, sR0, sB1, wave * 16 * MT2, l16, g4);
+    fwd_hidden<H1P, G::SW1, G::SH1, G::SH2, MT2>(sW1, sR1, sR0, sB1, wave * 16 * MT2, l16, g4);
     __syncthreads();
-    if (wave < 2) fwd_out<H2P, G::SH2, G::SH2>(sW2, sR0, sQN, sB2, p.output_relu, wave, l16, g4);
+    if (wave < 2) fwd_out<H2P, G::SW2, G::SH2>(sW2, sR0, sQN, sB2, p.output_relu, wave, l16, g4);
     __syncthreads();
     ST_STAMP(4);
     // ------------------------------------------------------------ P8: TD target, dQ, state write-back
@@ -482,9 +518,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
     __syncthreads();
     ST_STAMP(5);
     // ------------------------------------------------------------ P9-P10: backward (data)
-    bwd_data<OUTP, G::SH2, SQ, G::SH2, G::SH2, MT2>(sW2, sDQ, sH2, sR0, wave * 16 * MT2, l16, g4);
+    bwd_data<OUTP, G::SW2, SQ, G::SH2, G::SH2, MT2>(sW2, sDQ, sH2, sR0, wave * 16 * MT2, l16, g4);
     __syncthreads();
-    bwd_data<H2P, G::SH1, G::SH2, G::SH1, G::SH1, MT1>(sW1, sR0, sH1, sR1, wave * 16 * MT1, l16, g4);
+    bwd_data<H2P, G::SW1, G::SH2, G::SH1, G::SH1, MT1>(sW1, sR0, sH1, sR1, wave * 16 * MT1, l16, g4);
     __syncthreads();
     ST_STAMP(6);
     // ------------------------------------------------------------ P11: weight gradients (sum over envs)
@@ -563,18 +599,23 @@ __global__ void __launch_bounds__(NT, 1) qstep_fused_kernel(QStepParams p) {
   }
 }
 
-template <int INP, int H1P, int H2P>
-static hipError_t launch_t(const QStepParams& p, int grid, hipStream_t stream) {
+template <int INP, int H1P, int H2P, int FEAT>
+static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
   using G = Geo<INP, H1P, H2P>;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)qstep_fused_kernel<INP, H1P, H2P>,
+    hipError_t e = hipFuncSetAttribute((const void*)qstep_fused_kernel<INP, H1P, H2P, FEAT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((qstep_fused_kernel<INP, H1P, H2P>), dim3(grid), dim3(NT), G::BYTES, stream, p);
+  hipLaunchKernelGGL((qstep_fused_kernel<INP, H1P, H2P, FEAT>), dim3(grid), dim3(NT), G::BYTES, stream, p);
   return hipGetLastError();
+}
+
+template <int INP, int H1P, int H2P>
+static hipError_t launch_t(const QStepParams& p, int grid, hipStream_t stream) {
+  return p.feat_mode ? launch_f<INP, H1P, H2P, 1>(p, grid, stream) : launch_f<INP, H1P, H2P, 0>(p, grid, stream);
 }
 
 }  // namespace st

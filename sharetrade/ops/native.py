@@ -29,11 +29,11 @@ class NativeUnavailable(RuntimeError):
 
 class QStepParams(C.Structure):
     _fields_ = [
-        ("prices", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
+        ("prices", C.c_void_p), ("prices4", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
         ("pos", C.c_void_p), ("episodes", C.c_void_p), ("last_final", C.c_void_p), ("ret_sum", C.c_void_p),
         ("wq", C.c_void_p), ("wf", C.c_void_p), ("slab", C.c_void_p), ("stats", C.c_void_p),
         ("actions_out", C.c_void_p), ("rewards_out", C.c_void_p), ("ctrl", C.c_void_p),
-        ("T", C.c_int), ("E", C.c_int), ("H", C.c_int), ("P", C.c_int),
+        ("T", C.c_int), ("E", C.c_int), ("H", C.c_int), ("P", C.c_int), ("T4", C.c_int),
         ("off_w0", C.c_int), ("off_w1", C.c_int), ("off_b1", C.c_int), ("off_w2", C.c_int), ("off_b2", C.c_int),
         ("eps", C.c_float), ("inv_ramp", C.c_float), ("gamma", C.c_float), ("loss_coef", C.c_float),
         ("b0", C.c_float), ("inv_b0", C.c_float),
@@ -80,6 +80,8 @@ def lib() -> C.CDLL:
     L.st_random_walk.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_uint32,
                                  C.c_uint32, C.c_void_p]
     L.st_random_walk.restype = C.c_int
+    L.st_replicate4.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_replicate4.restype = C.c_int
     _bind_optional(L)
     _lib = L
     return L
@@ -117,6 +119,20 @@ def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float,
     E, T = out.shape
     check(lib().st_random_walk(ptr(out), E, T, start_price, vol, drift, key0 & 0xFFFFFFFF, key1 & 0xFFFFFFFF,
                                stream_handle()), "st_random_walk")
+
+
+def replica_stride(T: int) -> int:
+    """Row stride of the shifted price replicas (multiple of 4, >= T + 32 for the aligned over-read)."""
+    return (T + 32 + 3) // 4 * 4
+
+
+def replicate4(src: torch.Tensor) -> torch.Tensor:
+    """[E, T] -> [4, E, T4] shifted replicas (csrc/series.hip: replicate4)."""
+    E, T = src.shape
+    T4 = replica_stride(T)
+    out = torch.empty(4, E, T4, dtype=torch.float32, device=src.device)
+    check(lib().st_replicate4(ptr(src), ptr(out), E, T, T4, stream_handle()), "st_replicate4")
+    return out
 
 
 def to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:

@@ -46,12 +46,22 @@ def resolve_device(spec: str) -> torch.device:
     return torch.device(spec)
 
 
+BANK_TAIL = 64  # floats of zero padding after the bank: the fused kernel reads aligned 16-B slices
+
+
+def padded_bank(E: int, T: int, device: torch.device) -> torch.Tensor:
+    """Uninitialised [E, T] fp32 view on an allocation with BANK_TAIL zero floats behind it."""
+    flat = torch.empty(E * T + BANK_TAIL, dtype=torch.float32, device=device)
+    flat[E * T:].zero_()
+    return flat[:E * T].view(E, T)
+
+
 def make_price_bank(cfg: Config, E: int, device: torch.device, seed: int = 0) -> torch.Tensor:
-    """[E, T] fp32 price bank resident on ``device``."""
+    """[E, T] fp32 price bank resident on ``device`` (tail-padded, see BANK_TAIL)."""
     d = cfg.data
     if d.source == "random_walk":
         if device.type == "cuda":
-            out = torch.empty(E, d.length, dtype=torch.float32, device=device)
+            out = padded_bank(E, d.length, device)
             k0, k1 = rng.key_for(d.seed + 7919 * seed)
             native.random_walk(out, d.start_price, d.volatility, 0.0, int(k0), int(k1))
             return out
@@ -103,8 +113,12 @@ class VectorEngine:
             # fp32: the exact-fp32 row kernels (csrc/mlp_f32.hip) — any MLP up to 6 layers x 1024
             self.kernel = "bf16_fused" if fused_ok else "fp32_rows"
         # ------------------------------------------------------------ data
-        self.prices = prices.to(self.device, torch.float32).contiguous() if prices is not None else \
-            make_price_bank(cfg, self.E, self.device, seed=rank)
+        if prices is not None:
+            bank = padded_bank(prices.shape[0], prices.shape[1], self.device)
+            bank.copy_(prices)
+            self.prices = bank
+        else:
+            self.prices = make_price_bank(cfg, self.E, self.device, seed=rank)
         if self.prices.shape[0] != self.E:
             raise ValueError(f"price bank has {self.prices.shape[0]} rows, expected {self.E}")
         self.T = int(self.prices.shape[1])
@@ -153,6 +167,7 @@ class VectorEngine:
             self._f32 = F32EngineStep(self)
             return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
+        self.prices4 = native.replicate4(self.prices)   # aligned-gather replicas (4 x bank, HBM is plentiful)
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
         self.grid = max(1, min(props.multi_processor_count, self.E // 32))
@@ -164,6 +179,7 @@ class VectorEngine:
         cfg, L, st = self.cfg, self.layout, self.state
         seg = L.segments
         q = native.QStepParams()
+        q.prices4, q.T4 = native.ptr(self.prices4), int(self.prices4.shape[2])
         q.prices, q.budget, q.shares, q.value = (native.ptr(self.prices), native.ptr(st.budget),
                                                  native.ptr(st.shares), native.ptr(st.value))
         q.pos, q.episodes, q.last_final, q.ret_sum = (native.ptr(st.pos), native.ptr(st.episodes),

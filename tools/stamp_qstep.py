@@ -34,12 +34,12 @@ def main():
     eng.run(3)
     torch.cuda.synchronize()
     iters = (a.envs // 32 + eng.grid - 1) // eng.grid
-    st = torch.zeros(iters * 8 + 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(iters * 16 + 16, dtype=torch.int64, device=dev)
     eng._qp.stamps = st.data_ptr()
     eng.step()
     torch.cuda.synchronize()
     eng._qp.stamps = None
-    s = st.cpu().view(-1, 8)[:iters]
+    s = st.cpu().view(-1, 16)[:iters]
     rows = []
     tot = 0
     for ph in range(7):
@@ -52,6 +52,14 @@ def main():
     for n, v in rows:
         lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
     lines.append(f"| chunk loop (stamp0->stamp0) | {loop:.0f} | |")
+    wait = float((s[:, 8] - s[:, 0]).double().mean())
+    lines.append(f"| of P0: waiting for prefetched loads/stores (debug waitcnt) | {wait:.0f} | |")
+    rows_t = float((s[:, 9] - s[:, 8]).double().mean())
+    pre_t = float((s[:, 10] - s[:, 9]).double().mean())
+    bar_t = float((s[:, 1] - s[:, 10]).double().mean())
+    lines.append(f"| of P0: feature rows -> LDS | {rows_t:.0f} | |")
+    lines.append(f"| of P0: issue next chunk's loads | {pre_t:.0f} | |")
+    lines.append(f"| of P0: barrier | {bar_t:.0f} | |")
     txt = "\n".join(lines) + "\n"
     print(txt)
     if a.out:
