@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 65536)),
                     help="vectorised envs per GPU")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) | gloo (rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="all ranks on cuda:0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
     args = ap.parse_args()
 
@@ -49,6 +52,7 @@ def main() -> int:
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
         return 2
+    local = 0 if args.same_device else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
@@ -56,7 +60,8 @@ def main() -> int:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world, **kw)
         group = dist.group.WORLD
 
     import build as _build  # in-tree native build (no-op when up to date)
