@@ -362,7 +362,8 @@ class VectorEngine:
         for k in self.state.as_dict():
             getattr(self.state, k).copy_(d["env_" + k].to(self.device))
         if self.backend == "native":
-            native.to_bf16(self.params, self.params_bf)
+            if self.kernel == "bf16_fused":
+                native.to_bf16(self.params, self.params_bf)
             self.ctrl.fill_(self.step_count)
 
     def sync_params_from(self, src_rank: int = 0) -> None:
@@ -374,7 +375,7 @@ class VectorEngine:
         for t in (self.params, self.opt.s1, self.opt.s2):
             if t.numel():
                 dist.broadcast(t, src_rank, group=self.group)
-        if self.backend == "native":
+        if self.backend == "native" and self.kernel == "bf16_fused":
             native.to_bf16(self.params, self.params_bf)
 
     def synchronize(self) -> None:

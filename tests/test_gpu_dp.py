@@ -1,0 +1,74 @@
+"""Data parallelism through the native HIP step on the GPU (2 ranks sharing cuda:0 over
+gloo — the same engine code the 8-GPU RCCL run executes; the box has one GPU)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(kernel):
+    from sharetrade.config import preset_config
+
+    cfg = preset_config("flagship")
+    cfg.agent.optimizer = "sgd"
+    cfg.agent.lr = 1e-2
+    if kernel == "fp32":
+        cfg.engine.dtype = "fp32"
+    return cfg
+
+
+def _bank(n, T=400):
+    from sharetrade.data.prices import random_walk
+
+    return torch.from_numpy(random_walk(T, 50.0, 0.02, 3, n_series=n).astype(np.float32))
+
+
+def _worker(rank, world, port, E, steps, kernel, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from sharetrade.trainer.engine import VectorEngine
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(_cfg(kernel), prices=_bank(E * world)[rank * E:(rank + 1) * E], device=dev, rank=rank,
+                       world_size=world, group=dist.group.WORLD, envs=E)
+    assert eng.backend == "native"
+    eng.sync_params_from(0)
+    eng.run(steps)
+    torch.cuda.synchronize()
+    torch.save({"params": eng.params.cpu(), "budget": eng.state.budget.cpu()}, os.path.join(out, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kernel", ["bf16", "fp32"])
+def test_native_dp_two_ranks_match_single_process(native_built, kernel):
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, steps, world = 64, 4, 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _port(), E, steps, kernel, d), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert torch.equal(res[0]["params"], res[1]["params"])
+    single = VectorEngine(_cfg(kernel), prices=_bank(E * world), device=torch.device("cuda", 0), envs=E * world)
+    single.run(steps)
+    torch.cuda.synchronize()
+    p = single.params.cpu()
+    rel = float((res[0]["params"] - p).norm() / p.norm())
+    assert rel < (1e-5 if kernel == "fp32" else 1e-3), rel
+    assert torch.equal(torch.cat([res[0]["budget"], res[1]["budget"]]), single.state.budget.cpu())
