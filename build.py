@@ -71,7 +71,8 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
 
 
 def build_rt(force: bool = False) -> str:
-    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    srcs = sorted(f for f in glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))
+                  if not f.endswith("selftest.cpp"))   # standalone sanitizer driver (tests/test_sanitizers.py)
     hdrs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.h")))
     if not srcs:
         return ""

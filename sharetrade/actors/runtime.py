@@ -28,6 +28,7 @@ from __future__ import annotations
 import heapq
 import itertools
 import logging
+import os
 import threading
 import time
 import traceback
@@ -464,6 +465,14 @@ class ActorContext:
     def set_receive_timeout(self, seconds: Optional[float]) -> None:
         self._cell.receive_timeout = seconds
 
+    def assert_on_actor_thread(self) -> None:
+        """Race check: actor state may only be touched while the actor is
+        processing a message, on the dispatcher thread running it."""
+        owner = self._cell.running_thread
+        if owner != threading.get_ident():
+            raise AssertionError(f"{self._cell.ref.path}: state accessed off the actor thread "
+                                 f"(owner={owner}, caller={threading.get_ident()})")
+
 
 class ActorCell:
     _THROUGHPUT = 16
@@ -492,6 +501,7 @@ class ActorCell:
         self.receive_timeout: Optional[float] = None
         self.child_counter = itertools.count()
         self.failed_cause: Optional[BaseException] = None
+        self.running_thread: Optional[int] = None
 
     # ------------------------------------------------------------ creation
     def create(self) -> None:
@@ -541,6 +551,10 @@ class ActorCell:
 
     # ------------------------------------------------------------ processing
     def _run(self) -> None:
+        me = threading.get_ident()
+        if self.system.debug and self.running_thread not in (None, me):
+            raise AssertionError(f"{self.ref.path}: mailbox processed by two threads at once")
+        self.running_thread = me
         try:
             n = 0
             while n < self._THROUGHPUT:
@@ -561,6 +575,7 @@ class ActorCell:
                     self._invoke(*item)
                 n += 1
         finally:
+            self.running_thread = None
             with self.lock:
                 self.scheduled = False
             self._schedule()
@@ -802,8 +817,9 @@ class ActorSystem:
     """Hosts actors on a thread-pool dispatcher (Akka's default dispatcher)."""
 
     def __init__(self, name: str = "sharetrade", threads: int = 8, loglevel: str = "INFO",
-                 config=None):
+                 config=None, debug: Optional[bool] = None):
         self.name = name
+        self.debug = bool(int(os.environ.get("SHARETRADE_ACTOR_DEBUG", "0"))) if debug is None else debug
         self.config = config
         lvl = getattr(logging, str(loglevel).upper(), logging.INFO)
         self.event_stream = EventStream(lvl)
