@@ -43,6 +43,13 @@ def main(argv=None) -> int:
             p.add_argument("--steps", type=int, default=100)
             p.add_argument("--envs", type=int, default=None)
             p.add_argument("--device", default="auto")
+            p.add_argument("--metrics", default=None, help="JSONL metrics output path")
+            p.add_argument("--log-every", type=int, default=100)
+            p.add_argument("--ckpt-dir", default=None)
+            p.add_argument("--ckpt-every", type=int, default=0)
+            p.add_argument("--resume", action="store_true")
+            p.add_argument("--trace", default=None, help="Chrome trace output path (torch.profiler)")
+            p.add_argument("--no-graph", action="store_true")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -57,21 +64,18 @@ def main(argv=None) -> int:
         print(json.dumps(res))
         return 0 if res.get("completed") else 1
     if a.cmd == "engine":
-        import time
+        from .parallel import dist as D
+        from .trainer.engine import resolve_device
+        from .trainer.loop import train
 
-        import torch
-
-        from .trainer.engine import VectorEngine, resolve_device
-
-        dev = resolve_device(a.device)
-        eng = VectorEngine(cfg, device=dev, envs=a.envs)
-        t0 = time.perf_counter()
-        eng.run(a.steps)
-        eng.synchronize()
-        dt = time.perf_counter() - t0
-        out = {"backend": eng.backend, "kernel": getattr(eng, "kernel", None), "envs": eng.E, "steps": a.steps,
-               "env_steps_per_s": eng.E * a.steps / dt, **eng.stats_dict(), **eng.portfolio_summary()}
-        print(json.dumps(out))
+        ctx = D.init(device=None if a.device == "auto" else a.device)
+        dev = ctx.device if ctx.is_distributed or a.device == "auto" else resolve_device(a.device)
+        res = train(cfg, a.steps, device=dev, envs=a.envs, metrics_path=a.metrics, log_every=a.log_every,
+                    ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, trace_path=a.trace,
+                    graph=not a.no_graph, rank=ctx.rank, world_size=ctx.world_size, group=ctx.group)
+        if ctx.is_main:
+            print(json.dumps(res))
+        D.shutdown(ctx)
         return 0
     return 2
 

@@ -1,0 +1,63 @@
+"""Training loop around :class:`VectorEngine`: metrics, periodic checkpoints, resume, traces.
+
+Used by ``python -m sharetrade engine`` (single process or one rank of a
+torchrun / ElasticRunner job)."""
+from __future__ import annotations
+
+import os
+import time
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..config import Config
+from ..persist.checkpoint import CheckpointManager, load as load_ckpt
+from ..utils.metrics import MetricsLogger, WindowStats
+from .engine import VectorEngine
+
+
+def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: Optional[int] = None,
+          metrics_path: Optional[str] = None, log_every: int = 100, ckpt_dir: Optional[str] = None,
+          ckpt_every: int = 0, resume: bool = False, trace_path: Optional[str] = None, graph: bool = True,
+          rank: int = 0, world_size: int = 1, group=None) -> Dict[str, Any]:
+    eng = VectorEngine(cfg, device=device, envs=envs, rank=rank, world_size=world_size, group=group)
+    mgr = CheckpointManager(ckpt_dir, interval=ckpt_every) if ckpt_dir else None
+    if mgr and resume:
+        p = mgr.latest()
+        if p:
+            st, _ = load_ckpt(p)
+            eng.load_state_dict(st)
+    eng.sync_params_from(0)
+    if graph and eng.backend == "native" and world_size == 1:
+        eng.capture_graph(warmup=1)
+    ml = MetricsLogger(metrics_path)
+    ws = WindowStats()
+    ws.window(eng.stats_dict(), eng.step_count, eng.E, world_size)
+    prof = None
+    if trace_path:
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if eng.device.type == "cuda":
+            acts.append(torch.profiler.ProfilerActivity.CUDA)
+        prof = torch.profiler.profile(activities=acts)
+        prof.__enter__()
+    t0 = time.perf_counter()
+    start = eng.step_count
+    while eng.step_count < start + steps:
+        eng.step()
+        s = eng.step_count
+        if log_every and s % log_every == 0:
+            eng.synchronize()
+            ml.log(ws.window(eng.stats_dict(), s, eng.E, world_size))
+        if mgr and mgr.should_save(s) and rank == 0:
+            eng.synchronize()
+            mgr.save(s, eng.state_dict(), {"kind": "VectorEngine"})
+    eng.synchronize()
+    dt = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(os.path.dirname(os.path.abspath(trace_path)) or ".", exist_ok=True)
+        prof.export_chrome_trace(trace_path)
+    ml.close()
+    return {"backend": eng.backend, "kernel": eng.kernel, "envs": eng.E, "steps": steps,
+            "env_steps_per_s": eng.E * world_size * steps / dt, "seconds": dt, **eng.stats_dict(),
+            **eng.portfolio_summary()}
