@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""BASELINE.json config 4: 4x1024 MLP Q-net, 1M-transition replay buffer in HBM, batch 4096.
+
+One iteration = one env step of all E envs (act: gather -> 5 GEMMs -> select/env/replay
+insert) + ``--updates`` learner updates (sample 4096 -> 10 forward GEMMs -> TD -> 9
+backward GEMMs -> Adam), each captured in a HIP graph.  Prints one JSON line.
+Single GPU (DP for this config reuses the flat-bucket GradSync of the flagship).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=16384)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--hidden", default="1024,1024,1024,1024")
+    ap.add_argument("--replay", type=int, default=1 << 20)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=64, help="acting steps to pre-fill the replay ring")
+    ap.add_argument("--updates", type=int, default=1)
+    a = ap.parse_args()
+    import build
+
+    build.build_all()
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.deep import DeepDQN
+
+    cfg = preset_config("flagship")
+    cfg.model.hidden = [int(x) for x in a.hidden.split(",")]
+    cfg.agent.lr = 1e-4
+    dev = torch.device("cuda", 0)
+    d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay)
+    for _ in range(a.warmup):
+        d.act_step()
+    d.capture()
+    for _ in range(3):
+        d.iteration(a.updates)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        d.iteration(a.updates)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # time the two halves separately
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        d._g_act.replay()
+    torch.cuda.synchronize()
+    t_act = (time.perf_counter() - t1) / a.steps
+    t2 = time.perf_counter()
+    for _ in range(a.steps):
+        d._g_upd.replay()
+    torch.cuda.synchronize()
+    t_upd = (time.perf_counter() - t2) / a.steps
+    hid = cfg.model.hidden
+    dims = [256] + hid + [64]
+    mac = sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+    upd_flop = 2.0 * a.batch * mac * 3 + 2.0 * a.batch * mac  # fwd x + bwd (2x) + fwd x' (target)
+    s = d.stats_dict()
+    out = {
+        "metric": "env steps/sec + learner updates/sec, 4x1024 MLP Q-net, 1M HBM replay, batch 4096 (config 4)",
+        "n_gpus": 1, "dtype": "bf16", "data": "synthetic random-walk price bank; random-init weights",
+        "envs": a.envs, "batch": a.batch, "hidden": hid, "replay_capacity": a.replay,
+        "updates_per_step": a.updates, "ms_per_iteration": round(dt / a.steps * 1e3, 4),
+        "env_steps_per_s": round(a.envs * a.steps / dt, 1), "updates_per_s": round(a.updates * a.steps / dt, 1),
+        "act_ms": round(t_act * 1e3, 4), "update_ms": round(t_upd * 1e3, 4),
+        "update_tflops": round(upd_flop / t_upd / 1e12, 1), "replay_size": s["replay_size"],
+        "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

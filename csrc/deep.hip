@@ -1,0 +1,355 @@
+// Kernels of the deep-MLP replay learner (BASELINE config 4: 4x1024 MLP Q-net,
+// 1M-transition replay buffer resident in HBM, batch 4096).  The GEMMs are in
+// gemm_bf16.hip; these are the gather / env / TD / optimizer pieces around them.
+//
+// Replay layout (MI355X-first): a transition is NOT stored as two 203-float states
+// (1M x 1.6 KB = 1.6 GB of mostly duplicated price windows) but as the indices that
+// regenerate them from the HBM-resident price bank: {env, pos, budget, shares,
+// action, reward, budget', shares', done} = 36 B -> 36 MB for 1M transitions; states
+// are rebuilt by deep_gather directly into the bf16 GEMM operand (Hankel addressing).
+#include "common.h"
+
+namespace st {
+
+struct Replay {
+  int* env;
+  int* pos;
+  float* budget;
+  int* shares;
+  int* action;
+  float* reward;
+  float* budget2;
+  int* shares2;
+  int* done;
+  unsigned long long* ctrl;   // [0] = write cursor (monotonic), [1] = size (min(cursor, cap))
+  int cap;
+};
+
+struct DeepGather {
+  const float* prices;        // [E, T]
+  int T, H, in_p, feat_mode;
+  float inv_b0;
+  // mode 0: rows = current env states; mode 1: rows = sampled transitions (x and x')
+  int mode, B;
+  // env mode
+  const int* pos;
+  const float* budget;
+  const int* shares;
+  // replay mode
+  Replay rp;
+  uint32_t key0, key1;
+  const unsigned long long* step;   // sampling counter (device, graph-safe)
+  // outputs
+  bf16_t* X;                  // [B, in_p]
+  bf16_t* Xn;                 // [B, in_p] (replay mode)
+  float* r_out;               // [B]
+  int* a_out;                 // [B]
+  float* done_out;            // [B]
+};
+
+ST_DEV float dfeat_price(float w, float inv, int mode) { return mode ? (w * inv - 1.0f) : w; }
+
+// One wave per row: lane L owns columns 4L..4L+3 (in_p <= 256).
+__global__ void __launch_bounds__(256) deep_gather_kernel(DeepGather g) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= g.B) return;
+  int e, ps, s, s2 = 0;
+  float b, b2 = 0.f;
+  if (g.mode == 0) {
+    e = row;
+    ps = g.pos[e];
+    b = g.budget[e];
+    s = g.shares[e];
+  } else {
+    // uniform sample over the filled part of the ring (Philox, counter = (row, step))
+    const unsigned long long sz = g.rp.ctrl[1];
+    const unsigned long long st = g.step[0];
+    uint32_t c0 = (uint32_t)row, c1 = (uint32_t)(st & 0xFFFFFFFFull), c2 = (uint32_t)(st >> 32), c3 = 7u;
+    philox4x32(c0, c1, c2, c3, g.key0, g.key1);
+    const unsigned long long idx = ((((unsigned long long)c0) << 32) | c1) % (sz ? sz : 1ull);
+    e = g.rp.env[idx];
+    ps = g.rp.pos[idx];
+    b = g.rp.budget[idx];
+    s = g.rp.shares[idx];
+    b2 = g.rp.budget2[idx];
+    s2 = g.rp.shares2[idx];
+    if (lane == 0) {
+      g.r_out[row] = g.rp.reward[idx];
+      g.a_out[row] = g.rp.action[idx];
+      g.done_out[row] = (float)g.rp.done[idx];
+    }
+  }
+  const float* pr = g.prices + (size_t)e * g.T + ps;
+  const int H = g.H;
+  const float last = pr[H - 1], vnew = pr[H];
+  const float inv = 1.0f / last, invn = 1.0f / vnew;
+  float xv[4], xnv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 4 * lane + j;
+    const float w = pr[k < H ? k : H - 1];
+    const float wn = pr[k < H ? k + 1 : H];
+    float fb = g.feat_mode ? b * g.inv_b0 : b;
+    float fs = g.feat_mode ? (float)s * last * g.inv_b0 : (float)s;
+    float fb2 = g.feat_mode ? b2 * g.inv_b0 : b2;
+    float fs2 = g.feat_mode ? (float)s2 * vnew * g.inv_b0 : (float)s2;
+    xv[j] = k < H ? dfeat_price(w, inv, g.feat_mode) : (k == H ? fb : (k == H + 1 ? fs : 0.f));
+    xnv[j] = k < H ? dfeat_price(wn, invn, g.feat_mode) : (k == H ? fb2 : (k == H + 1 ? fs2 : 0.f));
+  }
+  if (4 * lane < g.in_p) {
+    lds_st4(g.X + (size_t)row * g.in_p + 4 * lane, xv[0], xv[1], xv[2], xv[3]);  // 8-byte global store
+    if (g.mode == 1) lds_st4(g.Xn + (size_t)row * g.in_p + 4 * lane, xnv[0], xnv[1], xnv[2], xnv[3]);
+  }
+}
+
+struct DeepEnv {
+  const float* prices;
+  int T, H, E, compat_env, s0, n_actions;
+  float b0, eps, inv_ramp;
+  float* budget;
+  int* shares;
+  float* value;
+  int* pos;
+  int* episodes;
+  float* last_final;
+  const float* q;             // [E, ldq] fp32 Q(x)
+  int ldq;
+  uint32_t key0, key1;
+  unsigned long long* ctrl;   // [0] = env step counter
+  Replay rp;
+  float* stats;               // [4]: reward sum, explore count, episodes done, final sum (atomics)
+};
+
+// epsilon-greedy + Buy/Sell/Hold transition + replay insert, one thread per env.
+__global__ void __launch_bounds__(256) deep_env_step_kernel(DeepEnv p) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long step = p.ctrl[0];
+  float r_ = 0.f, x_ = 0.f;
+  if (e < p.E) {
+    const float* q = p.q + (size_t)e * p.ldq;
+    int greedy = 0;
+    float best = q[0];
+    for (int a = 1; a < p.n_actions; ++a)
+      if (q[a] > best) { best = q[a]; greedy = a; }
+    const int ps = p.pos[e];
+    uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32), c3 = 0u;
+    philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+    const float u1 = u24(c0), u2 = u24(c1);
+    const bool exploit = u1 < fminf(p.eps, (float)ps * p.inv_ramp);
+    int rnd = (int)(u2 * 3.0f);
+    rnd = rnd > 2 ? 2 : rnd;
+    const int a = exploit ? greedy : rnd;
+    const float* pr = p.prices + (size_t)e * p.T + ps;
+    const float vnew = pr[p.H];
+    const float b = p.budget[e], vprev = p.value[e];
+    const int s = p.shares[e];
+    const float bd = p.compat_env ? p.b0 : b;
+    const int sd = p.compat_env ? p.s0 : s;
+    const bool buy = (a == 0) && (bd >= vnew);
+    const bool sell = (a == 1) && (sd > 0);
+    const float b2 = buy ? bd - vnew : (sell ? bd + vnew : bd);
+    const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
+    const float rew = (b2 + (float)s2 * vnew) - (b + (float)s * vprev);
+    const int np = ps + 1;
+    const bool done = np >= p.T - p.H;
+    // replay insert (ring)
+    const unsigned long long slot = (p.rp.ctrl[0] + (unsigned long long)e) % (unsigned long long)p.rp.cap;
+    p.rp.env[slot] = e;
+    p.rp.pos[slot] = ps;
+    p.rp.budget[slot] = b;
+    p.rp.shares[slot] = s;
+    p.rp.action[slot] = a;
+    p.rp.reward[slot] = rew;
+    p.rp.budget2[slot] = b2;
+    p.rp.shares2[slot] = s2;
+    p.rp.done[slot] = done ? 1 : 0;
+    if (done) {
+      const float fin = b2 + (float)s2 * vnew;
+      p.last_final[e] = fin;
+      p.episodes[e] += 1;
+      p.budget[e] = p.b0;
+      p.shares[e] = p.s0;
+      p.value[e] = 0.f;
+      p.pos[e] = 0;
+      atomicAdd(p.stats + 2, 1.f);
+      atomicAdd(p.stats + 3, fin);
+    } else {
+      p.budget[e] = b2;
+      p.shares[e] = s2;
+      p.value[e] = vnew;
+      p.pos[e] = np;
+    }
+    r_ = rew;
+    x_ = exploit ? 0.f : 1.f;
+  }
+  // wave-reduced statistics (all lanes take part)
+  r_ = wave_sum(r_);
+  x_ = wave_sum(x_);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(p.stats + 0, r_);
+    atomicAdd(p.stats + 1, x_);
+  }
+}
+
+// ring cursor advance after an env step (one thread): cursor += E, size = min(cursor, cap); step += 1
+__global__ void deep_advance_kernel(unsigned long long* rctrl, unsigned long long* ectrl, int E, int cap) {
+  rctrl[0] += (unsigned long long)E;
+  rctrl[1] = rctrl[0] < (unsigned long long)cap ? rctrl[0] : (unsigned long long)cap;
+  ectrl[0] += 1;
+}
+
+struct DeepTD {
+  const float* q;       // [B, ldq] Q(x) online
+  const float* qt;      // [B, ldq] Q(x') target net
+  const float* r;
+  const int* a;
+  const float* done;
+  bf16_t* dq;           // [B, ldq] bf16
+  bf16_t* dqT;          // [ldq, B]
+  float* loss;          // [1] (atomic)
+  int B, ldq, n_actions;
+  float gamma, coef;
+};
+
+__global__ void __launch_bounds__(256) deep_td_kernel(DeepTD p) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (b < p.B) {
+    const float* qt = p.qt + (size_t)b * p.ldq;
+    float mx = qt[0];
+    for (int a = 1; a < p.n_actions; ++a) mx = fmaxf(mx, qt[a]);
+    const float y = p.r[b] + p.gamma * (1.0f - p.done[b]) * mx;
+    const int a = p.a[b];
+    const float diff = p.q[(size_t)b * p.ldq + a] - y;
+    l = diff * diff;
+    for (int j = 0; j < p.ldq; ++j) {
+      const float v = (j == a) ? p.coef * diff : 0.f;
+      p.dq[(size_t)b * p.ldq + j] = f2bf(v);
+      p.dqT[(size_t)j * p.B + b] = f2bf(v);
+    }
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) atomicAdd(p.loss, l);
+}
+
+// bias gradient: db[o] = sum_b dZT[o][b]  (one workgroup per output row)
+__global__ void __launch_bounds__(256) row_sum_bf16_kernel(const bf16_t* __restrict__ X, int ld, int n, float* out) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += bf2f(X[(size_t)r * ld + i]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[r] = red[0] + red[1] + red[2] + red[3];
+}
+
+// bf16 transpose through LDS: out[c][r] = in[r][c], 64x64 tiles
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ in, int ldi, bf16_t* __restrict__ out,
+                                                             int ldo, int R, int Ccols) {
+  __shared__ bf16_t t[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i / 64, c = i % 64;
+    if (r0 + r < R && c0 + c < Ccols) t[r][c] = in[(size_t)(r0 + r) * ldi + c0 + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int c = i / 64, r = i % 64;
+    if (r0 + r < R && c0 + c < Ccols) out[(size_t)(c0 + c) * ldo + r0 + r] = t[r][c];
+  }
+}
+
+struct AdamLayer {
+  float* w;             // [O, I] fp32 master
+  const float* g;       // [O, I] grad
+  float* m;
+  float* v;
+  const float* mask;    // [O, I] trainable mask
+  bf16_t* wb;           // [O, I] bf16 copy
+  bf16_t* wbT;          // [I, O] bf16 transposed copy
+  const unsigned long long* t;   // device update counter (1-based t = *t + 1): graph-replay safe
+  int O, I;
+  float lr, beta1, beta2, eps;
+};
+
+// Adam over one weight matrix in 32x32 tiles; writes the bf16 copy and, through LDS,
+// the transposed bf16 copy with coalesced stores.
+__global__ void __launch_bounds__(256) adam_tile_kernel(AdamLayer p) {
+  __shared__ bf16_t t[32][34];
+  const int o0 = blockIdx.y * 32, i0 = blockIdx.x * 32;
+  const float tt = (float)(*p.t + 1ull);
+  const float c1 = 1.f / (1.f - powf(p.beta1, tt)), c2 = 1.f / (1.f - powf(p.beta2, tt));
+  for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+    const int oo = k / 32, ii = k % 32;
+    const int o = o0 + oo, i = i0 + ii;
+    bf16_t wb = 0;
+    if (o < p.O && i < p.I) {
+      const size_t idx = (size_t)o * p.I + i;
+      float w = p.w[idx];
+      const float mk = p.mask[idx];
+      if (mk != 0.f) {
+        const float g = p.g[idx] * mk;
+        const float m = p.beta1 * p.m[idx] + (1.f - p.beta1) * g;
+        const float v = p.beta2 * p.v[idx] + (1.f - p.beta2) * g * g;
+        p.m[idx] = m;
+        p.v[idx] = v;
+        w -= p.lr * (m * c1) / (sqrtf(v * c2) + p.eps);
+        p.w[idx] = w;
+      }
+      wb = f2bf(w);
+      p.wb[idx] = wb;
+    }
+    t[oo][ii] = wb;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+    const int ii = k / 32, oo = k % 32;
+    const int o = o0 + oo, i = i0 + ii;
+    if (p.wbT && o < p.O && i < p.I) p.wbT[(size_t)i * p.O + o] = t[oo][ii];
+  }
+}
+
+}  // namespace st
+
+extern "C" hipError_t st_deep_gather(const st::DeepGather* g, hipStream_t s) {
+  if (g->in_p > 256 || g->in_p % 4 || g->H + 2 > g->in_p) return hipErrorInvalidValue;
+  const int waves = g->B, per = 4;
+  hipLaunchKernelGGL(st::deep_gather_kernel, dim3((waves + per - 1) / per), dim3(256), 0, s, *g);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_deep_env_step(const st::DeepEnv* p, hipStream_t s) {
+  hipLaunchKernelGGL(st::deep_env_step_kernel, dim3((p->E + 255) / 256), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL(st::deep_advance_kernel, dim3(1), dim3(1), 0, s, p->rp.ctrl, p->ctrl, p->E, p->rp.cap);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_deep_td(const st::DeepTD* p, hipStream_t s) {
+  hipLaunchKernelGGL(st::deep_td_kernel, dim3((p->B + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_row_sum_bf16(const bf16_t* X, int ld, int rows, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(st::row_sum_bf16_kernel, dim3(rows), dim3(256), 0, s, X, ld, n, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_transpose_bf16(const bf16_t* in, int ldi, bf16_t* out, int ldo, int R, int Cc, hipStream_t s) {
+  hipLaunchKernelGGL(st::transpose_bf16_kernel, dim3((Cc + 63) / 64, (R + 63) / 64), dim3(256), 0, s, in, ldi, out, ldo,
+                     R, Cc);
+  return hipGetLastError();
+}
+
+__global__ void st_counter_inc_kernel(unsigned long long* c) { c[0] += 1; }
+
+extern "C" hipError_t st_counter_inc(unsigned long long* c, hipStream_t s) {
+  hipLaunchKernelGGL(st_counter_inc_kernel, dim3(1), dim3(1), 0, s, c);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_adam_tile(const st::AdamLayer* p, hipStream_t s) {
+  hipLaunchKernelGGL(st::adam_tile_kernel, dim3((p->I + 31) / 32, (p->O + 31) / 32), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}

@@ -1,0 +1,236 @@
+// bf16 MFMA GEMM with fused epilogues for the deep-MLP learner (BASELINE config 4:
+// 4x1024 MLP Q-net, batch 4096 from an HBM replay buffer).
+//
+//   C[M,N] = A[M,K] . B[N,K]^T      A, B bf16, K-contiguous rows (lda, ldb elements)
+//
+// Every product of the MLP is put in this "NT" form by keeping the operands the
+// next product needs in the right layout: the forward epilogue writes each hidden
+// activation both row-major H[m][n] and transposed H^T[n][m], the optimizer keeps bf16
+// copies of every weight as W[o][i] and W^T[i][o], so
+//   forward   H   = act(X . W^T + b)          -> gemm(A=X,    B=W)
+//   bwd-data  dH  = dZ . W     (masked)       -> gemm(A=dZ,   B=W^T)
+//   bwd-wgrad dW  = dZ^T . X                  -> gemm(A=dZ^T, B=X^T)
+//
+// Kernel: 256 threads (2x2 waves), BM x BN block tile, BK = 64, double-buffered LDS
+// filled by global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction) with the
+// XOR-(row&7) chunk swizzle applied on the global SOURCE address, so the 16x16x32
+// fragment reads (ds_read_b128) are bank-conflict-free; one barrier per K-tile
+// (cdna_hip_programming.md T2, T3+T4 minimum 2-phase form).  Epilogues are staged
+// through the (then idle) LDS buffers so that C and C^T leave in 16-byte stores.
+#include "common.h"
+
+namespace st {
+
+constexpr int GT = 256;   // threads
+constexpr int GBK = 64;   // K tile
+
+enum GemmEpi : int {
+  EPI_BF16 = 0,      // out = act(alpha*acc + bias) as bf16 [M][N] (+ optional outT [N][M])
+  EPI_RELU_GRAD = 1, // out = acc * (auxT[n][m] > 0) as bf16 [M][N] (+ outT)
+  EPI_F32 = 2,       // out = alpha*acc (+ bias[n]) (+ out if accumulate) as fp32 [M][N]
+};
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* out;
+  bf16_t* outT;          // optional transposed bf16 output
+  const float* bias;     // [N] or null
+  const bf16_t* auxT;    // [N][M] activations (relu-grad mask), EPI_RELU_GRAD
+  int M, N, K;
+  int lda, ldb, ldo, ldoT, ldaux;
+  int relu, accumulate;
+  float alpha;
+};
+
+template <int BM, int BN>
+struct GemmGeo {
+  static constexpr int A_EL = BM * GBK, B_EL = BN * GBK;
+  static constexpr int BUF_EL = A_EL + B_EL;
+  static constexpr int KLOOP_BYTES = 2 * BUF_EL * 2;
+  static constexpr int EPI_BYTES = (BM * (BN + 8) + BN * (BM + 8)) * 2;
+  static constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
+  static constexpr int WM = BM / 2, WN = BN / 2;    // per-wave output tile
+  static constexpr int TM = WM / 16, TN = WN / 16;  // 16x16 MFMA tiles per wave
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+  static_assert(LDS_BYTES * 2 <= 163840, "two blocks per CU");
+};
+
+// stage one operand tile (ROWS x 64 bf16) of K-tile k0 into a linear LDS image with the
+// chunk swizzle moved to the source address.  ROWS*8 16-B pieces, 64 per wave-instruction.
+template <int ROWS>
+ST_DEV void stage_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, bf16_t* lds, int wave, int lane) {
+  constexpr int INSTR = ROWS / 8;        // wave-instructions per tile
+#pragma unroll
+  for (int j = wave; j < INSTR; j += GT / 64) {
+    const int r = j * 8 + (lane >> 3);
+    const int c = lane & 7;
+    const int g = c ^ (r & 7);
+    const bf16_t* src = G + (size_t)(row0 + r) * ld + k0 + g * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + j * 512), 16, 0, 0);
+  }
+}
+
+// fragment (8 bf16) of row r, global chunk g of a staged tile
+ST_DEV s8v frag_sw(const bf16_t* lds, int r, int g) {
+  return lds_ld8(lds + r * GBK + ((g ^ (r & 7)) << 3));
+}
+
+template <int BM, int BN, int EPI>
+__global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
+  using G = GemmGeo<BM, BN>;
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  // XCD-aware tile order: neighbouring tiles (sharing A rows) on one XCD's L2
+  const int ntn = p.N / BN, ntm = p.M / BM, nwg = ntn * ntm;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f4v acc[G::TM][G::TN];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) acc[i][j] = zero4();
+
+  const int nk = p.K / GBK;
+  stage_tile<BM>(p.A, p.lda, m0, 0, buf, wave, lane);
+  stage_tile<BN>(p.B, p.ldb, n0, 0, buf + G::A_EL, wave, lane);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    bf16_t* cur = buf + (t & 1) * G::BUF_EL;
+    if (t + 1 < nk) {
+      bf16_t* nxt = buf + ((t + 1) & 1) * G::BUF_EL;
+      stage_tile<BM>(p.A, p.lda, m0, (t + 1) * GBK, nxt, wave, lane);
+      stage_tile<BN>(p.B, p.ldb, n0, (t + 1) * GBK, nxt + G::A_EL, wave, lane);
+    }
+    const bf16_t* cA = cur;
+    const bf16_t* cB = cur + G::A_EL;
+#pragma unroll
+    for (int kk = 0; kk < GBK / 32; ++kk) {
+      s8v a[G::TM], b[G::TN];
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i) a[i] = frag_sw(cA, wm * G::WM + 16 * i + l16, kk * 4 + g4);
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) b[j] = frag_sw(cB, wn * G::WN + 16 * j + l16, kk * 4 + g4);
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // next tile landed (and this tile's reads retired)
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogues
+  if constexpr (EPI == EPI_F32) {
+    float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) {
+        const int n = n0 + wn * G::WN + 16 * j + l16;
+        const float bb = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * G::WM + 16 * i + 4 * g4 + r;
+          float v = p.alpha * acc[i][j][r] + bb;
+          float* o = out + (size_t)m * p.ldo + n;
+          if (p.accumulate) v += *o;
+          *o = v;
+        }
+      }
+    return;
+  } else {
+    // stage C [BM][BN+8] and C^T [BN][BM+8] in LDS (the K-loop buffers are idle now)
+    constexpr int SC = BN + 8, SCT = BM + 8;
+    bf16_t* sC = buf;
+    bf16_t* sCT = buf + BM * SC;
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) {
+        const int nl = wn * G::WN + 16 * j + l16;          // local col
+        const int ml = wm * G::WM + 16 * i + 4 * g4;       // local row of r = 0
+        float v[4];
+        if constexpr (EPI == EPI_BF16) {
+          const float bb = p.bias ? p.bias[n0 + nl] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = p.alpha * acc[i][j][r] + bb;
+            v[r] = p.relu ? fmaxf(x, 0.f) : x;
+          }
+        } else {  // EPI_RELU_GRAD: mask by the forward activation (read from its transposed copy)
+          const s4v h = *reinterpret_cast<const s4v*>(p.auxT + (size_t)(n0 + nl) * p.ldaux + m0 + ml);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (bf2f((bf16_t)h[r]) > 0.f) ? acc[i][j][r] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sC[(ml + r) * SC + nl] = f2bf(v[r]);
+        lds_st4(sCT + nl * SCT + ml, v[0], v[1], v[2], v[3]);
+      }
+    __syncthreads();
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+    constexpr int CPR = BN / 8;   // 16-byte chunks per C row
+    for (int c = tid; c < BM * CPR; c += GT) {
+      const int r = c / CPR, k = (c % CPR) * 8;
+      *reinterpret_cast<uint4*>(out + (size_t)(m0 + r) * p.ldo + n0 + k) =
+          *reinterpret_cast<const uint4*>(sC + r * SC + k);
+    }
+    if (p.outT) {
+      constexpr int CPRT = BM / 8;
+      for (int c = tid; c < BN * CPRT; c += GT) {
+        const int r = c / CPRT, k = (c % CPRT) * 8;
+        *reinterpret_cast<uint4*>(p.outT + (size_t)(n0 + r) * p.ldoT + m0 + k) =
+            *reinterpret_cast<const uint4*>(sCT + r * SCT + k);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int EPI>
+static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
+  using G = GemmGeo<BM, BN>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nwg = (p.M / BM) * (p.N / BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI>), dim3(nwg), dim3(GT), G::LDS_BYTES, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace st
+
+// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN)
+extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
+  const int bm = tile == 0 ? 128 : (tile == 1 ? 64 : 128);
+  const int bn = tile == 0 ? 128 : 64;
+  if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
+  if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
+  if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
+  if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return hipErrorInvalidValue;
+#define ST_G(BM_, BN_)                                                                   \
+  switch (epi) {                                                                         \
+    case 0: return st::launch_gemm<BM_, BN_, 0>(*p, stream);                             \
+    case 1: return st::launch_gemm<BM_, BN_, 1>(*p, stream);                             \
+    case 2: return st::launch_gemm<BM_, BN_, 2>(*p, stream);                             \
+    default: return hipErrorInvalidValue;                                                \
+  }
+  if (tile == 0) { ST_G(128, 128) }
+  if (tile == 1) { ST_G(64, 64) }
+  if (tile == 2) { ST_G(128, 64) }
+#undef ST_G
+  return hipErrorInvalidValue;
+}

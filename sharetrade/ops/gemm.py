@@ -1,0 +1,86 @@
+"""Host wrapper of the bf16 MFMA GEMM (`csrc/gemm_bf16.hip`): ``C = A . B^T`` with
+fused epilogues.  Shapes are validated on the host before any launch (the kernel
+assumes whole tiles)."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import native
+
+EPI_BF16, EPI_RELU_GRAD, EPI_F32 = 0, 1, 2
+TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2}
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ("A", C.c_void_p), ("B", C.c_void_p), ("out", C.c_void_p), ("outT", C.c_void_p), ("bias", C.c_void_p),
+        ("auxT", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
+        ("ldo", C.c_int), ("ldoT", C.c_int), ("ldaux", C.c_int), ("relu", C.c_int), ("accumulate", C.c_int),
+        ("alpha", C.c_float),
+    ]
+
+
+def _bind():
+    L = native.lib()
+    if not getattr(L, "_gemm_bound", False):
+        L.st_gemm_nt.argtypes = [C.POINTER(GemmArgs), C.c_int, C.c_int, C.c_void_p]
+        L.st_gemm_nt.restype = C.c_int
+        L._gemm_bound = True
+    return L
+
+
+def pick_tile(M: int, N: int) -> tuple:
+    """128x128 when that still gives >= ~256 workgroups, else smaller tiles."""
+    if M % 128 == 0 and N % 128 == 0 and (M // 128) * (N // 128) >= 200:
+        return (128, 128)
+    if M % 128 == 0 and N % 64 == 0 and (M // 128) * (N // 64) >= 200:
+        return (128, 64)
+    return (64, 64)
+
+
+def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, outT: Optional[torch.Tensor] = None,
+              bias: Optional[torch.Tensor] = None, auxT: Optional[torch.Tensor] = None, relu: bool = False,
+              accumulate: bool = False, alpha: float = 1.0) -> GemmArgs:
+    M, K = A.shape
+    N, K2 = B.shape
+    if K != K2:
+        raise ValueError(f"gemm_nt: K mismatch {A.shape} x {B.shape}^T")
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16:
+        raise TypeError("gemm_nt operands must be bf16")
+    if A.stride(1) != 1 or B.stride(1) != 1 or out.stride(1) != 1:
+        raise ValueError("gemm_nt needs row-major (K-contiguous) operands")
+    if tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm_nt: out {tuple(out.shape)} != {(M, N)}")
+    if epi == EPI_F32 and out.dtype != torch.float32:
+        raise TypeError("EPI_F32 writes fp32")
+    if epi != EPI_F32 and out.dtype != torch.bfloat16:
+        raise TypeError("bf16 epilogues write bf16")
+    if outT is not None and tuple(outT.shape) != (N, M):
+        raise ValueError("outT must be [N, M]")
+    if auxT is not None and tuple(auxT.shape) != (N, M):
+        raise ValueError("auxT must be [N, M]")
+    if bias is not None and bias.numel() < N:
+        raise ValueError("bias too short")
+    g = GemmArgs()
+    g.A, g.B, g.out = A.data_ptr(), B.data_ptr(), out.data_ptr()
+    g.outT = outT.data_ptr() if outT is not None else None
+    g.bias = bias.data_ptr() if bias is not None else None
+    g.auxT = auxT.data_ptr() if auxT is not None else None
+    g.M, g.N, g.K = M, N, K
+    g.lda, g.ldb, g.ldo = A.stride(0), B.stride(0), out.stride(0)
+    g.ldoT = outT.stride(0) if outT is not None else 0
+    g.ldaux = auxT.stride(0) if auxT is not None else 0
+    g.relu, g.accumulate, g.alpha = int(relu), int(accumulate), float(alpha)
+    return g
+
+
+def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_BF16, tile=None, **kw) -> torch.Tensor:
+    g = make_args(A, B, out, epi, **kw)
+    t = tile or pick_tile(g.M, g.N)
+    if g.M % t[0] or g.N % t[1] or g.K % 64:
+        raise ValueError(f"gemm_nt: shape {g.M}x{g.N}x{g.K} not a multiple of tile {t} / BK 64")
+    native.check(_bind().st_gemm_nt(g, epi, TILES[t], native.stream_handle()), "st_gemm_nt")
+    return out

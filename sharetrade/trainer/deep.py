@@ -1,0 +1,351 @@
+"""DeepDQN — the 4x1024 MLP Q-net with an HBM replay buffer (BASELINE.json config 4).
+
+Not in the reference (its learner is a 203->200->3 net trained online at batch 1,
+`QDecisionPolicyActor.scala:38-77`); this is the north-star scale-up of the same
+agent/env: E vectorised trading envs act with the current Q-net, every transition
+goes into a 1M-entry replay ring resident in HBM, and each learner update samples
+a batch of 4096 transitions, rebuilds their states from the price bank, and runs a
+DQN update (target network, Adam) — all on MFMA GEMMs (`csrc/gemm_bf16.hip`) with
+fused bias/ReLU/ReLU-grad epilogues, plus the gather / env / TD / Adam kernels of
+`csrc/deep.hip`.  One rollout step and one learner update are each captured in a
+HIP graph.
+
+Every product is in ``C = A . B^T`` form (see gemm_bf16.hip): activations are kept
+as ``A`` and ``A^T``, weights as bf16 ``W`` and ``W^T`` (written by the Adam kernel).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..config import Config
+from ..ops import gemm as gm
+from ..ops import native
+from ..utils import rng
+
+ACT_PAD = 64  # output layer rows padded to a GEMM tile
+
+
+class _Replay(C.Structure):
+    _fields_ = [("env", C.c_void_p), ("pos", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p),
+                ("action", C.c_void_p), ("reward", C.c_void_p), ("budget2", C.c_void_p), ("shares2", C.c_void_p),
+                ("done", C.c_void_p), ("ctrl", C.c_void_p), ("cap", C.c_int)]
+
+
+class _Gather(C.Structure):
+    _fields_ = [("prices", C.c_void_p), ("T", C.c_int), ("H", C.c_int), ("in_p", C.c_int), ("feat_mode", C.c_int),
+                ("inv_b0", C.c_float), ("mode", C.c_int), ("B", C.c_int), ("pos", C.c_void_p),
+                ("budget", C.c_void_p), ("shares", C.c_void_p), ("rp", _Replay), ("key0", C.c_uint32),
+                ("key1", C.c_uint32), ("step", C.c_void_p), ("X", C.c_void_p), ("Xn", C.c_void_p),
+                ("r_out", C.c_void_p), ("a_out", C.c_void_p), ("done_out", C.c_void_p)]
+
+
+class _Env(C.Structure):
+    _fields_ = [("prices", C.c_void_p), ("T", C.c_int), ("H", C.c_int), ("E", C.c_int), ("compat_env", C.c_int),
+                ("s0", C.c_int), ("n_actions", C.c_int), ("b0", C.c_float), ("eps", C.c_float),
+                ("inv_ramp", C.c_float), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
+                ("pos", C.c_void_p), ("episodes", C.c_void_p), ("last_final", C.c_void_p), ("q", C.c_void_p),
+                ("ldq", C.c_int), ("key0", C.c_uint32), ("key1", C.c_uint32), ("ctrl", C.c_void_p),
+                ("rp", _Replay), ("stats", C.c_void_p)]
+
+
+class _TD(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("qt", C.c_void_p), ("r", C.c_void_p), ("a", C.c_void_p), ("done", C.c_void_p),
+                ("dq", C.c_void_p), ("dqT", C.c_void_p), ("loss", C.c_void_p), ("B", C.c_int), ("ldq", C.c_int),
+                ("n_actions", C.c_int), ("gamma", C.c_float), ("coef", C.c_float)]
+
+
+class _Adam(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("mask", C.c_void_p),
+                ("wb", C.c_void_p), ("wbT", C.c_void_p), ("t", C.c_void_p), ("O", C.c_int), ("I", C.c_int),
+                ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float)]
+
+
+def _bind():
+    L = native.lib()
+    if not getattr(L, "_deep_bound", False):
+        for fn, args in (("st_deep_gather", [C.POINTER(_Gather), C.c_void_p]),
+                         ("st_deep_env_step", [C.POINTER(_Env), C.c_void_p]),
+                         ("st_deep_td", [C.POINTER(_TD), C.c_void_p]),
+                         ("st_row_sum_bf16", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+                         ("st_transpose_bf16", [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                C.c_void_p]),
+                         ("st_adam_tile", [C.POINTER(_Adam), C.c_void_p]),
+                         ("st_counter_inc", [C.c_void_p, C.c_void_p])):
+            f = getattr(L, fn)
+            f.argtypes = args
+            f.restype = C.c_int
+        L._deep_bound = True
+    return L
+
+
+def _p(t: Optional[torch.Tensor]):
+    return t.data_ptr() if t is not None else None
+
+
+class DeepDQN:
+    """E envs + replay ring + deep MLP learner on one GPU."""
+
+    def __init__(self, cfg: Config, device: torch.device, envs: int = 16384, batch: int = 4096,
+                 replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
+                 prices: Optional[torch.Tensor] = None, seed: Optional[int] = None):
+        if device.type != "cuda":
+            raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
+        self.cfg, self.dev = cfg, device
+        self.E, self.B, self.cap = int(envs), int(batch), int(replay_capacity)
+        self.H = cfg.model.history
+        self.in_real = self.H + 2
+        self.in_p = 256
+        if self.in_real > self.in_p:
+            raise ValueError("history too long for the 256-wide input tile")
+        hid = list(hidden or cfg.model.hidden)
+        if any(h % 128 for h in hid):
+            raise ValueError("hidden widths must be multiples of 128 (GEMM tiles)")
+        if self.E % 128 or self.B % 128:
+            raise ValueError("envs and batch must be multiples of 128")
+        self.n_act = cfg.model.n_actions
+        self.dims = [self.in_real] + hid + [self.n_act]
+        self.pdims = [self.in_p] + hid + [ACT_PAD]
+        self.L = len(self.pdims) - 1
+        self.target_every = int(target_every)
+        self.seed = cfg.agent.seed if seed is None else seed
+        self.k = _bind()
+        f32, b16, i32 = torch.float32, torch.bfloat16, torch.int32
+        dev = device
+        # ------------------------------------------------------------ parameters (+ Adam, bf16 copies, target)
+        g = torch.Generator().manual_seed(int(self.seed))
+        self.W, self.b, self.Wm, self.Wv, self.bm, self.bv = [], [], [], [], [], []
+        self.Wb, self.WbT, self.Wt, self.bt, self.Wmask, self.bmask, self.dW, self.db = [], [], [], [], [], [], [], []
+        for l in range(self.L):
+            o, i = self.pdims[l + 1], self.pdims[l]
+            ro, ri = self.dims[l + 1], self.dims[l]
+            w = torch.zeros(o, i)
+            std = math.sqrt(2.0 / ri) if l < self.L - 1 else 0.01
+            w[:ro, :ri] = torch.randn(ro, ri, generator=g) * std
+            mask = torch.zeros(o, i)
+            mask[:ro, :ri] = 1.0
+            bm = torch.zeros(1, o)
+            bm[0, :ro] = 1.0
+            self.W.append(w.to(dev))
+            self.b.append(torch.zeros(1, o, device=dev))
+            self.Wmask.append(mask.to(dev))
+            self.bmask.append(bm.to(dev))
+            for lst, shape in ((self.Wm, (o, i)), (self.Wv, (o, i)), (self.bm, (1, o)), (self.bv, (1, o))):
+                lst.append(torch.zeros(*shape, device=dev))
+            self.Wb.append(self.W[l].to(b16).contiguous())
+            self.WbT.append(self.W[l].t().contiguous().to(b16))
+            self.Wt.append(self.Wb[l].clone())
+            self.bt.append(self.b[l].clone())
+            self.dW.append(torch.zeros(o, i, device=dev))
+            self.db.append(torch.zeros(1, o, device=dev))
+        self._bT_scratch = torch.zeros(max(self.pdims), 1, dtype=b16, device=dev)
+        self.t_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        # ------------------------------------------------------------ data, envs, replay
+        from .engine import make_price_bank, padded_bank
+
+        if prices is not None:
+            bank = padded_bank(prices.shape[0], prices.shape[1], dev)
+            bank.copy_(prices)
+            self.prices = bank
+        else:
+            self.prices = make_price_bank(cfg, self.E, dev, seed=0)
+        if self.prices.shape[0] != self.E:
+            raise ValueError("price bank rows != envs")
+        self.T = int(self.prices.shape[1])
+        e = cfg.env
+        self.budget = torch.full((self.E,), float(e.budget), device=dev)
+        self.shares = torch.full((self.E,), int(e.shares), dtype=i32, device=dev)
+        self.value = torch.zeros(self.E, device=dev)
+        self.pos = torch.zeros(self.E, dtype=i32, device=dev)
+        self.episodes = torch.zeros(self.E, dtype=i32, device=dev)
+        self.last_final = torch.full((self.E,), float("nan"), device=dev)
+        self.env_ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.rp = {k: torch.zeros(self.cap, dtype=(f32 if k in ("budget", "reward", "budget2") else i32), device=dev)
+                   for k in ("env", "pos", "budget", "shares", "action", "reward", "budget2", "shares2", "done")}
+        self.rp_ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.stats = torch.zeros(4, device=dev)
+        self.loss = torch.zeros(1, device=dev)
+        # ------------------------------------------------------------ activations
+        M = self.B
+        self.X = torch.zeros(M, self.in_p, dtype=b16, device=dev)
+        self.XT = torch.zeros(self.in_p, M, dtype=b16, device=dev)
+        self.Xn = torch.zeros(M, self.in_p, dtype=b16, device=dev)
+        self.Act = [None] + [torch.zeros(M, h, dtype=b16, device=dev) for h in hid]
+        self.ActT = [None] + [torch.zeros(h, M, dtype=b16, device=dev) for h in hid]
+        self.ActN = [None] + [torch.zeros(M, h, dtype=b16, device=dev) for h in hid]
+        self.G = [torch.zeros(M, self.pdims[l + 1], dtype=b16, device=dev) for l in range(self.L)]
+        self.GT = [torch.zeros(self.pdims[l + 1], M, dtype=b16, device=dev) for l in range(self.L)]
+        self.Q = torch.zeros(M, ACT_PAD, device=dev)
+        self.Qt = torch.zeros(M, ACT_PAD, device=dev)
+        self.r_b = torch.zeros(M, device=dev)
+        self.a_b = torch.zeros(M, dtype=i32, device=dev)
+        self.d_b = torch.zeros(M, device=dev)
+        # acting buffers (M = E)
+        self.Xe = torch.zeros(self.E, self.in_p, dtype=b16, device=dev)
+        self.Acte = [None] + [torch.zeros(self.E, h, dtype=b16, device=dev) for h in hid]
+        self.Qe = torch.zeros(self.E, ACT_PAD, device=dev)
+        self.key0, self.key1 = (int(x) for x in rng.key_for(self.seed, 0))
+        self.updates = 0
+        self.env_steps = 0
+        self._g_act = None
+        self._g_upd = None
+        self._build_structs()
+
+    # ---------------------------------------------------------------- ctypes structs
+    def _replay_struct(self) -> _Replay:
+        r = _Replay()
+        for k in ("env", "pos", "budget", "shares", "action", "reward", "budget2", "shares2", "done"):
+            setattr(r, k, self.rp[k].data_ptr())
+        r.ctrl, r.cap = self.rp_ctrl.data_ptr(), self.cap
+        return r
+
+    def _build_structs(self) -> None:
+        cfg = self.cfg
+        from ..env.trading import FEATURES
+
+        fm = FEATURES[cfg.env.features]
+        ib0 = float(np.float32(1.0 / cfg.env.budget))
+        ge = _Gather()
+        ge.prices, ge.T, ge.H, ge.in_p, ge.feat_mode, ge.inv_b0 = self.prices.data_ptr(), self.T, self.H, self.in_p, fm, ib0
+        ge.mode, ge.B = 0, self.E
+        ge.pos, ge.budget, ge.shares = self.pos.data_ptr(), self.budget.data_ptr(), self.shares.data_ptr()
+        ge.rp = self._replay_struct()
+        ge.key0, ge.key1, ge.step = self.key0, self.key1, self.t_ctr.data_ptr()
+        ge.X = self.Xe.data_ptr()
+        self._gather_env = ge
+        gr = _Gather()
+        C.pointer(gr)[0] = ge
+        gr.mode, gr.B = 1, self.B
+        gr.X, gr.Xn = self.X.data_ptr(), self.Xn.data_ptr()
+        gr.r_out, gr.a_out, gr.done_out = self.r_b.data_ptr(), self.a_b.data_ptr(), self.d_b.data_ptr()
+        self._gather_rp = gr
+        ev = _Env()
+        ev.prices, ev.T, ev.H, ev.E = self.prices.data_ptr(), self.T, self.H, self.E
+        ev.compat_env, ev.s0, ev.n_actions = int(cfg.env.compat_decisions), int(cfg.env.shares), self.n_act
+        ev.b0, ev.eps, ev.inv_ramp = float(cfg.env.budget), float(cfg.agent.epsilon), float(np.float32(1 / cfg.agent.ramp))
+        ev.budget, ev.shares, ev.value, ev.pos = (self.budget.data_ptr(), self.shares.data_ptr(), self.value.data_ptr(),
+                                                  self.pos.data_ptr())
+        ev.episodes, ev.last_final = self.episodes.data_ptr(), self.last_final.data_ptr()
+        ev.q, ev.ldq, ev.key0, ev.key1 = self.Qe.data_ptr(), ACT_PAD, self.key0, self.key1
+        ev.ctrl, ev.rp, ev.stats = self.env_ctrl.data_ptr(), self._replay_struct(), self.stats.data_ptr()
+        self._env = ev
+        td = _TD()
+        td.q, td.qt, td.r, td.a, td.done = (self.Q.data_ptr(), self.Qt.data_ptr(), self.r_b.data_ptr(),
+                                            self.a_b.data_ptr(), self.d_b.data_ptr())
+        td.dq, td.dqT, td.loss = self.G[-1].data_ptr(), self.GT[-1].data_ptr(), self.loss.data_ptr()
+        td.B, td.ldq, td.n_actions = self.B, ACT_PAD, self.n_act
+        td.gamma, td.coef = float(cfg.agent.gamma), 2.0 / self.B
+        self._td = td
+        a = cfg.agent
+        self._adam = []
+        for l in range(self.L):
+            for (w, g_, m, v, mk, wb, wbT, O, I) in (
+                    (self.W[l], self.dW[l], self.Wm[l], self.Wv[l], self.Wmask[l], self.Wb[l], self.WbT[l],
+                     self.pdims[l + 1], self.pdims[l]),
+                    (self.b[l], self.db[l], self.bm[l], self.bv[l], self.bmask[l], None, None, 1, self.pdims[l + 1])):
+                ad = _Adam()
+                ad.w, ad.g, ad.m, ad.v, ad.mask = w.data_ptr(), g_.data_ptr(), m.data_ptr(), v.data_ptr(), mk.data_ptr()
+                ad.wb = wb.data_ptr() if wb is not None else self._bscratch(l).data_ptr()
+                ad.wbT = wbT.data_ptr() if wbT is not None else None
+                ad.t, ad.O, ad.I = self.t_ctr.data_ptr(), O, I
+                ad.lr, ad.beta1, ad.beta2, ad.eps = float(a.lr), float(a.adam_betas[0]), float(a.adam_betas[1]), \
+                    float(a.adam_eps)
+                self._adam.append(ad)
+
+    def _bscratch(self, l: int) -> torch.Tensor:
+        if not hasattr(self, "_bias_bf"):
+            self._bias_bf = [torch.zeros(1, self.pdims[k + 1], dtype=torch.bfloat16, device=self.dev)
+                             for k in range(self.L)]
+        return self._bias_bf[l]
+
+    # ---------------------------------------------------------------- forward
+    def _forward(self, X, acts, actsT, Wb, bias, Q) -> None:
+        """acts[l+1] = relu(acts[l] . W_l^T + b_l); Q = acts[L-1] . W_{L-1}^T + b_{L-1} (fp32)."""
+        a = X
+        for l in range(self.L):
+            if l < self.L - 1:
+                gm.gemm_nt(a, Wb[l], acts[l + 1], gm.EPI_BF16, outT=actsT[l + 1] if actsT else None,
+                           bias=bias[l], relu=True)
+                a = acts[l + 1]
+            else:
+                gm.gemm_nt(a, Wb[l], Q, gm.EPI_F32, bias=bias[l])
+
+    def act_step(self) -> None:
+        """One env step of all E envs: gather -> Q forward -> select/transition/replay insert."""
+        sh = native.stream_handle()
+        native.check(self.k.st_deep_gather(self._gather_env, sh), "deep_gather(env)")
+        self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe)
+        native.check(self.k.st_deep_env_step(self._env, sh), "deep_env_step")
+
+    def update_step(self) -> None:
+        """One DQN update: sample B transitions, Q(x) online / Q(x') target, TD, backward, Adam."""
+        sh = native.stream_handle()
+        k = self.k
+        native.check(k.st_deep_gather(self._gather_rp, sh), "deep_gather(replay)")
+        native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
+                                         self.in_p, sh), "transpose X")
+        acts = [self.X] + self.Act[1:]
+        actsT = [self.XT] + self.ActT[1:]
+        self._forward(self.X, acts, actsT, self.Wb, self.b, self.Q)
+        self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)
+        native.check(k.st_deep_td(self._td, sh), "deep_td")
+        for l in reversed(range(self.L)):
+            # weight / bias gradients of layer l: dW = G_l^T . A_l
+            gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32)
+            native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
+                                           self.db[l].data_ptr(), sh), "bias grad")
+            if l > 0:
+                # G_{l-1} = (G_l . W_l) * (A_l > 0)
+                gm.gemm_nt(self.G[l], self.WbT[l], self.G[l - 1], gm.EPI_RELU_GRAD, outT=self.GT[l - 1],
+                           auxT=actsT[l])
+        for ad in self._adam:
+            native.check(k.st_adam_tile(ad, sh), "adam")
+        native.check(k.st_counter_inc(self.t_ctr.data_ptr(), sh), "t++")
+
+    def sync_target(self) -> None:
+        for l in range(self.L):
+            self.Wt[l].copy_(self.Wb[l])
+            self.bt[l].copy_(self.b[l])
+
+    # ---------------------------------------------------------------- driver
+    def capture(self) -> None:
+        """Capture one act step and one update into HIP graphs (after a warm-up of each)."""
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self.act_step()
+            self.update_step()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        self.env_steps += 1
+        self.updates += 1
+        self._g_act = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_act):
+            self.act_step()
+        self._g_upd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_upd):
+            self.update_step()
+
+    def iteration(self, updates_per_step: int = 1) -> None:
+        if self._g_act is not None:
+            self._g_act.replay()
+        else:
+            self.act_step()
+        self.env_steps += 1
+        for _ in range(updates_per_step):
+            if self._g_upd is not None:
+                self._g_upd.replay()
+            else:
+                self.update_step()
+            self.updates += 1
+            if self.target_every and self.updates % self.target_every == 0:
+                self.sync_target()
+
+    def stats_dict(self) -> Dict[str, float]:
+        s = self.stats.cpu().tolist()
+        return {"reward_sum": s[0], "explore": s[1], "episodes_done": s[2], "final_sum": s[3],
+                "loss_sum": float(self.loss.item()), "replay_size": int(self.rp_ctrl[1].item()),
+                "updates": self.updates, "env_steps": self.env_steps * self.E}

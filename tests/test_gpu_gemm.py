@@ -1,0 +1,67 @@
+"""bf16 MFMA GEMM (csrc/gemm_bf16.hip) vs the fp32 PyTorch reference of the same op."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).cuda()
+
+
+@pytest.mark.parametrize("M,N,K,tile", [(256, 256, 128, (128, 128)), (512, 1024, 1024, (128, 128)),
+                                        (128, 192, 64, (64, 64)), (4096, 64, 1024, (128, 64)),
+                                        (1024, 1024, 4096, (64, 64))])
+def test_gemm_f32_epilogue(native_built, M, N, K, tile):
+    from sharetrade.ops.gemm import EPI_F32, gemm_nt
+
+    A, B = _bf((M, K), 1), _bf((N, K), 2)
+    out = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    gemm_nt(A, B, out, EPI_F32, tile=tile, alpha=0.5)
+    ref = 0.5 * (A.float() @ B.float().t())
+    torch.cuda.synchronize()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
+    # accumulate
+    gemm_nt(A, B, out, EPI_F32, tile=tile, alpha=0.5, accumulate=True)
+    assert torch.allclose(out, 2 * ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("tile", [(128, 128), (64, 64)])
+def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
+    from sharetrade.ops.gemm import EPI_BF16, gemm_nt
+
+    M, N, K = 512, 256, 320
+    A, B = _bf((M, K), 3), _bf((N, K), 4)
+    bias = torch.randn(N, device="cuda")
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    outT = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
+    gemm_nt(A, B, out, EPI_BF16, tile=tile, outT=outT, bias=bias, relu=True)
+    ref = torch.relu(A.float() @ B.float().t() + bias)
+    torch.cuda.synchronize()
+    assert torch.allclose(out.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    assert torch.equal(outT, out.t().contiguous())
+
+
+def test_gemm_relu_grad_epilogue(native_built):
+    from sharetrade.ops.gemm import EPI_RELU_GRAD, gemm_nt
+
+    M, N, K = 256, 128, 64
+    A, B = _bf((M, K), 5), _bf((N, K), 6)
+    act = torch.relu(torch.randn(M, N, device="cuda")).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    outT = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
+    gemm_nt(A, B, out, EPI_RELU_GRAD, tile=(64, 64), outT=outT, auxT=act.t().contiguous())
+    ref = (A.float() @ B.float().t()) * (act.float() > 0)
+    torch.cuda.synchronize()
+    assert torch.allclose(out.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    assert torch.equal(outT, out.t().contiguous())
+
+
+def test_gemm_rejects_bad_shapes(native_built):
+    from sharetrade.ops.gemm import EPI_F32, gemm_nt
+
+    A, B = _bf((100, 64), 1), _bf((128, 64), 2)
+    with pytest.raises(ValueError):
+        gemm_nt(A, B, torch.empty(100, 128, device="cuda"), EPI_F32)
