@@ -247,7 +247,8 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
   float* sB1 = reinterpret_cast<float*>(smem + G::fB1);
   float* sB2 = reinterpret_cast<float*>(smem + G::fB2);
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: wave-specialised phases branch, not mask
   const int H = p.H;
   const unsigned long long step = p.ctrl[0];
 
@@ -314,29 +315,40 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
   float eA_b = 0.f, eA_val = 0.f, eA_rs = 0.f, eB_b = 0.f, eB_val = 0.f, eB_rs = 0.f;
   float4 w[RPW];              // lane L: prices[ps + 4L .. ps + 4L + 3] of each of the wave's rows
   float wl = 0.f, wv = 0.f;   // lane rr < RPW: prices[pos + H - 1] and prices[pos + H] of row rr
+// All gather loads are unconditional (chunk and lane indices clamped instead of branched on):
+// exec-masked loads merge with the destination's old value, and the compiler then has to
+// drain vmcnt before reusing the register - which serialised the whole prefetch.
 #define ST_LOAD_ENV(CH, POS, B, SH, VAL, RS, EP)                           \
-  if ((CH) < nchunks && lane < RPW) {                                      \
-    const int e_ = (CH) * C + wave * RPW + lane;                           \
+  {                                                                        \
+    const int ch_ = min((CH), nchunks - 1);                                \
+    const int e_ = ch_ * C + wave * RPW + min(lane, RPW - 1);              \
     POS = p.pos[e_]; B = p.budget[e_]; SH = p.shares[e_];                  \
     VAL = p.value[e_]; RS = p.ret_sum[e_]; EP = p.episodes[e_];            \
   }
 // One dwordx4 per lane per row: the window [ps, ps+H] is a run of aligned float4s in the
 // shifted replica ps & 3 of the bank (1 KiB contiguous per wave-instruction, no realignment).
 #define ST_LOAD_PRICES(CH, POS)                                            \
-  if ((CH) < nchunks) {                                                    \
+  {                                                                        \
+    const int ch_ = min((CH), nchunks - 1);                                \
+    /* each lane forms its own row's 64-bit replica pointer in VALU; the   \
+       per-row loads then only readlane the two halves (no SALU chains) */ \
+    const int sh_ = (POS) & 3;                                             \
+    const size_t off_ = ((size_t)sh_ * p.E + (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1))) \
+        * p.T4 + (size_t)((POS) - sh_);                                    \
+    const unsigned long long a_ = (unsigned long long)(p.prices4 + off_);  \
+    const unsigned alo_ = (unsigned)a_, ahi_ = (unsigned)(a_ >> 32);       \
     _Pragma("unroll") for (int rr = 0; rr < RPW; ++rr) {                   \
-      const int ps_ = __builtin_amdgcn_readlane(POS, rr);                  \
-      const int sh_ = ps_ & 3;                                             \
-      const int e_ = (CH) * C + wave * RPW + rr;                           \
-      const float4* pr_ = reinterpret_cast<const float4*>(                 \
-          p.prices4 + ((size_t)sh_ * p.E + e_) * p.T4 + (ps_ - sh_));      \
-      if (lane < INP / 4) w[rr] = pr_[lane];                               \
+      const unsigned long long b_ =                                        \
+          ((unsigned long long)__builtin_amdgcn_readlane(ahi_, rr) << 32) | \
+          (unsigned)__builtin_amdgcn_readlane(alo_, rr);                   \
+      typedef float f4g_ __attribute__((ext_vector_type(4)));              \
+      const f4g_ v_ = reinterpret_cast<const __attribute__((address_space(1))) f4g_*>(b_)[lane]; \
+      w[rr] = make_float4(v_.x, v_.y, v_.z, v_.w);   /* replicas are tail-padded */ \
     }                                                                      \
-    if (lane < RPW) {                                                      \
-      const float* pl_ = p.prices + (size_t)((CH) * C + wave * RPW + lane) * p.T + (POS) + H; \
-      wl = pl_[-1];                                                        \
-      wv = pl_[0];                                                         \
-    }                                                                      \
+    const float* pl_ = p.prices +                                          \
+        (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1)) * p.T + (POS) + H; \
+    wl = pl_[-1];                                                          \
+    wv = pl_[0];                                                           \
   }
   ST_LOAD_ENV(blockIdx.x, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
   ST_LOAD_PRICES(blockIdx.x, eA_pos)

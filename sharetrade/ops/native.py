@@ -122,15 +122,17 @@ def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float,
 
 
 def replica_stride(T: int) -> int:
-    """Row stride of the shifted price replicas (multiple of 4, >= T + 32 for the aligned over-read)."""
-    return (T + 32 + 3) // 4 * 4
+    """Row stride of the shifted price replicas (multiple of 4, >= T + 64: every lane of a wave reads
+    one float4 of the window, 256 floats from its start)."""
+    return (T + 64 + 3) // 4 * 4
 
 
 def replicate4(src: torch.Tensor) -> torch.Tensor:
     """[E, T] -> [4, E, T4] shifted replicas (csrc/series.hip: replicate4)."""
     E, T = src.shape
     T4 = replica_stride(T)
-    out = torch.empty(4, E, T4, dtype=torch.float32, device=src.device)
+    flat = torch.zeros(4 * E * T4 + 64, dtype=torch.float32, device=src.device)   # +64: last row's over-read
+    out = flat[: 4 * E * T4].view(4, E, T4)
     check(lib().st_replicate4(ptr(src), ptr(out), E, T, T4, stream_handle()), "st_replicate4")
     return out
 
