@@ -266,7 +266,7 @@ struct AdamLayer {
   const float* g;       // [O, I] grad
   float* m;
   float* v;
-  const float* mask;    // [O, I] trainable mask
+  const float* mask;    // [O, I] trainable mask (null = all trainable)
   bf16_t* wb;           // [O, I] bf16 copy
   bf16_t* wbT;          // [I, O] bf16 transposed copy
   const unsigned long long* t;   // device update counter (1-based t = *t + 1): graph-replay safe
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(256) adam_tile_kernel(AdamLayer p) {
     if (o < p.O && i < p.I) {
       const size_t idx = (size_t)o * p.I + i;
       float w = p.w[idx];
-      const float mk = p.mask[idx];
+      const float mk = p.mask ? p.mask[idx] : 1.f;
       if (mk != 0.f) {
         const float g = p.g[idx] * mk;
         const float m = p.beta1 * p.m[idx] + (1.f - p.beta1) * g;

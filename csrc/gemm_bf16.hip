@@ -41,6 +41,8 @@ struct GemmArgs {
   int lda, ldb, ldo, ldoT, ldaux;
   int relu, accumulate;
   float alpha;
+  int splitk;            // EPI_F32 only: K split over splitk workgroups per tile, atomically
+                         // added into out (which then holds the prior value / zeros)
 };
 
 template <int BM, int BN>
@@ -85,11 +87,14 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   // XCD-aware tile order: neighbouring tiles (sharing A rows) on one XCD's L2
   const int ntn = p.N / BN, ntm = p.M / BM, nwg = ntn * ntm;
+  const int nsplit = p.splitk > 1 ? p.splitk : 1, ntot = nwg * nsplit;
   int bid = blockIdx.x;
   {
-    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    const int xcd = bid % 8, q = ntot / 8, r = ntot % 8;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
   }
+  const int ks = bid / nwg;   // K split (split-major: one split's tiles stay on one XCD's L2)
+  bid -= ks * nwg;
   const int tm = bid / ntn, tn = bid % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = wave >> 1, wn = wave & 1;
@@ -100,17 +105,18 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) acc[i][j] = zero4();
 
-  const int nk = p.K / GBK;
-  stage_tile<BM>(p.A, p.lda, m0, 0, buf, wave, lane);
-  stage_tile<BN>(p.B, p.ldb, n0, 0, buf + G::A_EL, wave, lane);
+  const int nk = p.K / GBK / nsplit;
+  const int kb = ks * nk * GBK;
+  stage_tile<BM>(p.A, p.lda, m0, kb, buf, wave, lane);
+  stage_tile<BN>(p.B, p.ldb, n0, kb, buf + G::A_EL, wave, lane);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     bf16_t* cur = buf + (t & 1) * G::BUF_EL;
     if (t + 1 < nk) {
       bf16_t* nxt = buf + ((t + 1) & 1) * G::BUF_EL;
-      stage_tile<BM>(p.A, p.lda, m0, (t + 1) * GBK, nxt, wave, lane);
-      stage_tile<BN>(p.B, p.ldb, n0, (t + 1) * GBK, nxt + G::A_EL, wave, lane);
+      stage_tile<BM>(p.A, p.lda, m0, kb + (t + 1) * GBK, nxt, wave, lane);
+      stage_tile<BN>(p.B, p.ldb, n0, kb + (t + 1) * GBK, nxt + G::A_EL, wave, lane);
     }
     const bf16_t* cA = cur;
     const bf16_t* cB = cur + G::A_EL;
@@ -138,14 +144,18 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < G::TN; ++j) {
         const int n = n0 + wn * G::WN + 16 * j + l16;
-        const float bb = p.bias ? p.bias[n] : 0.f;
+        const float bb = (p.bias && ks == 0) ? p.bias[n] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * G::WM + 16 * i + 4 * g4 + r;
           float v = p.alpha * acc[i][j][r] + bb;
           float* o = out + (size_t)m * p.ldo + n;
-          if (p.accumulate) v += *o;
-          *o = v;
+          if (nsplit > 1) {
+            atomicAdd(o, v);   // fp32 L2 atomic; the host zeroed out unless accumulating
+          } else {
+            if (p.accumulate) v += *o;
+            *o = v;
+          }
         }
       }
     return;
@@ -206,7 +216,7 @@ static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int nwg = (p.M / BM) * (p.N / BN);
+  const int nwg = (p.M / BM) * (p.N / BN) * (p.splitk > 1 ? p.splitk : 1);
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI>), dim3(nwg), dim3(GT), G::LDS_BYTES, s, p);
   return hipGetLastError();
 }
@@ -221,6 +231,7 @@ extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipSt
   if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
   if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
   if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return hipErrorInvalidValue;
+  if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return hipErrorInvalidValue;
 #define ST_G(BM_, BN_)                                                                   \
   switch (epi) {                                                                         \
     case 0: return st::launch_gemm<BM_, BN_, 0>(*p, stream);                             \

@@ -1,0 +1,863 @@
+// GRU(256) recurrent Q-net on minute-bar sequences (BASELINE config 5), MI355X-native.
+//
+// Not in the reference (its Q-net is a 203->200->3 MLP over a flattened 201-price
+// window, QDecisionPolicyActor.scala:38-50); this is the north-star recurrent variant
+// of the same Buy/Sell/Hold agent (action order 0,1,2 as QDecisionPolicyActor.scala:17).
+//
+// Actor (gru_act_kernel) — the fp8 MFMA path:
+//   * one workgroup = 8 waves owns a chunk of 32 envs and runs S env steps on-chip;
+//     wave w owns hidden units 32w..32w+31 of all three gates (r, z, n: torch.nn.GRUCell
+//     order), so the whole GRU update of a unit happens in the lane that holds it;
+//   * W_hh (768x256) lives in VGPRs for the life of the kernel as block-scaled MX-fp8
+//     (OCP e4m3 + one E8M0 scale per 32-element block: the gfx950 scaled MFMA
+//     v_mfma_scale_f32_16x16x128_f8f6f4, 2x the bf16 MFMA rate); W_ih (x part, K=32)
+//     is bf16 in LDS (one 16x16x32 bf16 MFMA per tile);
+//   * 16x16x128 operand layout (measured, tools/mx_layout_probe.py): lane l = i + 16g holds
+//     row/col i, K = [16g, 16g+16) in bytes 0..15 and [64+16g, 64+16g+16) in bytes 16..31;
+//     the E8M0 scale of (row i, K-block s = [32s, 32s+32)) is read from lane i + 16s --
+//     so a lane's scale is NOT the scale of its own bytes;
+//   * h is fp32 in registers (exact recurrence) and is re-quantized every step into an
+//     LDS fp8 tile with per-(env, 32-unit block) E8M0 scales -- each scale block is
+//     exactly one wave's unit range, so amax is a 4-lane reduction;
+//   * Q = W_q h is reduced across waves through LDS; wave 0 runs epsilon-greedy
+//     (Philox), the minute-bar trading env, and writes the replay segment.
+// Learner: bf16 MFMA GEMMs (gemm_bf16.hip) for the gate products + the fused
+// elementwise kernels below (forward with saves, TD, backward-through-time).
+#include "common.h"
+
+namespace st {
+
+typedef int i8v __attribute__((ext_vector_type(8)));   // 32 fp8 bytes: one MX A/B fragment
+
+constexpr int RH = 256;            // hidden units
+constexpr int RG = 3 * RH;         // gate rows
+constexpr int RF = 32;             // actor x width (bf16, one K=32 MFMA step)
+constexpr int RFL = 64;            // learner x width (GEMM K multiple of 64)
+constexpr int RMF = 8;             // market features per bar
+constexpr int RW = 8;              // waves per actor workgroup
+constexpr int RN = 32;             // envs per actor chunk
+constexpr int RT = RW * 64;
+constexpr int XS = RF + 8;         // sX row stride (bf16) = 80 B: conflict-free ds_read_b128
+constexpr int HS = RH + 16;        // sH8 row stride (bytes) = 272 B
+constexpr int SCS = 9;             // scale row stride (ints)
+
+// ---------------------------------------------------------------- MX-fp8 helpers
+ST_DEV f4v mx_mfma(const i8v& a, const i8v& b, f4v c, int sa, int sb) {
+  // fmt 0/0 = e4m3 x e4m3; scales are E8M0 bytes (byte 0 of sa / sb)
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+// same, with the A scale taken from byte SEL of a packed register (op_sel), 4 scales per VGPR
+template <int SEL>
+ST_DEV f4v mx_mfma_sel(const i8v& a, const i8v& b, f4v c, int sa4, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, SEL, sa4, 0, sb);
+}
+// smallest e with amax / 2^e <= 448 (e4m3 max): e = ceil(log2(amax / 448))
+ST_DEV int mx_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int e;
+  const float m = frexpf(amax * (1.0f / 448.0f), &e);
+  if (m == 0.5f) e -= 1;
+  if (ldexpf(amax, -e) > 448.f) e += 1;
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+ST_DEV uint32_t fp8x4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+ST_DEV float sigm(float x) { return __frcp_rn(1.f + __expf(-x)); }
+ST_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
+
+// ---------------------------------------------------------------- synthetic minute bars
+struct MinuteBars {
+  float* close;        // [E][T]
+  bf16_t* feat;        // [E][T][RMF]
+  int E, T, day;       // bars per session (U-shaped intraday volatility / volume)
+  float sigma, phi, alpha, beta, p0;
+  uint32_t key0, key1;
+};
+
+// one thread per env, sequential over time: AR(1) log returns with GARCH(1,1) variance
+// and a U-shaped intraday profile; OHLC + volume -> 8 features per bar.
+__global__ void __launch_bounds__(256) minute_bars_kernel(MinuteBars g) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.E) return;
+  uint32_t c0 = (uint32_t)e, c1 = 0xFFFFFFFFu, c2 = 0u, c3 = 0x4D424152u;
+  philox4x32(c0, c1, c2, c3, g.key0, g.key1);
+  float c = g.p0 * (0.5f + u24(c0));
+  float var = g.sigma * g.sigma, rprev = 0.f;
+  const float omega = g.sigma * g.sigma * (1.f - g.alpha - g.beta);
+  float r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f;   // previous 4 returns (5-bar momentum)
+  for (int t = 0; t < g.T; ++t) {
+    uint32_t a0 = (uint32_t)e, a1 = (uint32_t)t, a2 = 0u, a3 = 0x4D424152u;
+    philox4x32(a0, a1, a2, a3, g.key0, g.key1);
+    const float u0 = fmaxf(u24(a0), 1e-7f), u1 = u24(a1), u2 = fmaxf(u24(a2), 1e-7f), u3 = u24(a3);
+    const float rad0 = sqrtf(-2.f * logf(u0)), rad1 = sqrtf(-2.f * logf(u2));
+    const float n1 = rad0 * cosf(6.2831853f * u1), n2 = rad0 * sinf(6.2831853f * u1);
+    const float n3 = rad1 * cosf(6.2831853f * u3), n4 = rad1 * sinf(6.2831853f * u3);
+    const int tod = t % g.day;
+    const float x = (2.f * (float)tod / (float)g.day) - 1.f;
+    const float ush = 1.f + 0.8f * x * x;
+    const float sig = sqrtf(var) * ush;
+    const float ret = g.phi * rprev + sig * n1;
+    const float open = c;
+    c = open * expf(ret);
+    const float hi = fmaxf(open, c) * expf(0.5f * sig * fabsf(n2));
+    const float lo = fminf(open, c) * expf(-0.5f * sig * fabsf(n3));
+    const float vol = expf(0.5f * n4) * ush;
+    const float dsr = ret / ush;   // de-seasonalised: the U-shape must not feed the GARCH recursion
+    var = omega + g.alpha * dsr * dsr + g.beta * var;
+    const float mom = ret + r1 + r2 + r3 + r4;
+    r4 = r3; r3 = r2; r2 = r1; r1 = ret;
+    rprev = ret;
+    const float ang = 6.2831853f * (float)tod / (float)g.day;
+    const size_t o = (size_t)e * g.T + t;
+    g.close[o] = c;
+    uint4 w;
+    w.x = pack_bf2(ret * 100.f, (hi - lo) / c * 100.f);
+    w.y = pack_bf2((c - lo) / fmaxf(hi - lo, 1e-12f) - 0.5f, logf(vol));
+    w.z = pack_bf2(sinf(ang), cosf(ang));
+    w.w = pack_bf2(mom * 100.f, sig * 100.f);
+    *reinterpret_cast<uint4*>(g.feat + o * RMF) = w;
+  }
+}
+
+// ---------------------------------------------------------------- actor weight packing
+struct GruPack {
+  const float* w_hh;   // [RG][RH] fp32 master
+  const float* w_ih;   // [RG][RFL] fp32 master (the actor uses the first RF columns)
+  const float* b_ih;
+  const float* b_hh;   // [RG]
+  const float* w_q;    // [3][RH]
+  const float* b_q;    // [3]
+  i8v* whh8;           // [RW][3][2][2][64] fragments
+  int* whhs;           // [RW][3][2][2][64] E8M0 scales (byte 0)
+  s8v* wih;            // [RW][3][2][64]
+  float* bias4;        // [4][RH]: b_ir+b_hr, b_iz+b_hz, b_in, b_hn
+  float* wq;           // [4][RH]: W_q rows, row 3 = b_q (first 3 entries)
+};
+
+// one thread per (wave, gate, m-tile, k-step, lane) fragment
+__global__ void __launch_bounds__(256) gru_pack_kernel(GruPack p) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid < RH) {
+    const int u = tid;
+    p.bias4[u] = p.b_ih[u] + p.b_hh[u];
+    p.bias4[RH + u] = p.b_ih[RH + u] + p.b_hh[RH + u];
+    p.bias4[2 * RH + u] = p.b_ih[2 * RH + u];
+    p.bias4[3 * RH + u] = p.b_hh[2 * RH + u];
+    for (int a = 0; a < 3; ++a) p.wq[a * RH + u] = p.w_q[a * RH + u];
+    p.wq[3 * RH + u] = u < 3 ? p.b_q[u] : 0.f;
+  }
+  if (tid >= RW * 3 * 2 * 2 * 64) return;
+  const int lane = tid & 63, f = tid >> 6;
+  const int ks = f & 1, m = (f >> 1) & 1, g = (f >> 2) % 3, w = (f >> 2) / 3;
+  const int row = g * RH + 32 * w + 16 * m + (lane & 15);
+  const int gl = lane >> 4;
+  const float* wr = p.w_hh + (size_t)row * RH + 128 * ks;
+  // block exponent of K-block b (32 columns) of this row within the K step
+  auto blk_e = [&](int b) {
+    float amax = 0.f;
+    for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(wr[32 * b + j]));
+    return mx_exp(amax);
+  };
+  const int e_lo = blk_e(gl >> 1), e_hi = blk_e(2 + (gl >> 1));   // blocks of this lane's two 16-byte halves
+  const float* lo = wr + 16 * gl;
+  const float* hi = wr + 64 + 16 * gl;
+  i8v frag;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    frag[j] = (int)fp8x4(ldexpf(lo[4 * j], -e_lo), ldexpf(lo[4 * j + 1], -e_lo), ldexpf(lo[4 * j + 2], -e_lo),
+                         ldexpf(lo[4 * j + 3], -e_lo));
+    frag[4 + j] = (int)fp8x4(ldexpf(hi[4 * j], -e_hi), ldexpf(hi[4 * j + 1], -e_hi), ldexpf(hi[4 * j + 2], -e_hi),
+                             ldexpf(hi[4 * j + 3], -e_hi));
+  }
+  p.whh8[tid] = frag;
+  p.whhs[tid] = blk_e(gl) + 127;      // the scale slot of lane i + 16g belongs to K-block g
+  if (ks == 0) {
+    s8v x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (short)f2bf(p.w_ih[(size_t)row * RFL + 8 * (lane >> 4) + j]);
+    p.wih[((w * 3 + g) * 2 + m) * 64 + lane] = x;
+  }
+}
+
+// ---------------------------------------------------------------- actor
+struct GruAct {
+  const i8v* whh8;
+  const int* whhs;
+  const s8v* wih;
+  const float* bias4;
+  const float* wq;
+  const bf16_t* feat;          // [E][T][RMF]
+  const float* close;          // [E][T]
+  int E, T, S, ep_len;
+  float eps, inv_ramp, cost;
+  float* h;                    // [E][RH] fp32 recurrent state between launches
+  int* pos;                    // [E] bar index
+  int* ep_start;
+  int* position;               // 0 flat / 1 long
+  float* entry;
+  float* ep_ret;
+  int* episodes;
+  float* last_ret;
+  // replay: one segment (S steps) per env per launch
+  bf16_t* rx;                  // [cap][S+1][RF]
+  unsigned char* ra;           // [cap][S]
+  float* rr;                   // [cap][S]
+  unsigned char* rd;           // [cap][S]
+  bf16_t* rh0;                 // [cap][RH]
+  unsigned long long* rctrl;   // [0] segments written (monotonic), [1] size
+  int cap;
+  uint32_t key0, key1;
+  unsigned long long* ctrl;    // [0] actor launches so far
+  float* stats;                // [4] reward sum, explore count, episodes done, finished-episode return sum
+  float* q_out;                // optional [E][4]: Q of the last step (tests)
+};
+
+struct ActLds {
+  static constexpr int WX = 0;                                   // RW*6*64 s8v
+  static constexpr int X = WX + RW * 6 * 64 * 16;                // [2][RN*XS] bf16
+  static constexpr int H8 = X + 2 * RN * XS * 2;                 // [2][RN*HS] bytes
+  static constexpr int SC = H8 + 2 * RN * HS;                    // [2][RN*SCS] int
+  static constexpr int B = SC + 2 * RN * SCS * 4;                // [4*RH] float
+  static constexpr int WQ = B + 4 * RH * 4;                      // [4*RH] float
+  static constexpr int QP = WQ + 4 * RH * 4;                     // [RW][3][RN] float
+  static constexpr int DN = QP + RW * 3 * RN * 4;                // [RN] int
+  static constexpr int BYTES = DN + RN * 4;
+};
+static_assert(ActLds::BYTES <= 160 * 1024, "actor LDS");
+
+// quantize the lane's h values (units of this wave, 2 env tiles) into an LDS fp8 tile
+ST_DEV void quant_h(const float (&hr)[2][2][4], unsigned char* sH8, int* sSc, int wave, int l16, int g4) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    float amax = 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(hr[m][n][i]));
+    amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+    const int e = mx_exp(amax);
+    const int row = 16 * n + l16;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      *reinterpret_cast<uint32_t*>(sH8 + row * HS + 32 * wave + 16 * m + 4 * g4) =
+          fp8x4(ldexpf(hr[m][n][0], -e), ldexpf(hr[m][n][1], -e), ldexpf(hr[m][n][2], -e), ldexpf(hr[m][n][3], -e));
+    if (g4 == 0) sSc[row * SCS + wave] = e + 127;
+  }
+}
+
+// build the x row (bf16 [RF]) from bar features mf / close c into LDS and (if rx_row) the replay segment
+ST_DEV void build_x(const GruAct& p, uint4 mf, float c, int t, int es, int pz, float entry, bf16_t* sx_row,
+                    bf16_t* rx_row) {
+  const float upnl = pz ? (c / entry - 1.f) * 100.f : 0.f;
+  uint4 w1;
+  w1.x = pack_bf2((float)pz, upnl);
+  w1.y = pack_bf2((float)(t - es) / (float)p.ep_len, 1.f);
+  w1.z = 0u;
+  w1.w = 0u;
+  const uint4 z = {0u, 0u, 0u, 0u};
+  uint4* d = reinterpret_cast<uint4*>(sx_row);
+  d[0] = mf; d[1] = w1; d[2] = z; d[3] = z;
+  if (rx_row) {
+    uint4* r = reinterpret_cast<uint4*>(rx_row);
+    r[0] = mf; r[1] = w1; r[2] = z; r[3] = z;
+  }
+}
+ST_DEV uint4 bar_feat(const GruAct& p, int e, int t) {
+  return *reinterpret_cast<const uint4*>(p.feat + ((size_t)e * p.T + t) * RMF);
+}
+
+__global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const s8v* sWx = reinterpret_cast<const s8v*>(lds + ActLds::WX);
+  bf16_t* sX = reinterpret_cast<bf16_t*>(lds + ActLds::X);
+  unsigned char* sH8 = lds + ActLds::H8;
+  int* sSc = reinterpret_cast<int*>(lds + ActLds::SC);
+  float* sB = reinterpret_cast<float*>(lds + ActLds::B);
+  float* sWq = reinterpret_cast<float*>(lds + ActLds::WQ);
+  float* sQp = reinterpret_cast<float*>(lds + ActLds::QP);
+  int* sDone = reinterpret_cast<int*>(lds + ActLds::DN);
+
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < RW * 6 * 64; i += RT) reinterpret_cast<s8v*>(lds + ActLds::WX)[i] = p.wih[i];
+  for (int i = tid; i < 4 * RH; i += RT) {
+    sB[i] = p.bias4[i];
+    sWq[i] = p.wq[i];
+  }
+  // resident MX-fp8 W_hh fragments of this wave's 32 units x 3 gates (96 VGPRs + 12 scales)
+  i8v Wh[3][2][2];
+  int Ws4[3] = {0, 0, 0};   // 12 E8M0 scales packed 4 per VGPR: (g, m, ks) -> reg g, byte 2m + ks
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int idx = (((wave * 3 + g) * 2 + m) * 2 + ks) * 64 + lane;
+        Wh[g][m][ks] = p.whh8[idx];
+        Ws4[g] |= (p.whhs[idx] & 0xFF) << (8 * (2 * m + ks));
+      }
+  const s8v* myWx = sWx + wave * 6 * 64 + lane;
+  const unsigned long long launch = p.ctrl[0];
+  const unsigned long long seg0 = p.rctrl[0];
+  const int nchunks = p.E / RN, S = p.S;
+  __syncthreads();
+
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int e0 = chunk * RN;
+    float hr[2][2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int e = e0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
+        const float4 v = *reinterpret_cast<const float4*>(p.h + (size_t)e * RH + u0);
+        hr[m][n][0] = v.x; hr[m][n][1] = v.y; hr[m][n][2] = v.z; hr[m][n][3] = v.w;
+        const size_t slot = (size_t)((seg0 + (unsigned long long)e) % (unsigned long long)p.cap);
+        lds_st4(p.rh0 + slot * RH + u0, v.x, v.y, v.z, v.w);   // 8-byte global store of h0 (bf16)
+      }
+    quant_h(hr, sH8, sSc, wave, l16, g4);
+    // env state lives in wave 0: lane l and l + 32 both carry env e0 + (l & 31) (the upper half
+    // mirrors the lower one so every load is unconditional; only lanes < RN store)
+    int t_ = 0, es_ = 0, pz_ = 0, eps_ = 0;
+    float en_ = 0.f, er_ = 0.f, lr_ = 0.f;
+    float cA = 0.f, cB = 0.f;      // close[t], close[t+1] (prefetched one env phase ahead)
+    uint4 fB = {0u, 0u, 0u, 0u};   // features of bar t+1
+    float st_rew = 0.f, st_exp = 0.f, st_fin = 0.f, st_dn = 0.f;
+    size_t slot_ = 0;
+    const int me = e0 + (lane & (RN - 1));
+    const bool writer = lane < RN;
+    if (wave == 0) {
+      t_ = p.pos[me]; es_ = p.ep_start[me]; pz_ = p.position[me]; en_ = p.entry[me]; er_ = p.ep_ret[me];
+      eps_ = p.episodes[me]; lr_ = p.last_ret[me];
+      slot_ = (size_t)((seg0 + (unsigned long long)me) % (unsigned long long)p.cap);
+      const size_t o = (size_t)me * p.T + t_;
+      cA = p.close[o];
+      cB = p.close[o + 1];
+      fB = bar_feat(p, me, t_ + 1);
+      const uint4 f0 = bar_feat(p, me, t_);
+      if (writer) build_x(p, f0, cA, t_, es_, pz_, en_, sX + lane * XS, p.rx + slot_ * (size_t)(S + 1) * RF);
+    }
+    __syncthreads();
+
+    for (int s = 0; s < S; ++s) {
+      const int cur = s & 1, nxt = cur ^ 1;
+      const bf16_t* cX = sX + cur * RN * XS;
+      const unsigned char* cH = sH8 + cur * RN * HS;
+      const int* cS = sSc + cur * RN * SCS;
+      // one 16-env tile at a time keeps the accumulators at 32 VGPRs (W_hh holds 108)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        f4v ar[2], az[2], anx[2], anh[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) { ar[m] = zero4(); az[m] = zero4(); anx[m] = zero4(); anh[m] = zero4(); }
+        const int row = 16 * n + l16;
+        // x part: bf16 16x16x32 (W_ih fragments from LDS)
+        {
+          const s8v xb = lds_ld8(cX + row * XS + 8 * g4);
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            ar[m] = mfma32(myWx[(0 * 2 + m) * 64], xb, ar[m]);
+            az[m] = mfma32(myWx[(1 * 2 + m) * 64], xb, az[m]);
+            anx[m] = mfma32(myWx[(2 * 2 + m) * 64], xb, anx[m]);
+          }
+        }
+        // h part: MX-fp8 16x16x128, two K steps over the 256 hidden units
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          // bytes 0..15: units 128ks + 16g4 + [0,16); bytes 16..31: units 128ks + 64 + 16g4 + [0,16)
+          const uint4 h0 = *reinterpret_cast<const uint4*>(cH + row * HS + 128 * ks + 16 * g4);
+          const uint4 h1 = *reinterpret_cast<const uint4*>(cH + row * HS + 128 * ks + 64 + 16 * g4);
+          i8v hb;
+          hb[0] = (int)h0.x; hb[1] = (int)h0.y; hb[2] = (int)h0.z; hb[3] = (int)h0.w;
+          hb[4] = (int)h1.x; hb[5] = (int)h1.y; hb[6] = (int)h1.z; hb[7] = (int)h1.w;
+          const int sc = cS[row * SCS + 4 * ks + g4];   // scale of K-block g4 = units of wave 4ks + g4
+#define ST_MX3(M, KS)                                                              \
+  ar[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[0][M][KS], hb, ar[M], Ws4[0], sc);          \
+  az[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[1][M][KS], hb, az[M], Ws4[1], sc);          \
+  anh[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[2][M][KS], hb, anh[M], Ws4[2], sc);
+          if (ks == 0) { ST_MX3(0, 0) ST_MX3(1, 0) } else { ST_MX3(0, 1) ST_MX3(1, 1) }
+#undef ST_MX3
+        }
+        // GRU update in registers (lane: units u0..u0+3 of tile m, env 16n + l16)
+        float qa0 = 0.f, qa1 = 0.f, qa2 = 0.f;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int u0 = 32 * wave + 16 * m + 4 * g4;
+          const f4v br = *reinterpret_cast<const f4v*>(sB + u0);
+          const f4v bz = *reinterpret_cast<const f4v*>(sB + RH + u0);
+          const f4v bi = *reinterpret_cast<const f4v*>(sB + 2 * RH + u0);
+          const f4v bh = *reinterpret_cast<const f4v*>(sB + 3 * RH + u0);
+          const f4v w0 = *reinterpret_cast<const f4v*>(sWq + u0);
+          const f4v w1 = *reinterpret_cast<const f4v*>(sWq + RH + u0);
+          const f4v w2 = *reinterpret_cast<const f4v*>(sWq + 2 * RH + u0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float r = sigm(ar[m][i] + br[i]);
+            const float z = sigm(az[m][i] + bz[i]);
+            const float nn = tanh_f(anx[m][i] + bi[i] + r * (anh[m][i] + bh[i]));
+            const float hv = nn + z * (hr[m][n][i] - nn);
+            hr[m][n][i] = hv;
+            qa0 += w0[i] * hv;
+            qa1 += w1[i] * hv;
+            qa2 += w2[i] * hv;
+          }
+        }
+        // Q partials over this wave's units, reduced across the 4 lane groups
+        qa0 += __shfl_xor(qa0, 16, 64); qa0 += __shfl_xor(qa0, 32, 64);
+        qa1 += __shfl_xor(qa1, 16, 64); qa1 += __shfl_xor(qa1, 32, 64);
+        qa2 += __shfl_xor(qa2, 16, 64); qa2 += __shfl_xor(qa2, 32, 64);
+        if (g4 == 0) {
+          sQp[(wave * 3 + 0) * RN + row] = qa0;
+          sQp[(wave * 3 + 1) * RN + row] = qa1;
+          sQp[(wave * 3 + 2) * RN + row] = qa2;
+        }
+      }
+      quant_h(hr, sH8 + nxt * RN * HS, sSc + nxt * RN * SCS, wave, l16, g4);
+      __syncthreads();
+      // ---------------------------------------------------------- env step (wave 0)
+      if (wave == 0) {
+        float q[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          float v = sWq[3 * RH + a];
+#pragma unroll
+          for (int w = 0; w < RW; ++w) v += sQp[(w * 3 + a) * RN + (lane & (RN - 1))];
+          q[a] = v;
+        }
+        int greedy = 0;
+        if (q[1] > q[greedy]) greedy = 1;
+        if (q[2] > q[greedy]) greedy = 2;
+        const unsigned long long step = launch * (unsigned long long)S + (unsigned long long)s;
+        uint32_t c0 = (uint32_t)me, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32),
+                 c3 = 0x47525531u;
+        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+        const bool exploit = u24(c0) < fminf(p.eps, (float)step * p.inv_ramp);
+        const int rnd = min((int)(u24(c1) * 3.0f), 2);
+        const int a = exploit ? greedy : rnd;
+        const float c_t = cA, c_n = cB;
+        const int np = a == 0 ? 1 : (a == 1 ? 0 : pz_);
+        const bool trade = np != pz_;
+        if (trade && np == 1) en_ = c_t;
+        const float rew = (float)np * (c_n / c_t - 1.f) * 100.f - (trade ? p.cost : 0.f);
+        er_ += rew;
+        int t1 = t_ + 1;
+        const bool done = (t1 - es_) >= p.ep_len;
+        float fin = 0.f;
+        if (done) {
+          eps_ += 1;
+          lr_ = er_;
+          fin = er_;
+          es_ = min((int)(u24(c2) * (float)(p.T - p.ep_len - 1)), p.T - p.ep_len - 2);
+          t1 = es_;
+          pz_ = 0;
+          er_ = 0.f;
+        } else {
+          pz_ = np;
+        }
+        t_ = t1;
+        // bar t1's features: prefetched unless the episode restarted (rare: load now)
+        uint4 fx = fB;
+        float cx = cB;
+        if (__builtin_amdgcn_ballot_w64(done) != 0ull) {
+          const uint4 fr = bar_feat(p, me, t_);
+          const float cr = p.close[(size_t)me * p.T + t_];
+          fx = done ? fr : fx;
+          cx = done ? cr : cx;
+        }
+        if (writer) {
+          p.ra[slot_ * S + s] = (unsigned char)a;
+          p.rr[slot_ * S + s] = rew;
+          p.rd[slot_ * S + s] = done ? 1 : 0;
+          build_x(p, fx, cx, t_, es_, pz_, en_, sX + nxt * RN * XS + lane * XS,
+                  p.rx + (slot_ * (size_t)(S + 1) + (size_t)(s + 1)) * RF);
+          sDone[lane] = done ? 1 : 0;
+          if (done) {   // the next step starts from h = 0
+            uint4* hz = reinterpret_cast<uint4*>(sH8 + nxt * RN * HS + lane * HS);
+            const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < RH / 16; ++j) hz[j] = z;
+          }
+          if (p.q_out && s == S - 1) {
+            float* qo = p.q_out + (size_t)me * 4;
+            qo[0] = q[0]; qo[1] = q[1]; qo[2] = q[2]; qo[3] = (float)a;
+          }
+          st_rew += rew;
+          st_exp += exploit ? 0.f : 1.f;
+          st_fin += fin;
+          st_dn += done ? 1.f : 0.f;
+        }
+        // prefetch bar t1+1 for the next env phase (issued last: a whole MFMA phase to land)
+        cA = cx;
+        const size_t o1 = (size_t)me * p.T + min(t_ + 1, p.T - 1);
+        cB = p.close[o1];
+        fB = *reinterpret_cast<const uint4*>(p.feat + o1 * RMF);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        if (sDone[16 * n + l16]) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) hr[m][n][i] = 0.f;
+        }
+    }
+    // write back
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int e = e0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
+        *reinterpret_cast<float4*>(p.h + (size_t)e * RH + u0) =
+            make_float4(hr[m][n][0], hr[m][n][1], hr[m][n][2], hr[m][n][3]);
+      }
+    if (wave == 0) {
+      st_rew = wave_sum(st_rew);
+      st_exp = wave_sum(st_exp);
+      st_fin = wave_sum(st_fin);
+      st_dn = wave_sum(st_dn);
+      if (lane == 0) {
+        atomicAdd(p.stats + 0, st_rew);
+        atomicAdd(p.stats + 1, st_exp);
+        atomicAdd(p.stats + 2, st_dn);
+        atomicAdd(p.stats + 3, st_fin);
+      }
+    }
+    if (wave == 0 && writer) {
+      p.pos[me] = t_; p.ep_start[me] = es_; p.position[me] = pz_; p.entry[me] = en_; p.ep_ret[me] = er_;
+      p.episodes[me] = eps_; p.last_ret[me] = lr_;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void gru_advance_kernel(unsigned long long* rctrl, unsigned long long* ctrl, int E, int cap) {
+  rctrl[0] += (unsigned long long)E;
+  rctrl[1] = rctrl[0] < (unsigned long long)cap ? rctrl[0] : (unsigned long long)cap;
+  ctrl[0] += 1;
+}
+
+// ---------------------------------------------------------------- learner: sequence gather
+struct GruGather {
+  const bf16_t* rx;
+  const unsigned char* ra;
+  const float* rr;
+  const unsigned char* rd;
+  const bf16_t* rh0;
+  const unsigned long long* rctrl;
+  int cap, S, B;
+  uint32_t key0, key1;
+  const unsigned long long* step;   // update counter (device)
+  bf16_t* X;         // [(S+1)B][RFL] time-major rows t*B + b
+  bf16_t* Hm;        // [(S+1)B][RH] block 0 <- h0
+  bf16_t* Hm_t;      // target copy of block 0
+  float* Hf;         // [B][RH]
+  float* Hf_t;       // [B][RH]
+  int* A;            // [S][B]
+  float* R;
+  float* D;
+};
+
+// one wave per sampled segment
+__global__ void __launch_bounds__(256) gru_gather_kernel(GruGather g) {
+  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (b >= g.B) return;
+  const unsigned long long sz = g.rctrl[1], st = g.step[0];
+  uint32_t c0 = (uint32_t)b, c1 = (uint32_t)(st & 0xFFFFFFFFull), c2 = (uint32_t)(st >> 32), c3 = 0x53455131u;
+  philox4x32(c0, c1, c2, c3, g.key0, g.key1);
+  const size_t idx = (size_t)(((((unsigned long long)c0) << 32) | c1) % (sz ? sz : 1ull));
+  const int S = g.S;
+  const uint4 z = {0u, 0u, 0u, 0u};
+  for (int j = lane; j < (S + 1) * 8; j += 64) {
+    const int t = j >> 3, c = j & 7;
+    uint4 v = z;
+    if (c < RF / 8) v = reinterpret_cast<const uint4*>(g.rx + (idx * (size_t)(S + 1) + t) * RF)[c];
+    reinterpret_cast<uint4*>(g.X + ((size_t)t * g.B + b) * RFL)[c] = v;
+  }
+  {
+    const s4v hv = *reinterpret_cast<const s4v*>(g.rh0 + idx * RH + 4 * lane);
+    *reinterpret_cast<s4v*>(g.Hm + (size_t)b * RH + 4 * lane) = hv;
+    *reinterpret_cast<s4v*>(g.Hm_t + (size_t)b * RH + 4 * lane) = hv;
+    const float4 f = make_float4(bf2f((bf16_t)hv[0]), bf2f((bf16_t)hv[1]), bf2f((bf16_t)hv[2]), bf2f((bf16_t)hv[3]));
+    *reinterpret_cast<float4*>(g.Hf + (size_t)b * RH + 4 * lane) = f;
+    *reinterpret_cast<float4*>(g.Hf_t + (size_t)b * RH + 4 * lane) = f;
+  }
+  if (lane < S) {
+    g.A[(size_t)lane * g.B + b] = g.ra[idx * S + lane];
+    g.R[(size_t)lane * g.B + b] = g.rr[idx * S + lane];
+    g.D[(size_t)lane * g.B + b] = (float)g.rd[idx * S + lane];
+  }
+}
+
+// ---------------------------------------------------------------- learner: forward step
+struct GruFwd {
+  const float* Gx;    // [(S+1)B][RG] (x . W_ih^T + b_ih)
+  const float* Gh;    // [B][RG]      (h . W_hh^T + b_hh) of this step
+  float* Hf;          // [B][RH] in: masked h_{t-1}; out: masked h_t
+  bf16_t* Hm;         // [(S+1)B][RH]: row (t+1)B + b <- masked h_t (t < S)
+  const float* wq;    // [3][RH]
+  const float* bq;    // [3]
+  float* Q;           // [(S+1)B][4]
+  const float* D;     // [S][B]
+  float* sr;          // saves for the backward pass (online net, t < S) or null
+  float* sz;
+  float* sn;
+  float* sgh;
+  float* shp;
+  bf16_t* Hq;         // [S*B][RH] unmasked h_t (W_q gradient)
+  int B, S, t;
+};
+
+// one wave per batch row; lane owns units 4l..4l+3
+__global__ void __launch_bounds__(256) gru_fwd_kernel(GruFwd f) {
+  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (b >= f.B) return;
+  const int u = 4 * lane;
+  const size_t row = (size_t)f.t * f.B + b;
+  const float* gx = f.Gx + row * RG;
+  const float* gh = f.Gh + (size_t)b * RG;
+  const float4 xr = *reinterpret_cast<const float4*>(gx + u), xz = *reinterpret_cast<const float4*>(gx + RH + u),
+               xn = *reinterpret_cast<const float4*>(gx + 2 * RH + u);
+  const float4 hr_ = *reinterpret_cast<const float4*>(gh + u), hz_ = *reinterpret_cast<const float4*>(gh + RH + u),
+               hn_ = *reinterpret_cast<const float4*>(gh + 2 * RH + u);
+  const float4 hp4 = *reinterpret_cast<const float4*>(f.Hf + (size_t)b * RH + u);
+  const float ax[4] = {xr.x, xr.y, xr.z, xr.w}, az_[4] = {xz.x, xz.y, xz.z, xz.w}, an[4] = {xn.x, xn.y, xn.z, xn.w};
+  const float bx[4] = {hr_.x, hr_.y, hr_.z, hr_.w}, bz_[4] = {hz_.x, hz_.y, hz_.z, hz_.w},
+              bn[4] = {hn_.x, hn_.y, hn_.z, hn_.w};
+  const float hp[4] = {hp4.x, hp4.y, hp4.z, hp4.w};
+  float r[4], z[4], n[4], h[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r[i] = 1.f / (1.f + expf(-(ax[i] + bx[i])));
+    z[i] = 1.f / (1.f + expf(-(az_[i] + bz_[i])));
+    n[i] = tanhf(an[i] + r[i] * bn[i]);
+    h[i] = (1.f - z[i]) * n[i] + z[i] * hp[i];
+  }
+  float q[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float4 w = *reinterpret_cast<const float4*>(f.wq + a * RH + u);
+    q[a] = wave_sum(w.x * h[0] + w.y * h[1] + w.z * h[2] + w.w * h[3]);
+  }
+  if (lane == 0) {
+    float* qo = f.Q + row * 4;
+    qo[0] = q[0] + f.bq[0]; qo[1] = q[1] + f.bq[1]; qo[2] = q[2] + f.bq[2]; qo[3] = 0.f;
+  }
+  if (f.t < f.S) {
+    if (f.sr) {
+      const size_t o = row * RH + u;
+      *reinterpret_cast<float4*>(f.sr + o) = make_float4(r[0], r[1], r[2], r[3]);
+      *reinterpret_cast<float4*>(f.sz + o) = make_float4(z[0], z[1], z[2], z[3]);
+      *reinterpret_cast<float4*>(f.sn + o) = make_float4(n[0], n[1], n[2], n[3]);
+      *reinterpret_cast<float4*>(f.sgh + o) = make_float4(bn[0], bn[1], bn[2], bn[3]);
+      *reinterpret_cast<float4*>(f.shp + o) = make_float4(hp[0], hp[1], hp[2], hp[3]);
+      lds_st4(f.Hq + o, h[0], h[1], h[2], h[3]);
+    }
+    const float keep = 1.f - f.D[row];
+    float hm[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hm[i] = keep * h[i];
+    *reinterpret_cast<float4*>(f.Hf + (size_t)b * RH + u) = make_float4(hm[0], hm[1], hm[2], hm[3]);
+    lds_st4(f.Hm + (row + f.B) * RH + u, hm[0], hm[1], hm[2], hm[3]);
+  }
+}
+
+// ---------------------------------------------------------------- learner: TD targets (double DQN)
+struct GruTD {
+  const float* Q;     // [(S+1)B][4] online
+  const float* Qt;    // [(S+1)B][4] target net
+  const int* A;
+  const float* R;
+  const float* D;     // [S][B]
+  float* dQ;          // [S*B][4]
+  float* loss;        // [1] (atomic)
+  int B, S, burn;
+  float gamma, coef;
+};
+
+__global__ void __launch_bounds__(256) gru_td_kernel(GruTD p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (i < p.S * p.B) {
+    const int t = i / p.B;
+    const float* qn = p.Q + ((size_t)i + p.B) * 4;
+    int as = 0;
+    if (qn[1] > qn[as]) as = 1;
+    if (qn[2] > qn[as]) as = 2;
+    const float y = p.R[i] + p.gamma * (1.f - p.D[i]) * p.Qt[((size_t)i + p.B) * 4 + as];
+    const int a = p.A[i];
+    const float d = p.Q[(size_t)i * 4 + a] - y;
+    const bool on = t >= p.burn;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (on) {
+      const float v = p.coef * d;
+      if (a == 0) g.x = v; else if (a == 1) g.y = v; else g.z = v;
+      l = d * d;
+    }
+    *reinterpret_cast<float4*>(p.dQ + (size_t)i * 4) = g;
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) atomicAdd(p.loss, l);
+}
+
+// ---------------------------------------------------------------- learner: backward step
+struct GruBwd {
+  const float* dQ;    // [S*B][4]
+  const float* D;     // [S][B]
+  float* DH;          // [B][RH]: in dL/d(masked h_t) from step t+1; out: direct part of dL/dh_{t-1}
+  const float* sr;
+  const float* sz;
+  const float* sn;
+  const float* sgh;
+  const float* shp;
+  const float* wq;    // [3][RH]
+  bf16_t* dGx;        // [S*B][RG]
+  bf16_t* dGh;        // [S*B][RG]
+  int B, S, t;
+};
+
+__global__ void __launch_bounds__(256) gru_bwd_kernel(GruBwd p) {
+  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (b >= p.B) return;
+  const int u = 4 * lane;
+  const size_t row = (size_t)p.t * p.B + b, o = row * RH + u;
+  const float4 dq = *reinterpret_cast<const float4*>(p.dQ + row * 4);
+  float dh[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.t < p.S - 1) {
+    const float keep = 1.f - p.D[row];
+    const float4 d = *reinterpret_cast<const float4*>(p.DH + (size_t)b * RH + u);
+    dh[0] = keep * d.x; dh[1] = keep * d.y; dh[2] = keep * d.z; dh[3] = keep * d.w;
+  }
+  {
+    const float4 w0 = *reinterpret_cast<const float4*>(p.wq + u), w1 = *reinterpret_cast<const float4*>(p.wq + RH + u),
+                 w2 = *reinterpret_cast<const float4*>(p.wq + 2 * RH + u);
+    dh[0] += dq.x * w0.x + dq.y * w1.x + dq.z * w2.x;
+    dh[1] += dq.x * w0.y + dq.y * w1.y + dq.z * w2.y;
+    dh[2] += dq.x * w0.z + dq.y * w1.z + dq.z * w2.z;
+    dh[3] += dq.x * w0.w + dq.y * w1.w + dq.z * w2.w;
+  }
+  const float4 r4 = *reinterpret_cast<const float4*>(p.sr + o), z4 = *reinterpret_cast<const float4*>(p.sz + o),
+               n4 = *reinterpret_cast<const float4*>(p.sn + o), g4_ = *reinterpret_cast<const float4*>(p.sgh + o),
+               h4 = *reinterpret_cast<const float4*>(p.shp + o);
+  const float r[4] = {r4.x, r4.y, r4.z, r4.w}, z[4] = {z4.x, z4.y, z4.z, z4.w}, n[4] = {n4.x, n4.y, n4.z, n4.w},
+              gh[4] = {g4_.x, g4_.y, g4_.z, g4_.w}, hp[4] = {h4.x, h4.y, h4.z, h4.w};
+  float dar[4], daz[4], dan[4], dghn[4], dhp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float dn = dh[i] * (1.f - z[i]);
+    const float dz = dh[i] * (hp[i] - n[i]);
+    dhp[i] = dh[i] * z[i];
+    dan[i] = dn * (1.f - n[i] * n[i]);
+    const float dr = dan[i] * gh[i];
+    dghn[i] = dan[i] * r[i];
+    dar[i] = dr * r[i] * (1.f - r[i]);
+    daz[i] = dz * z[i] * (1.f - z[i]);
+  }
+  bf16_t* gx = p.dGx + row * RG;
+  bf16_t* gh_ = p.dGh + row * RG;
+  lds_st4(gx + u, dar[0], dar[1], dar[2], dar[3]);
+  lds_st4(gx + RH + u, daz[0], daz[1], daz[2], daz[3]);
+  lds_st4(gx + 2 * RH + u, dan[0], dan[1], dan[2], dan[3]);
+  lds_st4(gh_ + u, dar[0], dar[1], dar[2], dar[3]);
+  lds_st4(gh_ + RH + u, daz[0], daz[1], daz[2], daz[3]);
+  lds_st4(gh_ + 2 * RH + u, dghn[0], dghn[1], dghn[2], dghn[3]);
+  *reinterpret_cast<float4*>(p.DH + (size_t)b * RH + u) = make_float4(dhp[0], dhp[1], dhp[2], dhp[3]);
+}
+
+// dW_q[a][u] = sum_rows dQ[row][a] h[row][u], db_q[a] = sum_rows dQ[row][a] (atomic partials)
+__global__ void __launch_bounds__(256) gru_wq_grad_kernel(const float* __restrict__ dQ, const bf16_t* __restrict__ Hq,
+                                                          int rows, int per, float* dwq, float* dbq) {
+  const int u = threadIdx.x;
+  const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, b0 = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const float4 d = *reinterpret_cast<const float4*>(dQ + (size_t)r * 4);
+    const float h = bf2f(Hq[(size_t)r * RH + u]);
+    a0 += d.x * h; a1 += d.y * h; a2 += d.z * h;
+    if (u < 3) b0 += u == 0 ? d.x : (u == 1 ? d.y : d.z);
+  }
+  atomicAdd(dwq + u, a0);
+  atomicAdd(dwq + RH + u, a1);
+  atomicAdd(dwq + 2 * RH + u, a2);
+  if (u < 3) atomicAdd(dbq + u, b0);
+}
+
+// MX-fp8 MFMA probe: D = (A * 2^(sa-127)) . (B * 2^(sb-127))^T for one 16x16x128 tile (layout tests)
+__global__ void mx_probe_kernel(const i8v* a, const i8v* b, const int* sa, const int* sb, f4v* d) {
+  const int l = threadIdx.x;
+  d[l] = mx_mfma(a[l], b[l], zero4(), sa[l], sb[l]);
+}
+
+}  // namespace st
+
+// ---------------------------------------------------------------- C ABI
+extern "C" hipError_t st_minute_bars(const st::MinuteBars* g, hipStream_t s) {
+  if (g->E <= 0 || g->T <= 1 || g->day <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::minute_bars_kernel, dim3((g->E + 255) / 256), dim3(256), 0, s, *g);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_pack(const st::GruPack* p, hipStream_t s) {
+  const int n = st::RW * 3 * 2 * 2 * 64;
+  hipLaunchKernelGGL(st::gru_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" int st_gru_act_lds_bytes() { return st::ActLds::BYTES; }
+
+extern "C" hipError_t st_gru_act(const st::GruAct* p, int grid, hipStream_t s) {
+  if (p->E % st::RN || p->S <= 0 || p->ep_len <= 0 || p->T < p->ep_len + 3 || p->cap <= 0 || grid <= 0)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)st::gru_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       st::ActLds::BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nch = p->E / st::RN;
+  hipLaunchKernelGGL(st::gru_act_kernel, dim3(grid < nch ? grid : nch), dim3(st::RT), st::ActLds::BYTES, s, *p);
+  hipLaunchKernelGGL(st::gru_advance_kernel, dim3(1), dim3(1), 0, s, p->rctrl, p->ctrl, p->E, p->cap);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_gather(const st::GruGather* g, hipStream_t s) {
+  if (g->S > 64 || g->S <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::gru_gather_kernel, dim3((g->B + 3) / 4), dim3(256), 0, s, *g);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_fwd(const st::GruFwd* f, hipStream_t s) {
+  hipLaunchKernelGGL(st::gru_fwd_kernel, dim3((f->B + 3) / 4), dim3(256), 0, s, *f);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_td(const st::GruTD* p, hipStream_t s) {
+  hipLaunchKernelGGL(st::gru_td_kernel, dim3((p->S * p->B + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_bwd(const st::GruBwd* p, hipStream_t s) {
+  hipLaunchKernelGGL(st::gru_bwd_kernel, dim3((p->B + 3) / 4), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_wq_grad(const float* dQ, const bf16_t* Hq, int rows, float* dwq, float* dbq,
+                                     hipStream_t s) {
+  const int per = 64;
+  hipLaunchKernelGGL(st::gru_wq_grad_kernel, dim3((rows + per - 1) / per), dim3(st::RH), 0, s, dQ, Hq, rows, per, dwq,
+                     dbq);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_mx_probe(const void* a, const void* b, const int* sa, const int* sb, float* d,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(st::mx_probe_kernel, dim3(1), dim3(64), 0, s, (const st::i8v*)a, (const st::i8v*)b, sa, sb,
+                     (f4v*)d);
+  return hipGetLastError();
+}

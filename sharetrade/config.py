@@ -260,6 +260,12 @@ def preset_config(name: str = "reference_compat") -> Config:
         cfg.engine.dtype = "bf16"
         cfg.engine.envs_per_rank = 65536
         return cfg
+    if name == "recurrent":
+        # BASELINE config 5: GRU(256) Q-net on minute bars (sharetrade/trainer/recurrent.py)
+        cfg = preset_config("flagship")
+        cfg.agent.lr = 3e-4
+        cfg.data.source = "minute_bars"
+        return cfg
     if name == "test":
         cfg.engine.dtype = "fp32"
         cfg.persist.journal_plugin = "inmemory"

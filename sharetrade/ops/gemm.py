@@ -19,7 +19,7 @@ class GemmArgs(C.Structure):
         ("A", C.c_void_p), ("B", C.c_void_p), ("out", C.c_void_p), ("outT", C.c_void_p), ("bias", C.c_void_p),
         ("auxT", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
         ("ldo", C.c_int), ("ldoT", C.c_int), ("ldaux", C.c_int), ("relu", C.c_int), ("accumulate", C.c_int),
-        ("alpha", C.c_float),
+        ("alpha", C.c_float), ("splitk", C.c_int),
     ]
 
 
@@ -43,7 +43,7 @@ def pick_tile(M: int, N: int) -> tuple:
 
 def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, outT: Optional[torch.Tensor] = None,
               bias: Optional[torch.Tensor] = None, auxT: Optional[torch.Tensor] = None, relu: bool = False,
-              accumulate: bool = False, alpha: float = 1.0) -> GemmArgs:
+              accumulate: bool = False, alpha: float = 1.0, splitk: int = 1) -> GemmArgs:
     M, K = A.shape
     N, K2 = B.shape
     if K != K2:
@@ -74,12 +74,34 @@ def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, out
     g.ldoT = outT.stride(0) if outT is not None else 0
     g.ldaux = auxT.stride(0) if auxT is not None else 0
     g.relu, g.accumulate, g.alpha = int(relu), int(accumulate), float(alpha)
+    if splitk > 1:
+        if epi != EPI_F32:
+            raise ValueError("split-K needs the fp32 epilogue (atomic accumulation)")
+        if (K // 64) % splitk:
+            raise ValueError(f"split-K {splitk} does not divide the {K // 64} K-tiles")
+    g.splitk = int(splitk)
     return g
 
 
+def pick_splitk(M: int, N: int, K: int, tile) -> int:
+    """Split K until the launch has >= ~256 workgroups (one per CU) or the K-tiles run out."""
+    wg = (M // tile[0]) * (N // tile[1])
+    s = 1
+    while wg * s < 256 and (K // 64) % (2 * s) == 0 and K // 64 // (2 * s) >= 4:
+        s *= 2
+    return s
+
+
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_BF16, tile=None, **kw) -> torch.Tensor:
-    g = make_args(A, B, out, epi, **kw)
-    t = tile or pick_tile(g.M, g.N)
+    """``out = A . B^T`` (+ epilogue).  ``splitk="auto"`` (fp32 epilogue only) splits long-K,
+    few-tile products (weight gradients) over extra workgroups with atomic accumulation."""
+    t = tile or pick_tile(A.shape[0], B.shape[0])
+    sk = kw.pop("splitk", 1)
+    if sk == "auto":
+        sk = pick_splitk(A.shape[0], B.shape[0], A.shape[1], t) if epi == EPI_F32 else 1
+    if sk > 1 and not kw.get("accumulate", False):
+        out.zero_()
+    g = make_args(A, B, out, epi, splitk=sk, **kw)
     if g.M % t[0] or g.N % t[1] or g.K % 64:
         raise ValueError(f"gemm_nt: shape {g.M}x{g.N}x{g.K} not a multiple of tile {t} / BK 64")
     native.check(_bind().st_gemm_nt(g, epi, TILES[t], native.stream_handle()), "st_gemm_nt")

@@ -295,7 +295,9 @@ class DeepDQN:
         native.check(k.st_deep_td(self._td, sh), "deep_td")
         for l in reversed(range(self.L)):
             # weight / bias gradients of layer l: dW = G_l^T . A_l
-            gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32)
+            # long-K, few-tile product: 128x128 tiles split over K (atomic fp32 accumulation)
+            wt = (128, 128) if self.pdims[l + 1] % 128 == 0 and self.pdims[l] % 128 == 0 else None
+            gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=wt, splitk="auto")
             native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
                                            self.db[l].data_ptr(), sh), "bias grad")
             if l > 0:

@@ -65,3 +65,22 @@ def test_gemm_rejects_bad_shapes(native_built):
     A, B = _bf((100, 64), 1), _bf((128, 64), 2)
     with pytest.raises(ValueError):
         gemm_nt(A, B, torch.empty(100, 128, device="cuda"), EPI_F32)
+
+
+@pytest.mark.parametrize("M,N,K,tile,sk", [(1024, 1024, 4096, (128, 128), "auto"), (768, 256, 16384, (64, 64), 8),
+                                           (768, 64, 16384, (64, 64), "auto")])
+def test_gemm_split_k(native_built, M, N, K, tile, sk):
+    from sharetrade.ops.gemm import EPI_F32, gemm_nt, pick_splitk
+
+    A, B = _bf((M, K), 7), _bf((N, K), 8)
+    bias = torch.randn(N, device="cuda")
+    out = torch.full((M, N), float("nan"), dtype=torch.float32, device="cuda")   # zeroed by the wrapper
+    gemm_nt(A, B, out, EPI_F32, tile=tile, splitk=sk, bias=bias)
+    ref = A.float() @ B.float().t() + bias
+    torch.cuda.synchronize()
+    if sk == "auto":
+        assert pick_splitk(M, N, K, tile) > 1
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
+    gemm_nt(A, B, out, EPI_F32, tile=tile, splitk=sk, accumulate=True)   # bias not re-added
+    assert torch.allclose(out, 2 * ref - bias, rtol=1e-4, atol=1e-3 * float(ref.abs().max()))

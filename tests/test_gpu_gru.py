@@ -1,0 +1,208 @@
+"""GRU(256) recurrent Q-net (BASELINE config 5): MX-fp8 actor + bf16 learner vs PyTorch references."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(eps=0.9):
+    from sharetrade.config import preset_config
+
+    cfg = preset_config("recurrent")
+    cfg.agent.epsilon = eps
+    return cfg
+
+
+def test_mx_probe_layout(native_built):
+    """v_mfma_scale_f32_16x16x128_f8f6f4: lane l = i + 16q holds row/col i, K 16q+[0,16) and 64+16q+[0,16);
+    the scale of (row i, K-block s) comes from lane i + 16s (tools/mx_layout_probe.py)."""
+    from sharetrade.ops.gru import mx_probe
+
+    g = torch.Generator().manual_seed(0)
+    vals = torch.randint(-8, 9, (2, 64, 32), generator=g).float() * 0.25      # exact in e4m3
+    a8 = vals[0].to(torch.float8_e4m3fn).view(torch.uint8).cuda()
+    b8 = vals[1].to(torch.float8_e4m3fn).view(torch.uint8).cuda()
+    sa = torch.randint(124, 131, (64,), generator=g, dtype=torch.int32)
+    sb = torch.randint(124, 131, (64,), generator=g, dtype=torch.int32)
+    D = mx_probe(a8, b8, sa.cuda(), sb.cuda()).cpu()
+    A = torch.zeros(16, 128)
+    Bm = torch.zeros(16, 128)
+    for l in range(64):
+        i, q = l & 15, l >> 4
+        for half, k0 in ((0, 16 * q), (1, 64 + 16 * q)):
+            A[i, k0:k0 + 16] = vals[0, l, 16 * half:16 * half + 16] * 2.0 ** (int(sa[i + 16 * (k0 // 32)]) - 127)
+            Bm[i, k0:k0 + 16] = vals[1, l, 16 * half:16 * half + 16] * 2.0 ** (int(sb[i + 16 * (k0 // 32)]) - 127)
+    ref = A.double() @ Bm.double().t()
+    assert torch.allclose(D.double(), ref, rtol=1e-6, atol=1e-6), (D - ref).abs().max()
+
+
+def test_minute_bars_gpu_matches_numpy(native_built):
+    from sharetrade.data import minute_bars as mb
+
+    close, feat = mb.generate_gpu(64, 300, torch.device("cuda", 0), seed=3)
+    c_np, f_np = mb.generate_numpy(64, 300, seed=3)
+    torch.cuda.synchronize()
+    rel = np.abs(close.cpu().numpy() - c_np) / c_np
+    assert rel.max() < 1e-4, rel.max()
+    f = feat.float().cpu().numpy()
+    assert np.allclose(f, f_np, rtol=2e-2, atol=2e-2)
+
+
+def _small(E=64, S=4, eps=0.9, **kw):
+    from sharetrade.trainer.recurrent import RecurrentDQN
+
+    kw.setdefault("bars", 600)
+    kw.setdefault("ep_len", 5)
+    kw.setdefault("batch", 128)
+    kw.setdefault("replay_segments", 1024)
+    return RecurrentDQN(_cfg(eps), torch.device("cuda", 0), envs=E, seq=S, burn_in=1, **kw)
+
+
+def test_pack_is_exact_mx_quantization(native_built):
+    from sharetrade.ops.gru import mx_roundtrip, unpack_whh
+
+    d = _small()
+    torch.cuda.synchronize()
+    W = d.P["w_hh"].cpu()
+    deq = unpack_whh(d.whh8, d.whhs)
+    assert torch.equal(deq, mx_roundtrip(W))   # 32-element blocks along K, same scale rule as the kernel
+    assert torch.allclose(deq, W, rtol=0.07, atol=1e-6)
+
+
+def _ref_actor(d, steps, eps_exploit):
+    """Host replay of one actor launch: env in float32 (bit-exact), GRU in fp32 with the
+    actor's quantization points (MX-fp8 W_hh and h, bf16 W_ih and x)."""
+    from sharetrade.env import minute as me
+    from sharetrade.ops.gru import mx_roundtrip, unpack_whh
+    from sharetrade.utils import rng
+
+    E, S, T = d.E, d.S, d.T
+    Whh = unpack_whh(d.whh8, d.whhs).double()
+    Wih = d.P["w_ih"].cpu()[:, :32].to(torch.bfloat16).double()
+    b_ih, b_hh = d.P["b_ih"].cpu().view(-1).double(), d.P["b_hh"].cpu().view(-1).double()
+    Wq, bq = d.P["w_q"].cpu().double(), d.P["b_q"].cpu().view(-1).double()
+    close = d.close.cpu().numpy()
+    feat = d.feat.float().cpu().numpy()
+    k0, k1 = rng.key_for(d.seed, 5)
+    pos, es = d.pos.cpu().numpy(), d.ep_start.cpu().numpy()
+    states = [me.MinuteEnvState(int(pos[e]), int(es[e])) for e in range(E)]
+    h = torch.zeros(E, 256, dtype=torch.float64)
+    xs, acts, rews, dones, qs = [], [], [], [], []
+    x = torch.tensor(np.stack([me.obs(feat[e, states[e].t], close[e, states[e].t], states[e], d.ep_len)
+                               for e in range(E)])).to(torch.bfloat16).double()
+    xs.append(x)
+    for s in range(S):
+        hq = mx_roundtrip(h.float()).double()
+        gx = x @ Wih.t() + b_ih
+        gh = hq @ Whh.t() + b_hh
+        r = torch.sigmoid(gx[:, :256] + gh[:, :256])
+        z = torch.sigmoid(gx[:, 256:512] + gh[:, 256:512])
+        n = torch.tanh(gx[:, 512:] + r * gh[:, 512:])
+        h = (1 - z) * n + z * h
+        q = h @ Wq.t() + bq
+        qs.append(q)
+        a_s, r_s, d_s, xn = [], [], [], []
+        for e in range(E):
+            gstep = s + int(d.ctrl[0]) * S
+            u_exp, u_act, u_rst = me.draws(e, gstep, k0, k1)
+            rnd = min(int(u_act * np.float32(3.0)), 2)
+            exploit = u_exp < min(np.float32(eps_exploit), np.float32(gstep) * np.float32(1.0 / d.cfg.agent.ramp))
+            a = int(torch.argmax(q[e])) if exploit else rnd
+            rew, done, _ = me.step(states[e], a, close[e], T, d.ep_len, d.cost, u_rst)
+            a_s.append(a); r_s.append(rew); d_s.append(done)
+            xn.append(me.obs(feat[e, states[e].t], close[e, states[e].t], states[e], d.ep_len))
+            if done:
+                h[e] = 0
+        acts.append(a_s); rews.append(r_s); dones.append(d_s)
+        x = torch.tensor(np.stack(xn)).to(torch.bfloat16).double()
+        xs.append(x)
+    return h, qs, acts, rews, dones, xs, states
+
+
+def test_actor_matches_reference(native_built):
+    """eps = 0 -> every action is the Philox random draw, so env/replay must match bit for bit
+    and the GRU state must match the quantization-aware fp32 reference."""
+    d = _small(eps=0.0)
+    q_out = torch.zeros(d.E, 4, device="cuda")
+    d._act.q_out = q_out.data_ptr()
+    h_ref, qs, acts, rews, dones, xs, states = _ref_actor(d, d.S, 0.0)
+    d.act()
+    torch.cuda.synchronize()
+    slots = np.arange(d.E)   # first launch: segment slot = env id
+    ra = d.ra.cpu().numpy()[slots]
+    rr = d.rr.cpu().numpy()[slots]
+    rd = d.rd.cpu().numpy()[slots]
+    assert np.array_equal(ra, np.array(acts).T)
+    assert np.array_equal(rr, np.array(rews, dtype=np.float32).T)
+    assert np.array_equal(rd.astype(bool), np.array(dones).T)
+    rx = d.rx.cpu().float()[slots]
+    for s in range(d.S + 1):
+        assert torch.equal(rx[:, s].double(), xs[s]), s
+    assert np.array_equal(d.pos.cpu().numpy(), np.array([st.t for st in states]))
+    assert np.array_equal(d.position.cpu().numpy(), np.array([st.pz for st in states]))
+    h = d.h.cpu().double()
+    err = float((h - h_ref).abs().max())
+    assert err < 3e-2, err
+    assert float((h - h_ref).abs().mean()) < 2e-3
+    qerr = float((q_out[:, :3].cpu().double() - qs[-1]).abs().max())
+    assert qerr < 1e-2, qerr
+    assert int(d.rctrl[0]) == d.E and int(d.ctrl[0]) == 1
+
+
+def test_learner_gradients_match_autograd(native_built):
+    from sharetrade.models import gru_qnet as gq
+    from sharetrade.utils import rng
+
+    d = _small(E=128, S=4, eps=0.5, batch=128)
+    for _ in range(3):
+        d.act()
+    P0 = {n: t.detach().clone() for n, t in d.P.items()}
+    tgt = {n: t.detach().clone() for n, t in d.tgt.items()}
+    d.update()
+    torch.cuda.synchronize()
+    # the sampled segments (Philox counter = (row, update 0))
+    size = int(d.rctrl[1])
+    k0, k1 = rng.key_for(d.seed, 7)
+    b = np.arange(d.B, dtype=np.uint32)
+    c0, c1, _, _ = rng.philox4x32(b, np.zeros_like(b), np.zeros_like(b), np.full_like(b, 0x53455131), k0, k1)
+    idx = torch.from_numpy(((c0.astype(np.uint64) << np.uint64(32)) | c1.astype(np.uint64)) % np.uint64(size))
+    idx = idx.long()
+    X = torch.zeros(d.S + 1, d.B, 64)
+    X[:, :, :32] = d.rx.cpu()[idx].float().transpose(0, 1)
+    A = d.ra.cpu()[idx].long().t()
+    R = d.rr.cpu()[idx].t()
+    D = d.rd.cpu()[idx].float().t()
+    h0 = d.rh0.cpu()[idx].float()
+    bf = lambda t: t.to(torch.bfloat16).float()
+    p = {"w_ih": bf(P0["w_ih"].cpu()).requires_grad_(True), "w_hh": bf(P0["w_hh"].cpu()).requires_grad_(True),
+         "b_ih": P0["b_ih"].cpu().view(-1).clone().requires_grad_(True),
+         "b_hh": P0["b_hh"].cpu().view(-1).clone().requires_grad_(True),
+         "w_q": P0["w_q"].cpu().clone().requires_grad_(True), "b_q": P0["b_q"].cpu().view(-1).clone().requires_grad_(True)}
+    pt = {"w_ih": tgt["w_ih"].cpu().float(), "w_hh": tgt["w_hh"].cpu().float(), "b_ih": tgt["b_ih"].cpu().view(-1),
+          "b_hh": tgt["b_hh"].cpu().view(-1), "w_q": tgt["w_q"].cpu(), "b_q": tgt["b_q"].cpu().view(-1)}
+    loss = gq.sequence_td_loss(p, pt, X, h0, A, R, D, d.gamma, d.burn)
+    loss.backward()
+    got_loss = float(d.loss) / (d.B * (d.S - d.burn))
+    assert abs(got_loss - float(loss)) < 2e-2 * float(loss) + 1e-7, (got_loss, float(loss))
+    for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w_q", "b_q"):
+        ref = p[n].grad.view(-1)
+        got = d.dP[n].cpu().view(-1)
+        rel = float((got - ref).norm() / (ref.norm() + 1e-20))
+        assert rel < 5e-2, (n, rel)
+
+
+def test_graph_iterations_train(native_built):
+    d = _small(E=256, S=8, eps=0.9, batch=256)
+    for _ in range(2):
+        d.act()
+    d.capture()
+    w0 = d.P["w_hh"].clone()
+    for _ in range(6):
+        d.iteration(1)
+    torch.cuda.synchronize()
+    s = d.stats_dict()
+    assert s["updates"] == 7 and np.isfinite(s["loss"])
+    assert s["episodes"] > 0 and np.isfinite(s["episode_return_mean"])
+    assert torch.isfinite(d.flat).all() and not torch.equal(w0, d.P["w_hh"])
+    assert int(d.t_ctr) == 7
