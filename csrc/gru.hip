@@ -65,7 +65,14 @@ ST_DEV uint32_t fp8x4(float a, float b, float c, float d) {
   v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
   return (uint32_t)v;
 }
-ST_DEV float sigm(float x) { return __frcp_rn(1.f + __expf(-x)); }
+// raw v_exp_f32 / v_rcp_f32 (1 ulp): __frcp_rn would expand to the IEEE division sequence
+ST_DEV float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+// actor epilogue forms: exp2 with the log2(e) scale folded, explicit FMAs (the build keeps
+// -ffp-contract=off for the bit-exact env arithmetic, so contraction is spelled out here)
+ST_DEV float sigm2(float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.44269504f)); }
+ST_DEV float tanh2(float x) {
+  return __builtin_fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -2.88539008f)), -1.f);
+}
 ST_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
 
 // ---------------------------------------------------------------- synthetic minute bars
@@ -213,6 +220,7 @@ struct GruAct {
   unsigned long long* ctrl;    // [0] actor launches so far
   float* stats;                // [4] reward sum, explore count, episodes done, finished-episode return sum
   float* q_out;                // optional [E][4]: Q of the last step (tests)
+  unsigned long long* stamps;  // optional debug: s_memtime of workgroup 0, waves 0 and 1: [step][2][8]
 };
 
 struct ActLds {
@@ -302,6 +310,18 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
         Ws4[g] |= (p.whhs[idx] & 0xFF) << (8 * (2 * m + ks));
       }
   const s8v* myWx = sWx + wave * 6 * 64 + lane;
+  // Q head as one bf16 MFMA per env tile: A = W_q rows (a < 3, zero-padded to 16) over this
+  // wave's 32 units, K ordered like the GRU accumulators the B operand is built from:
+  // element j of lane group q <-> unit 32w + (j < 4 ? 4q + j : 16 + 4q + j - 4)
+  s8v WqA;
+  {
+    const int a = l16;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int u = 32 * wave + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+      WqA[j] = (short)f2bf(a < 3 ? p.wq[a * RH + u] : 0.f);
+    }
+  }
   const unsigned long long launch = p.ctrl[0];
   const unsigned long long seg0 = p.rctrl[0];
   const int nchunks = p.E / RN, S = p.S;
@@ -346,15 +366,28 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
 
     for (int s = 0; s < S; ++s) {
       const int cur = s & 1, nxt = cur ^ 1;
+      // debug phase stamps (tools/stamp_gru.py): slot 0 step start, 1 after MFMAs of tile 0,
+      // 2 after tile 1 + GRU update, 3 after quantization, 4 after barrier 1, 5 after the env
+      // phase, 6 after barrier 2
+#define GR_STAMP(I)                                                                                       \
+  if (p.stamps != nullptr && blockIdx.x == 0 && chunk == 0 && wave < 2 && lane == 0)                      \
+    p.stamps[((size_t)s * 2 + wave) * 8 + (I)] = __builtin_amdgcn_s_memtime();
+      GR_STAMP(0)
       const bf16_t* cX = sX + cur * RN * XS;
       const unsigned char* cH = sH8 + cur * RN * HS;
       const int* cS = sSc + cur * RN * SCS;
       // one 16-env tile at a time keeps the accumulators at 32 VGPRs (W_hh holds 108)
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        f4v ar[2], az[2], anx[2], anh[2];
+        f4v ar[2], az[2], anx[2], anh[2];   // accumulators start at the biases (b_ir+b_hr, b_iz+b_hz, b_in, b_hn)
 #pragma unroll
-        for (int m = 0; m < 2; ++m) { ar[m] = zero4(); az[m] = zero4(); anx[m] = zero4(); anh[m] = zero4(); }
+        for (int m = 0; m < 2; ++m) {
+          const int u0 = 32 * wave + 16 * m + 4 * g4;
+          ar[m] = *reinterpret_cast<const f4v*>(sB + u0);
+          az[m] = *reinterpret_cast<const f4v*>(sB + RH + u0);
+          anx[m] = *reinterpret_cast<const f4v*>(sB + 2 * RH + u0);
+          anh[m] = *reinterpret_cast<const f4v*>(sB + 3 * RH + u0);
+        }
         const int row = 16 * n + l16;
         // x part: bf16 16x16x32 (W_ih fragments from LDS)
         {
@@ -383,42 +416,37 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
           if (ks == 0) { ST_MX3(0, 0) ST_MX3(1, 0) } else { ST_MX3(0, 1) ST_MX3(1, 1) }
 #undef ST_MX3
         }
+        if (n == 0) { GR_STAMP(1) }
         // GRU update in registers (lane: units u0..u0+3 of tile m, env 16n + l16)
-        float qa0 = 0.f, qa1 = 0.f, qa2 = 0.f;
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const int u0 = 32 * wave + 16 * m + 4 * g4;
-          const f4v br = *reinterpret_cast<const f4v*>(sB + u0);
-          const f4v bz = *reinterpret_cast<const f4v*>(sB + RH + u0);
-          const f4v bi = *reinterpret_cast<const f4v*>(sB + 2 * RH + u0);
-          const f4v bh = *reinterpret_cast<const f4v*>(sB + 3 * RH + u0);
-          const f4v w0 = *reinterpret_cast<const f4v*>(sWq + u0);
-          const f4v w1 = *reinterpret_cast<const f4v*>(sWq + RH + u0);
-          const f4v w2 = *reinterpret_cast<const f4v*>(sWq + 2 * RH + u0);
+        for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float r = sigm(ar[m][i] + br[i]);
-            const float z = sigm(az[m][i] + bz[i]);
-            const float nn = tanh_f(anx[m][i] + bi[i] + r * (anh[m][i] + bh[i]));
-            const float hv = nn + z * (hr[m][n][i] - nn);
-            hr[m][n][i] = hv;
-            qa0 += w0[i] * hv;
-            qa1 += w1[i] * hv;
-            qa2 += w2[i] * hv;
+            const float r = sigm2(ar[m][i]);
+            const float z = sigm2(az[m][i]);
+            const float nn = tanh2(__builtin_fmaf(r, anh[m][i], anx[m][i]));
+            hr[m][n][i] = __builtin_fmaf(z, hr[m][n][i] - nn, nn);
+          }
+        // Q partials of this wave's units: one MFMA, h (bf16) taken straight from the accumulator layout
+        {
+          s8v hb;
+          const uint32_t p0 = pack_bf2(hr[0][n][0], hr[0][n][1]), p1 = pack_bf2(hr[0][n][2], hr[0][n][3]);
+          const uint32_t p2 = pack_bf2(hr[1][n][0], hr[1][n][1]), p3 = pack_bf2(hr[1][n][2], hr[1][n][3]);
+          hb[0] = (short)(p0 & 0xFFFF); hb[1] = (short)(p0 >> 16); hb[2] = (short)(p1 & 0xFFFF); hb[3] = (short)(p1 >> 16);
+          hb[4] = (short)(p2 & 0xFFFF); hb[5] = (short)(p2 >> 16); hb[6] = (short)(p3 & 0xFFFF); hb[7] = (short)(p3 >> 16);
+          const f4v qp = mfma32(WqA, hb, zero4());
+          if (g4 == 0) {   // rows a = 0..2 of the 16x16 result live in lanes 0..15, registers 0..2
+            sQp[(wave * 3 + 0) * RN + row] = qp[0];
+            sQp[(wave * 3 + 1) * RN + row] = qp[1];
+            sQp[(wave * 3 + 2) * RN + row] = qp[2];
           }
         }
-        // Q partials over this wave's units, reduced across the 4 lane groups
-        qa0 += __shfl_xor(qa0, 16, 64); qa0 += __shfl_xor(qa0, 32, 64);
-        qa1 += __shfl_xor(qa1, 16, 64); qa1 += __shfl_xor(qa1, 32, 64);
-        qa2 += __shfl_xor(qa2, 16, 64); qa2 += __shfl_xor(qa2, 32, 64);
-        if (g4 == 0) {
-          sQp[(wave * 3 + 0) * RN + row] = qa0;
-          sQp[(wave * 3 + 1) * RN + row] = qa1;
-          sQp[(wave * 3 + 2) * RN + row] = qa2;
-        }
       }
+      GR_STAMP(2)
       quant_h(hr, sH8 + nxt * RN * HS, sSc + nxt * RN * SCS, wave, l16, g4);
+      GR_STAMP(3)
       __syncthreads();
+      GR_STAMP(4)
       // ---------------------------------------------------------- env step (wave 0)
       if (wave == 0) {
         float q[3];
@@ -497,7 +525,9 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
         cB = p.close[o1];
         fB = *reinterpret_cast<const uint4*>(p.feat + o1 * RMF);
       }
+      GR_STAMP(5)
       __syncthreads();
+      GR_STAMP(6)
 #pragma unroll
       for (int n = 0; n < 2; ++n)
         if (sDone[16 * n + l16]) {
