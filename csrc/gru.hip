@@ -198,8 +198,9 @@ struct GruAct {
   const float* wq;
   const bf16_t* feat;          // [E][T][RMF]
   const float* close;          // [E][T]
+  const float* ret;            // [E][T]: (close[t+1] / close[t] - 1) * 100 (last bar 0)
   int E, T, S, ep_len;
-  float eps, inv_ramp, cost;
+  float eps, inv_ramp, cost, inv_ep_len;
   float* h;                    // [E][RH] fp32 recurrent state between launches
   int* pos;                    // [E] bar index
   int* ep_start;
@@ -232,7 +233,8 @@ struct ActLds {
   static constexpr int WQ = B + 4 * RH * 4;                      // [4*RH] float
   static constexpr int QP = WQ + 4 * RH * 4;                     // [RW][3][RN] float
   static constexpr int DN = QP + RW * 3 * RN * 4;                // [RN] int
-  static constexpr int BYTES = DN + RN * 4;
+  static constexpr int U = DN + RN * 4;                          // [S<=64][RN][4] float: Philox draws
+  static constexpr int BYTES = U + 64 * RN * 16;
 };
 static_assert(ActLds::BYTES <= 160 * 1024, "actor LDS");
 
@@ -263,7 +265,7 @@ ST_DEV void build_x(const GruAct& p, uint4 mf, float c, int t, int es, int pz, f
   const float upnl = pz ? (c / entry - 1.f) * 100.f : 0.f;
   uint4 w1;
   w1.x = pack_bf2((float)pz, upnl);
-  w1.y = pack_bf2((float)(t - es) / (float)p.ep_len, 1.f);
+  w1.y = pack_bf2((float)(t - es) * p.inv_ep_len, 1.f);
   w1.z = 0u;
   w1.w = 0u;
   const uint4 z = {0u, 0u, 0u, 0u};
@@ -288,6 +290,7 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
   float* sWq = reinterpret_cast<float*>(lds + ActLds::WQ);
   float* sQp = reinterpret_cast<float*>(lds + ActLds::QP);
   int* sDone = reinterpret_cast<int*>(lds + ActLds::DN);
+  f4v* sU = reinterpret_cast<f4v*>(lds + ActLds::U);
 
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -346,6 +349,7 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
     int t_ = 0, es_ = 0, pz_ = 0, eps_ = 0;
     float en_ = 0.f, er_ = 0.f, lr_ = 0.f;
     float cA = 0.f, cB = 0.f;      // close[t], close[t+1] (prefetched one env phase ahead)
+    float rA = 0.f, rB = 0.f;      // ret[t], ret[t+1]
     uint4 fB = {0u, 0u, 0u, 0u};   // features of bar t+1
     float st_rew = 0.f, st_exp = 0.f, st_fin = 0.f, st_dn = 0.f;
     size_t slot_ = 0;
@@ -358,9 +362,22 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
       const size_t o = (size_t)me * p.T + t_;
       cA = p.close[o];
       cB = p.close[o + 1];
+      rA = p.ret[o];
+      rB = p.ret[o + 1];
       fB = bar_feat(p, me, t_ + 1);
       const uint4 f0 = bar_feat(p, me, t_);
       if (writer) build_x(p, f0, cA, t_, es_, pz_, en_, sX + lane * XS, p.rx + slot_ * (size_t)(S + 1) * RF);
+    }
+    // the chunk's Philox draws for all S steps, by every thread (off the env phase's serial path)
+    for (int i = tid; i < S * RN; i += RT) {
+      const int ss = i / RN, e = e0 + (i % RN);
+      const unsigned long long step = launch * (unsigned long long)S + (unsigned long long)ss;
+      uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32),
+               c3 = 0x47525531u;
+      philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+      f4v u;
+      u[0] = u24(c0); u[1] = u24(c1); u[2] = u24(c2); u[3] = (float)step;
+      sU[i] = u;
     }
     __syncthreads();
 
@@ -460,18 +477,14 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
         int greedy = 0;
         if (q[1] > q[greedy]) greedy = 1;
         if (q[2] > q[greedy]) greedy = 2;
-        const unsigned long long step = launch * (unsigned long long)S + (unsigned long long)s;
-        uint32_t c0 = (uint32_t)me, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32),
-                 c3 = 0x47525531u;
-        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
-        const bool exploit = u24(c0) < fminf(p.eps, (float)step * p.inv_ramp);
-        const int rnd = min((int)(u24(c1) * 3.0f), 2);
+        const f4v u = sU[s * RN + (lane & (RN - 1))];   // (explore coin, random action, reset, step)
+        const bool exploit = u[0] < fminf(p.eps, u[3] * p.inv_ramp);
+        const int rnd = min((int)(u[1] * 3.0f), 2);
         const int a = exploit ? greedy : rnd;
-        const float c_t = cA, c_n = cB;
         const int np = a == 0 ? 1 : (a == 1 ? 0 : pz_);
         const bool trade = np != pz_;
-        if (trade && np == 1) en_ = c_t;
-        const float rew = (float)np * (c_n / c_t - 1.f) * 100.f - (trade ? p.cost : 0.f);
+        if (trade && np == 1) en_ = cA;
+        const float rew = (float)np * rA - (trade ? p.cost : 0.f);
         er_ += rew;
         int t1 = t_ + 1;
         const bool done = (t1 - es_) >= p.ep_len;
@@ -480,7 +493,7 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
           eps_ += 1;
           lr_ = er_;
           fin = er_;
-          es_ = min((int)(u24(c2) * (float)(p.T - p.ep_len - 1)), p.T - p.ep_len - 2);
+          es_ = min((int)(u[2] * (float)(p.T - p.ep_len - 1)), p.T - p.ep_len - 2);
           t1 = es_;
           pz_ = 0;
           er_ = 0.f;
@@ -490,12 +503,14 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
         t_ = t1;
         // bar t1's features: prefetched unless the episode restarted (rare: load now)
         uint4 fx = fB;
-        float cx = cB;
+        float cx = cB, rx = rB;
         if (__builtin_amdgcn_ballot_w64(done) != 0ull) {
+          const size_t o = (size_t)me * p.T + t_;
           const uint4 fr = bar_feat(p, me, t_);
-          const float cr = p.close[(size_t)me * p.T + t_];
+          const float cr = p.close[o], rr = p.ret[o];
           fx = done ? fr : fx;
           cx = done ? cr : cx;
+          rx = done ? rr : rx;
         }
         if (writer) {
           p.ra[slot_ * S + s] = (unsigned char)a;
@@ -521,8 +536,10 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
         }
         // prefetch bar t1+1 for the next env phase (issued last: a whole MFMA phase to land)
         cA = cx;
+        rA = rx;
         const size_t o1 = (size_t)me * p.T + min(t_ + 1, p.T - 1);
         cB = p.close[o1];
+        rB = p.ret[o1];
         fB = *reinterpret_cast<const uint4*>(p.feat + o1 * RMF);
       }
       GR_STAMP(5)
@@ -841,7 +858,7 @@ extern "C" hipError_t st_gru_pack(const st::GruPack* p, hipStream_t s) {
 extern "C" int st_gru_act_lds_bytes() { return st::ActLds::BYTES; }
 
 extern "C" hipError_t st_gru_act(const st::GruAct* p, int grid, hipStream_t s) {
-  if (p->E % st::RN || p->S <= 0 || p->ep_len <= 0 || p->T < p->ep_len + 3 || p->cap <= 0 || grid <= 0)
+  if (p->E % st::RN || p->S <= 0 || p->S > 64 || p->ep_len <= 0 || p->T < p->ep_len + 3 || p->cap <= 0 || grid <= 0)
     return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {

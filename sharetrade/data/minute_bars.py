@@ -110,3 +110,15 @@ def generate_gpu(E: int, T: int, device: torch.device, bp: BarParams = BarParams
                          bp.p0, k0, k1)
     native.check(G.lib().st_minute_bars(a, native.stream_handle()), "st_minute_bars")
     return close, feat
+
+
+def bar_returns(close):
+    """ret[:, t] = (close[:, t+1] / close[:, t] - 1) * 100 (float32, last bar 0) -- the env's
+    per-bar reward of a long unit, precomputed once so the actor's env step has no division."""
+    if isinstance(close, np.ndarray):
+        r = np.zeros_like(close, dtype=np.float32)
+        r[:, :-1] = (close[:, 1:] / close[:, :-1] - np.float32(1)) * np.float32(100)
+        return r
+    r = torch.zeros_like(close)
+    r[:, :-1] = (close[:, 1:] / close[:, :-1] - 1.0) * 100.0
+    return r

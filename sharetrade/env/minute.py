@@ -5,7 +5,8 @@ Semantics (a per-bar version of the reference's Buy/Sell/Hold decisions,
 `TrainerChildActor.scala:118-123`, with one share like its ``shares`` counter):
 
 * action 0 Buy -> long 1 unit (entry = close_t when opening), 1 Sell -> flat, 2 Hold -> keep;
-* reward = position' * (close_{t+1} / close_t - 1) * 100 - cost * [position changed];
+* reward = position' * ret_t - cost * [position changed], ret_t = (close_{t+1} / close_t - 1) * 100
+  precomputed per bar (``data.minute_bars.bar_returns``);
 * an episode is ``ep_len`` bars from a random start; on the last bar the env resets to a new
   Philox-drawn start, flat, and the recurrent state restarts from zero;
 * exploration: exploit with probability ``min(eps, step * inv_ramp)`` (``step`` = global actor
@@ -42,7 +43,7 @@ def obs(feat_row: np.ndarray, close_t: float, st: MinuteEnvState, ep_len: int) -
     x[:8] = feat_row
     x[8] = f32(st.pz)
     x[9] = (f32(close_t) / f32(st.entry) - f32(1)) * f32(100) if st.pz else f32(0)
-    x[10] = f32(st.t - st.es) / f32(ep_len)
+    x[10] = f32(st.t - st.es) * f32(1.0 / ep_len)
     x[11] = f32(1)
     return x
 
@@ -54,14 +55,15 @@ def draws(env: int, step: int, key0, key1):
     return rng.u24(c0), rng.u24(c1), rng.u24(c2)
 
 
-def step(st: MinuteEnvState, a: int, close: np.ndarray, T: int, ep_len: int, cost: float, u_reset: float):
+def step(st: MinuteEnvState, a: int, close: np.ndarray, ret: np.ndarray, T: int, ep_len: int, cost: float,
+         u_reset: float):
     """Apply action ``a`` at bar ``st.t`` in place; returns (reward, done, finished-episode return)."""
-    c_t, c_n = f32(close[st.t]), f32(close[st.t + 1])
+    c_t = f32(close[st.t])
     np_ = 1 if a == 0 else (0 if a == 1 else st.pz)
     trade = np_ != st.pz
     if trade and np_ == 1:
         st.entry = float(c_t)
-    rew = f32(np_) * (c_n / c_t - f32(1)) * f32(100) - (f32(cost) if trade else f32(0))
+    rew = f32(np_) * f32(ret[st.t]) - (f32(cost) if trade else f32(0))
     st.ep_ret = float(f32(st.ep_ret) + rew)
     t1 = st.t + 1
     done = (t1 - st.es) >= ep_len

@@ -44,9 +44,9 @@ class PackArgs(C.Structure):
 
 class ActArgs(C.Structure):
     _fields_ = [("whh8", C.c_void_p), ("whhs", C.c_void_p), ("wih", C.c_void_p), ("bias4", C.c_void_p),
-                ("wq", C.c_void_p), ("feat", C.c_void_p), ("close", C.c_void_p),
+                ("wq", C.c_void_p), ("feat", C.c_void_p), ("close", C.c_void_p), ("ret", C.c_void_p),
                 ("E", C.c_int), ("T", C.c_int), ("S", C.c_int), ("ep_len", C.c_int),
-                ("eps", C.c_float), ("inv_ramp", C.c_float), ("cost", C.c_float),
+                ("eps", C.c_float), ("inv_ramp", C.c_float), ("cost", C.c_float), ("inv_ep_len", C.c_float),
                 ("h", C.c_void_p), ("pos", C.c_void_p), ("ep_start", C.c_void_p), ("position", C.c_void_p),
                 ("entry", C.c_void_p), ("ep_ret", C.c_void_p), ("episodes", C.c_void_p), ("last_ret", C.c_void_p),
                 ("rx", C.c_void_p), ("ra", C.c_void_p), ("rr", C.c_void_p), ("rd", C.c_void_p), ("rh0", C.c_void_p),

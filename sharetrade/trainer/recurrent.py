@@ -16,8 +16,8 @@ actor-learner style (R2D2-like stored-state sequence replay):
   actor's fp8 weights.  Both halves are captured in HIP graphs.
 
 Env (minute-bar trading, long-only single unit like the reference's share count):
-Buy -> long, Sell -> flat, Hold -> keep; reward = position * (c_{t+1}/c_t - 1) * 100
-minus ``cost`` per position change; episodes are ``ep_len`` bars from a random start.
+Buy -> long, Sell -> flat, Hold -> keep; reward = position * ret_t - ``cost`` per position
+change, with ``ret_t = (c_{t+1}/c_t - 1) * 100`` precomputed per bar (``minute_bars.bar_returns``); episodes are ``ep_len`` bars from a random start.
 x_t = 8 market features ++ (position, unrealised pnl %, elapsed fraction, 1) zero-padded to 32.
 """
 from __future__ import annotations
@@ -105,6 +105,7 @@ class RecurrentDQN:
         # ---------------------------------------------------------------- data + envs
         self.bp = bar_params or mb.BarParams()
         self.close, self.feat = mb.generate_gpu(self.E, self.T, dev, self.bp, seed=self.seed)
+        self.ret = mb.bar_returns(self.close)
         g = np.random.default_rng(self.seed)
         start = torch.from_numpy(g.integers(0, self.T - self.ep_len - 1, size=self.E).astype(np.int32)).to(dev)
         self.h = torch.zeros(self.E, HID, device=dev)
@@ -165,10 +166,11 @@ class RecurrentDQN:
         a = G.ActArgs()
         a.whh8, a.whhs, a.wih, a.bias4, a.wq = (self.whh8.data_ptr(), self.whhs.data_ptr(), self.wih_pk.data_ptr(),
                                                 self.bias4.data_ptr(), self.wq4.data_ptr())
-        a.feat, a.close = self.feat.data_ptr(), self.close.data_ptr()
+        a.feat, a.close, a.ret = self.feat.data_ptr(), self.close.data_ptr(), self.ret.data_ptr()
         a.E, a.T, a.S, a.ep_len = self.E, self.T, self.S, self.ep_len
         ag = self.cfg.agent
         a.eps, a.inv_ramp, a.cost = float(ag.epsilon), float(np.float32(1.0 / ag.ramp)), self.cost
+        a.inv_ep_len = float(np.float32(1.0 / self.ep_len))
         for n in ("h", "pos", "ep_start", "position", "entry", "ep_ret", "episodes", "last_ret"):
             setattr(a, n, getattr(self, n).data_ptr())
         a.rx, a.ra, a.rr, a.rd, a.rh0 = (self.rx.data_ptr(), self.ra.data_ptr(), self.rr.data_ptr(),

@@ -83,6 +83,7 @@ def _ref_actor(d, steps, eps_exploit):
     b_ih, b_hh = d.P["b_ih"].cpu().view(-1).double(), d.P["b_hh"].cpu().view(-1).double()
     Wq, bq = d.P["w_q"].cpu().double(), d.P["b_q"].cpu().view(-1).double()
     close = d.close.cpu().numpy()
+    ret = d.ret.cpu().numpy()
     feat = d.feat.float().cpu().numpy()
     k0, k1 = rng.key_for(d.seed, 5)
     pos, es = d.pos.cpu().numpy(), d.ep_start.cpu().numpy()
@@ -109,7 +110,7 @@ def _ref_actor(d, steps, eps_exploit):
             rnd = min(int(u_act * np.float32(3.0)), 2)
             exploit = u_exp < min(np.float32(eps_exploit), np.float32(gstep) * np.float32(1.0 / d.cfg.agent.ramp))
             a = int(torch.argmax(q[e])) if exploit else rnd
-            rew, done, _ = me.step(states[e], a, close[e], T, d.ep_len, d.cost, u_rst)
+            rew, done, _ = me.step(states[e], a, close[e], ret[e], T, d.ep_len, d.cost, u_rst)
             a_s.append(a); r_s.append(rew); d_s.append(done)
             xn.append(me.obs(feat[e, states[e].t], close[e, states[e].t], states[e], d.ep_len))
             if done:

@@ -79,17 +79,19 @@ def test_sequence_loss_masks_and_backprops():
 
 def test_minute_env_semantics():
     close = np.array([10.0, 11.0, 12.1, 12.1, 13.0, 14.0, 15.0, 16.0, 17.0, 18.0], np.float32)
+    ret = mb.bar_returns(close[None])[0]
+    assert abs(ret[0] - 10.0) < 1e-4 and ret[-1] == 0
     st = me.MinuteEnvState(t=0, es=0)
-    r, done, _ = me.step(st, 0, close, len(close), 3, 0.5, 0.0)              # buy at 10 -> +10% - cost
+    r, done, _ = me.step(st, 0, close, ret, len(close), 3, 0.5, 0.0)         # buy at 10 -> +10% - cost
     assert st.pz == 1 and st.entry == 10.0 and not done
     assert abs(r - (10.0 - 0.5)) < 1e-4
-    r, done, _ = me.step(st, 2, close, len(close), 3, 0.5, 0.0)              # hold long 11 -> 12.1
+    r, done, _ = me.step(st, 2, close, ret, len(close), 3, 0.5, 0.0)         # hold long 11 -> 12.1
     assert abs(r - 10.0) < 1e-3 and st.pz == 1
     x = me.obs(np.zeros(8, np.float32), close[st.t], st, 3)
     assert x[8] == 1 and abs(x[9] - 21.0) < 1e-3 and abs(x[10] - 2 / 3) < 1e-6 and x[11] == 1
-    r, done, fin = me.step(st, 1, close, len(close), 3, 0.5, 0.5)            # sell (flat: 0 - cost), episode ends
+    r, done, fin = me.step(st, 1, close, ret, len(close), 3, 0.5, 0.5)       # sell (flat: 0 - cost), episode ends
     assert done and abs(r + 0.5) < 1e-6 and st.pz == 0 and st.episodes == 1
     assert abs(fin - (9.5 + 10.0 - 0.5)) < 1e-3
     assert st.es == min(int(np.float32(0.5) * np.float32(len(close) - 3 - 1)), len(close) - 3 - 2) == st.t
-    r, _, _ = me.step(st, 1, close, len(close), 3, 0.5, 0.0)                 # sell while flat: no trade
+    r, _, _ = me.step(st, 1, close, ret, len(close), 3, 0.5, 0.0)            # sell while flat: no trade
     assert r == 0.0 and st.pz == 0
