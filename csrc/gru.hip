@@ -21,59 +21,10 @@
 //     exactly one wave's unit range, so amax is a 4-lane reduction;
 //   * Q = W_q h is reduced across waves through LDS; wave 0 runs epsilon-greedy
 //     (Philox), the minute-bar trading env, and writes the replay segment.
-// Learner: bf16 MFMA GEMMs (gemm_bf16.hip) for the gate products + the fused
-// elementwise kernels below (forward with saves, TD, backward-through-time).
-#include "common.h"
+// Learner: csrc/gru_learn.hip.
+#include "gru_common.h"
 
 namespace st {
-
-typedef int i8v __attribute__((ext_vector_type(8)));   // 32 fp8 bytes: one MX A/B fragment
-
-constexpr int RH = 256;            // hidden units
-constexpr int RG = 3 * RH;         // gate rows
-constexpr int RF = 32;             // actor x width (bf16, one K=32 MFMA step)
-constexpr int RFL = 64;            // learner x width (GEMM K multiple of 64)
-constexpr int RMF = 8;             // market features per bar
-constexpr int RW = 8;              // waves per actor workgroup
-constexpr int RN = 32;             // envs per actor chunk
-constexpr int RT = RW * 64;
-constexpr int XS = RF + 8;         // sX row stride (bf16) = 80 B: conflict-free ds_read_b128
-constexpr int HS = RH + 16;        // sH8 row stride (bytes) = 272 B
-constexpr int SCS = 9;             // scale row stride (ints)
-
-// ---------------------------------------------------------------- MX-fp8 helpers
-ST_DEV f4v mx_mfma(const i8v& a, const i8v& b, f4v c, int sa, int sb) {
-  // fmt 0/0 = e4m3 x e4m3; scales are E8M0 bytes (byte 0 of sa / sb)
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
-}
-// same, with the A scale taken from byte SEL of a packed register (op_sel), 4 scales per VGPR
-template <int SEL>
-ST_DEV f4v mx_mfma_sel(const i8v& a, const i8v& b, f4v c, int sa4, int sb) {
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, SEL, sa4, 0, sb);
-}
-// smallest e with amax / 2^e <= 448 (e4m3 max): e = ceil(log2(amax / 448))
-ST_DEV int mx_exp(float amax) {
-  if (!(amax > 0.f)) return -127;
-  int e;
-  const float m = frexpf(amax * (1.0f / 448.0f), &e);
-  if (m == 0.5f) e -= 1;
-  if (ldexpf(amax, -e) > 448.f) e += 1;
-  return e < -127 ? -127 : (e > 127 ? 127 : e);
-}
-ST_DEV uint32_t fp8x4(float a, float b, float c, float d) {
-  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
-  return (uint32_t)v;
-}
-// raw v_exp_f32 / v_rcp_f32 (1 ulp): __frcp_rn would expand to the IEEE division sequence
-ST_DEV float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-// actor epilogue forms: exp2 with the log2(e) scale folded, explicit FMAs (the build keeps
-// -ffp-contract=off for the bit-exact env arithmetic, so contraction is spelled out here)
-ST_DEV float sigm2(float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -1.44269504f)); }
-ST_DEV float tanh2(float x) {
-  return __builtin_fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -2.88539008f)), -1.f);
-}
-ST_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
 
 // ---------------------------------------------------------------- synthetic minute bars
 struct MinuteBars {
@@ -237,27 +188,6 @@ struct ActLds {
   static constexpr int BYTES = U + 64 * RN * 16;
 };
 static_assert(ActLds::BYTES <= 160 * 1024, "actor LDS");
-
-// quantize the lane's h values (units of this wave, 2 env tiles) into an LDS fp8 tile
-ST_DEV void quant_h(const float (&hr)[2][2][4], unsigned char* sH8, int* sSc, int wave, int l16, int g4) {
-#pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    float amax = 0.f;
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(hr[m][n][i]));
-    amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-    amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
-    const int e = mx_exp(amax);
-    const int row = 16 * n + l16;
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-      *reinterpret_cast<uint32_t*>(sH8 + row * HS + 32 * wave + 16 * m + 4 * g4) =
-          fp8x4(ldexpf(hr[m][n][0], -e), ldexpf(hr[m][n][1], -e), ldexpf(hr[m][n][2], -e), ldexpf(hr[m][n][3], -e));
-    if (g4 == 0) sSc[row * SCS + wave] = e + 127;
-  }
-}
 
 // build the x row (bf16 [RF]) from bar features mf / close c into LDS and (if rx_row) the replay segment
 ST_DEV void build_x(const GruAct& p, uint4 mf, float c, int t, int es, int pz, float entry, bf16_t* sx_row,
@@ -589,251 +519,6 @@ __global__ void gru_advance_kernel(unsigned long long* rctrl, unsigned long long
   ctrl[0] += 1;
 }
 
-// ---------------------------------------------------------------- learner: sequence gather
-struct GruGather {
-  const bf16_t* rx;
-  const unsigned char* ra;
-  const float* rr;
-  const unsigned char* rd;
-  const bf16_t* rh0;
-  const unsigned long long* rctrl;
-  int cap, S, B;
-  uint32_t key0, key1;
-  const unsigned long long* step;   // update counter (device)
-  bf16_t* X;         // [(S+1)B][RFL] time-major rows t*B + b
-  bf16_t* Hm;        // [(S+1)B][RH] block 0 <- h0
-  bf16_t* Hm_t;      // target copy of block 0
-  float* Hf;         // [B][RH]
-  float* Hf_t;       // [B][RH]
-  int* A;            // [S][B]
-  float* R;
-  float* D;
-};
-
-// one wave per sampled segment
-__global__ void __launch_bounds__(256) gru_gather_kernel(GruGather g) {
-  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (b >= g.B) return;
-  const unsigned long long sz = g.rctrl[1], st = g.step[0];
-  uint32_t c0 = (uint32_t)b, c1 = (uint32_t)(st & 0xFFFFFFFFull), c2 = (uint32_t)(st >> 32), c3 = 0x53455131u;
-  philox4x32(c0, c1, c2, c3, g.key0, g.key1);
-  const size_t idx = (size_t)(((((unsigned long long)c0) << 32) | c1) % (sz ? sz : 1ull));
-  const int S = g.S;
-  const uint4 z = {0u, 0u, 0u, 0u};
-  for (int j = lane; j < (S + 1) * 8; j += 64) {
-    const int t = j >> 3, c = j & 7;
-    uint4 v = z;
-    if (c < RF / 8) v = reinterpret_cast<const uint4*>(g.rx + (idx * (size_t)(S + 1) + t) * RF)[c];
-    reinterpret_cast<uint4*>(g.X + ((size_t)t * g.B + b) * RFL)[c] = v;
-  }
-  {
-    const s4v hv = *reinterpret_cast<const s4v*>(g.rh0 + idx * RH + 4 * lane);
-    *reinterpret_cast<s4v*>(g.Hm + (size_t)b * RH + 4 * lane) = hv;
-    *reinterpret_cast<s4v*>(g.Hm_t + (size_t)b * RH + 4 * lane) = hv;
-    const float4 f = make_float4(bf2f((bf16_t)hv[0]), bf2f((bf16_t)hv[1]), bf2f((bf16_t)hv[2]), bf2f((bf16_t)hv[3]));
-    *reinterpret_cast<float4*>(g.Hf + (size_t)b * RH + 4 * lane) = f;
-    *reinterpret_cast<float4*>(g.Hf_t + (size_t)b * RH + 4 * lane) = f;
-  }
-  if (lane < S) {
-    g.A[(size_t)lane * g.B + b] = g.ra[idx * S + lane];
-    g.R[(size_t)lane * g.B + b] = g.rr[idx * S + lane];
-    g.D[(size_t)lane * g.B + b] = (float)g.rd[idx * S + lane];
-  }
-}
-
-// ---------------------------------------------------------------- learner: forward step
-struct GruFwd {
-  const float* Gx;    // [(S+1)B][RG] (x . W_ih^T + b_ih)
-  const float* Gh;    // [B][RG]      (h . W_hh^T + b_hh) of this step
-  float* Hf;          // [B][RH] in: masked h_{t-1}; out: masked h_t
-  bf16_t* Hm;         // [(S+1)B][RH]: row (t+1)B + b <- masked h_t (t < S)
-  const float* wq;    // [3][RH]
-  const float* bq;    // [3]
-  float* Q;           // [(S+1)B][4]
-  const float* D;     // [S][B]
-  float* sr;          // saves for the backward pass (online net, t < S) or null
-  float* sz;
-  float* sn;
-  float* sgh;
-  float* shp;
-  bf16_t* Hq;         // [S*B][RH] unmasked h_t (W_q gradient)
-  int B, S, t;
-};
-
-// one wave per batch row; lane owns units 4l..4l+3
-__global__ void __launch_bounds__(256) gru_fwd_kernel(GruFwd f) {
-  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (b >= f.B) return;
-  const int u = 4 * lane;
-  const size_t row = (size_t)f.t * f.B + b;
-  const float* gx = f.Gx + row * RG;
-  const float* gh = f.Gh + (size_t)b * RG;
-  const float4 xr = *reinterpret_cast<const float4*>(gx + u), xz = *reinterpret_cast<const float4*>(gx + RH + u),
-               xn = *reinterpret_cast<const float4*>(gx + 2 * RH + u);
-  const float4 hr_ = *reinterpret_cast<const float4*>(gh + u), hz_ = *reinterpret_cast<const float4*>(gh + RH + u),
-               hn_ = *reinterpret_cast<const float4*>(gh + 2 * RH + u);
-  const float4 hp4 = *reinterpret_cast<const float4*>(f.Hf + (size_t)b * RH + u);
-  const float ax[4] = {xr.x, xr.y, xr.z, xr.w}, az_[4] = {xz.x, xz.y, xz.z, xz.w}, an[4] = {xn.x, xn.y, xn.z, xn.w};
-  const float bx[4] = {hr_.x, hr_.y, hr_.z, hr_.w}, bz_[4] = {hz_.x, hz_.y, hz_.z, hz_.w},
-              bn[4] = {hn_.x, hn_.y, hn_.z, hn_.w};
-  const float hp[4] = {hp4.x, hp4.y, hp4.z, hp4.w};
-  float r[4], z[4], n[4], h[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    r[i] = 1.f / (1.f + expf(-(ax[i] + bx[i])));
-    z[i] = 1.f / (1.f + expf(-(az_[i] + bz_[i])));
-    n[i] = tanhf(an[i] + r[i] * bn[i]);
-    h[i] = (1.f - z[i]) * n[i] + z[i] * hp[i];
-  }
-  float q[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const float4 w = *reinterpret_cast<const float4*>(f.wq + a * RH + u);
-    q[a] = wave_sum(w.x * h[0] + w.y * h[1] + w.z * h[2] + w.w * h[3]);
-  }
-  if (lane == 0) {
-    float* qo = f.Q + row * 4;
-    qo[0] = q[0] + f.bq[0]; qo[1] = q[1] + f.bq[1]; qo[2] = q[2] + f.bq[2]; qo[3] = 0.f;
-  }
-  if (f.t < f.S) {
-    if (f.sr) {
-      const size_t o = row * RH + u;
-      *reinterpret_cast<float4*>(f.sr + o) = make_float4(r[0], r[1], r[2], r[3]);
-      *reinterpret_cast<float4*>(f.sz + o) = make_float4(z[0], z[1], z[2], z[3]);
-      *reinterpret_cast<float4*>(f.sn + o) = make_float4(n[0], n[1], n[2], n[3]);
-      *reinterpret_cast<float4*>(f.sgh + o) = make_float4(bn[0], bn[1], bn[2], bn[3]);
-      *reinterpret_cast<float4*>(f.shp + o) = make_float4(hp[0], hp[1], hp[2], hp[3]);
-      lds_st4(f.Hq + o, h[0], h[1], h[2], h[3]);
-    }
-    const float keep = 1.f - f.D[row];
-    float hm[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) hm[i] = keep * h[i];
-    *reinterpret_cast<float4*>(f.Hf + (size_t)b * RH + u) = make_float4(hm[0], hm[1], hm[2], hm[3]);
-    lds_st4(f.Hm + (row + f.B) * RH + u, hm[0], hm[1], hm[2], hm[3]);
-  }
-}
-
-// ---------------------------------------------------------------- learner: TD targets (double DQN)
-struct GruTD {
-  const float* Q;     // [(S+1)B][4] online
-  const float* Qt;    // [(S+1)B][4] target net
-  const int* A;
-  const float* R;
-  const float* D;     // [S][B]
-  float* dQ;          // [S*B][4]
-  float* loss;        // [1] (atomic)
-  int B, S, burn;
-  float gamma, coef;
-};
-
-__global__ void __launch_bounds__(256) gru_td_kernel(GruTD p) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  float l = 0.f;
-  if (i < p.S * p.B) {
-    const int t = i / p.B;
-    const float* qn = p.Q + ((size_t)i + p.B) * 4;
-    int as = 0;
-    if (qn[1] > qn[as]) as = 1;
-    if (qn[2] > qn[as]) as = 2;
-    const float y = p.R[i] + p.gamma * (1.f - p.D[i]) * p.Qt[((size_t)i + p.B) * 4 + as];
-    const int a = p.A[i];
-    const float d = p.Q[(size_t)i * 4 + a] - y;
-    const bool on = t >= p.burn;
-    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (on) {
-      const float v = p.coef * d;
-      if (a == 0) g.x = v; else if (a == 1) g.y = v; else g.z = v;
-      l = d * d;
-    }
-    *reinterpret_cast<float4*>(p.dQ + (size_t)i * 4) = g;
-  }
-  l = wave_sum(l);
-  if ((threadIdx.x & 63) == 0) atomicAdd(p.loss, l);
-}
-
-// ---------------------------------------------------------------- learner: backward step
-struct GruBwd {
-  const float* dQ;    // [S*B][4]
-  const float* D;     // [S][B]
-  float* DH;          // [B][RH]: in dL/d(masked h_t) from step t+1; out: direct part of dL/dh_{t-1}
-  const float* sr;
-  const float* sz;
-  const float* sn;
-  const float* sgh;
-  const float* shp;
-  const float* wq;    // [3][RH]
-  bf16_t* dGx;        // [S*B][RG]
-  bf16_t* dGh;        // [S*B][RG]
-  int B, S, t;
-};
-
-__global__ void __launch_bounds__(256) gru_bwd_kernel(GruBwd p) {
-  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (b >= p.B) return;
-  const int u = 4 * lane;
-  const size_t row = (size_t)p.t * p.B + b, o = row * RH + u;
-  const float4 dq = *reinterpret_cast<const float4*>(p.dQ + row * 4);
-  float dh[4] = {0.f, 0.f, 0.f, 0.f};
-  if (p.t < p.S - 1) {
-    const float keep = 1.f - p.D[row];
-    const float4 d = *reinterpret_cast<const float4*>(p.DH + (size_t)b * RH + u);
-    dh[0] = keep * d.x; dh[1] = keep * d.y; dh[2] = keep * d.z; dh[3] = keep * d.w;
-  }
-  {
-    const float4 w0 = *reinterpret_cast<const float4*>(p.wq + u), w1 = *reinterpret_cast<const float4*>(p.wq + RH + u),
-                 w2 = *reinterpret_cast<const float4*>(p.wq + 2 * RH + u);
-    dh[0] += dq.x * w0.x + dq.y * w1.x + dq.z * w2.x;
-    dh[1] += dq.x * w0.y + dq.y * w1.y + dq.z * w2.y;
-    dh[2] += dq.x * w0.z + dq.y * w1.z + dq.z * w2.z;
-    dh[3] += dq.x * w0.w + dq.y * w1.w + dq.z * w2.w;
-  }
-  const float4 r4 = *reinterpret_cast<const float4*>(p.sr + o), z4 = *reinterpret_cast<const float4*>(p.sz + o),
-               n4 = *reinterpret_cast<const float4*>(p.sn + o), g4_ = *reinterpret_cast<const float4*>(p.sgh + o),
-               h4 = *reinterpret_cast<const float4*>(p.shp + o);
-  const float r[4] = {r4.x, r4.y, r4.z, r4.w}, z[4] = {z4.x, z4.y, z4.z, z4.w}, n[4] = {n4.x, n4.y, n4.z, n4.w},
-              gh[4] = {g4_.x, g4_.y, g4_.z, g4_.w}, hp[4] = {h4.x, h4.y, h4.z, h4.w};
-  float dar[4], daz[4], dan[4], dghn[4], dhp[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float dn = dh[i] * (1.f - z[i]);
-    const float dz = dh[i] * (hp[i] - n[i]);
-    dhp[i] = dh[i] * z[i];
-    dan[i] = dn * (1.f - n[i] * n[i]);
-    const float dr = dan[i] * gh[i];
-    dghn[i] = dan[i] * r[i];
-    dar[i] = dr * r[i] * (1.f - r[i]);
-    daz[i] = dz * z[i] * (1.f - z[i]);
-  }
-  bf16_t* gx = p.dGx + row * RG;
-  bf16_t* gh_ = p.dGh + row * RG;
-  lds_st4(gx + u, dar[0], dar[1], dar[2], dar[3]);
-  lds_st4(gx + RH + u, daz[0], daz[1], daz[2], daz[3]);
-  lds_st4(gx + 2 * RH + u, dan[0], dan[1], dan[2], dan[3]);
-  lds_st4(gh_ + u, dar[0], dar[1], dar[2], dar[3]);
-  lds_st4(gh_ + RH + u, daz[0], daz[1], daz[2], daz[3]);
-  lds_st4(gh_ + 2 * RH + u, dghn[0], dghn[1], dghn[2], dghn[3]);
-  *reinterpret_cast<float4*>(p.DH + (size_t)b * RH + u) = make_float4(dhp[0], dhp[1], dhp[2], dhp[3]);
-}
-
-// dW_q[a][u] = sum_rows dQ[row][a] h[row][u], db_q[a] = sum_rows dQ[row][a] (atomic partials)
-__global__ void __launch_bounds__(256) gru_wq_grad_kernel(const float* __restrict__ dQ, const bf16_t* __restrict__ Hq,
-                                                          int rows, int per, float* dwq, float* dbq) {
-  const int u = threadIdx.x;
-  const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, b0 = 0.f;
-  for (int r = r0; r < r1; ++r) {
-    const float4 d = *reinterpret_cast<const float4*>(dQ + (size_t)r * 4);
-    const float h = bf2f(Hq[(size_t)r * RH + u]);
-    a0 += d.x * h; a1 += d.y * h; a2 += d.z * h;
-    if (u < 3) b0 += u == 0 ? d.x : (u == 1 ? d.y : d.z);
-  }
-  atomicAdd(dwq + u, a0);
-  atomicAdd(dwq + RH + u, a1);
-  atomicAdd(dwq + 2 * RH + u, a2);
-  if (u < 3) atomicAdd(dbq + u, b0);
-}
-
 // MX-fp8 MFMA probe: D = (A * 2^(sa-127)) . (B * 2^(sb-127))^T for one 16x16x128 tile (layout tests)
 __global__ void mx_probe_kernel(const i8v* a, const i8v* b, const int* sa, const int* sb, f4v* d) {
   const int l = threadIdx.x;
@@ -873,34 +558,10 @@ extern "C" hipError_t st_gru_act(const st::GruAct* p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-extern "C" hipError_t st_gru_gather(const st::GruGather* g, hipStream_t s) {
-  if (g->S > 64 || g->S <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(st::gru_gather_kernel, dim3((g->B + 3) / 4), dim3(256), 0, s, *g);
-  return hipGetLastError();
-}
 
-extern "C" hipError_t st_gru_fwd(const st::GruFwd* f, hipStream_t s) {
-  hipLaunchKernelGGL(st::gru_fwd_kernel, dim3((f->B + 3) / 4), dim3(256), 0, s, *f);
-  return hipGetLastError();
-}
 
-extern "C" hipError_t st_gru_td(const st::GruTD* p, hipStream_t s) {
-  hipLaunchKernelGGL(st::gru_td_kernel, dim3((p->S * p->B + 255) / 256), dim3(256), 0, s, *p);
-  return hipGetLastError();
-}
 
-extern "C" hipError_t st_gru_bwd(const st::GruBwd* p, hipStream_t s) {
-  hipLaunchKernelGGL(st::gru_bwd_kernel, dim3((p->B + 3) / 4), dim3(256), 0, s, *p);
-  return hipGetLastError();
-}
 
-extern "C" hipError_t st_gru_wq_grad(const float* dQ, const bf16_t* Hq, int rows, float* dwq, float* dbq,
-                                     hipStream_t s) {
-  const int per = 64;
-  hipLaunchKernelGGL(st::gru_wq_grad_kernel, dim3((rows + per - 1) / per), dim3(st::RH), 0, s, dQ, Hq, rows, per, dwq,
-                     dbq);
-  return hipGetLastError();
-}
 
 extern "C" hipError_t st_mx_probe(const void* a, const void* b, const int* sa, const int* sb, float* d,
                                   hipStream_t s) {

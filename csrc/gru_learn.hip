@@ -1,0 +1,576 @@
+// Fused learner of the GRU(256) recurrent Q-net (BASELINE config 5).
+//
+// Replaces a per-time-step chain of GEMM + elementwise launches (~130 kernels per update)
+// with two persistent kernels; a workgroup owns 32 sampled sequences for all time steps,
+// wave w owns hidden units 32w..32w+31 of all three gates (the actor's tiling, gru.hip):
+//
+//   gru_seq_fwd_kernel  (grid B/32 x 2: online and target net in one launch)
+//     S+1 steps of the recurrence on-chip, exactly the actor's arithmetic: W_hh as MX-fp8
+//     fragments resident in VGPRs (v_mfma_scale_f32_16x16x128_f8f6f4), W_ih bf16 in LDS,
+//     h fp32 in registers, re-quantized per step; Q head as one bf16 MFMA per tile.
+//     The online net saves r, z, n, gh_n, h_prev (bf16, in the lanes' own accumulator
+//     order -> one 16-byte store / load per quantity and tile) and the masked h rows the
+//     weight-gradient GEMM needs.
+//   gru_seq_bwd_kernel  (grid B/32)
+//     backward through time: the recurrent gradient dL/dh stays in registers; per step
+//     the fused GRU backward writes dGx / dGh (bf16) and the dGh tile to LDS, then
+//     dh_{t-1} = dGh . W_hh is one 32x256x768 product per workgroup on bf16 MFMAs with
+//     W_hh^T streamed from L2 (384 KB shared by all workgroups) through a register ring.
+//     Bias and W_q gradients are reduced in registers and added once per workgroup.
+// The forward uses the quantized W_hh, the backward the bf16 master copy (straight-through,
+// the usual fp8-training split); weight gradients dW_hh / dW_ih stay split-K GEMMs.
+#include "gru_common.h"
+
+namespace st {
+
+constexpr int LB = 32;      // sequences per workgroup
+constexpr int NSV = 5;      // saved quantities: r, z, n, gh_n, h_prev
+constexpr int GS = RG + 8;  // dGh LDS tile row stride (bf16): 1552 B, 16-B aligned
+
+// ---------------------------------------------------------------- sequence gather
+struct GruGather {
+  const bf16_t* rx;
+  const unsigned char* ra;
+  const float* rr;
+  const unsigned char* rd;
+  const bf16_t* rh0;
+  const unsigned long long* rctrl;
+  int cap, S, B;
+  uint32_t key0, key1;
+  const unsigned long long* step;   // update counter (device, graph-replay safe)
+  bf16_t* X;         // [(S+1)B][RFL] time-major rows t*B + b (columns >= RF zero)
+  float* H0;         // [B][RH]
+  int* A;            // [S][B]
+  float* R;
+  float* D;
+};
+
+// one wave per sampled segment (uniform over the filled ring, Philox counter = (row, update))
+__global__ void __launch_bounds__(256) gru_gather_kernel(GruGather g) {
+  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (b >= g.B) return;
+  const unsigned long long sz = g.rctrl[1], st = g.step[0];
+  uint32_t c0 = (uint32_t)b, c1 = (uint32_t)(st & 0xFFFFFFFFull), c2 = (uint32_t)(st >> 32), c3 = 0x53455131u;
+  philox4x32(c0, c1, c2, c3, g.key0, g.key1);
+  const size_t idx = (size_t)(((((unsigned long long)c0) << 32) | c1) % (sz ? sz : 1ull));
+  const int S = g.S;
+  const uint4 z = {0u, 0u, 0u, 0u};
+  for (int j = lane; j < (S + 1) * 8; j += 64) {
+    const int t = j >> 3, c = j & 7;
+    uint4 v = z;
+    if (c < RF / 8) v = reinterpret_cast<const uint4*>(g.rx + (idx * (size_t)(S + 1) + t) * RF)[c];
+    reinterpret_cast<uint4*>(g.X + ((size_t)t * g.B + b) * RFL)[c] = v;
+  }
+  const s4v hv = *reinterpret_cast<const s4v*>(g.rh0 + idx * RH + 4 * lane);
+  *reinterpret_cast<float4*>(g.H0 + (size_t)b * RH + 4 * lane) =
+      make_float4(bf2f((bf16_t)hv[0]), bf2f((bf16_t)hv[1]), bf2f((bf16_t)hv[2]), bf2f((bf16_t)hv[3]));
+  if (lane < S) {
+    g.A[(size_t)lane * g.B + b] = g.ra[idx * S + lane];
+    g.R[(size_t)lane * g.B + b] = g.rr[idx * S + lane];
+    g.D[(size_t)lane * g.B + b] = (float)g.rd[idx * S + lane];
+  }
+}
+
+// ---------------------------------------------------------------- fused forward
+struct GruNetW {
+  const i8v* whh8;
+  const int* whhs;
+  const s8v* wih;
+  const float* bias4;
+  const float* wq;
+};
+
+struct GruSeqFwd {
+  GruNetW on, tg;       // online / target packed weights (gru_pack_kernel layout)
+  const bf16_t* X;      // [(S+1)B][RFL]
+  const float* H0;      // [B][RH]
+  const float* D;       // [S][B]
+  float* Q;             // [(S+1)B][4] online
+  float* Qt;            // [(S+1)B][4] target
+  bf16_t* Hm;           // [(S+1)B][RH] online: block t = masked h_{t-1} (block 0 = h0)
+  uint4* sv;            // online saves [S][B/LB][RW][NSV][2][64] x 16 B
+  int B, S;
+};
+
+struct FwdLds {
+  static constexpr int WX = 0;                          // RW*6*64 s8v
+  static constexpr int X = WX + RW * 6 * 64 * 16;       // [2][LB*XS] bf16
+  static constexpr int H8 = X + 2 * LB * XS * 2;        // [2][LB*HS] bytes
+  static constexpr int SC = H8 + 2 * LB * HS;           // [2][LB*SCS] int
+  static constexpr int B = SC + 2 * LB * SCS * 4;       // [4*RH] float
+  static constexpr int WQ = B + 4 * RH * 4;             // [4*RH] float
+  static constexpr int QP = WQ + 4 * RH * 4;            // [2][RW][3][LB] float
+  static constexpr int BYTES = QP + 2 * RW * 3 * LB * 4;
+};
+static_assert(FwdLds::BYTES <= 160 * 1024, "fwd LDS");
+
+ST_DEV uint4 pack8_bf(const float (&v)[8]) {
+  uint4 r;
+  r.x = pack_bf2(v[0], v[1]);
+  r.y = pack_bf2(v[2], v[3]);
+  r.z = pack_bf2(v[4], v[5]);
+  r.w = pack_bf2(v[6], v[7]);
+  return r;
+}
+ST_DEV void unpack8_bf(uint4 u, float (&v)[8]) {
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xFFFF0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xFFFF0000u);
+}
+
+__global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  bf16_t* sX = reinterpret_cast<bf16_t*>(lds + FwdLds::X);
+  unsigned char* sH8 = lds + FwdLds::H8;
+  int* sSc = reinterpret_cast<int*>(lds + FwdLds::SC);
+  float* sB = reinterpret_cast<float*>(lds + FwdLds::B);
+  float* sWq = reinterpret_cast<float*>(lds + FwdLds::WQ);
+  float* sQp = reinterpret_cast<float*>(lds + FwdLds::QP);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool online = blockIdx.y == 0;
+  const i8v* whh8 = online ? p.on.whh8 : p.tg.whh8;
+  const int* whhs = online ? p.on.whhs : p.tg.whhs;
+  const s8v* wih = online ? p.on.wih : p.tg.wih;
+  const float* bias4 = online ? p.on.bias4 : p.tg.bias4;
+  const float* wq = online ? p.on.wq : p.tg.wq;
+  float* Qout = online ? p.Q : p.Qt;
+  const int B = p.B, S = p.S, b0 = blockIdx.x * LB;
+
+  for (int i = tid; i < RW * 6 * 64; i += RT) reinterpret_cast<s8v*>(lds + FwdLds::WX)[i] = wih[i];
+  for (int i = tid; i < 4 * RH; i += RT) {
+    sB[i] = bias4[i];
+    sWq[i] = wq[i];
+  }
+  i8v Wh[3][2][2];
+  int Ws4[3] = {0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int idx = (((wave * 3 + g) * 2 + m) * 2 + ks) * 64 + lane;
+        Wh[g][m][ks] = whh8[idx];
+        Ws4[g] |= (whhs[idx] & 0xFF) << (8 * (2 * m + ks));
+      }
+  const s8v* myWx = reinterpret_cast<const s8v*>(lds + FwdLds::WX) + wave * 6 * 64 + lane;
+  s8v WqA;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int u = 32 * wave + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+    WqA[j] = (short)f2bf(l16 < 3 ? wq[l16 * RH + u] : 0.f);
+  }
+  // h0 and x_0
+  float hr[2][2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int b = b0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
+      const float4 v = *reinterpret_cast<const float4*>(p.H0 + (size_t)b * RH + u0);
+      hr[m][n][0] = v.x; hr[m][n][1] = v.y; hr[m][n][2] = v.z; hr[m][n][3] = v.w;
+      if (online) lds_st4(p.Hm + (size_t)b * RH + u0, v.x, v.y, v.z, v.w);
+    }
+  quant_h(hr, sH8, sSc, wave, l16, g4);
+  // x rows: thread tid < LB*4 moves 16 B (row tid/4, chunk tid%4); x_{t+1} is prefetched a step ahead
+  const int xr = tid >> 2, xc = tid & 3;
+  const bool xmover = tid < LB * 4;
+  uint4 xnext = {0u, 0u, 0u, 0u};
+  if (xmover) {
+    reinterpret_cast<uint4*>(sX + xr * XS)[xc] = reinterpret_cast<const uint4*>(p.X + (size_t)(b0 + xr) * RFL)[xc];
+    xnext = reinterpret_cast<const uint4*>(p.X + ((size_t)B + b0 + xr) * RFL)[xc];
+  }
+  __syncthreads();
+  const size_t nblk = (size_t)(B / LB);
+
+  for (int t = 0; t <= S; ++t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    const bf16_t* cX = sX + cur * LB * XS;
+    const unsigned char* cH = sH8 + cur * LB * HS;
+    const int* cS = sSc + cur * LB * SCS;
+    float* qp = sQp + cur * RW * 3 * LB;
+    const bool save = online && t < S;
+    float keep[2] = {1.f, 1.f};
+    if (t < S) {
+      keep[0] = 1.f - p.D[(size_t)t * B + b0 + l16];
+      keep[1] = 1.f - p.D[(size_t)t * B + b0 + 16 + l16];
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      f4v ar[2], az[2], anx[2], anh[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int u0 = 32 * wave + 16 * m + 4 * g4;
+        ar[m] = *reinterpret_cast<const f4v*>(sB + u0);
+        az[m] = *reinterpret_cast<const f4v*>(sB + RH + u0);
+        anx[m] = *reinterpret_cast<const f4v*>(sB + 2 * RH + u0);
+        anh[m] = *reinterpret_cast<const f4v*>(sB + 3 * RH + u0);
+      }
+      const int row = 16 * n + l16;
+      {
+        const s8v xb = lds_ld8(cX + row * XS + 8 * g4);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          ar[m] = mfma32(myWx[(0 * 2 + m) * 64], xb, ar[m]);
+          az[m] = mfma32(myWx[(1 * 2 + m) * 64], xb, az[m]);
+          anx[m] = mfma32(myWx[(2 * 2 + m) * 64], xb, anx[m]);
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 h0 = *reinterpret_cast<const uint4*>(cH + row * HS + 128 * ks + 16 * g4);
+        const uint4 h1 = *reinterpret_cast<const uint4*>(cH + row * HS + 128 * ks + 64 + 16 * g4);
+        i8v hb;
+        hb[0] = (int)h0.x; hb[1] = (int)h0.y; hb[2] = (int)h0.z; hb[3] = (int)h0.w;
+        hb[4] = (int)h1.x; hb[5] = (int)h1.y; hb[6] = (int)h1.z; hb[7] = (int)h1.w;
+        const int sc = cS[row * SCS + 4 * ks + g4];
+#define ST_MX3(M, KS)                                                              \
+  ar[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[0][M][KS], hb, ar[M], Ws4[0], sc);          \
+  az[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[1][M][KS], hb, az[M], Ws4[1], sc);          \
+  anh[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[2][M][KS], hb, anh[M], Ws4[2], sc);
+        if (ks == 0) { ST_MX3(0, 0) ST_MX3(1, 0) } else { ST_MX3(0, 1) ST_MX3(1, 1) }
+#undef ST_MX3
+      }
+      float vr[8], vz[8], vn[8], vg[8], vh[8];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float r = sigm2(ar[m][i]);
+          const float z = sigm2(az[m][i]);
+          const float nn = tanh2(__builtin_fmaf(r, anh[m][i], anx[m][i]));
+          vr[4 * m + i] = r; vz[4 * m + i] = z; vn[4 * m + i] = nn; vg[4 * m + i] = anh[m][i];
+          vh[4 * m + i] = hr[m][n][i];
+          hr[m][n][i] = __builtin_fmaf(z, hr[m][n][i] - nn, nn);
+        }
+      if (save) {
+        uint4* sv = p.sv + ((((size_t)t * nblk + blockIdx.x) * RW + wave) * NSV * 2) * 64 + lane;
+        sv[(0 * 2 + n) * 64] = pack8_bf(vr);
+        sv[(1 * 2 + n) * 64] = pack8_bf(vz);
+        sv[(2 * 2 + n) * 64] = pack8_bf(vn);
+        sv[(3 * 2 + n) * 64] = pack8_bf(vg);
+        sv[(4 * 2 + n) * 64] = pack8_bf(vh);
+      }
+      {
+        s8v hb;
+        const uint32_t p0 = pack_bf2(hr[0][n][0], hr[0][n][1]), p1 = pack_bf2(hr[0][n][2], hr[0][n][3]);
+        const uint32_t p2 = pack_bf2(hr[1][n][0], hr[1][n][1]), p3 = pack_bf2(hr[1][n][2], hr[1][n][3]);
+        hb[0] = (short)(p0 & 0xFFFF); hb[1] = (short)(p0 >> 16); hb[2] = (short)(p1 & 0xFFFF); hb[3] = (short)(p1 >> 16);
+        hb[4] = (short)(p2 & 0xFFFF); hb[5] = (short)(p2 >> 16); hb[6] = (short)(p3 & 0xFFFF); hb[7] = (short)(p3 >> 16);
+        const f4v q = mfma32(WqA, hb, zero4());
+        if (g4 == 0) {
+          qp[(wave * 3 + 0) * LB + row] = q[0];
+          qp[(wave * 3 + 1) * LB + row] = q[1];
+          qp[(wave * 3 + 2) * LB + row] = q[2];
+        }
+      }
+    }
+    if (t < S) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hr[m][n][i] *= keep[n];
+      if (online) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const int b = b0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
+            lds_st4(p.Hm + ((size_t)(t + 1) * B + b) * RH + u0, hr[m][n][0], hr[m][n][1], hr[m][n][2], hr[m][n][3]);
+          }
+      }
+      quant_h(hr, sH8 + nxt * LB * HS, sSc + nxt * LB * SCS, wave, l16, g4);
+      if (xmover) {
+        reinterpret_cast<uint4*>(sX + nxt * LB * XS + xr * XS)[xc] = xnext;
+        if (t + 2 <= S) xnext = reinterpret_cast<const uint4*>(p.X + ((size_t)(t + 2) * B + b0 + xr) * RFL)[xc];
+      }
+    }
+    __syncthreads();
+    if (wave == 0 && lane < LB) {
+      float q[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        float v = sWq[3 * RH + a];
+#pragma unroll
+        for (int w = 0; w < RW; ++w) v += qp[(w * 3 + a) * LB + lane];
+        q[a] = v;
+      }
+      *reinterpret_cast<float4*>(Qout + ((size_t)t * B + b0 + lane) * 4) = make_float4(q[0], q[1], q[2], 0.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- TD targets (double DQN)
+struct GruTD {
+  const float* Q;     // [(S+1)B][4] online
+  const float* Qt;    // [(S+1)B][4] target net
+  const int* A;
+  const float* R;
+  const float* D;     // [S][B]
+  float* dQ;          // [S*B][4]
+  float* loss;        // [1] (atomic)
+  int B, S, burn;
+  float gamma, coef;
+};
+
+__global__ void __launch_bounds__(256) gru_td_kernel(GruTD p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (i < p.S * p.B) {
+    const int t = i / p.B;
+    const float* qn = p.Q + ((size_t)i + p.B) * 4;
+    int as = 0;
+    if (qn[1] > qn[as]) as = 1;
+    if (qn[2] > qn[as]) as = 2;
+    const float y = p.R[i] + p.gamma * (1.f - p.D[i]) * p.Qt[((size_t)i + p.B) * 4 + as];
+    const int a = p.A[i];
+    const float d = p.Q[(size_t)i * 4 + a] - y;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t >= p.burn) {
+      const float v = p.coef * d;
+      if (a == 0) g.x = v; else if (a == 1) g.y = v; else g.z = v;
+      l = d * d;
+    }
+    *reinterpret_cast<float4*>(p.dQ + (size_t)i * 4) = g;
+  }
+  l = wave_sum(l);
+  if ((threadIdx.x & 63) == 0) atomicAdd(p.loss, l);
+}
+
+// ---------------------------------------------------------------- fused backward through time
+struct GruSeqBwd {
+  const uint4* sv;      // forward saves
+  const float* dQ;      // [S*B][4]
+  const float* D;       // [S][B]
+  const bf16_t* WhhT;   // [RH][RG] bf16 (W_hh^T, written by the optimizer)
+  const float* wq;      // [3][RH] online fp32
+  bf16_t* dGx;          // [S*B][RG]
+  bf16_t* dGh;          // [S*B][RG]
+  float* gwq;           // [3][RH]   (+= ; zeroed by the host each update)
+  float* gbq;           // [3]
+  float* gbih;          // [RG]
+  float* gbhh;          // [RG]
+  int B, S;
+};
+
+struct BwdLds {
+  static constexpr int G = 0;                       // [2][LB][GS] bf16 dGh tiles
+  static constexpr int WQ = G + 2 * LB * GS * 2;    // [3][RH] float
+  static constexpr int BYTES = WQ + 3 * RH * 4;
+};
+static_assert(BwdLds::BYTES <= 160 * 1024, "bwd LDS");
+
+constexpr int BK = RG / 32;   // 24 K-steps of the dh GEMM
+constexpr int BLA = 4;        // W_hh^T fragment look-ahead (K-steps)
+
+ST_DEV float row16_sum(float v) {   // sum over the 16 lanes of a row (same lane group)
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  bf16_t* sG = reinterpret_cast<bf16_t*>(lds + BwdLds::G);
+  float* sWq = reinterpret_cast<float*>(lds + BwdLds::WQ);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int B = p.B, S = p.S, b0 = blockIdx.x * LB;
+  const size_t nblk = (size_t)(B / LB);
+  for (int i = tid; i < 3 * RH; i += RT) sWq[i] = p.wq[i];
+
+  float rec[2][2][4];        // dL/d(masked h_t) arriving from step t+1 (direct + GEMM)
+  float gq[3][2][4];         // W_q gradient partials (units m, i), summed over this lane's seqs / steps
+  float gr[2][4], gz[2][4], gnx[2][4], gnh[2][4];   // bias gradient partials
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rec[m][0][i] = rec[m][1][i] = 0.f;
+      gq[0][m][i] = gq[1][m][i] = gq[2][m][i] = 0.f;
+      gr[m][i] = gz[m][i] = gnx[m][i] = gnh[m][i] = 0.f;
+    }
+  float gbq0 = 0.f, gbq1 = 0.f, gbq2 = 0.f;
+  // W_hh^T rows of this wave's output units (A operand of the dh GEMM), 16 B per fragment
+  const bf16_t* wrow0 = p.WhhT + (size_t)(32 * wave + l16) * RG + 8 * g4;
+  const bf16_t* wrow1 = wrow0 + (size_t)16 * RG;
+  __syncthreads();
+
+  for (int t = S - 1; t >= 0; --t) {
+    const int cur = t & 1;
+    bf16_t* cG = sG + cur * LB * GS;
+    const uint4* sv = p.sv + ((((size_t)t * nblk + blockIdx.x) * RW + wave) * NSV * 2) * 64 + lane;
+    float nrec[2][2][4];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int row = 16 * n + l16, b = b0 + row;
+      const float4 dq = *reinterpret_cast<const float4*>(p.dQ + ((size_t)t * B + b) * 4);
+      const float keep = (t < S - 1) ? 1.f - p.D[(size_t)t * B + b] : 0.f;
+      float vr[8], vz[8], vn[8], vg[8], vh[8];
+      unpack8_bf(sv[(0 * 2 + n) * 64], vr);
+      unpack8_bf(sv[(1 * 2 + n) * 64], vz);
+      unpack8_bf(sv[(2 * 2 + n) * 64], vn);
+      unpack8_bf(sv[(3 * 2 + n) * 64], vg);
+      unpack8_bf(sv[(4 * 2 + n) * 64], vh);
+      if (wave == 0 && g4 == 0) { gbq0 += dq.x; gbq1 += dq.y; gbq2 += dq.z; }
+      float dar[8], daz[8], dan[8], dgn[8];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int u0 = 32 * wave + 16 * m + 4 * g4;
+        const f4v w0 = *reinterpret_cast<const f4v*>(sWq + u0);
+        const f4v w1 = *reinterpret_cast<const f4v*>(sWq + RH + u0);
+        const f4v w2 = *reinterpret_cast<const f4v*>(sWq + 2 * RH + u0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * m + i;
+          const float r = vr[k], z = vz[k], nn = vn[k], gh = vg[k], hp = vh[k];
+          float dh = keep * rec[m][n][i];
+          dh = __builtin_fmaf(dq.x, w0[i], dh);
+          dh = __builtin_fmaf(dq.y, w1[i], dh);
+          dh = __builtin_fmaf(dq.z, w2[i], dh);
+          const float h = __builtin_fmaf(z, hp - nn, nn);      // unmasked h_t (Q input)
+          gq[0][m][i] = __builtin_fmaf(dq.x, h, gq[0][m][i]);
+          gq[1][m][i] = __builtin_fmaf(dq.y, h, gq[1][m][i]);
+          gq[2][m][i] = __builtin_fmaf(dq.z, h, gq[2][m][i]);
+          const float dn = dh * (1.f - z);
+          const float dz = dh * (hp - nn);
+          nrec[m][n][i] = dh * z;                               // direct path into h_{t-1}
+          const float a_n = dn * (1.f - nn * nn);
+          const float a_r = a_n * gh * r * (1.f - r);
+          const float a_z = dz * z * (1.f - z);
+          dar[k] = a_r; daz[k] = a_z; dan[k] = a_n; dgn[k] = a_n * r;
+          gr[m][i] += a_r; gz[m][i] += a_z; gnx[m][i] += a_n; gnh[m][i] += a_n * r;
+        }
+      }
+      bf16_t* gx = p.dGx + ((size_t)t * B + b) * RG;
+      bf16_t* gh_ = p.dGh + ((size_t)t * B + b) * RG;
+      bf16_t* lg = cG + row * GS;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int u0 = 32 * wave + 16 * m + 4 * g4, k = 4 * m;
+        lds_st4(gx + u0, dar[k], dar[k + 1], dar[k + 2], dar[k + 3]);
+        lds_st4(gx + RH + u0, daz[k], daz[k + 1], daz[k + 2], daz[k + 3]);
+        lds_st4(gx + 2 * RH + u0, dan[k], dan[k + 1], dan[k + 2], dan[k + 3]);
+        lds_st4(gh_ + u0, dar[k], dar[k + 1], dar[k + 2], dar[k + 3]);
+        lds_st4(gh_ + RH + u0, daz[k], daz[k + 1], daz[k + 2], daz[k + 3]);
+        lds_st4(gh_ + 2 * RH + u0, dgn[k], dgn[k + 1], dgn[k + 2], dgn[k + 3]);
+        lds_st4(lg + u0, dar[k], dar[k + 1], dar[k + 2], dar[k + 3]);
+        lds_st4(lg + RH + u0, daz[k], daz[k + 1], daz[k + 2], daz[k + 3]);
+        lds_st4(lg + 2 * RH + u0, dgn[k], dgn[k + 1], dgn[k + 2], dgn[k + 3]);
+      }
+    }
+    if (t == 0) break;
+    __syncthreads();
+    // dh_{t-1} (through the recurrence) = direct + dGh_t . W_hh  (D[unit][seq], K = 768)
+    f4v acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        acc[m][n][0] = nrec[m][n][0]; acc[m][n][1] = nrec[m][n][1];
+        acc[m][n][2] = nrec[m][n][2]; acc[m][n][3] = nrec[m][n][3];
+      }
+    s8v wa[BLA][2];
+#pragma unroll
+    for (int j = 0; j < BLA; ++j) {
+      wa[j][0] = *reinterpret_cast<const s8v*>(wrow0 + 32 * j);
+      wa[j][1] = *reinterpret_cast<const s8v*>(wrow1 + 32 * j);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK; ++ks) {
+      const s8v a0 = wa[ks % BLA][0], a1 = wa[ks % BLA][1];
+      if (ks + BLA < BK) {
+        wa[ks % BLA][0] = *reinterpret_cast<const s8v*>(wrow0 + 32 * (ks + BLA));
+        wa[ks % BLA][1] = *reinterpret_cast<const s8v*>(wrow1 + 32 * (ks + BLA));
+      }
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const s8v bb = lds_ld8(cG + (16 * n + l16) * GS + 32 * ks + 8 * g4);
+        acc[0][n] = mfma32(a0, bb, acc[0][n]);
+        acc[1][n] = mfma32(a1, bb, acc[1][n]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rec[m][n][i] = acc[m][n][i];
+  }
+  // reduce the per-lane partials over the 16 sequences of a lane group, then one atomic per unit
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = 32 * wave + 16 * m + 4 * g4 + i;
+      const float v0 = row16_sum(gq[0][m][i]), v1 = row16_sum(gq[1][m][i]), v2 = row16_sum(gq[2][m][i]);
+      const float r_ = row16_sum(gr[m][i]), z_ = row16_sum(gz[m][i]);
+      const float nx = row16_sum(gnx[m][i]), nh = row16_sum(gnh[m][i]);
+      if (l16 == 0) {
+        atomicAdd(p.gwq + u, v0);
+        atomicAdd(p.gwq + RH + u, v1);
+        atomicAdd(p.gwq + 2 * RH + u, v2);
+        atomicAdd(p.gbih + u, r_);
+        atomicAdd(p.gbih + RH + u, z_);
+        atomicAdd(p.gbih + 2 * RH + u, nx);
+        atomicAdd(p.gbhh + u, r_);
+        atomicAdd(p.gbhh + RH + u, z_);
+        atomicAdd(p.gbhh + 2 * RH + u, nh);
+      }
+    }
+  if (wave == 0) {
+    gbq0 = wave_sum(gbq0);
+    gbq1 = wave_sum(gbq1);
+    gbq2 = wave_sum(gbq2);
+    if (lane == 0) {
+      atomicAdd(p.gbq + 0, gbq0);
+      atomicAdd(p.gbq + 1, gbq1);
+      atomicAdd(p.gbq + 2, gbq2);
+    }
+  }
+}
+
+}  // namespace st
+
+extern "C" hipError_t st_gru_gather(const st::GruGather* g, hipStream_t s) {
+  if (g->S > 64 || g->S <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::gru_gather_kernel, dim3((g->B + 3) / 4), dim3(256), 0, s, *g);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_seq_fwd(const st::GruSeqFwd* p, hipStream_t s) {
+  if (p->B % st::LB || p->S <= 0 || p->S > 64) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)st::gru_seq_fwd_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, st::FwdLds::BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(st::gru_seq_fwd_kernel, dim3(p->B / st::LB, 2), dim3(st::RT), st::FwdLds::BYTES, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_td(const st::GruTD* p, hipStream_t s) {
+  hipLaunchKernelGGL(st::gru_td_kernel, dim3((p->S * p->B + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_seq_bwd(const st::GruSeqBwd* p, hipStream_t s) {
+  if (p->B % st::LB || p->S <= 0 || p->S > 64) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)st::gru_seq_bwd_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, st::BwdLds::BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(st::gru_seq_bwd_kernel, dim3(p->B / st::LB), dim3(st::RT), st::BwdLds::BYTES, s, *p);
+  return hipGetLastError();
+}

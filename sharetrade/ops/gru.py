@@ -27,7 +27,7 @@ import torch
 from . import native
 
 HID, GATES, XA, XL, NMF = 256, 768, 32, 64, 8
-RW, RN = 8, 32
+RW, RN, LB, NSV = 8, 32, 32, 5
 
 
 class MinuteBarsArgs(C.Structure):
@@ -57,16 +57,19 @@ class ActArgs(C.Structure):
 class GatherArgs(C.Structure):
     _fields_ = [("rx", C.c_void_p), ("ra", C.c_void_p), ("rr", C.c_void_p), ("rd", C.c_void_p), ("rh0", C.c_void_p),
                 ("rctrl", C.c_void_p), ("cap", C.c_int), ("S", C.c_int), ("B", C.c_int), ("key0", C.c_uint32),
-                ("key1", C.c_uint32), ("step", C.c_void_p), ("X", C.c_void_p), ("Hm", C.c_void_p),
-                ("Hm_t", C.c_void_p), ("Hf", C.c_void_p), ("Hf_t", C.c_void_p), ("A", C.c_void_p), ("R", C.c_void_p),
-                ("D", C.c_void_p)]
+                ("key1", C.c_uint32), ("step", C.c_void_p), ("X", C.c_void_p), ("H0", C.c_void_p),
+                ("A", C.c_void_p), ("R", C.c_void_p), ("D", C.c_void_p)]
 
 
-class FwdArgs(C.Structure):
-    _fields_ = [("Gx", C.c_void_p), ("Gh", C.c_void_p), ("Hf", C.c_void_p), ("Hm", C.c_void_p), ("wq", C.c_void_p),
-                ("bq", C.c_void_p), ("Q", C.c_void_p), ("D", C.c_void_p), ("sr", C.c_void_p), ("sz", C.c_void_p),
-                ("sn", C.c_void_p), ("sgh", C.c_void_p), ("shp", C.c_void_p), ("Hq", C.c_void_p),
-                ("B", C.c_int), ("S", C.c_int), ("t", C.c_int)]
+class NetW(C.Structure):
+    _fields_ = [("whh8", C.c_void_p), ("whhs", C.c_void_p), ("wih", C.c_void_p), ("bias4", C.c_void_p),
+                ("wq", C.c_void_p)]
+
+
+class SeqFwdArgs(C.Structure):
+    _fields_ = [("on", NetW), ("tg", NetW), ("X", C.c_void_p), ("H0", C.c_void_p), ("D", C.c_void_p),
+                ("Q", C.c_void_p), ("Qt", C.c_void_p), ("Hm", C.c_void_p), ("sv", C.c_void_p),
+                ("B", C.c_int), ("S", C.c_int)]
 
 
 class TDArgs(C.Structure):
@@ -75,10 +78,10 @@ class TDArgs(C.Structure):
                 ("gamma", C.c_float), ("coef", C.c_float)]
 
 
-class BwdArgs(C.Structure):
-    _fields_ = [("dQ", C.c_void_p), ("D", C.c_void_p), ("DH", C.c_void_p), ("sr", C.c_void_p), ("sz", C.c_void_p),
-                ("sn", C.c_void_p), ("sgh", C.c_void_p), ("shp", C.c_void_p), ("wq", C.c_void_p), ("dGx", C.c_void_p),
-                ("dGh", C.c_void_p), ("B", C.c_int), ("S", C.c_int), ("t", C.c_int)]
+class SeqBwdArgs(C.Structure):
+    _fields_ = [("sv", C.c_void_p), ("dQ", C.c_void_p), ("D", C.c_void_p), ("WhhT", C.c_void_p), ("wq", C.c_void_p),
+                ("dGx", C.c_void_p), ("dGh", C.c_void_p), ("gwq", C.c_void_p), ("gbq", C.c_void_p),
+                ("gbih", C.c_void_p), ("gbhh", C.c_void_p), ("B", C.c_int), ("S", C.c_int)]
 
 
 def lib():
@@ -89,10 +92,9 @@ def lib():
                          ("st_gru_pack", [C.POINTER(PackArgs), vp]),
                          ("st_gru_act", [C.POINTER(ActArgs), i, vp]),
                          ("st_gru_gather", [C.POINTER(GatherArgs), vp]),
-                         ("st_gru_fwd", [C.POINTER(FwdArgs), vp]),
+                         ("st_gru_seq_fwd", [C.POINTER(SeqFwdArgs), vp]),
                          ("st_gru_td", [C.POINTER(TDArgs), vp]),
-                         ("st_gru_bwd", [C.POINTER(BwdArgs), vp]),
-                         ("st_gru_wq_grad", [vp, vp, i, vp, vp, vp]),
+                         ("st_gru_seq_bwd", [C.POINTER(SeqBwdArgs), vp]),
                          ("st_mx_probe", [vp, vp, vp, vp, vp, vp])):
             f = getattr(L, fn)
             f.argtypes = args

@@ -92,16 +92,23 @@ class RecurrentDQN:
         self.Whh_b = self.P["w_hh"].to(b16).contiguous()
         self.WhhT_b = self.P["w_hh"].t().contiguous().to(b16)
         self._scratch = {n: torch.zeros(self.P[n].shape, dtype=b16, device=dev) for n in ("b_ih", "b_hh", "w_q", "b_q")}
-        self.tgt = {"w_ih": self.Wih_b.clone(), "w_hh": self.Whh_b.clone(), "b_ih": self.P["b_ih"].clone(),
-                    "b_hh": self.P["b_hh"].clone(), "w_q": self.P["w_q"].clone(), "b_q": self.P["b_q"].clone()}
         self.t_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-        # packed actor weights
+        # target net: an fp32 copy of the flat parameters, packed like the actor's weights
+        self.tflat = self.flat.clone()
+        self.T_P = {}
+        o = 0
+        for n, sz in zip(self._names, sizes):
+            self.T_P[n] = self.tflat[o:o + sz].view(*self.P[n].shape)
+            o += sz
+        # packed weights (gru_pack_kernel layout): online (actor + learner fwd) and target
         nfr = G.RW * 3 * 2 * 2 * 64
-        self.whh8 = torch.zeros(nfr * 8, dtype=i32, device=dev)
-        self.whhs = torch.zeros(nfr, dtype=i32, device=dev)
-        self.wih_pk = torch.zeros(G.RW * 6 * 64 * 8, dtype=torch.int16, device=dev)
-        self.bias4 = torch.zeros(4 * HID, device=dev)
-        self.wq4 = torch.zeros(4 * HID, device=dev)
+        self.pk = {}
+        for net in ("on", "tg"):
+            self.pk[net] = {"whh8": torch.zeros(nfr * 8, dtype=i32, device=dev),
+                            "whhs": torch.zeros(nfr, dtype=i32, device=dev),
+                            "wih": torch.zeros(G.RW * 6 * 64 * 8, dtype=torch.int16, device=dev),
+                            "bias4": torch.zeros(4 * HID, device=dev), "wq": torch.zeros(4 * HID, device=dev)}
+        self.whh8, self.whhs = self.pk["on"]["whh8"], self.pk["on"]["whhs"]
         # ---------------------------------------------------------------- data + envs
         self.bp = bar_params or mb.BarParams()
         self.close, self.feat = mb.generate_gpu(self.E, self.T, dev, self.bp, seed=self.seed)
@@ -129,26 +136,21 @@ class RecurrentDQN:
         self.loss = torch.zeros(1, device=dev)
         # ---------------------------------------------------------------- learner buffers (time-major rows t*B + b)
         B, R1, RS = self.B, (S + 1) * self.B, S * self.B
+        if B % G.LB:
+            raise ValueError(f"batch must be a multiple of {G.LB}")
         self.X = torch.zeros(R1, XL, dtype=b16, device=dev)
         self.XT = torch.zeros(XL, R1, dtype=b16, device=dev)
+        self.H0 = torch.zeros(B, HID, device=dev)
         self.Hm = torch.zeros(R1, HID, dtype=b16, device=dev)
-        self.Hm_t = torch.zeros(R1, HID, dtype=b16, device=dev)
         self.HT = torch.zeros(HID, R1, dtype=b16, device=dev)
-        self.Hf = torch.zeros(B, HID, device=dev)
-        self.Hf_t = torch.zeros(B, HID, device=dev)
         self.A = torch.zeros(S, B, dtype=i32, device=dev)
         self.R = torch.zeros(S, B, device=dev)
         self.D = torch.zeros(S, B, device=dev)
-        self.Gx = torch.zeros(R1, GATES, device=dev)
-        self.Gx_t = torch.zeros(R1, GATES, device=dev)
-        self.Gh = torch.zeros(B, GATES, device=dev)
-        self.Gh_t = torch.zeros(B, GATES, device=dev)
         self.Q = torch.zeros(R1, 4, device=dev)
         self.Q_t = torch.zeros(R1, 4, device=dev)
-        self.sv = {k: torch.zeros(RS, HID, device=dev) for k in ("r", "z", "n", "gh", "hp")}
-        self.Hq = torch.zeros(RS, HID, dtype=b16, device=dev)
+        # forward saves (r, z, n, gh_n, h_prev as bf16 in the kernels' lane order): 16 B per lane/tile/quantity
+        self.sv = torch.zeros(S * (B // G.LB) * G.RW * G.NSV * 2 * 64 * 4, dtype=i32, device=dev)
         self.dQ = torch.zeros(RS, 4, device=dev)
-        self.DH = torch.zeros(B, HID, device=dev)
         self.dGx = torch.zeros(RS, GATES, dtype=b16, device=dev)
         self.dGh = torch.zeros(RS, GATES, dtype=b16, device=dev)
         self.dGxT = torch.zeros(GATES, RS, dtype=b16, device=dev)
@@ -159,13 +161,14 @@ class RecurrentDQN:
         self._g_act = None
         self._g_upd = None
         self._build_structs()
-        self.pack()
+        self.pack("on")
+        self.pack("tg")
 
     # ---------------------------------------------------------------- structs
     def _build_structs(self) -> None:
         a = G.ActArgs()
-        a.whh8, a.whhs, a.wih, a.bias4, a.wq = (self.whh8.data_ptr(), self.whhs.data_ptr(), self.wih_pk.data_ptr(),
-                                                self.bias4.data_ptr(), self.wq4.data_ptr())
+        po = self.pk["on"]
+        a.whh8, a.whhs, a.wih, a.bias4, a.wq = (po[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
         a.feat, a.close, a.ret = self.feat.data_ptr(), self.close.data_ptr(), self.ret.data_ptr()
         a.E, a.T, a.S, a.ep_len = self.E, self.T, self.S, self.ep_len
         ag = self.cfg.agent
@@ -179,53 +182,43 @@ class RecurrentDQN:
         a.key0, a.key1 = (int(x) for x in rng.key_for(self.seed, 5))
         a.ctrl, a.stats, a.q_out = self.ctrl.data_ptr(), self.stats.data_ptr(), None
         self._act = a
-        p = G.PackArgs()
-        p.w_hh, p.w_ih, p.b_ih, p.b_hh, p.w_q, p.b_q = (self.P[n].data_ptr() for n in
-                                                         ("w_hh", "w_ih", "b_ih", "b_hh", "w_q", "b_q"))
-        p.whh8, p.whhs, p.wih, p.bias4, p.wq = (self.whh8.data_ptr(), self.whhs.data_ptr(), self.wih_pk.data_ptr(),
-                                                self.bias4.data_ptr(), self.wq4.data_ptr())
-        self._pack = p
+        self._packs = {}
+        for net, src in (("on", self.P), ("tg", self.T_P)):
+            p = G.PackArgs()
+            p.w_hh, p.w_ih, p.b_ih, p.b_hh, p.w_q, p.b_q = (src[n].data_ptr() for n in
+                                                             ("w_hh", "w_ih", "b_ih", "b_hh", "w_q", "b_q"))
+            pk = self.pk[net]
+            p.whh8, p.whhs, p.wih, p.bias4, p.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
+            self._packs[net] = p
         ga = G.GatherArgs()
         ga.rx, ga.ra, ga.rr, ga.rd, ga.rh0 = (self.rx.data_ptr(), self.ra.data_ptr(), self.rr.data_ptr(),
                                               self.rd.data_ptr(), self.rh0.data_ptr())
         ga.rctrl, ga.cap, ga.S, ga.B = self.rctrl.data_ptr(), self.cap, self.S, self.B
         ga.key0, ga.key1, ga.step = self.key0, self.key1, self.t_ctr.data_ptr()
-        ga.X, ga.Hm, ga.Hm_t, ga.Hf, ga.Hf_t = (self.X.data_ptr(), self.Hm.data_ptr(), self.Hm_t.data_ptr(),
-                                                self.Hf.data_ptr(), self.Hf_t.data_ptr())
+        ga.X, ga.H0 = self.X.data_ptr(), self.H0.data_ptr()
         ga.A, ga.R, ga.D = self.A.data_ptr(), self.R.data_ptr(), self.D.data_ptr()
         self._gather = ga
-        self._fwd_on, self._fwd_tg = [], []
-        for t in range(self.S + 1):
-            for net, lst in (("on", self._fwd_on), ("tg", self._fwd_tg)):
-                f = G.FwdArgs()
-                on = net == "on"
-                f.Gx = (self.Gx if on else self.Gx_t).data_ptr()
-                f.Gh = (self.Gh if on else self.Gh_t).data_ptr()
-                f.Hf = (self.Hf if on else self.Hf_t).data_ptr()
-                f.Hm = (self.Hm if on else self.Hm_t).data_ptr()
-                f.wq = (self.P["w_q"] if on else self.tgt["w_q"]).data_ptr()
-                f.bq = (self.P["b_q"] if on else self.tgt["b_q"]).data_ptr()
-                f.Q = (self.Q if on else self.Q_t).data_ptr()
-                f.D = self.D.data_ptr()
-                if on and t < self.S:
-                    f.sr, f.sz, f.sn, f.sgh, f.shp = (self.sv[k].data_ptr() for k in ("r", "z", "n", "gh", "hp"))
-                    f.Hq = self.Hq.data_ptr()
-                f.B, f.S, f.t = self.B, self.S, t
-                lst.append(f)
+        f = G.SeqFwdArgs()
+        for net, w in (("on", f.on), ("tg", f.tg)):
+            pk = self.pk[net]
+            w.whh8, w.whhs, w.wih, w.bias4, w.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
+        f.X, f.H0, f.D = self.X.data_ptr(), self.H0.data_ptr(), self.D.data_ptr()
+        f.Q, f.Qt, f.Hm, f.sv = self.Q.data_ptr(), self.Q_t.data_ptr(), self.Hm.data_ptr(), self.sv.data_ptr()
+        f.B, f.S = self.B, self.S
+        self._fwd = f
         td = G.TDArgs()
         td.Q, td.Qt, td.A, td.R, td.D = (self.Q.data_ptr(), self.Q_t.data_ptr(), self.A.data_ptr(), self.R.data_ptr(),
                                          self.D.data_ptr())
         td.dQ, td.loss, td.B, td.S, td.burn = self.dQ.data_ptr(), self.loss.data_ptr(), self.B, self.S, self.burn
         td.gamma, td.coef = self.gamma, 2.0 / (self.B * (self.S - self.burn))
         self._td = td
-        self._bwd = []
-        for t in range(self.S):
-            b = G.BwdArgs()
-            b.dQ, b.D, b.DH = self.dQ.data_ptr(), self.D.data_ptr(), self.DH.data_ptr()
-            b.sr, b.sz, b.sn, b.sgh, b.shp = (self.sv[k].data_ptr() for k in ("r", "z", "n", "gh", "hp"))
-            b.wq, b.dGx, b.dGh = self.P["w_q"].data_ptr(), self.dGx.data_ptr(), self.dGh.data_ptr()
-            b.B, b.S, b.t = self.B, self.S, t
-            self._bwd.append(b)
+        bw = G.SeqBwdArgs()
+        bw.sv, bw.dQ, bw.D, bw.WhhT, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
+                                              self.WhhT_b.data_ptr(), self.P["w_q"].data_ptr())
+        bw.dGx, bw.dGh = self.dGx.data_ptr(), self.dGh.data_ptr()
+        bw.gwq, bw.gbq, bw.gbih, bw.gbhh = (self.dP[n].data_ptr() for n in ("w_q", "b_q", "b_ih", "b_hh"))
+        bw.B, bw.S = self.B, self.S
+        self._bwd = bw
         ag = self.cfg.agent
         self._adam = []
         for n in self._names:
@@ -242,68 +235,44 @@ class RecurrentDQN:
             self._adam.append(ad)
 
     # ---------------------------------------------------------------- actor
-    def pack(self) -> None:
-        """fp32 masters -> the actor's MX-fp8 W_hh fragments, bf16 W_ih fragments, biases, W_q."""
-        native.check(self.k.st_gru_pack(self._pack, native.stream_handle()), "st_gru_pack")
+    def pack(self, net: str = "on") -> None:
+        """fp32 masters -> MX-fp8 W_hh fragments, bf16 W_ih fragments, biases, W_q (actor/learner layout)."""
+        native.check(self.k.st_gru_pack(self._packs[net], native.stream_handle()), "st_gru_pack")
 
     def act(self) -> None:
         """All E envs advance S minute bars (one actor launch) and write one replay segment each."""
         native.check(self.k.st_gru_act(self._act, self.grid, native.stream_handle()), "st_gru_act")
 
     # ---------------------------------------------------------------- learner
-    def _forward(self, on: bool) -> None:
-        sh = native.stream_handle()
-        Wih = self.Wih_b if on else self.tgt["w_ih"]
-        Whh = self.Whh_b if on else self.tgt["w_hh"]
-        bih = (self.P["b_ih"] if on else self.tgt["b_ih"]).view(-1)
-        bhh = (self.P["b_hh"] if on else self.tgt["b_hh"]).view(-1)
-        Gx, Gh, Hm = (self.Gx, self.Gh, self.Hm) if on else (self.Gx_t, self.Gh_t, self.Hm_t)
-        fw = self._fwd_on if on else self._fwd_tg
-        gm.gemm_nt(self.X, Wih, Gx, gm.EPI_F32, bias=bih)
-        B = self.B
-        for t in range(self.S + 1):
-            gm.gemm_nt(Hm[t * B:(t + 1) * B], Whh, Gh, gm.EPI_F32, bias=bhh)
-            native.check(self.k.st_gru_fwd(fw[t], sh), "st_gru_fwd")
-
     def update(self) -> None:
-        """One learner update on B sampled segments (sample -> unroll x2 -> TD -> BPTT -> Adam -> repack)."""
+        """One learner update on B sampled segments: gather -> fused unroll of both nets (MX-fp8) ->
+        TD -> fused BPTT (bf16) -> split-K weight-gradient GEMMs -> Adam -> repack the actor weights."""
         sh = native.stream_handle()
         k, kd = self.k, self.kd
         S, B = self.S, self.B
         RS, R1 = S * B, (S + 1) * B
         native.check(k.st_gru_gather(self._gather, sh), "st_gru_gather")
-        self._forward(True)
-        self._forward(False)
+        native.check(k.st_gru_seq_fwd(self._fwd, sh), "st_gru_seq_fwd")
         self.loss.zero_()
         native.check(k.st_gru_td(self._td, sh), "st_gru_td")
         self.gflat.zero_()
-        for t in reversed(range(S)):
-            native.check(k.st_gru_bwd(self._bwd[t], sh), "st_gru_bwd")
-            if t > 0:
-                gm.gemm_nt(self.dGh[t * B:(t + 1) * B], self.WhhT_b, self.DH, gm.EPI_F32, accumulate=True,
-                           splitk="auto")
+        native.check(k.st_gru_seq_bwd(self._bwd, sh), "st_gru_seq_bwd")
         native.check(kd.st_transpose_bf16(self.dGh.data_ptr(), GATES, self.dGhT.data_ptr(), RS, RS, GATES, sh), "T dGh")
         native.check(kd.st_transpose_bf16(self.dGx.data_ptr(), GATES, self.dGxT.data_ptr(), RS, RS, GATES, sh), "T dGx")
         native.check(kd.st_transpose_bf16(self.Hm.data_ptr(), HID, self.HT.data_ptr(), R1, RS, HID, sh), "T H")
         native.check(kd.st_transpose_bf16(self.X.data_ptr(), XL, self.XT.data_ptr(), R1, RS, XL, sh), "T X")
         gm.gemm_nt(self.dGhT, self.HT[:, :RS], self.dP["w_hh"], gm.EPI_F32, accumulate=True, splitk="auto")
         gm.gemm_nt(self.dGxT, self.XT[:, :RS], self.dP["w_ih"], gm.EPI_F32, accumulate=True, splitk="auto")
-        native.check(kd.st_row_sum_bf16(self.dGxT.data_ptr(), RS, GATES, RS, self.dP["b_ih"].data_ptr(), sh), "db_ih")
-        native.check(kd.st_row_sum_bf16(self.dGhT.data_ptr(), RS, GATES, RS, self.dP["b_hh"].data_ptr(), sh), "db_hh")
-        native.check(k.st_gru_wq_grad(self.dQ.data_ptr(), self.Hq.data_ptr(), RS, self.dP["w_q"].data_ptr(),
-                                      self.dP["b_q"].data_ptr(), sh), "dWq")
         if self.grad_sync is not None:
             self.grad_sync(self.gflat)
         for ad in self._adam:
             native.check(kd.st_adam_tile(ad, sh), "adam")
         native.check(kd.st_counter_inc(self.t_ctr.data_ptr(), sh), "t++")
-        self.pack()
+        self.pack("on")
 
     def sync_target(self) -> None:
-        self.tgt["w_ih"].copy_(self.Wih_b)
-        self.tgt["w_hh"].copy_(self.Whh_b)
-        for n in ("b_ih", "b_hh", "w_q", "b_q"):
-            self.tgt[n].copy_(self.P[n])
+        self.tflat.copy_(self.flat)
+        self.pack("tg")
 
     # ---------------------------------------------------------------- driver
     def capture(self) -> None:

@@ -151,41 +151,69 @@ def test_actor_matches_reference(native_built):
     assert int(d.rctrl[0]) == d.E and int(d.ctrl[0]) == 1
 
 
+def _ref_unroll(X, h0, p, D, Wdeq):
+    """Quantization-aware reference of gru_seq_fwd_kernel: the value of W_hh h is the MX-fp8
+    product (quantized W_hh and h), its gradient flows through the bf16 master (straight-through)."""
+    from sharetrade.ops.gru import mx_roundtrip
+
+    h, qs = h0, []
+    for t in range(X.shape[0]):
+        gx = X[t][:, :32] @ p["w_ih"][:, :32].t() + p["b_ih"]
+        gh_e = h @ p["w_hh"].t() + p["b_hh"]
+        gh_q = mx_roundtrip(h.detach()) @ Wdeq.t() + p["b_hh"]
+        gh = gh_e + (gh_q - gh_e).detach()
+        r = torch.sigmoid(gx[:, :256] + gh[:, :256])
+        z = torch.sigmoid(gx[:, 256:512] + gh[:, 256:512])
+        n = torch.tanh(gx[:, 512:] + r * gh[:, 512:])
+        h = (1 - z) * n + z * h
+        qs.append(h @ p["w_q"].t() + p["b_q"])
+        if t < D.shape[0]:
+            h = h * (1 - D[t])[:, None]
+    return torch.stack(qs)
+
+
 def test_learner_gradients_match_autograd(native_built):
-    from sharetrade.models import gru_qnet as gq
+    from sharetrade.ops.gru import unpack_whh
     from sharetrade.utils import rng
 
     d = _small(E=128, S=4, eps=0.5, batch=128)
     for _ in range(3):
         d.act()
-    P0 = {n: t.detach().clone() for n, t in d.P.items()}
-    tgt = {n: t.detach().clone() for n, t in d.tgt.items()}
+    P0 = {n: t.detach().clone().cpu() for n, t in d.P.items()}
+    T0 = {n: t.detach().clone().cpu() for n, t in d.T_P.items()}
+    W_on = unpack_whh(d.pk["on"]["whh8"], d.pk["on"]["whhs"])
+    W_tg = unpack_whh(d.pk["tg"]["whh8"], d.pk["tg"]["whhs"])
     d.update()
     torch.cuda.synchronize()
-    # the sampled segments (Philox counter = (row, update 0))
     size = int(d.rctrl[1])
     k0, k1 = rng.key_for(d.seed, 7)
     b = np.arange(d.B, dtype=np.uint32)
     c0, c1, _, _ = rng.philox4x32(b, np.zeros_like(b), np.zeros_like(b), np.full_like(b, 0x53455131), k0, k1)
-    idx = torch.from_numpy(((c0.astype(np.uint64) << np.uint64(32)) | c1.astype(np.uint64)) % np.uint64(size))
-    idx = idx.long()
-    X = torch.zeros(d.S + 1, d.B, 64)
-    X[:, :, :32] = d.rx.cpu()[idx].float().transpose(0, 1)
+    idx = torch.from_numpy(((c0.astype(np.uint64) << np.uint64(32)) | c1.astype(np.uint64)) % np.uint64(size)).long()
+    X = d.rx.cpu()[idx].float().transpose(0, 1)          # [S+1, B, 32]
     A = d.ra.cpu()[idx].long().t()
     R = d.rr.cpu()[idx].t()
     D = d.rd.cpu()[idx].float().t()
     h0 = d.rh0.cpu()[idx].float()
     bf = lambda t: t.to(torch.bfloat16).float()
-    p = {"w_ih": bf(P0["w_ih"].cpu()).requires_grad_(True), "w_hh": bf(P0["w_hh"].cpu()).requires_grad_(True),
-         "b_ih": P0["b_ih"].cpu().view(-1).clone().requires_grad_(True),
-         "b_hh": P0["b_hh"].cpu().view(-1).clone().requires_grad_(True),
-         "w_q": P0["w_q"].cpu().clone().requires_grad_(True), "b_q": P0["b_q"].cpu().view(-1).clone().requires_grad_(True)}
-    pt = {"w_ih": tgt["w_ih"].cpu().float(), "w_hh": tgt["w_hh"].cpu().float(), "b_ih": tgt["b_ih"].cpu().view(-1),
-          "b_hh": tgt["b_hh"].cpu().view(-1), "w_q": tgt["w_q"].cpu(), "b_q": tgt["b_q"].cpu().view(-1)}
-    loss = gq.sequence_td_loss(p, pt, X, h0, A, R, D, d.gamma, d.burn)
+    p = {"w_ih": bf(P0["w_ih"]).requires_grad_(True), "w_hh": bf(P0["w_hh"]).requires_grad_(True)}
+    for n in ("b_ih", "b_hh", "w_q", "b_q"):
+        p[n] = P0[n].view(P0[n].shape if n == "w_q" else (-1,)).clone().requires_grad_(True)
+    pt = {"w_ih": bf(T0["w_ih"]), "w_hh": bf(T0["w_hh"]), "b_ih": T0["b_ih"].view(-1), "b_hh": T0["b_hh"].view(-1),
+          "w_q": T0["w_q"], "b_q": T0["b_q"].view(-1)}
+    q = _ref_unroll(X, h0, p, D, W_on)
+    with torch.no_grad():
+        qt = _ref_unroll(X, h0, pt, D, W_tg)
+        a_star = q[1:].argmax(-1, keepdim=True)
+        y = R + d.gamma * (1 - D) * qt[1:].gather(-1, a_star)[..., 0]
+    qa = q[:d.S].gather(-1, A[..., None])[..., 0]
+    loss = ((qa - y)[d.burn:] ** 2).mean()
     loss.backward()
+    # forward values: online / target Q of the kernels vs the reference unroll
+    assert torch.allclose(d.Q.cpu()[:, :3].view(d.S + 1, d.B, 3), q.detach(), atol=2e-3, rtol=2e-2)
+    assert torch.allclose(d.Q_t.cpu()[:, :3].view(d.S + 1, d.B, 3), qt, atol=2e-3, rtol=2e-2)
     got_loss = float(d.loss) / (d.B * (d.S - d.burn))
-    assert abs(got_loss - float(loss)) < 2e-2 * float(loss) + 1e-7, (got_loss, float(loss))
+    assert abs(got_loss - float(loss.detach())) < 3e-2 * float(loss.detach()) + 1e-7, (got_loss, float(loss))
     for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w_q", "b_q"):
         ref = p[n].grad.view(-1)
         got = d.dP[n].cpu().view(-1)
