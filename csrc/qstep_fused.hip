@@ -41,19 +41,14 @@ constexpr int NSTAT = 8;
 struct QStepParams {
   const float* prices;      // [E, T] env-major
   const float* prices4;     // [4][E][T4] shifted replicas (series.hip: replicate4)
-  float* budget;
-  int* shares;
-  float* value;
-  int* pos;
-  int* episodes;
-  float* last_final;
-  float* ret_sum;
+  // env state + per-step outputs as ONE struct-of-arrays buffer [ENV_ROWS][E] of 4-byte
+  // words (rows below): one base pointer instead of nine keeps the kernel's scalar
+  // registers from spilling across the chunk loop
+  int* env;
   const bf16_t* wq;         // bf16 flat params (kernel layout)
   const float* wf;          // fp32 flat params (biases read from here)
   float* slab;              // [G][P] per-workgroup partial gradients
   float* stats;             // [G][NSTAT]
-  int* actions_out;         // [E] or null
-  float* rewards_out;       // [E] or null
   unsigned long long* ctrl;   // ctrl[0] = step index (read), ctrl[1] = step+1 (written by block 0)
   int T, E, H, P, T4;
   int off_w0, off_w1, off_b1, off_w2, off_b2;
@@ -63,6 +58,12 @@ struct QStepParams {
   int env_offset;
   unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][16]) or null
 };
+
+// rows of QStepParams::env
+enum EnvRow : int { ER_POS = 0, ER_BUDGET, ER_SHARES, ER_VALUE, ER_RET_SUM, ER_EPISODES, ER_LAST_FINAL,
+                    ER_ACTION, ER_REWARD, ENV_ROWS };
+#define ENV_I(R, e) (p.env[(size_t)(R) * p.E + (e)])
+#define ENV_F(R, e) (reinterpret_cast<float*>(p.env)[(size_t)(R) * p.E + (e)])
 
 template <int INP, int H1P, int H2P>
 struct Geo {
@@ -322,8 +323,8 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
   {                                                                        \
     const int ch_ = min((CH), nchunks - 1);                                \
     const int e_ = ch_ * C + wave * RPW + min(lane, RPW - 1);              \
-    POS = p.pos[e_]; B = p.budget[e_]; SH = p.shares[e_];                  \
-    VAL = p.value[e_]; RS = p.ret_sum[e_]; EP = p.episodes[e_];            \
+    POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                  \
+    VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);            \
   }
 // One dwordx4 per lane per row: the window [ps, ps+H] is a run of aligned float4s in the
 // shifted replica ps & 3 of the bank (1 KiB contiguous per wave-instruction, no realignment).
@@ -467,8 +468,8 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
       xn[H + 1] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
       xn[H + 2] = f2bf(1.0f);
       st_explore += exploit ? 0.f : 1.f;
-      if (p.actions_out) p.actions_out[e] = a;
-      if (p.rewards_out) p.rewards_out[e] = rew;
+      ENV_I(ER_ACTION, e) = a;
+      ENV_F(ER_REWARD, e) = rew;
     }
     __syncthreads();
     ST_STAMP(3);
@@ -509,22 +510,22 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
       const float rs = sEnv[r * 8 + 5] + rew;
       if (np >= p.T - H) {
         const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
-        p.last_final[e] = fin;
-        p.episodes[e] = sEnvI[r * 4 + 3] + 1;
-        p.budget[e] = p.b0;
-        p.shares[e] = p.s0;
-        p.value[e] = 0.f;
-        p.pos[e] = 0;
-        p.ret_sum[e] = 0.f;
+        ENV_F(ER_LAST_FINAL, e) = fin;
+        ENV_I(ER_EPISODES, e) = sEnvI[r * 4 + 3] + 1;
+        ENV_F(ER_BUDGET, e) = p.b0;
+        ENV_I(ER_SHARES, e) = p.s0;
+        ENV_F(ER_VALUE, e) = 0.f;
+        ENV_I(ER_POS, e) = 0;
+        ENV_F(ER_RET_SUM, e) = 0.f;
         st_done += 1.f;
         st_fsum += fin;
         st_fsq += fin * fin;
       } else {
-        p.budget[e] = b2;
-        p.shares[e] = s2;
-        p.value[e] = vnew;
-        p.pos[e] = np;
-        p.ret_sum[e] = rs;
+        ENV_F(ER_BUDGET, e) = b2;
+        ENV_I(ER_SHARES, e) = s2;
+        ENV_F(ER_VALUE, e) = vnew;
+        ENV_I(ER_POS, e) = np;
+        ENV_F(ER_RET_SUM, e) = rs;
       }
     }
     __syncthreads();

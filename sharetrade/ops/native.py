@@ -29,10 +29,8 @@ class NativeUnavailable(RuntimeError):
 
 class QStepParams(C.Structure):
     _fields_ = [
-        ("prices", C.c_void_p), ("prices4", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
-        ("pos", C.c_void_p), ("episodes", C.c_void_p), ("last_final", C.c_void_p), ("ret_sum", C.c_void_p),
-        ("wq", C.c_void_p), ("wf", C.c_void_p), ("slab", C.c_void_p), ("stats", C.c_void_p),
-        ("actions_out", C.c_void_p), ("rewards_out", C.c_void_p), ("ctrl", C.c_void_p),
+        ("prices", C.c_void_p), ("prices4", C.c_void_p), ("env", C.c_void_p),
+        ("wq", C.c_void_p), ("wf", C.c_void_p), ("slab", C.c_void_p), ("stats", C.c_void_p), ("ctrl", C.c_void_p),
         ("T", C.c_int), ("E", C.c_int), ("H", C.c_int), ("P", C.c_int), ("T4", C.c_int),
         ("off_w0", C.c_int), ("off_w1", C.c_int), ("off_b1", C.c_int), ("off_w2", C.c_int), ("off_b2", C.c_int),
         ("eps", C.c_float), ("inv_ramp", C.c_float), ("gamma", C.c_float), ("loss_coef", C.c_float),
@@ -53,6 +51,10 @@ class OptimParams(C.Structure):
         ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int), ("nstat", C.c_int),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
     ]
+
+
+# rows of QStepParams::env (csrc/qstep_fused.hip EnvRow): int32 / fp32 words
+ENV_ROWS = ("pos", "budget", "shares", "value", "ret_sum", "episodes", "last_final", "actions_out", "rewards_out")
 
 
 def available() -> bool:

@@ -157,8 +157,19 @@ class VectorEngine:
         dev = self.device
         L = self.layout
         self.ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.actions_out = torch.zeros(self.E, dtype=torch.int32, device=dev)
-        self.rewards_out = torch.zeros(self.E, dtype=torch.float32, device=dev)
+        # env state + step outputs live in one [rows][E] 4-byte buffer (the fused kernel takes ONE
+        # base pointer); the EnvState tensors become row views of it, values carried over
+        self.env_soa = torch.zeros(len(native.ENV_ROWS), self.E, dtype=torch.int32, device=dev)
+        rows = {}
+        for i, k in enumerate(native.ENV_ROWS):
+            src = getattr(self.state, k, None)
+            dt = torch.float32 if k in ("budget", "value", "ret_sum", "last_final", "rewards_out") else torch.int32
+            rows[k] = self.env_soa[i].view(dt)
+            if src is not None:
+                rows[k].copy_(src)
+        for k in self.state.as_dict():
+            setattr(self.state, k, rows[k])
+        self.actions_out, self.rewards_out = rows["actions_out"], rows["rewards_out"]
         self.grad = torch.zeros(L.numel, dtype=torch.float32, device=dev)
         self.stat_acc = torch.zeros(NSTAT, dtype=torch.float64, device=dev)
         if self.kernel == "fp32_rows":
@@ -180,13 +191,9 @@ class VectorEngine:
         seg = L.segments
         q = native.QStepParams()
         q.prices4, q.T4 = native.ptr(self.prices4), int(self.prices4.shape[2])
-        q.prices, q.budget, q.shares, q.value = (native.ptr(self.prices), native.ptr(st.budget),
-                                                 native.ptr(st.shares), native.ptr(st.value))
-        q.pos, q.episodes, q.last_final, q.ret_sum = (native.ptr(st.pos), native.ptr(st.episodes),
-                                                      native.ptr(st.last_final), native.ptr(st.ret_sum))
+        q.prices, q.env = native.ptr(self.prices), native.ptr(self.env_soa)
         q.wq, q.wf = native.ptr(self.params_bf), native.ptr(self.params)
         q.slab, q.stats = native.ptr(self.slab), native.ptr(self.stat_slab)
-        q.actions_out, q.rewards_out = native.ptr(self.actions_out), native.ptr(self.rewards_out)
         q.ctrl = native.ptr(self.ctrl)
         q.T, q.E, q.H, q.P = self.T, self.E, self.H, L.numel
         q.off_w0, q.off_w1, q.off_b1 = seg["W0"].offset, seg["W1"].offset, seg["b1"].offset
