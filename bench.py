@@ -117,6 +117,17 @@ def main() -> int:
         dist.all_reduce(ret)
         dist.all_reduce(stats)
     el = float(elapsed[0])
+    allreduce_ms = None
+    if world > 1 and eng._sync is not None:
+        # gradient all-reduce time, measured on a few extra steps AFTER the timed window
+        eng._sync.enable_timing()
+        for _ in range(min(20, args.steps)):
+            eng.step()
+        ms = eng._sync.pop_timing_ms()
+        eng._sync.enable_timing(False)
+        t = torch.tensor([ms if ms is not None else 0.0], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        allreduce_ms = round(float(t[0]), 4)
     total_steps = eng.E * world * args.steps
     value = total_steps / el
     if rank == 0:
@@ -149,6 +160,8 @@ def main() -> int:
             "mean_td_loss": st[1] / max(n_trans, 1),
             "vs_reference_floor": round(value / REFERENCE_FLOOR, 1),
         }
+        if allreduce_ms is not None:
+            out["allreduce_ms_per_step"] = allreduce_ms
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

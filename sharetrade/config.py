@@ -184,6 +184,11 @@ class Config:
             import tomli
 
             d = tomli.loads(raw.decode())
+        elif path.endswith(".conf") or path.endswith(".hocon"):
+            # Akka-style application.conf (the reference's configuration format)
+            from .utils import hocon
+
+            d, _ = hocon.akka_to_config(hocon.loads(raw.decode()))
         else:
             d = json.loads(raw.decode())
         _merge(cfg, d)

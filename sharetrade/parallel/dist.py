@@ -24,6 +24,7 @@ from __future__ import annotations
 import datetime
 import math
 import os
+import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -101,10 +102,49 @@ class GradSync:
         self.slices = [(o, min(numel, o + per)) for o in range(0, numel, per)]
         self._wire: Optional[torch.Tensor] = None
         self.calls = 0
+        self.timing = False
+        self._events = []        # (start, end) CUDA events of timed calls, or (t0, t1) host seconds
+        self._timed_ms = 0.0
+        self._timed_n = 0
+
+    def enable_timing(self, on: bool = True) -> None:
+        """Record the wall time of every all-reduce on the stream (metrics ``allreduce_ms``)."""
+        self.timing = on
+
+    def pop_timing_ms(self) -> Optional[float]:
+        """Mean all-reduce time (ms) over the calls since the last pop; synchronizes recorded events."""
+        for a, b in self._events:
+            if isinstance(a, float):
+                self._timed_ms += (b - a) * 1e3
+            else:
+                b.synchronize()
+                self._timed_ms += a.elapsed_time(b)
+            self._timed_n += 1
+        self._events = []
+        if self._timed_n == 0:
+            return None
+        m = self._timed_ms / self._timed_n
+        self._timed_ms, self._timed_n = 0.0, 0
+        return m
 
     def all_reduce(self, grad: torch.Tensor, async_op: bool = False):
         if not self.ctx.is_distributed:
             return None
+        if self.timing and not async_op:
+            if grad.is_cuda:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                self._all_reduce(grad, False)
+                b.record()
+            else:
+                a = time.perf_counter()
+                self._all_reduce(grad, False)
+                b = time.perf_counter()
+            self._events.append((a, b))
+            return None
+        return self._all_reduce(grad, async_op)
+
+    def _all_reduce(self, grad: torch.Tensor, async_op: bool = False):
         g = self.ctx.group
         self.calls += 1
         if self.compress == "bf16":

@@ -30,6 +30,8 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
     eng.sync_params_from(0)
     if graph and eng.backend == "native" and world_size == 1:
         eng.capture_graph(warmup=1)
+    if eng._sync is not None:
+        eng._sync.enable_timing()          # metrics: mean all-reduce ms per logging window
     ml = MetricsLogger(metrics_path)
     ws = WindowStats()
     ws.window(eng.stats_dict(), eng.step_count, eng.E, world_size)
@@ -47,7 +49,12 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
         s = eng.step_count
         if log_every and s % log_every == 0:
             eng.synchronize()
-            ml.log(ws.window(eng.stats_dict(), s, eng.E, world_size))
+            rec = ws.window(eng.stats_dict(), s, eng.E, world_size)
+            if eng._sync is not None:
+                ms = eng._sync.pop_timing_ms()
+                if ms is not None:
+                    rec["allreduce_ms"] = ms
+            ml.log(rec)
         if mgr and mgr.should_save(s) and rank == 0:
             eng.synchronize()
             mgr.save(s, eng.state_dict(), {"kind": "VectorEngine"})

@@ -101,3 +101,32 @@ def test_dp_bf16_wire_compression_stays_close():
     res32 = _run_dp(2, 3, 4, opt="sgd", compress="")
     rel = float((res[0]["params"] - res32[0]["params"]).norm() / res32[0]["params"].norm())
     assert rel < 1e-2
+
+
+def _timing_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from sharetrade.parallel import dist as D
+
+    ctx = D.init(backend="gloo", device="cpu")
+    gs = D.GradSync(ctx, 1000)
+    g = torch.full((1000,), float(rank + 1))
+    assert gs.pop_timing_ms() is None
+    gs.enable_timing()
+    for _ in range(3):
+        gs.all_reduce(g)
+    ms = gs.pop_timing_ms()
+    torch.save({"ms": ms, "g0": float(g[0]), "calls": gs.calls, "again": gs.pop_timing_ms()},
+               os.path.join(out_dir, f"t{rank}.pt"))
+    D.shutdown(ctx)
+
+
+def test_grad_sync_records_allreduce_time():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_timing_worker, args=(2, port, d), nprocs=2, join=True, start_method="spawn")
+        res = [torch.load(os.path.join(d, f"t{r}.pt"), weights_only=True) for r in range(2)]
+    for r in res:
+        assert r["ms"] is not None and r["ms"] >= 0.0 and r["again"] is None
+        assert r["calls"] == 3 and r["g0"] == 3.0 * 2 ** 2   # 1 + 2, then doubled by each further in-place sum
