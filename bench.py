@@ -44,6 +44,9 @@ def main() -> int:
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on cuda:0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
+    ap.add_argument("--sync-dp", action="store_true",
+                    help="N>1: strict sync DP (all-reduce exposed) instead of the all-reduce overlapped with the "
+                         "next step's kernel (one-step delayed gradient, identical on every rank)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -76,6 +79,7 @@ def main() -> int:
 
     cfg = preset_config("flagship")
     cfg.engine.envs_per_rank = args.envs
+    cfg.engine.dp_overlap = not args.sync_dp
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 
@@ -119,10 +123,11 @@ def main() -> int:
     el = float(elapsed[0])
     allreduce_ms = None
     if world > 1 and eng._sync is not None:
-        # gradient all-reduce time, measured on a few extra steps AFTER the timed window
+        # latency of the gradient all-reduce (same size, same group), measured AFTER the timed window
+        scratch = torch.zeros_like(eng.params)
         eng._sync.enable_timing()
-        for _ in range(min(20, args.steps)):
-            eng.step()
+        for _ in range(20):
+            eng._sync.all_reduce(scratch)
         ms = eng._sync.pop_timing_ms()
         eng._sync.enable_timing(False)
         t = torch.tensor([ms if ms is not None else 0.0], dtype=torch.float64, device=dev)
@@ -151,6 +156,9 @@ def main() -> int:
                 "global_batch": eng.E * world,
                 "seq_len": cfg.model.history,
                 "parallelism": f"dp{world}",
+                "dp_gradient_sync": ("none" if world == 1 else
+                                     "sync all-reduce" if args.sync_dp else
+                                     "all-reduce overlapped with next step (1-step delayed)"),
                 "envs_per_gpu": eng.E,
                 "hip_graph": use_graph,
             },

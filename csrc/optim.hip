@@ -29,6 +29,7 @@ struct OptimParams {
   int G, P, kind, mode;    // mode: 0 = reduce+update, 1 = reduce only, 2 = update only
   int nstat;
   float lr, beta1, beta2, eps, scale;
+  int tdelay;              // updates lagging the step counter (overlapped DP applies step t-1's gradient at t)
 };
 
 constexpr int RT = 256;   // threads per workgroup
@@ -84,8 +85,9 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
       g.x *= p.scale; g.y *= p.scale; g.z *= p.scale; g.w *= p.scale;
     }
   }
-  const unsigned long long t = p.ctrl[1];
-  if (blockIdx.x == 0 && tid == 0) p.ctrl[0] = t;  // next step index (read by the next step kernel)
+  const unsigned long long tstep = p.ctrl[1];
+  if (blockIdx.x == 0 && tid == 0) p.ctrl[0] = tstep;  // next step index (read by the next step kernel)
+  const unsigned long long t = tstep - (unsigned long long)p.tdelay;   // 1-based optimizer update count
   if (col4 >= P4) return;
   float gg[4] = {g.x, g.y, g.z, g.w};
   const float4 m4 = reinterpret_cast<const float4*>(p.mask)[col4];
@@ -132,6 +134,8 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
 
 // ctrl[1] = ctrl[0] + 1 : the 1-based update count of the step about to run.
 __global__ void advance_kernel(unsigned long long* ctrl) { ctrl[1] = ctrl[0] + 1; }
+// ctrl[0] = ctrl[1] : commit the step index without an optimizer update (first overlapped-DP step)
+__global__ void commit_kernel(unsigned long long* ctrl) { ctrl[0] = ctrl[1]; }
 
 __global__ void to_bf16_kernel(const float* __restrict__ in, bf16_t* __restrict__ out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -149,6 +153,11 @@ extern "C" hipError_t st_reduce_optim(const st::OptimParams* p, hipStream_t stre
 
 extern "C" hipError_t st_advance(unsigned long long* ctrl, hipStream_t stream) {
   hipLaunchKernelGGL(st::advance_kernel, dim3(1), dim3(1), 0, stream, ctrl);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_commit_step(unsigned long long* ctrl, hipStream_t stream) {
+  hipLaunchKernelGGL(st::commit_kernel, dim3(1), dim3(1), 0, stream, ctrl);
   return hipGetLastError();
 }
 

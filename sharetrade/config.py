@@ -143,6 +143,11 @@ class EngineConfig:
     backend: str = "auto"           # auto | native | torch
     bucket_mb: float = 4.0          # DP gradient all-reduce bucket (one call below this size)
     grad_compress: str = ""         # "" | "bf16" (wire format of the DP all-reduce)
+    # DP gradient all-reduce overlapped with the next step's fused kernel: the gradient of step t
+    # is applied after step t+1's kernel (one-step delay, identical on every rank).  The reference
+    # applies updates asynchronously through one mailbox; False = strict sync DP (bit-equal to one
+    # process holding all envs).
+    dp_overlap: bool = False
 
 
 @dataclass

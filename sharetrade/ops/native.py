@@ -50,6 +50,7 @@ class OptimParams(C.Structure):
         ("stats", C.c_void_p), ("stat_acc", C.c_void_p),
         ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int), ("nstat", C.c_int),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
+        ("tdelay", C.c_int),
     ]
 
 
@@ -77,6 +78,8 @@ def lib() -> C.CDLL:
     L.st_reduce_optim.restype = C.c_int
     L.st_advance.argtypes = [C.c_void_p, C.c_void_p]
     L.st_advance.restype = C.c_int
+    L.st_commit_step.argtypes = [C.c_void_p, C.c_void_p]
+    L.st_commit_step.restype = C.c_int
     L.st_to_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.st_to_bf16.restype = C.c_int
     L.st_random_walk.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_uint32,

@@ -144,6 +144,22 @@ class GradSync:
             return None
         return self._all_reduce(grad, async_op)
 
+    def start(self, grad: torch.Tensor):
+        """Enqueue the all-reduce of ``grad`` without waiting (fp32 wire); returns ``wait()``, which
+        makes the CURRENT stream wait for the result (host never blocks on RCCL)."""
+        if not self.ctx.is_distributed:
+            return lambda: None
+        if self.compress:
+            self.all_reduce(grad)
+            return lambda: None
+        hs = self._all_reduce(grad, async_op=True)
+        hs = hs if isinstance(hs, list) else [hs]
+
+        def wait():
+            for h in hs:
+                h.wait()
+        return wait
+
     def _all_reduce(self, grad: torch.Tensor, async_op: bool = False):
         g = self.ctx.group
         self.calls += 1

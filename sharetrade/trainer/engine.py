@@ -236,7 +236,9 @@ class VectorEngine:
         sh = native.stream_handle()
         native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],
                                        self.layout.pdims[2], self.grid, sh), "qstep")
-        if self.world_size > 1:
+        if self.world_size > 1 and self.cfg.engine.dp_overlap:
+            self._overlap_step(L, sh)
+        elif self.world_size > 1:
             self._op.mode = 1
             native.check(L.st_reduce_optim(self._op, sh), "reduce")
             self._sync.all_reduce(self.grad)
@@ -245,6 +247,52 @@ class VectorEngine:
         else:
             self._op.mode = 0
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
+
+    def _overlap_step(self, L, sh) -> None:
+        """DP step with the all-reduce hidden behind the next fused kernel: reduce this step's slabs
+        into one of two gradient buffers, enqueue its all-reduce, then apply the PREVIOUS step's
+        reduced gradient (identical on every rank); the first step only commits the step counter."""
+        if not hasattr(self, "_ov"):
+            import ctypes as C
+
+            bufs = [self.grad, torch.zeros_like(self.grad)]
+            ops = []
+            for b in bufs:
+                o = native.OptimParams()
+                C.pointer(o)[0] = self._op
+                o.grad = native.ptr(b)
+                o.tdelay = 1
+                ops.append(o)
+            self._ov = {"bufs": bufs, "ops": ops, "parity": 0, "pending": None}
+        ov = self._ov
+        i = ov["parity"]
+        op = ov["ops"][i]
+        op.mode = 1
+        native.check(L.st_reduce_optim(op, sh), "reduce")
+        wait_new = self._sync.start(ov["bufs"][i])
+        if ov["pending"] is not None:
+            wait_prev, j = ov["pending"]
+            wait_prev()
+            upd = ov["ops"][j]
+            upd.mode = 2
+            native.check(L.st_reduce_optim(upd, sh), "update")
+        else:
+            native.check(L.st_commit_step(native.ptr(self.ctrl), sh), "commit")
+        ov["pending"] = (wait_new, i)
+        ov["parity"] = i ^ 1
+
+    def flush_pending(self) -> None:
+        """Apply a gradient still in flight (overlapped DP) -- before checkpoints and at the end of training."""
+        ov = getattr(self, "_ov", None)
+        if ov is None or ov["pending"] is None:
+            return
+        wait_prev, j = ov["pending"]
+        wait_prev()
+        upd = ov["ops"][j]
+        upd.mode, upd.tdelay = 2, 0          # the last step's own update count
+        native.check(native.lib().st_reduce_optim(upd, native.stream_handle()), "update")
+        upd.tdelay = 1
+        ov["pending"] = None
 
     def _f32_stats(self) -> None:
         r = self.rewards_out.double()
@@ -351,6 +399,7 @@ class VectorEngine:
 
     # ---------------------------------------------------------------- state
     def state_dict(self) -> Dict[str, torch.Tensor]:
+        self.flush_pending()
         d = {"params": self.params, "opt_s1": self.opt.s1, "opt_s2": self.opt.s2,
              "opt_t": torch.tensor([self.opt.t], dtype=torch.int64),
              "step": torch.tensor([self.step_count], dtype=torch.int64)}

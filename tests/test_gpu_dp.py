@@ -37,7 +37,7 @@ def _bank(n, T=400):
     return torch.from_numpy(random_walk(T, 50.0, 0.02, 3, n_series=n).astype(np.float32))
 
 
-def _worker(rank, world, port, E, steps, kernel, out):
+def _worker(rank, world, port, E, steps, kernel, out, overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -45,11 +45,14 @@ def _worker(rank, world, port, E, steps, kernel, out):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
-    eng = VectorEngine(_cfg(kernel), prices=_bank(E * world)[rank * E:(rank + 1) * E], device=dev, rank=rank,
+    cfg = _cfg(kernel)
+    cfg.engine.dp_overlap = overlap
+    eng = VectorEngine(cfg, prices=_bank(E * world)[rank * E:(rank + 1) * E], device=dev, rank=rank,
                        world_size=world, group=dist.group.WORLD, envs=E)
     assert eng.backend == "native"
     eng.sync_params_from(0)
     eng.run(steps)
+    eng.flush_pending()
     torch.cuda.synchronize()
     torch.save({"params": eng.params.cpu(), "budget": eng.state.budget.cpu()}, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
@@ -72,3 +75,20 @@ def test_native_dp_two_ranks_match_single_process(native_built, kernel):
     rel = float((res[0]["params"] - p).norm() / p.norm())
     assert rel < (1e-5 if kernel == "fp32" else 1e-3), rel
     assert torch.equal(torch.cat([res[0]["budget"], res[1]["budget"]]), single.state.budget.cpu())
+
+
+def test_overlapped_dp_is_rank_consistent_and_one_step_delayed(native_built):
+    """dp_overlap: every rank applies the same (one-step delayed) gradients; the trajectory stays
+    close to strict sync DP and the first step is identical (same initial weights)."""
+    E, steps, world = 64, 6, 2
+    out = {}
+    for ov in (False, True):
+        with tempfile.TemporaryDirectory() as d:
+            mp.start_processes(_worker, args=(world, _port(), E, steps, "bf16", d, ov), nprocs=world, join=True,
+                               start_method="spawn")
+            out[ov] = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    a, b = out[True]
+    assert torch.equal(a["params"], b["params"]) and torch.isfinite(a["params"]).all()
+    p_sync = out[False][0]["params"]
+    rel = float((a["params"] - p_sync).norm() / p_sync.norm())
+    assert 0.0 < rel < 5e-2, rel
