@@ -93,6 +93,10 @@ struct GruPack {
   s8v* wih;            // [RW][3][2][64]
   float* bias4;        // [4][RH]: b_ir+b_hr, b_iz+b_hz, b_in, b_hn
   float* wq;           // [4][RH]: W_q rows, row 3 = b_q (first 3 entries)
+  // optional: W_hh^T as MX-fp8 A fragments of the learner's backward dh GEMM (rows = units,
+  // K = the 768 gate rows): [RW][2 m][6 ks][64] fragments + scales, or null
+  i8v* whhT8;
+  int* whhTs;
 };
 
 // one thread per (wave, gate, m-tile, k-step, lane) fragment
@@ -132,6 +136,30 @@ __global__ void __launch_bounds__(256) gru_pack_kernel(GruPack p) {
   }
   p.whh8[tid] = frag;
   p.whhs[tid] = blk_e(gl) + 127;      // the scale slot of lane i + 16g belongs to K-block g
+  if (p.whhT8 != nullptr) {
+    // backward fragment: the same thread count covers [RW][2][6][64]
+    const int f2 = tid >> 6, ks2 = f2 % 6, m2 = (f2 / 6) & 1, w2 = f2 / 12;
+    const int u = 32 * w2 + 16 * m2 + (lane & 15);      // row of W_hh^T = hidden unit
+    const float* col = p.w_hh + (size_t)(128 * ks2) * RH + u;   // W_hh[g][u], g = 128 ks2 + ...
+    auto blk_t = [&](int b) {
+      float amax = 0.f;
+      for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(col[(size_t)(32 * b + j) * RH]));
+      return mx_exp(amax);
+    };
+    const int t_lo = blk_t(gl >> 1), t_hi = blk_t(2 + (gl >> 1));
+    i8v fr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* lo2 = col + (size_t)(16 * gl + 4 * j) * RH;
+      const float* hi2 = col + (size_t)(64 + 16 * gl + 4 * j) * RH;
+      fr[j] = (int)fp8x4(ldexpf(lo2[0], -t_lo), ldexpf(lo2[RH], -t_lo), ldexpf(lo2[2 * RH], -t_lo),
+                         ldexpf(lo2[3 * RH], -t_lo));
+      fr[4 + j] = (int)fp8x4(ldexpf(hi2[0], -t_hi), ldexpf(hi2[RH], -t_hi), ldexpf(hi2[2 * RH], -t_hi),
+                             ldexpf(hi2[3 * RH], -t_hi));
+    }
+    p.whhT8[tid] = fr;
+    p.whhTs[tid] = blk_t(gl) + 127;
+  }
   if (ks == 0) {
     s8v x;
 #pragma unroll

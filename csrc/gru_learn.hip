@@ -25,7 +25,6 @@ namespace st {
 
 constexpr int LB = 32;      // sequences per workgroup
 constexpr int NSV = 5;      // saved quantities: r, z, n, gh_n, h_prev
-constexpr int GS = RG + 8;  // dGh LDS tile row stride (bf16): 1552 B, 16-B aligned
 
 // ---------------------------------------------------------------- sequence gather
 struct GruGather {
@@ -59,6 +58,7 @@ __global__ void __launch_bounds__(256) gru_gather_kernel(GruGather g) {
     const int t = j >> 3, c = j & 7;
     uint4 v = z;
     if (c < RF / 8) v = reinterpret_cast<const uint4*>(g.rx + (idx * (size_t)(S + 1) + t) * RF)[c];
+    if (c == RF / 8) v.x = 0x3F80u;   // column RF = 1.0: the dW_ih GEMM's column RF is then db_ih
     reinterpret_cast<uint4*>(g.X + ((size_t)t * g.B + b) * RFL)[c] = v;
   }
   const s4v hv = *reinterpret_cast<const s4v*>(g.rh0 + idx * RH + 4 * lane);
@@ -346,26 +346,29 @@ struct GruSeqBwd {
   const uint4* sv;      // forward saves
   const float* dQ;      // [S*B][4]
   const float* D;       // [S][B]
-  const bf16_t* WhhT;   // [RH][RG] bf16 (W_hh^T, written by the optimizer)
+  const i8v* whhT8;     // W_hh^T MX-fp8 A fragments [RW][2][6][64] (gru_pack_kernel, online net)
+  const int* whhTs;     // their E8M0 scales
   const float* wq;      // [3][RH] online fp32
   bf16_t* dGx;          // [S*B][RG]
   bf16_t* dGh;          // [S*B][RG]
   float* gwq;           // [3][RH]   (+= ; zeroed by the host each update)
   float* gbq;           // [3]
-  float* gbih;          // [RG]
-  float* gbhh;          // [RG]
   int B, S;
 };
 
+constexpr int GQS = RG + 16;      // dGh fp8 tile row stride (bytes): 784, conflict-free b128 reads
+constexpr int GSC = RG / 32 + 1;  // scale row stride (ints): 24 K-blocks + pad
+
+constexpr int LBB = 16;          // sequences per backward workgroup (one MFMA env tile: register budget)
+
 struct BwdLds {
-  static constexpr int G = 0;                       // [2][LB][GS] bf16 dGh tiles
-  static constexpr int WQ = G + 2 * LB * GS * 2;    // [3][RH] float
+  // [2 buffers][hi, lo][LBB][GQS] bytes, then scales [2][hi, lo][LBB][GSC] ints, then W_q
+  static constexpr int G8 = 0;
+  static constexpr int SC = G8 + 2 * 2 * LBB * GQS;
+  static constexpr int WQ = SC + 2 * 2 * LBB * GSC * 4;
   static constexpr int BYTES = WQ + 3 * RH * 4;
 };
 static_assert(BwdLds::BYTES <= 160 * 1024, "bwd LDS");
-
-constexpr int BK = RG / 32;   // 24 K-steps of the dh GEMM
-constexpr int BLA = 4;        // W_hh^T fragment look-ahead (K-steps)
 
 ST_DEV float row16_sum(float v) {   // sum over the 16 lanes of a row (same lane group)
   v += __shfl_xor(v, 1, 64);
@@ -374,52 +377,120 @@ ST_DEV float row16_sum(float v) {   // sum over the 16 lanes of a row (same lane
   v += __shfl_xor(v, 8, 64);
   return v;
 }
+template <int BYTE>
+ST_DEV float fp8_to_f32(uint32_t word) {
+  return __builtin_amdgcn_cvt_f32_fp8((int)word, BYTE);
+}
+
+// dGh of one gate for this lane's (m, i) units of env tile n, as an MX-fp8 hi/lo pair:
+// hi = q(x), lo = q(x - deq(hi)), each with its own E8M0 scale per (seq, 32-unit block = this
+// wave's units): ~bf16-level precision for the recurrent GEMM's B operand.
+ST_DEV void quant_hilo(const float (&x)[8], unsigned char* hiRow, unsigned char* loRow, int* scHi, int* scLo,
+                       int off, int blk, int g4) {
+  float amax = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(x[k]));
+  amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  const int eh = mx_exp(amax);
+  uint32_t hw[2];
+  float res[8];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    hw[m] = fp8x4(ldexpf(x[4 * m], -eh), ldexpf(x[4 * m + 1], -eh), ldexpf(x[4 * m + 2], -eh),
+                  ldexpf(x[4 * m + 3], -eh));
+    res[4 * m + 0] = x[4 * m + 0] - ldexpf(fp8_to_f32<0>(hw[m]), eh);
+    res[4 * m + 1] = x[4 * m + 1] - ldexpf(fp8_to_f32<1>(hw[m]), eh);
+    res[4 * m + 2] = x[4 * m + 2] - ldexpf(fp8_to_f32<2>(hw[m]), eh);
+    res[4 * m + 3] = x[4 * m + 3] - ldexpf(fp8_to_f32<3>(hw[m]), eh);
+  }
+  float rmax = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) rmax = fmaxf(rmax, fabsf(res[k]));
+  rmax = fmaxf(rmax, __shfl_xor(rmax, 16, 64));
+  rmax = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
+  const int el = mx_exp(rmax);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    *reinterpret_cast<uint32_t*>(hiRow + off + 16 * m) = hw[m];
+    *reinterpret_cast<uint32_t*>(loRow + off + 16 * m) =
+        fp8x4(ldexpf(res[4 * m], -el), ldexpf(res[4 * m + 1], -el), ldexpf(res[4 * m + 2], -el),
+              ldexpf(res[4 * m + 3], -el));
+  }
+  if (g4 == 0) {
+    scHi[blk] = eh + 127;
+    scLo[blk] = el + 127;
+  }
+}
 
 __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  bf16_t* sG = reinterpret_cast<bf16_t*>(lds + BwdLds::G);
+  int* sSc = reinterpret_cast<int*>(lds + BwdLds::SC);
   float* sWq = reinterpret_cast<float*>(lds + BwdLds::WQ);
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int B = p.B, S = p.S, b0 = blockIdx.x * LB;
+  const int B = p.B, S = p.S, b0 = blockIdx.x * LBB;
   const size_t nblk = (size_t)(B / LB);
+  const int fblk = blockIdx.x >> 1, fn = blockIdx.x & 1;   // forward block / env tile of the saves
   for (int i = tid; i < 3 * RH; i += RT) sWq[i] = p.wq[i];
+  // resident W_hh^T (this wave's 32 units x 768 gates) as MX-fp8: 96 VGPRs + 3 packed scale regs
+  i8v Wt[2][6];
+  int Wts4[3] = {0, 0, 0};   // (m, ks) -> reg (6m + ks) >> 2, byte (6m + ks) & 3
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      const int idx = ((wave * 2 + m) * 6 + ks) * 64 + lane;
+      const int q = 6 * m + ks;
+      Wt[m][ks] = p.whhT8[idx];
+      Wts4[q >> 2] |= (p.whhTs[idx] & 0xFF) << (8 * (q & 3));
+    }
 
-  float rec[2][2][4];        // dL/d(masked h_t) arriving from step t+1 (direct + GEMM)
-  float gq[3][2][4];         // W_q gradient partials (units m, i), summed over this lane's seqs / steps
-  float gr[2][4], gz[2][4], gnx[2][4], gnh[2][4];   // bias gradient partials
+  float rec[2][4];           // dL/d(masked h_t) arriving from step t+1 (direct + GEMM)
+  float gq[3][2][4];         // W_q gradient partials (units m, i), summed over this lane's steps
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      rec[m][0][i] = rec[m][1][i] = 0.f;
+      rec[m][i] = 0.f;
       gq[0][m][i] = gq[1][m][i] = gq[2][m][i] = 0.f;
-      gr[m][i] = gz[m][i] = gnx[m][i] = gnh[m][i] = 0.f;
     }
   float gbq0 = 0.f, gbq1 = 0.f, gbq2 = 0.f;
-  // W_hh^T rows of this wave's output units (A operand of the dh GEMM), 16 B per fragment
-  const bf16_t* wrow0 = p.WhhT + (size_t)(32 * wave + l16) * RG + 8 * g4;
-  const bf16_t* wrow1 = wrow0 + (size_t)16 * RG;
+  // step inputs (saves, dQ rows, done flags) are loaded one step ahead
+  uint4 pf[NSV];
+  float4 pdq;
+  float pkeep;
+  auto load_step = [&](int tt) {
+    const uint4* sv = p.sv + ((((size_t)tt * nblk + fblk) * RW + wave) * NSV * 2) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < NSV; ++q) pf[q] = sv[(q * 2 + fn) * 64];
+    const int b = b0 + l16;
+    pdq = *reinterpret_cast<const float4*>(p.dQ + ((size_t)tt * B + b) * 4);
+    pkeep = (tt < S - 1) ? 1.f - p.D[(size_t)tt * B + b] : 0.f;
+  };
+  load_step(S - 1);
   __syncthreads();
 
   for (int t = S - 1; t >= 0; --t) {
     const int cur = t & 1;
-    bf16_t* cG = sG + cur * LB * GS;
-    const uint4* sv = p.sv + ((((size_t)t * nblk + blockIdx.x) * RW + wave) * NSV * 2) * 64 + lane;
-    float nrec[2][2][4];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int row = 16 * n + l16, b = b0 + row;
-      const float4 dq = *reinterpret_cast<const float4*>(p.dQ + ((size_t)t * B + b) * 4);
-      const float keep = (t < S - 1) ? 1.f - p.D[(size_t)t * B + b] : 0.f;
+    unsigned char* gHi = lds + BwdLds::G8 + (cur * 2 + 0) * LBB * GQS;
+    unsigned char* gLo = lds + BwdLds::G8 + (cur * 2 + 1) * LBB * GQS;
+    int* sHi = sSc + (cur * 2 + 0) * LBB * GSC;
+    int* sLo = sSc + (cur * 2 + 1) * LBB * GSC;
+    const int row = l16, b = b0 + row;
+    float nrec[2][4];
+    float dghv[3][8];      // dGh per gate (r, z, n_h), (m, i)
+    {
+      const float4 dq = pdq;
+      const float keep = pkeep;
       float vr[8], vz[8], vn[8], vg[8], vh[8];
-      unpack8_bf(sv[(0 * 2 + n) * 64], vr);
-      unpack8_bf(sv[(1 * 2 + n) * 64], vz);
-      unpack8_bf(sv[(2 * 2 + n) * 64], vn);
-      unpack8_bf(sv[(3 * 2 + n) * 64], vg);
-      unpack8_bf(sv[(4 * 2 + n) * 64], vh);
+      unpack8_bf(pf[0], vr);
+      unpack8_bf(pf[1], vz);
+      unpack8_bf(pf[2], vn);
+      unpack8_bf(pf[3], vg);
+      unpack8_bf(pf[4], vh);
       if (wave == 0 && g4 == 0) { gbq0 += dq.x; gbq1 += dq.y; gbq2 += dq.z; }
-      float dar[8], daz[8], dan[8], dgn[8];
+      float dan[8];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int u0 = 32 * wave + 16 * m + 4 * g4;
@@ -430,7 +501,7 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
         for (int i = 0; i < 4; ++i) {
           const int k = 4 * m + i;
           const float r = vr[k], z = vz[k], nn = vn[k], gh = vg[k], hp = vh[k];
-          float dh = keep * rec[m][n][i];
+          float dh = keep * rec[m][i];
           dh = __builtin_fmaf(dq.x, w0[i], dh);
           dh = __builtin_fmaf(dq.y, w1[i], dh);
           dh = __builtin_fmaf(dq.z, w2[i], dh);
@@ -440,88 +511,76 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
           gq[2][m][i] = __builtin_fmaf(dq.z, h, gq[2][m][i]);
           const float dn = dh * (1.f - z);
           const float dz = dh * (hp - nn);
-          nrec[m][n][i] = dh * z;                               // direct path into h_{t-1}
+          nrec[m][i] = dh * z;                                  // direct path into h_{t-1}
           const float a_n = dn * (1.f - nn * nn);
-          const float a_r = a_n * gh * r * (1.f - r);
-          const float a_z = dz * z * (1.f - z);
-          dar[k] = a_r; daz[k] = a_z; dan[k] = a_n; dgn[k] = a_n * r;
-          gr[m][i] += a_r; gz[m][i] += a_z; gnx[m][i] += a_n; gnh[m][i] += a_n * r;
+          dghv[0][k] = a_n * gh * r * (1.f - r);
+          dghv[1][k] = dz * z * (1.f - z);
+          dghv[2][k] = a_n * r;
+          dan[k] = a_n;
         }
       }
       bf16_t* gx = p.dGx + ((size_t)t * B + b) * RG;
       bf16_t* gh_ = p.dGh + ((size_t)t * B + b) * RG;
-      bf16_t* lg = cG + row * GS;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int u0 = 32 * wave + 16 * m + 4 * g4, k = 4 * m;
-        lds_st4(gx + u0, dar[k], dar[k + 1], dar[k + 2], dar[k + 3]);
-        lds_st4(gx + RH + u0, daz[k], daz[k + 1], daz[k + 2], daz[k + 3]);
+        lds_st4(gx + u0, dghv[0][k], dghv[0][k + 1], dghv[0][k + 2], dghv[0][k + 3]);
+        lds_st4(gx + RH + u0, dghv[1][k], dghv[1][k + 1], dghv[1][k + 2], dghv[1][k + 3]);
         lds_st4(gx + 2 * RH + u0, dan[k], dan[k + 1], dan[k + 2], dan[k + 3]);
-        lds_st4(gh_ + u0, dar[k], dar[k + 1], dar[k + 2], dar[k + 3]);
-        lds_st4(gh_ + RH + u0, daz[k], daz[k + 1], daz[k + 2], daz[k + 3]);
-        lds_st4(gh_ + 2 * RH + u0, dgn[k], dgn[k + 1], dgn[k + 2], dgn[k + 3]);
-        lds_st4(lg + u0, dar[k], dar[k + 1], dar[k + 2], dar[k + 3]);
-        lds_st4(lg + RH + u0, daz[k], daz[k + 1], daz[k + 2], daz[k + 3]);
-        lds_st4(lg + 2 * RH + u0, dgn[k], dgn[k + 1], dgn[k + 2], dgn[k + 3]);
+        lds_st4(gh_ + u0, dghv[0][k], dghv[0][k + 1], dghv[0][k + 2], dghv[0][k + 3]);
+        lds_st4(gh_ + RH + u0, dghv[1][k], dghv[1][k + 1], dghv[1][k + 2], dghv[1][k + 3]);
+        lds_st4(gh_ + 2 * RH + u0, dghv[2][k], dghv[2][k + 1], dghv[2][k + 2], dghv[2][k + 3]);
       }
     }
     if (t == 0) break;
+    load_step(t - 1);          // next step's inputs land during the quantization + GEMM
+    // dGh -> MX-fp8 hi/lo tiles [seq][gate row] (+ scales per (seq, 32-row block = gate*8 + wave))
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt)
+      quant_hilo(dghv[gt], gHi + row * GQS, gLo + row * GQS, sHi + row * GSC, sLo + row * GSC,
+                 gt * RH + 32 * wave + 4 * g4, gt * 8 + wave, g4);
     __syncthreads();
-    // dh_{t-1} (through the recurrence) = direct + dGh_t . W_hh  (D[unit][seq], K = 768)
-    f4v acc[2][2];
+    // dh_{t-1} (through the recurrence) = direct + dGh_t . W_hh  (D[unit][seq], K = 768 gate rows)
+    f4v acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      acc[m][0] = nrec[m][0]; acc[m][1] = nrec[m][1]; acc[m][2] = nrec[m][2]; acc[m][3] = nrec[m][3];
+    }
+#define BW_KS(KS)                                                                                        \
+    {                                                                                                    \
+      i8v bh, bl;                                                                                        \
+      const uint4 h0 = *reinterpret_cast<const uint4*>(gHi + row * GQS + 128 * (KS) + 16 * g4);          \
+      const uint4 h1 = *reinterpret_cast<const uint4*>(gHi + row * GQS + 128 * (KS) + 64 + 16 * g4);     \
+      bh[0] = (int)h0.x; bh[1] = (int)h0.y; bh[2] = (int)h0.z; bh[3] = (int)h0.w;                        \
+      bh[4] = (int)h1.x; bh[5] = (int)h1.y; bh[6] = (int)h1.z; bh[7] = (int)h1.w;                        \
+      const uint4 l0 = *reinterpret_cast<const uint4*>(gLo + row * GQS + 128 * (KS) + 16 * g4);          \
+      const uint4 l1 = *reinterpret_cast<const uint4*>(gLo + row * GQS + 128 * (KS) + 64 + 16 * g4);     \
+      bl[0] = (int)l0.x; bl[1] = (int)l0.y; bl[2] = (int)l0.z; bl[3] = (int)l0.w;                        \
+      bl[4] = (int)l1.x; bl[5] = (int)l1.y; bl[6] = (int)l1.z; bl[7] = (int)l1.w;                        \
+      const int sch = sHi[row * GSC + 4 * (KS) + g4], scl = sLo[row * GSC + 4 * (KS) + g4];             \
+      acc[0] = mx_mfma_sel<(KS) & 3>(Wt[0][KS], bh, acc[0], Wts4[(KS) >> 2], sch);                       \
+      acc[0] = mx_mfma_sel<(KS) & 3>(Wt[0][KS], bl, acc[0], Wts4[(KS) >> 2], scl);                       \
+      acc[1] = mx_mfma_sel<(6 + (KS)) & 3>(Wt[1][KS], bh, acc[1], Wts4[(6 + (KS)) >> 2], sch);           \
+      acc[1] = mx_mfma_sel<(6 + (KS)) & 3>(Wt[1][KS], bl, acc[1], Wts4[(6 + (KS)) >> 2], scl);           \
+    }
+    BW_KS(0) BW_KS(1) BW_KS(2) BW_KS(3) BW_KS(4) BW_KS(5)
+#undef BW_KS
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        acc[m][n][0] = nrec[m][n][0]; acc[m][n][1] = nrec[m][n][1];
-        acc[m][n][2] = nrec[m][n][2]; acc[m][n][3] = nrec[m][n][3];
-      }
-    s8v wa[BLA][2];
-#pragma unroll
-    for (int j = 0; j < BLA; ++j) {
-      wa[j][0] = *reinterpret_cast<const s8v*>(wrow0 + 32 * j);
-      wa[j][1] = *reinterpret_cast<const s8v*>(wrow1 + 32 * j);
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK; ++ks) {
-      const s8v a0 = wa[ks % BLA][0], a1 = wa[ks % BLA][1];
-      if (ks + BLA < BK) {
-        wa[ks % BLA][0] = *reinterpret_cast<const s8v*>(wrow0 + 32 * (ks + BLA));
-        wa[ks % BLA][1] = *reinterpret_cast<const s8v*>(wrow1 + 32 * (ks + BLA));
-      }
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const s8v bb = lds_ld8(cG + (16 * n + l16) * GS + 32 * ks + 8 * g4);
-        acc[0][n] = mfma32(a0, bb, acc[0][n]);
-        acc[1][n] = mfma32(a1, bb, acc[1][n]);
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rec[m][n][i] = acc[m][n][i];
+      for (int i = 0; i < 4; ++i) rec[m][i] = acc[m][i];
   }
-  // reduce the per-lane partials over the 16 sequences of a lane group, then one atomic per unit
+  // W_q / b_q gradients: reduce the per-lane partials over the 16 sequences of a lane group
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int u = 32 * wave + 16 * m + 4 * g4 + i;
       const float v0 = row16_sum(gq[0][m][i]), v1 = row16_sum(gq[1][m][i]), v2 = row16_sum(gq[2][m][i]);
-      const float r_ = row16_sum(gr[m][i]), z_ = row16_sum(gz[m][i]);
-      const float nx = row16_sum(gnx[m][i]), nh = row16_sum(gnh[m][i]);
       if (l16 == 0) {
         atomicAdd(p.gwq + u, v0);
         atomicAdd(p.gwq + RH + u, v1);
         atomicAdd(p.gwq + 2 * RH + u, v2);
-        atomicAdd(p.gbih + u, r_);
-        atomicAdd(p.gbih + RH + u, z_);
-        atomicAdd(p.gbih + 2 * RH + u, nx);
-        atomicAdd(p.gbhh + u, r_);
-        atomicAdd(p.gbhh + RH + u, z_);
-        atomicAdd(p.gbhh + 2 * RH + u, nh);
       }
     }
   if (wave == 0) {
@@ -571,6 +630,6 @@ extern "C" hipError_t st_gru_seq_bwd(const st::GruSeqBwd* p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(st::gru_seq_bwd_kernel, dim3(p->B / st::LB), dim3(st::RT), st::BwdLds::BYTES, s, *p);
+  hipLaunchKernelGGL(st::gru_seq_bwd_kernel, dim3(p->B / st::LBB), dim3(st::RT), st::BwdLds::BYTES, s, *p);
   return hipGetLastError();
 }

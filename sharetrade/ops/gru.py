@@ -39,7 +39,8 @@ class MinuteBarsArgs(C.Structure):
 class PackArgs(C.Structure):
     _fields_ = [("w_hh", C.c_void_p), ("w_ih", C.c_void_p), ("b_ih", C.c_void_p), ("b_hh", C.c_void_p),
                 ("w_q", C.c_void_p), ("b_q", C.c_void_p), ("whh8", C.c_void_p), ("whhs", C.c_void_p),
-                ("wih", C.c_void_p), ("bias4", C.c_void_p), ("wq", C.c_void_p)]
+                ("wih", C.c_void_p), ("bias4", C.c_void_p), ("wq", C.c_void_p), ("whhT8", C.c_void_p),
+                ("whhTs", C.c_void_p)]
 
 
 class ActArgs(C.Structure):
@@ -79,9 +80,9 @@ class TDArgs(C.Structure):
 
 
 class SeqBwdArgs(C.Structure):
-    _fields_ = [("sv", C.c_void_p), ("dQ", C.c_void_p), ("D", C.c_void_p), ("WhhT", C.c_void_p), ("wq", C.c_void_p),
-                ("dGx", C.c_void_p), ("dGh", C.c_void_p), ("gwq", C.c_void_p), ("gbq", C.c_void_p),
-                ("gbih", C.c_void_p), ("gbhh", C.c_void_p), ("B", C.c_int), ("S", C.c_int)]
+    _fields_ = [("sv", C.c_void_p), ("dQ", C.c_void_p), ("D", C.c_void_p), ("whhT8", C.c_void_p),
+                ("whhTs", C.c_void_p), ("wq", C.c_void_p), ("dGx", C.c_void_p), ("dGh", C.c_void_p),
+                ("gwq", C.c_void_p), ("gbq", C.c_void_p), ("B", C.c_int), ("S", C.c_int)]
 
 
 def lib():
@@ -151,6 +152,25 @@ def unpack_whh(whh8: torch.Tensor, whhs: torch.Tensor) -> torch.Tensor:
                             sc = 2.0 ** float(e[w, g, m, ks, i + 16 * blk])
                             W[r, 128 * ks + k0:128 * ks + k0 + 16] = vals[w, g, m, ks, l, 16 * half:16 * half + 16] * sc
     return W
+
+
+def unpack_whhT(whhT8: torch.Tensor, whhTs: torch.Tensor) -> torch.Tensor:
+    """Backward-pack fragments (W_hh^T rows = units, K = gate rows) -> the dequantized W_hh [768, 256]
+    the learner's dh GEMM multiplies with (32-gate blocks per unit, so it differs from unpack_whh)."""
+    b = whhT8.detach().cpu().contiguous().view(torch.uint8).view(RW, 2, 6, 64, 32)
+    e = whhTs.detach().cpu().view(RW, 2, 6, 64).to(torch.int32) - 127
+    vals = b.view(torch.float8_e4m3fn).float()
+    WT = torch.zeros(HID, GATES)
+    for w in range(RW):
+        for m in range(2):
+            for ks in range(6):
+                for l in range(64):
+                    i, q = l & 15, l >> 4
+                    u = 32 * w + 16 * m + i
+                    for half, k0 in ((0, 16 * q), (1, 64 + 16 * q)):
+                        sc = 2.0 ** float(e[w, m, ks, i + 16 * (k0 // 32)])
+                        WT[u, 128 * ks + k0:128 * ks + k0 + 16] = vals[w, m, ks, l, 16 * half:16 * half + 16] * sc
+    return WT.t().contiguous()
 
 
 def mx_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:

@@ -9,11 +9,12 @@ actor-learner style (R2D2-like stored-state sequence replay):
   S minute bars.  W_hh is block-scaled MX-fp8 resident in VGPRs and the gate products run
   on ``v_mfma_scale_f32_16x16x128_f8f6f4`` (the fp8 MFMA path); h stays fp32 on-chip for
   all S steps; every env writes one replay *segment* {x_0..x_S, a, r, done, h_0}.
-* **learner** (``update``): samples B segments, unrolls online and target nets over S+1
-  steps (bf16 MFMA GEMMs for the gate products, fused elementwise GRU kernels with the
-  Q head folded in), double-DQN TD over steps [burn_in, S), backward through time (per-step
-  dh GEMM + fused GRU backward), split-K weight-gradient GEMMs, Adam, then re-packs the
-  actor's fp8 weights.  Both halves are captured in HIP graphs.
+* **learner** (``update``): samples B segments; ``csrc/gru_learn.hip`` unrolls online and target
+  nets over S+1 steps in one persistent launch (the actor's MX-fp8 arithmetic), double-DQN TD
+  over steps [burn_in, S), then backward through time in one persistent launch (W_hh^T
+  resident as MX-fp8, the dGh operand as an fp8 hi/lo pair, the recurrent gradient in
+  registers), split-K bf16 weight-gradient GEMMs, Adam, and re-packs the fp8 weights.
+  Both halves are captured in HIP graphs.
 
 Env (minute-bar trading, long-only single unit like the reference's share count):
 Buy -> long, Sell -> flat, Hold -> keep; reward = position * ret_t - ``cost`` per position
@@ -90,7 +91,6 @@ class RecurrentDQN:
         # bf16 operand copies (written by the Adam kernel) and the target net
         self.Wih_b = self.P["w_ih"].to(b16).contiguous()
         self.Whh_b = self.P["w_hh"].to(b16).contiguous()
-        self.WhhT_b = self.P["w_hh"].t().contiguous().to(b16)
         self._scratch = {n: torch.zeros(self.P[n].shape, dtype=b16, device=dev) for n in ("b_ih", "b_hh", "w_q", "b_q")}
         self.t_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         # target net: an fp32 copy of the flat parameters, packed like the actor's weights
@@ -108,6 +108,9 @@ class RecurrentDQN:
                             "whhs": torch.zeros(nfr, dtype=i32, device=dev),
                             "wih": torch.zeros(G.RW * 6 * 64 * 8, dtype=torch.int16, device=dev),
                             "bias4": torch.zeros(4 * HID, device=dev), "wq": torch.zeros(4 * HID, device=dev)}
+        # the learner's backward dh GEMM reads W_hh^T as resident MX-fp8 fragments too (online net only)
+        self.pk["on"]["whhT8"] = torch.zeros(nfr * 8, dtype=i32, device=dev)
+        self.pk["on"]["whhTs"] = torch.zeros(nfr, dtype=i32, device=dev)
         self.whh8, self.whhs = self.pk["on"]["whh8"], self.pk["on"]["whhs"]
         # ---------------------------------------------------------------- data + envs
         self.bp = bar_params or mb.BarParams()
@@ -142,7 +145,10 @@ class RecurrentDQN:
         self.XT = torch.zeros(XL, R1, dtype=b16, device=dev)
         self.H0 = torch.zeros(B, HID, device=dev)
         self.Hm = torch.zeros(R1, HID, dtype=b16, device=dev)
-        self.HT = torch.zeros(HID, R1, dtype=b16, device=dev)
+        # h_{t-1}^T for the dW_hh GEMM, with a ones row at HID: column HID of that GEMM is then db_hh
+        self.HT = torch.zeros(HID + 64, R1, dtype=b16, device=dev)
+        self.HT[HID].fill_(1.0)
+        self.dWhh_ext = torch.zeros(GATES, HID + 64, device=dev)
         self.A = torch.zeros(S, B, dtype=i32, device=dev)
         self.R = torch.zeros(S, B, device=dev)
         self.D = torch.zeros(S, B, device=dev)
@@ -189,6 +195,8 @@ class RecurrentDQN:
                                                              ("w_hh", "w_ih", "b_ih", "b_hh", "w_q", "b_q"))
             pk = self.pk[net]
             p.whh8, p.whhs, p.wih, p.bias4, p.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
+            if "whhT8" in pk:
+                p.whhT8, p.whhTs = pk["whhT8"].data_ptr(), pk["whhTs"].data_ptr()
             self._packs[net] = p
         ga = G.GatherArgs()
         ga.rx, ga.ra, ga.rr, ga.rd, ga.rh0 = (self.rx.data_ptr(), self.ra.data_ptr(), self.rr.data_ptr(),
@@ -213,10 +221,11 @@ class RecurrentDQN:
         td.gamma, td.coef = self.gamma, 2.0 / (self.B * (self.S - self.burn))
         self._td = td
         bw = G.SeqBwdArgs()
-        bw.sv, bw.dQ, bw.D, bw.WhhT, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
-                                              self.WhhT_b.data_ptr(), self.P["w_q"].data_ptr())
+        bw.sv, bw.dQ, bw.D, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
+                                     self.P["w_q"].data_ptr())
+        bw.whhT8, bw.whhTs = self.pk["on"]["whhT8"].data_ptr(), self.pk["on"]["whhTs"].data_ptr()
         bw.dGx, bw.dGh = self.dGx.data_ptr(), self.dGh.data_ptr()
-        bw.gwq, bw.gbq, bw.gbih, bw.gbhh = (self.dP[n].data_ptr() for n in ("w_q", "b_q", "b_ih", "b_hh"))
+        bw.gwq, bw.gbq = self.dP["w_q"].data_ptr(), self.dP["b_q"].data_ptr()
         bw.B, bw.S = self.B, self.S
         self._bwd = bw
         ag = self.cfg.agent
@@ -228,7 +237,7 @@ class RecurrentDQN:
                 self.M2[n].data_ptr(), None
             wb = {"w_ih": self.Wih_b, "w_hh": self.Whh_b}.get(n, self._scratch.get(n))
             ad.wb = wb.data_ptr()
-            ad.wbT = self.WhhT_b.data_ptr() if n == "w_hh" else None
+            ad.wbT = None
             ad.t, ad.O, ad.I = self.t_ctr.data_ptr(), int(w.shape[0]), int(w.shape[1])
             ad.lr, ad.beta1, ad.beta2, ad.eps = self.lr, float(ag.adam_betas[0]), float(ag.adam_betas[1]), \
                 float(ag.adam_eps)
@@ -261,8 +270,13 @@ class RecurrentDQN:
         native.check(kd.st_transpose_bf16(self.dGx.data_ptr(), GATES, self.dGxT.data_ptr(), RS, RS, GATES, sh), "T dGx")
         native.check(kd.st_transpose_bf16(self.Hm.data_ptr(), HID, self.HT.data_ptr(), R1, RS, HID, sh), "T H")
         native.check(kd.st_transpose_bf16(self.X.data_ptr(), XL, self.XT.data_ptr(), R1, RS, XL, sh), "T X")
-        gm.gemm_nt(self.dGhT, self.HT[:, :RS], self.dP["w_hh"], gm.EPI_F32, accumulate=True, splitk="auto")
+        # weight gradients; the ones row of HT / ones column RF of X give the bias gradients for free
+        gm.gemm_nt(self.dGhT, self.HT[:, :RS], self.dWhh_ext, gm.EPI_F32, splitk="auto")
+        self.dP["w_hh"].copy_(self.dWhh_ext[:, :HID])
+        self.dP["b_hh"].view(-1).copy_(self.dWhh_ext[:, HID])
         gm.gemm_nt(self.dGxT, self.XT[:, :RS], self.dP["w_ih"], gm.EPI_F32, accumulate=True, splitk="auto")
+        self.dP["b_ih"].view(-1).copy_(self.dP["w_ih"][:, XA])
+        self.dP["w_ih"][:, XA].zero_()
         if self.grad_sync is not None:
             self.grad_sync(self.gflat)
         for ad in self._adam:

@@ -151,17 +151,22 @@ def test_actor_matches_reference(native_built):
     assert int(d.rctrl[0]) == d.E and int(d.ctrl[0]) == 1
 
 
-def _ref_unroll(X, h0, p, D, Wdeq):
-    """Quantization-aware reference of gru_seq_fwd_kernel: the value of W_hh h is the MX-fp8
-    product (quantized W_hh and h), its gradient flows through the bf16 master (straight-through)."""
+def _ref_unroll(X, h0, p, D, Wdeq, Wbwd=None):
+    """Quantization-aware reference of the fused learner: the VALUE of W_hh h is the MX-fp8 product
+    (forward-packed W_hh, quantized h); the gradient w.r.t. h flows through the backward-packed
+    MX-fp8 W_hh (``Wbwd``), the gradient w.r.t. W_hh through the bf16 master (straight-through)."""
     from sharetrade.ops.gru import mx_roundtrip
 
     h, qs = h0, []
     for t in range(X.shape[0]):
         gx = X[t][:, :32] @ p["w_ih"][:, :32].t() + p["b_ih"]
-        gh_e = h @ p["w_hh"].t() + p["b_hh"]
         gh_q = mx_roundtrip(h.detach()) @ Wdeq.t() + p["b_hh"]
-        gh = gh_e + (gh_q - gh_e).detach()
+        if Wbwd is None:
+            gh = gh_q
+        else:
+            gh_h = h @ Wbwd.t()
+            gh_w = h.detach() @ p["w_hh"].t() + p["b_hh"]
+            gh = gh_q.detach() + (gh_h - gh_h.detach()) + (gh_w - gh_w.detach())
         r = torch.sigmoid(gx[:, :256] + gh[:, :256])
         z = torch.sigmoid(gx[:, 256:512] + gh[:, 256:512])
         n = torch.tanh(gx[:, 512:] + r * gh[:, 512:])
@@ -173,7 +178,7 @@ def _ref_unroll(X, h0, p, D, Wdeq):
 
 
 def test_learner_gradients_match_autograd(native_built):
-    from sharetrade.ops.gru import unpack_whh
+    from sharetrade.ops.gru import unpack_whh, unpack_whhT
     from sharetrade.utils import rng
 
     d = _small(E=128, S=4, eps=0.5, batch=128)
@@ -183,6 +188,8 @@ def test_learner_gradients_match_autograd(native_built):
     T0 = {n: t.detach().clone().cpu() for n, t in d.T_P.items()}
     W_on = unpack_whh(d.pk["on"]["whh8"], d.pk["on"]["whhs"])
     W_tg = unpack_whh(d.pk["tg"]["whh8"], d.pk["tg"]["whhs"])
+    W_bwd = unpack_whhT(d.pk["on"]["whhT8"], d.pk["on"]["whhTs"])
+    assert torch.allclose(W_bwd, P0["w_hh"], rtol=0.07, atol=1e-6)
     d.update()
     torch.cuda.synchronize()
     size = int(d.rctrl[1])
@@ -201,7 +208,7 @@ def test_learner_gradients_match_autograd(native_built):
         p[n] = P0[n].view(P0[n].shape if n == "w_q" else (-1,)).clone().requires_grad_(True)
     pt = {"w_ih": bf(T0["w_ih"]), "w_hh": bf(T0["w_hh"]), "b_ih": T0["b_ih"].view(-1), "b_hh": T0["b_hh"].view(-1),
           "w_q": T0["w_q"], "b_q": T0["b_q"].view(-1)}
-    q = _ref_unroll(X, h0, p, D, W_on)
+    q = _ref_unroll(X, h0, p, D, W_on, W_bwd)
     with torch.no_grad():
         qt = _ref_unroll(X, h0, pt, D, W_tg)
         a_star = q[1:].argmax(-1, keepdim=True)
