@@ -349,8 +349,8 @@ struct GruSeqBwd {
   const i8v* whhT8;     // W_hh^T MX-fp8 A fragments [RW][2][6][64] (gru_pack_kernel, online net)
   const int* whhTs;     // their E8M0 scales
   const float* wq;      // [3][RH] online fp32
-  bf16_t* dGx;          // [S*B][RG]
-  bf16_t* dGh;          // [S*B][RG]
+  bf16_t* dGxT;         // [RG][S*B]: weight-gradient GEMM operands, written transposed (staged in LDS)
+  bf16_t* dGhT;         // [RG][S*B]
   float* gwq;           // [3][RH]   (+= ; zeroed by the host each update)
   float* gbq;           // [3]
   int B, S;
@@ -366,7 +366,8 @@ struct BwdLds {
   static constexpr int G8 = 0;
   static constexpr int SC = G8 + 2 * 2 * LBB * GQS;
   static constexpr int WQ = SC + 2 * 2 * LBB * GSC * 4;
-  static constexpr int BYTES = WQ + 3 * RH * 4;
+  static constexpr int TR = WQ + 3 * RH * 4;                 // [2 buffers][dGh, dGx][RG][LBB] bf16
+  static constexpr int BYTES = TR + 2 * 2 * RG * LBB * 2;
 };
 static_assert(BwdLds::BYTES <= 160 * 1024, "bwd LDS");
 
@@ -427,6 +428,8 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int* sSc = reinterpret_cast<int*>(lds + BwdLds::SC);
   float* sWq = reinterpret_cast<float*>(lds + BwdLds::WQ);
+  bf16_t* sT = reinterpret_cast<bf16_t*>(lds + BwdLds::TR);
+  const size_t RS = (size_t)p.S * p.B;
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int B = p.B, S = p.S, b0 = blockIdx.x * LBB;
@@ -477,7 +480,7 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
     unsigned char* gLo = lds + BwdLds::G8 + (cur * 2 + 1) * LBB * GQS;
     int* sHi = sSc + (cur * 2 + 0) * LBB * GSC;
     int* sLo = sSc + (cur * 2 + 1) * LBB * GSC;
-    const int row = l16, b = b0 + row;
+    const int row = l16;
     float nrec[2][4];
     float dghv[3][8];      // dGh per gate (r, z, n_h), (m, i)
     {
@@ -519,27 +522,40 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
           dan[k] = a_n;
         }
       }
-      bf16_t* gx = p.dGx + ((size_t)t * B + b) * RG;
-      bf16_t* gh_ = p.dGh + ((size_t)t * B + b) * RG;
+      // transposed staging [gate row][seq] (dGh, dGx share the r / z rows; n differs)
+      bf16_t* th = sT + (cur * 2 + 0) * RG * LBB;
+      bf16_t* tx = sT + (cur * 2 + 1) * RG * LBB;
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const int u0 = 32 * wave + 16 * m + 4 * g4, k = 4 * m;
-        lds_st4(gx + u0, dghv[0][k], dghv[0][k + 1], dghv[0][k + 2], dghv[0][k + 3]);
-        lds_st4(gx + RH + u0, dghv[1][k], dghv[1][k + 1], dghv[1][k + 2], dghv[1][k + 3]);
-        lds_st4(gx + 2 * RH + u0, dan[k], dan[k + 1], dan[k + 2], dan[k + 3]);
-        lds_st4(gh_ + u0, dghv[0][k], dghv[0][k + 1], dghv[0][k + 2], dghv[0][k + 3]);
-        lds_st4(gh_ + RH + u0, dghv[1][k], dghv[1][k + 1], dghv[1][k + 2], dghv[1][k + 3]);
-        lds_st4(gh_ + 2 * RH + u0, dghv[2][k], dghv[2][k + 1], dghv[2][k + 2], dghv[2][k + 3]);
-      }
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int u = 32 * wave + 16 * m + 4 * g4 + i, k = 4 * m + i;
+          const bf16_t vr_ = f2bf(dghv[0][k]), vz_ = f2bf(dghv[1][k]);
+          th[(0 * RH + u) * LBB + row] = vr_;
+          th[(1 * RH + u) * LBB + row] = vz_;
+          th[(2 * RH + u) * LBB + row] = f2bf(dghv[2][k]);
+          tx[(0 * RH + u) * LBB + row] = vr_;
+          tx[(1 * RH + u) * LBB + row] = vz_;
+          tx[(2 * RH + u) * LBB + row] = f2bf(dan[k]);
+        }
+    }
+    if (t > 0) {
+      load_step(t - 1);          // next step's inputs land during the quantization + GEMM
+      // dGh -> MX-fp8 hi/lo tiles [seq][gate row] (+ scales per (seq, 32-row block = gate*8 + wave))
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt)
+        quant_hilo(dghv[gt], gHi + row * GQS, gLo + row * GQS, sHi + row * GSC, sLo + row * GSC,
+                   gt * RH + 32 * wave + 4 * g4, gt * 8 + wave, g4);
+    }
+    __syncthreads();
+    // dGh^T / dGx^T rows of this step: 32 B per gate row (16 sequences), written as 16-B pieces
+    for (int c = tid; c < 2 * RG * 2; c += RT) {
+      const int mat = c / (RG * 2), rem = c % (RG * 2), gr = rem >> 1, half = rem & 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(sT + ((cur * 2 + mat) * RG + gr) * LBB + 8 * half);
+      bf16_t* dst = (mat ? p.dGxT : p.dGhT) + (size_t)gr * RS + (size_t)t * B + b0 + 8 * half;
+      *reinterpret_cast<uint4*>(dst) = v;
     }
     if (t == 0) break;
-    load_step(t - 1);          // next step's inputs land during the quantization + GEMM
-    // dGh -> MX-fp8 hi/lo tiles [seq][gate row] (+ scales per (seq, 32-row block = gate*8 + wave))
-#pragma unroll
-    for (int gt = 0; gt < 3; ++gt)
-      quant_hilo(dghv[gt], gHi + row * GQS, gLo + row * GQS, sHi + row * GSC, sLo + row * GSC,
-                 gt * RH + 32 * wave + 4 * g4, gt * 8 + wave, g4);
-    __syncthreads();
     // dh_{t-1} (through the recurrence) = direct + dGh_t . W_hh  (D[unit][seq], K = 768 gate rows)
     f4v acc[2];
 #pragma unroll
@@ -595,6 +611,21 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_bwd_kernel(GruSeqBwd p) {
   }
 }
 
+// Gradient fix-up after the weight-gradient GEMMs (one launch instead of four strided copies):
+// dW_hh <- ext[:, :RH], db_hh <- ext[:, RH] (ones row of h^T), db_ih <- dW_ih[:, RF] (ones column
+// of x), dW_ih[:, RF] <- 0.
+__global__ void __launch_bounds__(256) gru_grad_fixup_kernel(const float* __restrict__ ext, int ldx, float* dwhh,
+                                                             float* dbhh, float* dwih, float* dbih) {
+  const int g = blockIdx.x;   // gate row
+  const float* e = ext + (size_t)g * ldx;
+  for (int u = threadIdx.x; u < RH; u += blockDim.x) dwhh[(size_t)g * RH + u] = e[u];
+  if (threadIdx.x == 0) {
+    dbhh[g] = e[RH];
+    dbih[g] = dwih[(size_t)g * RFL + RF];
+    dwih[(size_t)g * RFL + RF] = 0.f;
+  }
+}
+
 }  // namespace st
 
 extern "C" hipError_t st_gru_gather(const st::GruGather* g, hipStream_t s) {
@@ -631,5 +662,11 @@ extern "C" hipError_t st_gru_seq_bwd(const st::GruSeqBwd* p, hipStream_t s) {
     attr = true;
   }
   hipLaunchKernelGGL(st::gru_seq_bwd_kernel, dim3(p->B / st::LBB), dim3(st::RT), st::BwdLds::BYTES, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_gru_grad_fixup(const float* ext, int ldx, float* dwhh, float* dbhh, float* dwih, float* dbih,
+                                        hipStream_t s) {
+  hipLaunchKernelGGL(st::gru_grad_fixup_kernel, dim3(st::RG), dim3(256), 0, s, ext, ldx, dwhh, dbhh, dwih, dbih);
   return hipGetLastError();
 }

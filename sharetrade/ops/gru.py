@@ -81,7 +81,7 @@ class TDArgs(C.Structure):
 
 class SeqBwdArgs(C.Structure):
     _fields_ = [("sv", C.c_void_p), ("dQ", C.c_void_p), ("D", C.c_void_p), ("whhT8", C.c_void_p),
-                ("whhTs", C.c_void_p), ("wq", C.c_void_p), ("dGx", C.c_void_p), ("dGh", C.c_void_p),
+                ("whhTs", C.c_void_p), ("wq", C.c_void_p), ("dGxT", C.c_void_p), ("dGhT", C.c_void_p),
                 ("gwq", C.c_void_p), ("gbq", C.c_void_p), ("B", C.c_int), ("S", C.c_int)]
 
 
@@ -96,6 +96,7 @@ def lib():
                          ("st_gru_seq_fwd", [C.POINTER(SeqFwdArgs), vp]),
                          ("st_gru_td", [C.POINTER(TDArgs), vp]),
                          ("st_gru_seq_bwd", [C.POINTER(SeqBwdArgs), vp]),
+                         ("st_gru_grad_fixup", [vp, i, vp, vp, vp, vp, vp]),
                          ("st_mx_probe", [vp, vp, vp, vp, vp, vp])):
             f = getattr(L, fn)
             f.argtypes = args

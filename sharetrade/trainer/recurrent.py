@@ -157,8 +157,6 @@ class RecurrentDQN:
         # forward saves (r, z, n, gh_n, h_prev as bf16 in the kernels' lane order): 16 B per lane/tile/quantity
         self.sv = torch.zeros(S * (B // G.LB) * G.RW * G.NSV * 2 * 64 * 4, dtype=i32, device=dev)
         self.dQ = torch.zeros(RS, 4, device=dev)
-        self.dGx = torch.zeros(RS, GATES, dtype=b16, device=dev)
-        self.dGh = torch.zeros(RS, GATES, dtype=b16, device=dev)
         self.dGxT = torch.zeros(GATES, RS, dtype=b16, device=dev)
         self.dGhT = torch.zeros(GATES, RS, dtype=b16, device=dev)
         self.key0, self.key1 = (int(x) for x in rng.key_for(self.seed, 7))
@@ -224,7 +222,7 @@ class RecurrentDQN:
         bw.sv, bw.dQ, bw.D, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
                                      self.P["w_q"].data_ptr())
         bw.whhT8, bw.whhTs = self.pk["on"]["whhT8"].data_ptr(), self.pk["on"]["whhTs"].data_ptr()
-        bw.dGx, bw.dGh = self.dGx.data_ptr(), self.dGh.data_ptr()
+        bw.dGxT, bw.dGhT = self.dGxT.data_ptr(), self.dGhT.data_ptr()
         bw.gwq, bw.gbq = self.dP["w_q"].data_ptr(), self.dP["b_q"].data_ptr()
         bw.B, bw.S = self.B, self.S
         self._bwd = bw
@@ -266,17 +264,14 @@ class RecurrentDQN:
         native.check(k.st_gru_td(self._td, sh), "st_gru_td")
         self.gflat.zero_()
         native.check(k.st_gru_seq_bwd(self._bwd, sh), "st_gru_seq_bwd")
-        native.check(kd.st_transpose_bf16(self.dGh.data_ptr(), GATES, self.dGhT.data_ptr(), RS, RS, GATES, sh), "T dGh")
-        native.check(kd.st_transpose_bf16(self.dGx.data_ptr(), GATES, self.dGxT.data_ptr(), RS, RS, GATES, sh), "T dGx")
         native.check(kd.st_transpose_bf16(self.Hm.data_ptr(), HID, self.HT.data_ptr(), R1, RS, HID, sh), "T H")
         native.check(kd.st_transpose_bf16(self.X.data_ptr(), XL, self.XT.data_ptr(), R1, RS, XL, sh), "T X")
         # weight gradients; the ones row of HT / ones column RF of X give the bias gradients for free
         gm.gemm_nt(self.dGhT, self.HT[:, :RS], self.dWhh_ext, gm.EPI_F32, splitk="auto")
-        self.dP["w_hh"].copy_(self.dWhh_ext[:, :HID])
-        self.dP["b_hh"].view(-1).copy_(self.dWhh_ext[:, HID])
         gm.gemm_nt(self.dGxT, self.XT[:, :RS], self.dP["w_ih"], gm.EPI_F32, accumulate=True, splitk="auto")
-        self.dP["b_ih"].view(-1).copy_(self.dP["w_ih"][:, XA])
-        self.dP["w_ih"][:, XA].zero_()
+        native.check(k.st_gru_grad_fixup(self.dWhh_ext.data_ptr(), HID + 64, self.dP["w_hh"].data_ptr(),
+                                         self.dP["b_hh"].data_ptr(), self.dP["w_ih"].data_ptr(),
+                                         self.dP["b_ih"].data_ptr(), sh), "grad fixup")
         if self.grad_sync is not None:
             self.grad_sync(self.gflat)
         for ad in self._adam:
