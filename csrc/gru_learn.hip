@@ -87,7 +87,8 @@ struct GruSeqFwd {
   const float* D;       // [S][B]
   float* Q;             // [(S+1)B][4] online
   float* Qt;            // [(S+1)B][4] target
-  bf16_t* Hm;           // [(S+1)B][RH] online: block t = masked h_{t-1} (block 0 = h0)
+  bf16_t* HT;           // online: h_{t-1}^T (masked) for the dW_hh GEMM, [RH][ldht], column t*B + b
+  int ldht;
   uint4* sv;            // online saves [S][B/LB][RW][NSV][2][64] x 16 B
   int B, S;
 };
@@ -100,7 +101,8 @@ struct FwdLds {
   static constexpr int B = SC + 2 * LB * SCS * 4;       // [4*RH] float
   static constexpr int WQ = B + 4 * RH * 4;             // [4*RH] float
   static constexpr int QP = WQ + 4 * RH * 4;            // [2][RW][3][LB] float
-  static constexpr int BYTES = QP + 2 * RW * 3 * LB * 4;
+  static constexpr int HT = QP + 2 * RW * 3 * LB * 4;    // [2][RH][LB] bf16: h^T staging
+  static constexpr int BYTES = HT + 2 * RH * LB * 2;
 };
 static_assert(FwdLds::BYTES <= 160 * 1024, "fwd LDS");
 
@@ -127,9 +129,26 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
   float* sB = reinterpret_cast<float*>(lds + FwdLds::B);
   float* sWq = reinterpret_cast<float*>(lds + FwdLds::WQ);
   float* sQp = reinterpret_cast<float*>(lds + FwdLds::QP);
+  bf16_t* sHT = reinterpret_cast<bf16_t*>(lds + FwdLds::HT);
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool online = blockIdx.y == 0;
+  // h (masked) -> transposed staging [unit][seq] (bf16), then 64-B rows of HT after the next barrier
+  auto stage_h = [&](bf16_t* st, const float (&h)[2][2][4]) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[(32 * wave + 16 * m + 4 * g4 + i) * LB + 16 * n + l16] = f2bf(h[m][n][i]);
+  };
+  auto flush_h = [&](const bf16_t* st, int blk) {
+    for (int c = tid; c < RH * (LB / 8); c += RT) {
+      const int u = c / (LB / 8), j = c % (LB / 8);
+      *reinterpret_cast<uint4*>(p.HT + (size_t)u * p.ldht + (size_t)blk * p.B + blockIdx.x * LB + 8 * j) =
+          *reinterpret_cast<const uint4*>(st + u * LB + 8 * j);
+    }
+  };
   const i8v* whh8 = online ? p.on.whh8 : p.tg.whh8;
   const int* whhs = online ? p.on.whhs : p.tg.whhs;
   const s8v* wih = online ? p.on.wih : p.tg.wih;
@@ -171,8 +190,8 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
       const int b = b0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
       const float4 v = *reinterpret_cast<const float4*>(p.H0 + (size_t)b * RH + u0);
       hr[m][n][0] = v.x; hr[m][n][1] = v.y; hr[m][n][2] = v.z; hr[m][n][3] = v.w;
-      if (online) lds_st4(p.Hm + (size_t)b * RH + u0, v.x, v.y, v.z, v.w);
     }
+  if (online) stage_h(sHT + RH * LB, hr);   // block 0 = h0, staged in buffer 1
   quant_h(hr, sH8, sSc, wave, l16, g4);
   // x rows: thread tid < LB*4 moves 16 B (row tid/4, chunk tid%4); x_{t+1} is prefetched a step ahead
   const int xr = tid >> 2, xc = tid & 3;
@@ -183,6 +202,7 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
     xnext = reinterpret_cast<const uint4*>(p.X + ((size_t)B + b0 + xr) * RFL)[xc];
   }
   __syncthreads();
+  if (online) flush_h(sHT + RH * LB, 0);
   const size_t nblk = (size_t)(B / LB);
 
   for (int t = 0; t <= S; ++t) {
@@ -274,15 +294,7 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int i = 0; i < 4; ++i) hr[m][n][i] *= keep[n];
-      if (online) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            const int b = b0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
-            lds_st4(p.Hm + ((size_t)(t + 1) * B + b) * RH + u0, hr[m][n][0], hr[m][n][1], hr[m][n][2], hr[m][n][3]);
-          }
-      }
+      if (online && t + 1 < S) stage_h(sHT + cur * RH * LB, hr);   // HT block t+1 = masked h_t
       quant_h(hr, sH8 + nxt * LB * HS, sSc + nxt * LB * SCS, wave, l16, g4);
       if (xmover) {
         reinterpret_cast<uint4*>(sX + nxt * LB * XS + xr * XS)[xc] = xnext;
@@ -290,6 +302,7 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
       }
     }
     __syncthreads();
+    if (online && t + 1 < S) flush_h(sHT + cur * RH * LB, t + 1);
     if (wave == 0 && lane < LB) {
       float q[3];
 #pragma unroll

@@ -69,7 +69,7 @@ class NetW(C.Structure):
 
 class SeqFwdArgs(C.Structure):
     _fields_ = [("on", NetW), ("tg", NetW), ("X", C.c_void_p), ("H0", C.c_void_p), ("D", C.c_void_p),
-                ("Q", C.c_void_p), ("Qt", C.c_void_p), ("Hm", C.c_void_p), ("sv", C.c_void_p),
+                ("Q", C.c_void_p), ("Qt", C.c_void_p), ("HT", C.c_void_p), ("ldht", C.c_int), ("sv", C.c_void_p),
                 ("B", C.c_int), ("S", C.c_int)]
 
 

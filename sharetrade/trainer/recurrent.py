@@ -36,7 +36,7 @@ from ..ops import gemm as gm
 from ..ops import gru as G
 from ..ops import native
 from ..utils import rng
-from .deep import _Adam, _bind as _bind_deep
+from .deep import _bind as _bind_deep
 
 HID, GATES, XA, XL = G.HID, G.GATES, G.XA, G.XL
 
@@ -74,10 +74,12 @@ class RecurrentDQN:
         self._names = ["w_ih", "w_hh", "b_ih", "b_hh", "w_q", "b_q"]
         sizes = [p0[n].numel() for n in self._names]
         self.n_params = sum(sizes)
-        self.flat = torch.zeros(self.n_params, device=dev)
-        self.gflat = torch.zeros(self.n_params, device=dev)
-        self.mflat = torch.zeros(self.n_params, device=dev)
-        self.vflat = torch.zeros(self.n_params, device=dev)
+        npad = (self.n_params + 3) // 4 * 4          # float4 columns of the flat Adam kernel; tail stays 0
+        self.flat = torch.zeros(npad, device=dev)
+        self.gflat = torch.zeros(npad, device=dev)
+        self.mflat = torch.zeros(npad, device=dev)
+        self.vflat = torch.zeros(npad, device=dev)
+        self.ones = torch.ones(npad, device=dev)
         self.P, self.dP, self.M1, self.M2 = {}, {}, {}, {}
         o = 0
         for n, sz in zip(self._names, sizes):
@@ -88,11 +90,10 @@ class RecurrentDQN:
             self.M2[n] = self.vflat[o:o + sz].view(*shp)
             self.P[n].copy_(p0[n].view(*shp))
             o += sz
-        # bf16 operand copies (written by the Adam kernel) and the target net
-        self.Wih_b = self.P["w_ih"].to(b16).contiguous()
-        self.Whh_b = self.P["w_hh"].to(b16).contiguous()
-        self._scratch = {n: torch.zeros(self.P[n].shape, dtype=b16, device=dev) for n in ("b_ih", "b_hh", "w_q", "b_q")}
-        self.t_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        # optimizer control words (csrc/optim.hip): ctrl[0] = completed updates (also the replay
+        # sampling counter), ctrl[1] = 1-based count of the update in flight
+        self.opt_ctrl = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.t_ctr = self.opt_ctrl[:1]
         # target net: an fp32 copy of the flat parameters, packed like the actor's weights
         self.tflat = self.flat.clone()
         self.T_P = {}
@@ -144,7 +145,6 @@ class RecurrentDQN:
         self.X = torch.zeros(R1, XL, dtype=b16, device=dev)
         self.XT = torch.zeros(XL, R1, dtype=b16, device=dev)
         self.H0 = torch.zeros(B, HID, device=dev)
-        self.Hm = torch.zeros(R1, HID, dtype=b16, device=dev)
         # h_{t-1}^T for the dW_hh GEMM, with a ones row at HID: column HID of that GEMM is then db_hh
         self.HT = torch.zeros(HID + 64, R1, dtype=b16, device=dev)
         self.HT[HID].fill_(1.0)
@@ -209,7 +209,8 @@ class RecurrentDQN:
             pk = self.pk[net]
             w.whh8, w.whhs, w.wih, w.bias4, w.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
         f.X, f.H0, f.D = self.X.data_ptr(), self.H0.data_ptr(), self.D.data_ptr()
-        f.Q, f.Qt, f.Hm, f.sv = self.Q.data_ptr(), self.Q_t.data_ptr(), self.Hm.data_ptr(), self.sv.data_ptr()
+        f.Q, f.Qt, f.sv = self.Q.data_ptr(), self.Q_t.data_ptr(), self.sv.data_ptr()
+        f.HT, f.ldht = self.HT.data_ptr(), int(self.HT.stride(0))
         f.B, f.S = self.B, self.S
         self._fwd = f
         td = G.TDArgs()
@@ -227,19 +228,14 @@ class RecurrentDQN:
         bw.B, bw.S = self.B, self.S
         self._bwd = bw
         ag = self.cfg.agent
-        self._adam = []
-        for n in self._names:
-            ad = _Adam()
-            w = self.P[n]
-            ad.w, ad.g, ad.m, ad.v, ad.mask = w.data_ptr(), self.dP[n].data_ptr(), self.M1[n].data_ptr(), \
-                self.M2[n].data_ptr(), None
-            wb = {"w_ih": self.Wih_b, "w_hh": self.Whh_b}.get(n, self._scratch.get(n))
-            ad.wb = wb.data_ptr()
-            ad.wbT = None
-            ad.t, ad.O, ad.I = self.t_ctr.data_ptr(), int(w.shape[0]), int(w.shape[1])
-            ad.lr, ad.beta1, ad.beta2, ad.eps = self.lr, float(ag.adam_betas[0]), float(ag.adam_betas[1]), \
-                float(ag.adam_eps)
-            self._adam.append(ad)
+        op = native.OptimParams()
+        op.params, op.mask, op.s1, op.s2 = (self.flat.data_ptr(), self.ones.data_ptr(), self.mflat.data_ptr(),
+                                            self.vflat.data_ptr())
+        op.grad, op.ctrl = self.gflat.data_ptr(), self.opt_ctrl.data_ptr()
+        op.G, op.P, op.kind, op.mode = 0, self.flat.numel(), 2, 2
+        op.lr, op.beta1, op.beta2, op.eps, op.scale = (self.lr, float(ag.adam_betas[0]), float(ag.adam_betas[1]),
+                                                       float(ag.adam_eps), 1.0)
+        self._opt = op
 
     # ---------------------------------------------------------------- actor
     def pack(self, net: str = "on") -> None:
@@ -264,7 +260,6 @@ class RecurrentDQN:
         native.check(k.st_gru_td(self._td, sh), "st_gru_td")
         self.gflat.zero_()
         native.check(k.st_gru_seq_bwd(self._bwd, sh), "st_gru_seq_bwd")
-        native.check(kd.st_transpose_bf16(self.Hm.data_ptr(), HID, self.HT.data_ptr(), R1, RS, HID, sh), "T H")
         native.check(kd.st_transpose_bf16(self.X.data_ptr(), XL, self.XT.data_ptr(), R1, RS, XL, sh), "T X")
         # weight gradients; the ones row of HT / ones column RF of X give the bias gradients for free
         gm.gemm_nt(self.dGhT, self.HT[:, :RS], self.dWhh_ext, gm.EPI_F32, splitk="auto")
@@ -274,9 +269,9 @@ class RecurrentDQN:
                                          self.dP["b_ih"].data_ptr(), sh), "grad fixup")
         if self.grad_sync is not None:
             self.grad_sync(self.gflat)
-        for ad in self._adam:
-            native.check(kd.st_adam_tile(ad, sh), "adam")
-        native.check(kd.st_counter_inc(self.t_ctr.data_ptr(), sh), "t++")
+        nl = native.lib()
+        native.check(nl.st_advance(self.opt_ctrl.data_ptr(), sh), "advance")
+        native.check(nl.st_reduce_optim(self._opt, sh), "adam")
         self.pack("on")
 
     def sync_target(self) -> None:
