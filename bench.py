@@ -44,6 +44,8 @@ def main() -> int:
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on cuda:0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="envs per chunk of the fused step kernel: 0 = auto (64 when envs %% 64 == 0), 32, 64")
     ap.add_argument("--sync-dp", action="store_true",
                     help="N>1: strict sync DP (all-reduce exposed) instead of the all-reduce overlapped with the "
                          "next step's kernel (one-step delayed gradient, identical on every rank)")
@@ -80,6 +82,7 @@ def main() -> int:
     cfg = preset_config("flagship")
     cfg.engine.envs_per_rank = args.envs
     cfg.engine.dp_overlap = not args.sync_dp
+    cfg.engine.chunk = args.chunk
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 
@@ -161,6 +164,7 @@ def main() -> int:
                                      "all-reduce overlapped with next step (1-step delayed)"),
                 "envs_per_gpu": eng.E,
                 "hip_graph": use_graph,
+                "kernel_chunk": eng.chunk,
             },
             "episode_return_mean": round(float(ret[0] / ret[1]), 4),
             "episode_return_window_steps": args.steps,

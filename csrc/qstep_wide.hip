@@ -1,0 +1,591 @@
+// Wide-chunk fused online-DQN engine step on CDNA4 (gfx950): the same step as
+// qstep_fused.hip (gather -> Q(x) -> epsilon-greedy + env step -> Q(x') -> TD ->
+// backward -> per-workgroup weight-gradient slabs; QDecisionPolicyActor.scala:54-77,
+// TrainerChildActor.scala:82-146), re-tiled so that every workgroup barrier covers
+// twice the work.
+//
+// qstep_fused.hip keeps all bf16 weights (~94 KB) resident in LDS, which leaves room
+// for 32-env activation chunks only; its chunk loop is latency/barrier bound (in-kernel
+// stamps: ~15.7k cycles per 32-env chunk, MFMA pipes ~11 % busy, profiles/).  Here:
+//
+//  * layer-1 weights (W0^T, the 59 KB image) live in VGPRs: each of the 4 waves owns
+//    32 hidden units of both hidden layers, i.e. two 16x224 A operands = 14 fragments
+//    = 56 VGPRs per lane, loaded once per launch straight from the bf16 parameters;
+//  * LDS holds W1^T / W2^T (forward row reads + hardware-transposed backward reads) and
+//    64-env activation chunks: the 9 barriers of a chunk serve 64 envs instead of 32,
+//    every A fragment feeds 4 MFMAs (4 env tiles) and every B fragment 2 (2 m-tiles);
+//    activations are read from LDS by 4 waves instead of 8 (half the B-operand traffic);
+//  * the output layer runs on the 4 waves (one 16-env tile each) and the epsilon-greedy
+//    + Buy/Sell/Hold env step / TD target run in the lanes that hold the Q values
+//    (16 lanes x 4 waves instead of one wave), removing a barrier per forward;
+//  * one wave per SIMD, __launch_bounds__(256, 1): 512 registers per lane (VGPR + AGPR)
+//    hold the W0 fragments, the weight-gradient accumulators (which never leave registers
+//    until the launch ends: ~190 per lane) and a full chunk of prefetched price windows.
+#include "qstep.h"
+
+namespace st {
+namespace wide {
+
+constexpr int C = 64;          // envs per chunk
+#ifndef ST_WIDE_WAVES
+#define ST_WIDE_WAVES 4
+#endif
+constexpr int NW = ST_WIDE_WAVES;   // waves per workgroup (4: one per SIMD, 8: two per SIMD)
+constexpr int NT = 64 * NW;
+constexpr int NET = C / 16;    // env tiles per chunk
+constexpr int RPW = C / NW;    // gather rows per wave
+constexpr int SQ = OUTP + 8;
+constexpr int ENVF = 6;        // fp32 words per env in sEnv
+static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w < NET");
+
+template <int INP, int H1P, int H2P>
+struct Geo {
+  static constexpr int SW1 = H1P + 8, SW2 = H2P + 8;
+  static constexpr int SX = INP + 16, SH1 = H1P + 16, SH2 = H2P + 16;
+  static constexpr int oW1 = 0;
+  static constexpr int oW2 = oW1 + H2P * SW1;
+  static constexpr int oX = oW2 + OUTP * SW2;
+  static constexpr int oH1 = oX + C * SX;
+  static constexpr int oH2 = oH1 + C * SH1;
+  static constexpr int oR0 = oH2 + C * SH2;          // X' / H2' / dZ2
+  static constexpr int R0SZ = (C * SX > C * SH2) ? C * SX : C * SH2;
+  static constexpr int oR1 = oR0 + R0SZ;             // H1' / dZ1
+  static constexpr int oDQ = oR1 + C * SH1;
+  static constexpr int BF16_END = oDQ + C * SQ;
+  static constexpr int fQ = BF16_END * 2;            // q(x)   [C][4] fp32 (also the end-of-launch stats scratch)
+  static constexpr int fENV = fQ + C * 4 * 4;        // [C][ENVF] floats
+  static constexpr int fENVI = fENV + C * ENVF * 4;  // [C][4] ints
+  static constexpr int fB1 = fENVI + C * 4 * 4;      // b1 [H2P]
+  static constexpr int fB2 = fB1 + H2P * 4;          // b2 [16]
+  static constexpr int BYTES = fB2 + OUTP * 4;
+  static_assert(BYTES <= 163840, "LDS budget exceeded");
+  static_assert(H1P % (16 * NW) == 0 && H2P % (16 * NW) == 0 && H1P == H2P, "m-tiles per wave");
+  static_assert(INP % 32 == 0 && H1P % 32 == 0, "padding");
+  static constexpr int MT = H1P / (16 * NW);   // 16-unit m-tiles per wave in each hidden layer
+  static constexpr int KS0 = INP / 32;         // layer-1 k-steps
+  static constexpr int NT0 = INP / 16 - 1;     // in-col tiles of dW0 (last tile is pure padding)
+  static constexpr int NT1 = H1P / 16;
+};
+
+// out^T[m][env] for this wave's MT m-tiles and the chunk's NET env tiles; A fragments given per
+// (m-tile, k-step) by the functor, B = activation rows.  Epilogue: + bias, ReLU, bf16 store into
+// out image [env][m].
+template <int MT, int K, int SB, int SO, typename AFrag>
+ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* bias, int m0, int l16, int g4) {
+  f4v acc[MT][NET];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < NET; ++n) acc[i][n] = zero4();
+#pragma unroll
+  for (int ks = 0; ks < K / 32; ++ks) {
+    s8v b[NET];
+#pragma unroll
+    for (int n = 0; n < NET; ++n) b[n] = frag_row(sB, SB, 16 * n, ks * 32, l16, g4);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const s8v a = afrag(i, ks);
+#pragma unroll
+      for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(a, b[n], acc[i][n]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m0 + 16 * i + 4 * g4;
+    float bb[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) { bb[0] = bias[m]; bb[1] = bias[m + 1]; bb[2] = bias[m + 2]; bb[3] = bias[m + 3]; }
+#pragma unroll
+    for (int n = 0; n < NET; ++n) {
+      const f4v v = acc[i][n];
+      lds_st4(sO + (16 * n + l16) * SO + m, fmaxf(v[0] + bb[0], 0.f), fmaxf(v[1] + bb[1], 0.f),
+              fmaxf(v[2] + bb[2], 0.f), fmaxf(v[3] + bb[3], 0.f));
+    }
+  }
+}
+
+// q^T[a][env] of env tile `nt` (lanes g4 == 0 end up holding q[0..3] of env 16*nt + l16)
+template <int K, int SA, int SB>
+ST_DEV f4v fwd_out(const bf16_t* sA, const bf16_t* sB, int nt, int l16, int g4) {
+  f4v acc = zero4();
+#pragma unroll
+  for (int ks = 0; ks < K / 32; ++ks) {
+    const s8v a = frag_row(sA, SA, 0, ks * 32, l16, g4);
+    const s8v b = frag_row(sB, SB, 16 * nt, ks * 32, l16, g4);
+    acc = mfma32(a, b, acc);
+  }
+  return acc;
+}
+
+// dA^T[m][env] = sum_k W[m][k] * dZ[env][k] (W read transposed from the W^T image [k][m]),
+// masked by (act[env][m] > 0), bf16 store into out image [env][m].
+template <int MT, int K, int SW, int SD, int SACT, int SO>
+ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, bf16_t* sO, int m0, int l16, int g4) {
+  f4v acc[MT][NET];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < NET; ++n) acc[i][n] = zero4();
+  if constexpr (K == 16) {
+    s4v b[NET];
+#pragma unroll
+    for (int n = 0; n < NET; ++n) b[n] = lds_ld4(sDZ + (16 * n + l16) * SD + 4 * g4);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const s4v a = lds_tr4(sWT + (4 * g4 + (l16 >> 2)) * SW + m0 + 16 * i + 4 * (l16 & 3));
+#pragma unroll
+      for (int n = 0; n < NET; ++n) acc[i][n] = mfma16(a, b[n], acc[i][n]);
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < K / 32; ++ks) {
+      s8v b[NET];
+#pragma unroll
+      for (int n = 0; n < NET; ++n) b[n] = frag_row(sDZ, SD, 16 * n, ks * 32, l16, g4);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const s8v a = frag_tr(sWT, SW, ks * 32, m0 + 16 * i, l16, g4);
+#pragma unroll
+        for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(a, b[n], acc[i][n]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m0 + 16 * i + 4 * g4;
+#pragma unroll
+    for (int n = 0; n < NET; ++n) {
+      const int env = 16 * n + l16;
+      const s4v h = lds_ld4(sAct + env * SACT + m);
+      const f4v v = acc[i][n];
+      lds_st4(sO + env * SO + m, h[0] > 0 ? v[0] : 0.f, h[1] > 0 ? v[1] : 0.f, h[2] > 0 ? v[2] : 0.f,
+              h[3] > 0 ? v[3] : 0.f);
+    }
+  }
+}
+
+template <int INP, int H1P, int H2P, int FEAT>
+__global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
+  using G = Geo<INP, H1P, H2P>;
+  constexpr int MT = G::MT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* sbf = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* sW1 = sbf + G::oW1;
+  bf16_t* sW2 = sbf + G::oW2;
+  bf16_t* sX = sbf + G::oX;
+  bf16_t* sH1 = sbf + G::oH1;
+  bf16_t* sH2 = sbf + G::oH2;
+  bf16_t* sR0 = sbf + G::oR0;
+  bf16_t* sR1 = sbf + G::oR1;
+  bf16_t* sDQ = sbf + G::oDQ;
+  float* sQ = reinterpret_cast<float*>(smem + G::fQ);
+  float* sEnv = reinterpret_cast<float*>(smem + G::fENV);
+  int* sEnvI = reinterpret_cast<int*>(smem + G::fENVI);
+  float* sB1 = reinterpret_cast<float*>(smem + G::fB1);
+  float* sB2 = reinterpret_cast<float*>(smem + G::fB2);
+
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.H;
+  const unsigned long long step = p.ctrl[0];
+  const int m0 = 16 * MT * wave;   // this wave's hidden units in both hidden layers
+
+  // ---------------------------------------------------------------- weights (once per launch)
+  // W0^T rows m0 + 16i + l16 -> MT x KS0 A fragments in VGPRs (global dwordx4; the 57 KB image is
+  // L2-resident across the workgroups of an XCD)
+  s8v aW0[MT][G::KS0];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const bf16_t* w0 = p.wq + p.off_w0 + (size_t)(m0 + 16 * i + l16) * INP + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < G::KS0; ++ks) aW0[i][ks] = *reinterpret_cast<const s8v*>(w0 + ks * 32);
+  }
+  {
+    const bf16_t* w1 = p.wq + p.off_w1;
+    for (int i = tid; i < H2P * H1P / 8; i += NT) {
+      const int r = i / (H1P / 8), c = (i % (H1P / 8)) * 8;
+      *reinterpret_cast<uint4*>(sW1 + r * G::SW1 + c) = *reinterpret_cast<const uint4*>(w1 + r * H1P + c);
+    }
+    const bf16_t* w2 = p.wq + p.off_w2;
+    for (int i = tid; i < OUTP * H2P / 8; i += NT) {
+      const int r = i / (H2P / 8), c = (i % (H2P / 8)) * 8;
+      *reinterpret_cast<uint4*>(sW2 + r * G::SW2 + c) = *reinterpret_cast<const uint4*>(w2 + r * H2P + c);
+    }
+    for (int i = tid; i < H2P; i += NT) sB1[i] = p.wf[p.off_b1 + i];
+    if (tid < OUTP) sB2[tid] = p.wf[p.off_b2 + tid];
+  }
+
+  // ---------------------------------------------------------------- gradient accumulators
+  constexpr int NT0 = G::NT0, NT1 = G::NT1;
+  f4v gW0[MT][NT0];
+  f4v gW1[MT][NT1];
+  f4v gB1[MT], gW2[MT];
+  f4v gB2 = zero4();
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int n = 0; n < NT0; ++n) gW0[i][n] = zero4();
+#pragma unroll
+    for (int n = 0; n < NT1; ++n) gW1[i][n] = zero4();
+    gB1[i] = zero4();
+    gW2[i] = zero4();
+  }
+  // ones fragment for bias gradients: B[k][n] = (n == 0)
+  s8v ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (l16 == 0) ? (short)0x3F80 : (short)0;
+
+  float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
+        st_qslot = 0.f;
+
+  const int nchunks = p.E / C;
+  int iter = 0;
+#define STW_STAMP(I) \
+  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[iter * 16 + (I)] = __builtin_amdgcn_s_memtime();
+
+  // ---------------------------------------------------------------- software-pipelined gather
+  // (same scheme as qstep_fused.hip: env state two chunks ahead, price windows one chunk ahead,
+  // every load unconditional with clamped indices; lanes rr < RPW own one row each)
+  int eA_pos = 0, eA_sh = 0, eA_ep = 0, eB_pos = 0, eB_sh = 0, eB_ep = 0;
+  float eA_b = 0.f, eA_val = 0.f, eA_rs = 0.f, eB_b = 0.f, eB_val = 0.f, eB_rs = 0.f;
+  float4 w[RPW];
+  float wl = 0.f, wv = 0.f;
+#define STW_LOAD_ENV(CH, POS, B, SH, VAL, RS, EP)                          \
+  {                                                                        \
+    const int ch_ = min((CH), nchunks - 1);                                \
+    const int e_ = ch_ * C + wave * RPW + min(lane, RPW - 1);              \
+    POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                  \
+    VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);            \
+  }
+#define STW_LOAD_PRICES(CH, POS)                                           \
+  {                                                                        \
+    const int ch_ = min((CH), nchunks - 1);                                \
+    const int sh_ = (POS) & 3;                                             \
+    const size_t off_ = ((size_t)sh_ * p.E + (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1))) \
+        * p.T4 + (size_t)((POS) - sh_);                                    \
+    const unsigned long long a_ = (unsigned long long)(p.prices4 + off_);  \
+    const unsigned alo_ = (unsigned)a_, ahi_ = (unsigned)(a_ >> 32);       \
+    _Pragma("unroll") for (int rr = 0; rr < RPW; ++rr) {                   \
+      const unsigned long long b_ =                                        \
+          ((unsigned long long)__builtin_amdgcn_readlane(ahi_, rr) << 32) | \
+          (unsigned)__builtin_amdgcn_readlane(alo_, rr);                   \
+      typedef float f4g_ __attribute__((ext_vector_type(4)));              \
+      const f4g_ v_ = reinterpret_cast<const __attribute__((address_space(1))) f4g_*>(b_)[lane]; \
+      w[rr] = make_float4(v_.x, v_.y, v_.z, v_.w);                         \
+    }                                                                      \
+    const float* pl_ = p.prices +                                          \
+        (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1)) * p.T + (POS) + H; \
+    wl = pl_[-1];                                                          \
+    wv = pl_[0];                                                           \
+  }
+  STW_LOAD_ENV(blockIdx.x, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
+  STW_LOAD_PRICES(blockIdx.x, eA_pos)
+  STW_LOAD_ENV(blockIdx.x + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
+  __syncthreads();
+
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    STW_STAMP(0);
+    const int ebase = chunk * C;
+    // ------------------------------------------------------------ P0: windows -> feature rows
+    // row-owner lanes (lane rr < RPW owns row wave*RPW + rr): env scalars -> LDS, 1/last, 1/new
+    float r_inv = 0.f, r_invn = 0.f;
+    if (lane < RPW) {
+      const int r = wave * RPW + lane;
+      sEnv[r * ENVF + 0] = eA_b;
+      sEnv[r * ENVF + 1] = eA_val;
+      sEnv[r * ENVF + 2] = wv;
+      sEnv[r * ENVF + 5] = eA_rs;
+      sEnvI[r * 4 + 0] = eA_pos;
+      sEnvI[r * 4 + 1] = eA_sh;
+      sEnvI[r * 4 + 3] = eA_ep;
+      r_inv = __fdiv_rn(1.0f, wl);
+      r_invn = __fdiv_rn(1.0f, wv);
+    }
+    // lane L < INP/4 owns window columns k = 4L..4L+3 of every row: price features, 0 for k >= H
+    // (the budget / shares / ones tail of x is written below by the row owners, the one of x' by
+    // the env step); one 8-byte LDS store per row for x and one for x'
+    if (lane < INP / 4) {
+      bool isp[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) isp[j] = 4 * lane + j < H;
+      bf16_t* px = sX + (wave * RPW) * G::SX + 4 * lane;
+      bf16_t* pxn = sR0 + (wave * RPW) * G::SX + 4 * lane;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_inv), rr));
+        const float invn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_invn), rr));
+        const float win[5] = {w[rr].x, w[rr].y, w[rr].z, w[rr].w, dpp_next_lane(w[rr].x)};
+        float xv[4], xnv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xv[j] = isp[j] ? feat_price(win[j], inv, FEAT) : 0.f;
+          xnv[j] = isp[j] ? feat_price(win[j + 1], invn, FEAT) : 0.f;
+        }
+        lds_st4(px + rr * G::SX, xv[0], xv[1], xv[2], xv[3]);
+        lds_st4(pxn + rr * G::SX, xnv[0], xnv[1], xnv[2], xnv[3]);
+      }
+    }
+    if (lane < RPW) {   // x tail: (budget, shares, 1) features (same wave, after its row stores)
+      bf16_t* xt = sX + (wave * RPW + lane) * G::SX + H;
+      xt[0] = f2bf(feat_budget(eA_b, p.inv_b0, FEAT));
+      xt[1] = f2bf(feat_shares(eA_sh, wl, p.inv_b0, FEAT));
+      xt[2] = f2bf(1.0f);
+    }
+    {
+      const int nxt = chunk + gridDim.x;
+      STW_LOAD_PRICES(nxt, eB_pos)
+      eA_pos = eB_pos; eA_b = eB_b; eA_sh = eB_sh; eA_val = eB_val; eA_rs = eB_rs; eA_ep = eB_ep;
+      STW_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
+    }
+    __syncthreads();
+    STW_STAMP(1);
+    // ------------------------------------------------------------ P1-P2: hidden layers of Q(x)
+    auto a_w0 = [&](int i, int ks) { return aW0[i][ks]; };
+    auto a_w1 = [&](int i, int ks) { return frag_row(sW1, G::SW1, m0 + 16 * i, ks * 32, l16, g4); };
+    fwd_hidden<MT, INP, G::SX, G::SH1>(a_w0, sX, sH1, nullptr, m0, l16, g4);
+    __syncthreads();
+    fwd_hidden<MT, H1P, G::SH1, G::SH2>(a_w1, sH1, sH2, sB1, m0, l16, g4);
+    __syncthreads();
+    STW_STAMP(2);
+    // ------------------------------------------------------------ P3: Q(x), epsilon-greedy, env step
+    // wave w < NET: output tile of env tile w; lanes g4 == 0 own env 16*w + l16
+    if (wave < NET) {
+      const f4v qa = fwd_out<H2P, G::SW2, G::SH2>(sW2, sH2, wave, l16, g4);
+      if (g4 == 0) {
+        const int r = 16 * wave + l16, e = ebase + r;
+        float q[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          q[j] = qa[j] + sB2[j];
+          if (p.output_relu) q[j] = fmaxf(q[j], 0.f);
+        }
+        sQ[r * 4 + 0] = q[0];
+        sQ[r * 4 + 1] = q[1];
+        sQ[r * 4 + 2] = q[2];
+        int greedy = 0;
+        float best = q[0];
+        if (q[1] > best) { best = q[1]; greedy = 1; }
+        if (q[2] > best) { best = q[2]; greedy = 2; }
+        const int ps = sEnvI[r * 4 + 0];
+        uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
+                 c2 = (uint32_t)(step >> 32), c3 = 0u;
+        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+        const float u1 = u24(c0), u2 = u24(c1);
+        const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)ps, p.inv_ramp));
+        int rnd = (int)(u2 * 3.0f);
+        rnd = rnd > 2 ? 2 : rnd;
+        const int a = exploit ? greedy : rnd;
+        const float b = sEnv[r * ENVF + 0], vprev = sEnv[r * ENVF + 1], vnew = sEnv[r * ENVF + 2];
+        const int s = sEnvI[r * 4 + 1];
+        const float bd = p.compat_env ? p.b0 : b;
+        const int sd = p.compat_env ? p.s0 : s;
+        const bool buy = (a == 0) && (bd >= vnew);
+        const bool sell = (a == 1) && (sd > 0);
+        const float b2 = buy ? __fsub_rn(bd, vnew) : (sell ? __fadd_rn(bd, vnew) : bd);
+        const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
+        const float cur = __fadd_rn(b, __fmul_rn((float)s, vprev));
+        const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
+        const float rew = __fsub_rn(nw, cur);
+        sEnv[r * ENVF + 3] = b2;
+        sEnv[r * ENVF + 4] = rew;
+        sEnvI[r * 4 + 1] = s2;
+        sEnvI[r * 4 + 2] = a;
+        bf16_t* xn = sR0 + r * G::SX;
+        xn[H] = f2bf(feat_budget(b2, p.inv_b0, FEAT));
+        xn[H + 1] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
+        xn[H + 2] = f2bf(1.0f);
+        st_explore += exploit ? 0.f : 1.f;
+        ENV_I(ER_ACTION, e) = a;
+        ENV_F(ER_REWARD, e) = rew;
+      }
+    }
+    __syncthreads();
+    STW_STAMP(3);
+    // ------------------------------------------------------------ P4-P5: hidden layers of Q(x')
+    fwd_hidden<MT, INP, G::SX, G::SH1>(a_w0, sR0, sR1, nullptr, m0, l16, g4);
+    __syncthreads();
+    fwd_hidden<MT, H1P, G::SH1, G::SH2>(a_w1, sR1, sR0, sB1, m0, l16, g4);
+    __syncthreads();
+    STW_STAMP(4);
+    // ------------------------------------------------------------ P6: Q(x'), TD target, dQ, state write-back
+    if (wave < NET) {
+      const f4v qn = fwd_out<H2P, G::SW2, G::SH2>(sW2, sR0, wave, l16, g4);
+      if (g4 == 0) {
+        const int r = 16 * wave + l16, e = ebase + r;
+        float n[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          n[j] = qn[j] + sB2[j];
+          if (p.output_relu) n[j] = fmaxf(n[j], 0.f);
+        }
+        int am = 0;
+        float mx = n[0];
+        if (n[1] > mx) { mx = n[1]; am = 1; }
+        if (n[2] > mx) { mx = n[2]; am = 2; }
+        const int a = sEnvI[r * 4 + 2];
+        const float rew = sEnv[r * ENVF + 4];
+        const int slot = p.target_compat ? am : a;
+        const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
+        const float qs = sQ[r * 4 + slot];
+        const float diff = __fsub_rn(qs, y);
+        float dq = p.loss_coef * diff;
+        if (p.output_relu && !(qs > 0.f)) dq = 0.f;
+        // dQ row: one nonzero at `slot`, written as two 16-byte stores
+        const uint32_t dqb = (uint32_t)f2bf(dq);
+        uint32_t wd[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wd[k] = (slot == 2 * k) ? dqb : (slot == 2 * k + 1) ? (dqb << 16) : 0u;
+        uint4* dqr = reinterpret_cast<uint4*>(sDQ + r * SQ);
+        dqr[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        dqr[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+        st_loss += diff * diff;
+        st_reward += rew;
+        st_qslot += qs;
+        const float b2 = sEnv[r * ENVF + 3], vnew = sEnv[r * ENVF + 2];
+        const int s2 = sEnvI[r * 4 + 1];
+        const int np = sEnvI[r * 4 + 0] + 1;
+        const float rs = sEnv[r * ENVF + 5] + rew;
+        if (np >= p.T - H) {
+          const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
+          ENV_F(ER_LAST_FINAL, e) = fin;
+          ENV_I(ER_EPISODES, e) = sEnvI[r * 4 + 3] + 1;
+          ENV_F(ER_BUDGET, e) = p.b0;
+          ENV_I(ER_SHARES, e) = p.s0;
+          ENV_F(ER_VALUE, e) = 0.f;
+          ENV_I(ER_POS, e) = 0;
+          ENV_F(ER_RET_SUM, e) = 0.f;
+          st_done += 1.f;
+          st_fsum += fin;
+          st_fsq += fin * fin;
+        } else {
+          ENV_F(ER_BUDGET, e) = b2;
+          ENV_I(ER_SHARES, e) = s2;
+          ENV_F(ER_VALUE, e) = vnew;
+          ENV_I(ER_POS, e) = np;
+          ENV_F(ER_RET_SUM, e) = rs;
+        }
+      }
+    }
+    __syncthreads();
+    STW_STAMP(5);
+    // ------------------------------------------------------------ P7-P8: backward (data)
+    bwd_data<MT, OUTP, G::SW2, SQ, G::SH2, G::SH2>(sW2, sDQ, sH2, sR0, m0, l16, g4);
+    __syncthreads();
+    bwd_data<MT, H2P, G::SW1, G::SH2, G::SH1, G::SH1>(sW1, sR0, sH1, sR1, m0, l16, g4);
+    __syncthreads();
+    STW_STAMP(6);
+    // ------------------------------------------------------------ P9: weight gradients (sum over the chunk's envs)
+#pragma unroll
+    for (int ks = 0; ks < C / 32; ++ks) {
+      const int k0 = 32 * ks;
+      // dW0^T[h1][in] += dZ1^T . X
+      s8v a1[MT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a1[i] = frag_tr(sR1, G::SH1, k0, m0 + 16 * i, l16, g4);
+#pragma unroll
+      for (int n = 0; n < NT0; ++n) {
+        const s8v bx = frag_tr(sX, G::SX, k0, n * 16, l16, g4);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) gW0[i][n] = mfma32(a1[i], bx, gW0[i][n]);
+      }
+      // dW1^T[h2][h1] += dZ2^T . H1 ; db1 += dZ2^T . 1
+      s8v a2[MT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a2[i] = frag_tr(sR0, G::SH2, k0, m0 + 16 * i, l16, g4);
+#pragma unroll
+      for (int n = 0; n < NT1; ++n) {
+        const s8v bh = frag_tr(sH1, G::SH1, k0, n * 16, l16, g4);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) gW1[i][n] = mfma32(a2[i], bh, gW1[i][n]);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) gB1[i] = mfma32(a2[i], ones, gB1[i]);
+      // dW2^T[out][h2] += dQ^T . H2 ; db2 += dQ^T . 1
+      const s8v aq = frag_tr(sDQ, SQ, k0, 0, l16, g4);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, frag_tr(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
+      gB2 = mfma32(aq, ones, gB2);   // every wave (branch-free accumulators); wave 0 writes it
+    }
+    __syncthreads();
+    STW_STAMP(7);
+    ++iter;
+  }
+#undef STW_LOAD_ENV
+#undef STW_LOAD_PRICES
+#undef STW_STAMP
+
+  // ---------------------------------------------------------------- gradient slab write-out
+  float* sl = p.slab + (size_t)blockIdx.x * p.P;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int h = m0 + 16 * i + 4 * g4;
+#pragma unroll
+    for (int n = 0; n < NT0; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sl[p.off_w0 + (h + j) * INP + n * 16 + l16] = gW0[i][n][j];
+#pragma unroll
+    for (int n = 0; n < NT1; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sl[p.off_w1 + (h + j) * H1P + n * 16 + l16] = gW1[i][n][j];
+    if (l16 == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sl[p.off_b1 + h + j] = gB1[i][j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sl[p.off_w2 + (4 * g4 + j) * H2P + m0 + 16 * i + l16] = gW2[i][j];
+  }
+  if (wave == 0 && l16 == 0)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sl[p.off_b2 + 4 * g4 + j] = gB2[j];
+
+  if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;  // 1-based update count for the optimizer
+  // ---------------------------------------------------------------- per-workgroup stats (waves -> LDS -> slab)
+  {
+    const float v0 = wave_sum(st_reward), v1 = wave_sum(st_loss), v2 = wave_sum(st_explore),
+                v3 = wave_sum(st_done), v4 = wave_sum(st_fsum), v5 = wave_sum(st_fsq), v6 = wave_sum(st_qslot);
+    if (lane == 0) {
+      float* so = sQ + wave * NSTAT;
+      so[0] = v0; so[1] = v1; so[2] = v2; so[3] = v3; so[4] = v4; so[5] = v5; so[6] = v6; so[7] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (tid < NSTAT) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) t += sQ[k * NSTAT + tid];
+    p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
+  }
+}
+
+template <int INP, int H1P, int H2P, int FEAT>
+static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
+  using G = Geo<INP, H1P, H2P>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)qstep_wide_kernel<INP, H1P, H2P, FEAT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((qstep_wide_kernel<INP, H1P, H2P, FEAT>), dim3(grid), dim3(NT), G::BYTES, stream, p);
+  return hipGetLastError();
+}
+
+}  // namespace wide
+}  // namespace st
+
+extern "C" int st_qstep_wide_lds_bytes(int inp, int h1p, int h2p) {
+  if (inp == 224 && h1p == 128 && h2p == 128) return st::wide::Geo<224, 128, 128>::BYTES;
+  return -1;
+}
+
+// Preconditions (checked here and by the host, sharetrade/trainer/engine.py): E % 64 == 0,
+// 1 <= grid <= E / 64, H + 3 <= inp - 16, 8-element aligned weight offsets (16-byte fragment loads).
+extern "C" hipError_t st_qstep_wide_launch(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
+                                           hipStream_t stream) {
+  if (p->E % st::wide::C != 0 || grid < 1 || grid > p->E / st::wide::C) return hipErrorInvalidValue;
+  if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
+  if (p->H + 3 > inp - 16) return hipErrorInvalidValue;
+  if (inp == 224 && h1p == 128 && h2p == 128)
+    return p->feat_mode ? st::wide::launch_f<224, 128, 128, 1>(*p, grid, stream)
+                        : st::wide::launch_f<224, 128, 128, 0>(*p, grid, stream);
+  return hipErrorInvalidValue;
+}

@@ -138,7 +138,9 @@ class EngineConfig:
     device: str = "auto"            # auto | cuda | cpu
     envs_per_rank: int = 10
     dtype: str = "bf16"             # bf16 (MFMA fused step) | fp32 (exact path)
-    chunk: int = 32                 # envs per LDS chunk inside the fused step kernel
+    # envs per LDS chunk of the fused bf16 step kernel: 0 = auto (64 when E % 64 == 0, else 32);
+    # 64 = csrc/qstep_wide.hip (layer-1 weights in VGPRs), 32 = csrc/qstep_fused.hip (weights in LDS)
+    chunk: int = 0
     graph: bool = True              # capture the step in a HIP graph
     backend: str = "auto"           # auto | native | torch
     bucket_mb: float = 4.0          # DP gradient all-reduce bucket (one call below this size)

@@ -112,6 +112,17 @@ class VectorEngine:
             # bf16: the fused MFMA step kernel (csrc/qstep_fused.hip);
             # fp32: the exact-fp32 row kernels (csrc/mlp_f32.hip) — any MLP up to 6 layers x 1024
             self.kernel = "bf16_fused" if fused_ok else "fp32_rows"
+        # envs per chunk of the fused kernel: 64 -> csrc/qstep_wide.hip, 32 -> csrc/qstep_fused.hip
+        self.chunk = 32
+        if self.kernel == "bf16_fused":
+            want = int(cfg.engine.chunk)
+            wide_ok = self.E % 64 == 0 and native.qstep_wide_supported(L.pdims[0], L.pdims[1], L.pdims[2])
+            if want == 64 and not wide_ok:
+                raise NotImplementedError(f"engine.chunk=64 needs E % 64 == 0 and padded dims (224, 128, 128); "
+                                          f"got E={self.E}, dims {L.pdims}")
+            if want not in (0, 32, 64):
+                raise ValueError(f"engine.chunk must be 0 (auto), 32 or 64, got {want}")
+            self.chunk = 64 if (want in (0, 64) and wide_ok) else 32
         # ------------------------------------------------------------ data
         if prices is not None:
             bank = padded_bank(prices.shape[0], prices.shape[1], self.device)
@@ -181,7 +192,7 @@ class VectorEngine:
         self.prices4 = native.replicate4(self.prices)   # aligned-gather replicas (4 x bank, HBM is plentiful)
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
-        self.grid = max(1, min(props.multi_processor_count, self.E // 32))
+        self.grid = max(1, min(props.multi_processor_count, self.E // self.chunk))
         self.slab = torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev)
         self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)
         self._build_structs()
@@ -234,8 +245,7 @@ class VectorEngine:
             return
         L = native.lib()
         sh = native.stream_handle()
-        native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],
-                                       self.layout.pdims[2], self.grid, sh), "qstep")
+        self._launch_qstep(L, sh)
         if self.world_size > 1 and self.cfg.engine.dp_overlap:
             self._overlap_step(L, sh)
         elif self.world_size > 1:
@@ -247,6 +257,11 @@ class VectorEngine:
         else:
             self._op.mode = 0
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
+
+    def _launch_qstep(self, L, sh) -> None:
+        fn = L.st_qstep_wide_launch if self.chunk == 64 else L.st_qstep_launch
+        d = self.layout.pdims
+        native.check(fn(self._qp, d[0], d[1], d[2], self.grid, sh), f"qstep(chunk={self.chunk})")
 
     def _overlap_step(self, L, sh) -> None:
         """DP step with the all-reduce hidden behind the next fused kernel: reduce this step's slabs
@@ -309,8 +324,7 @@ class VectorEngine:
             return self.grad
         L = native.lib()
         sh = native.stream_handle()
-        native.check(L.st_qstep_launch(self._qp, self.layout.pdims[0], self.layout.pdims[1],
-                                       self.layout.pdims[2], self.grid, sh), "qstep")
+        self._launch_qstep(L, sh)
         self._op.mode = 1
         native.check(L.st_reduce_optim(self._op, sh), "reduce")
         self.step_count += 1

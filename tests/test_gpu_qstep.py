@@ -34,7 +34,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("compat", [False, True])
-@pytest.mark.parametrize("E", [32, 96, 256])
+@pytest.mark.parametrize("E", [32, 96, 64, 192, 256])   # E % 64 == 0: csrc/qstep_wide.hip
 def test_qstep_matches_oracle(native_built, compat, E):
     from sharetrade.env import trading as tr
     from sharetrade.trainer.engine import VectorEngine
@@ -92,6 +92,37 @@ def test_qstep_matches_oracle(native_built, compat, E):
         epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
         loss_coef=eng.loss_coef, emulate_bf16=False, forced_actions=acts)
     assert _rel(grad, g32) < 0.1
+
+
+@pytest.mark.parametrize("compat", [False, True])
+def test_wide_and_narrow_kernels_agree(native_built, compat):
+    """csrc/qstep_wide.hip (64-env chunks) vs csrc/qstep_fused.hip (32-env chunks) on the same state:
+    identical env transitions, gradients equal up to fp32 summation order."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 512
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for chunk in (32, 64):
+        cfg = _cfg(compat)
+        cfg.agent.epsilon = 0.5
+        cfg.engine.chunk = chunk
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.chunk == chunk
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
+        eng.ctrl.fill_(9)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        out[chunk] = (g, eng.actions_out.cpu().clone(), eng.rewards_out.cpu().clone(),
+                      {k: v.cpu().clone() for k, v in eng.state.as_dict().items()}, eng.stat_slab.sum(0).cpu())
+    g32, a32, r32, s32, st32 = out[32]
+    g64, a64, r64, s64, st64 = out[64]
+    assert torch.equal(a32, a64) and torch.equal(r32, r64)
+    for k in s32:
+        assert torch.equal(s32[k].nan_to_num(-1.0), s64[k].nan_to_num(-1.0)), k
+    assert _rel(g64, g32) < 1e-4, _rel(g64, g32)
+    assert torch.allclose(st64, st32, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("opt", ["adam", "adagrad", "sgd"])

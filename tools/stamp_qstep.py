@@ -12,14 +12,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = ["P0 gather", "P1-3 fwd Q(x)", "P4 select+env", "P5-7 fwd Q(x')", "P8 TD+writeback",
-          "P9-10 bwd data", "P11 weight grads"]
+PHASES = {32: ["P0 gather", "P1-3 fwd Q(x)", "P4 select+env", "P5-7 fwd Q(x')", "P8 TD+writeback",
+               "P9-10 bwd data", "P11 weight grads"],
+          64: ["P0 gather", "P1-2 hidden Q(x)", "P3 out Q(x)+select+env", "P4-5 hidden Q(x')",
+               "P6 out Q(x')+TD+writeback", "P7-8 bwd data", "P9 weight grads"]}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--out", default="")
+    ap.add_argument("--chunk", type=int, default=0, help="0 = engine default, 32 or 64")
     a = ap.parse_args()
     import build
 
@@ -29,11 +32,13 @@ def main():
     from sharetrade.trainer.engine import VectorEngine
 
     cfg = preset_config("flagship")
+    cfg.engine.chunk = a.chunk
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=a.envs)
     eng.run(3)
     torch.cuda.synchronize()
-    iters = (a.envs // 32 + eng.grid - 1) // eng.grid
+    iters = (a.envs // eng.chunk + eng.grid - 1) // eng.grid
+    names = PHASES[eng.chunk]
     st = torch.zeros(iters * 16 + 16, dtype=torch.int64, device=dev)
     eng._qp.stamps = st.data_ptr()
     eng.step()
@@ -44,14 +49,20 @@ def main():
     tot = 0
     for ph in range(7):
         d = (s[:, ph + 1] - s[:, ph]).double()
-        rows.append((PHASES[ph], float(d.mean())))
+        rows.append((names[ph], float(d.mean())))
         tot += float(d.mean())
     loop = float((s[1:, 0] - s[:-1, 0]).double().mean()) if iters > 1 else tot
-    lines = [f"# fused step kernel phase breakdown (workgroup 0, {a.envs} envs, grid {eng.grid}, "
+    lines = [f"# fused step kernel phase breakdown (chunk {eng.chunk}, workgroup 0, {a.envs} envs, grid {eng.grid}, "
              f"{iters} chunks/WG; s_memtime ticks)\n", "| phase | ticks/chunk | % |", "|---|---|---|"]
     for n, v in rows:
         lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
     lines.append(f"| chunk loop (stamp0->stamp0) | {loop:.0f} | |")
+    if eng.chunk != 32:   # the P0 sub-stamps exist in the 32-env kernel only
+        txt = "\n".join(lines) + "\n"
+        print(txt)
+        if a.out:
+            open(a.out, "w").write(txt)
+        return
     wait = float((s[:, 8] - s[:, 0]).double().mean())
     lines.append(f"| of P0: waiting for prefetched loads/stores (debug waitcnt) | {wait:.0f} | |")
     rows_t = float((s[:, 9] - s[:, 8]).double().mean())
