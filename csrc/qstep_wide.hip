@@ -8,23 +8,29 @@
 // for 32-env activation chunks only; its chunk loop is latency/barrier bound (in-kernel
 // stamps: ~15.7k cycles per 32-env chunk, MFMA pipes ~11 % busy, profiles/).  Here:
 //
-//  * layer-1 weights (W0^T, the 59 KB image) live in VGPRs: each of the 4 waves owns
-//    32 hidden units of both hidden layers, i.e. two 16x224 A operands = 14 fragments
-//    = 56 VGPRs per lane, loaded once per launch straight from the bf16 parameters;
-//  * LDS holds W1^T / W2^T (forward row reads + hardware-transposed backward reads) and
-//    64-env activation chunks: the 9 barriers of a chunk serve 64 envs instead of 32,
-//    every A fragment feeds 4 MFMAs (4 env tiles) and every B fragment 2 (2 m-tiles);
-//    activations are read from LDS by 4 waves instead of 8 (half the B-operand traffic);
-//  * the output layer runs on the 4 waves (one 16-env tile each) and the epsilon-greedy
-//    + Buy/Sell/Hold env step / TD target run in the lanes that hold the Q values
-//    (16 lanes x 4 waves instead of one wave), removing a barrier per forward;
-//  * one wave per SIMD, __launch_bounds__(256, 1): 512 registers per lane (VGPR + AGPR)
-//    hold the W0 fragments, the weight-gradient accumulators (which never leave registers
-//    until the launch ends: ~190 per lane) and a full chunk of prefetched price windows.
+//  * layer-1 weights (W0^T, the 59 KB image) live in VGPRs: a wave owning 16 hidden units of both
+//    hidden layers holds one 16x224 A operand = 7 fragments = 28 VGPRs per lane, loaded once per
+//    launch straight from the bf16 parameters;
+//  * LDS holds W1^T / W2^T (forward row reads + hardware-transposed backward reads) and 64-env
+//    activation chunks: the barriers of a chunk serve 64 envs instead of 32 and every A fragment
+//    feeds 4 MFMAs (4 env tiles);
+//  * the output layer runs on 4 waves (one 16-env tile each) and the epsilon-greedy + Buy/Sell/Hold
+//    env step / TD target run in the lanes that hold the Q values (16 lanes x 4 waves instead of
+//    one wave), removing a barrier per forward;
+//  * the next chunk's price windows are issued at the start of the weight-gradient phase, so their
+//    registers are live only from there to the gather (not across the forward / backward phases);
+//  * two builds: 8 waves (two per SIMD, 256 registers per lane, 16 units per wave; this file via
+//    qstep_wide8.hip, the engine default: fastest measured, profiles/r1_stamps_wide_step.md) and
+//    4 waves (one per SIMD, 512 registers, 32 units per wave; this file).
 #include "qstep.h"
 
+#ifndef ST_WIDE_NS
+#define ST_WIDE_NS wide
+#define ST_WIDE_API(name) name
+#endif
+
 namespace st {
-namespace wide {
+namespace ST_WIDE_NS {
 
 constexpr int C = 64;          // envs per chunk
 #ifndef ST_WIDE_WAVES
@@ -34,6 +40,10 @@ constexpr int NW = ST_WIDE_WAVES;   // waves per workgroup (4: one per SIMD, 8: 
 constexpr int NT = 64 * NW;
 constexpr int NET = C / 16;    // env tiles per chunk
 constexpr int RPW = C / NW;    // gather rows per wave
+#ifndef ST_WIDE_PF_LATE
+#define ST_WIDE_PF_LATE 1
+#endif
+constexpr bool PF_LATE = ST_WIDE_PF_LATE;
 constexpr int SQ = OUTP + 8;
 constexpr int ENVF = 6;        // fp32 words per env in sEnv
 static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w < NET");
@@ -188,6 +198,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   const int H = p.H;
   const unsigned long long step = p.ctrl[0];
   const int m0 = 16 * MT * wave;   // this wave's hidden units in both hidden layers
+  // debug stamps outside the chunk loop: row (chunks of this workgroup) of the stamp array, slots 8..12
+  const int nmy = (p.E / C - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+#define STW_STAMPX(I) \
+  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[nmy * 16 + 8 + (I)] = __builtin_amdgcn_s_memtime();
+  STW_STAMPX(0);
 
   // ---------------------------------------------------------------- weights (once per launch)
   // W0^T rows m0 + 16i + l16 -> MT x KS0 A fragments in VGPRs (global dwordx4; the 57 KB image is
@@ -277,10 +292,20 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     wl = pl_[-1];                                                          \
     wv = pl_[0];                                                           \
   }
+// next chunk's price windows + the env state of the one after (PF_LATE: issued at the start of the
+// weight-gradient phase, so the window registers are live only from there to the next gather)
+#define STW_PREFETCH_NEXT()                                                \
+  {                                                                        \
+    const int nxt = chunk + gridDim.x;                                     \
+    STW_LOAD_PRICES(nxt, eB_pos)                                           \
+    eA_pos = eB_pos; eA_b = eB_b; eA_sh = eB_sh; eA_val = eB_val; eA_rs = eB_rs; eA_ep = eB_ep; \
+    STW_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep) \
+  }
   STW_LOAD_ENV(blockIdx.x, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
   STW_LOAD_PRICES(blockIdx.x, eA_pos)
   STW_LOAD_ENV(blockIdx.x + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
   __syncthreads();
+  STW_STAMPX(1);
 
   for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     STW_STAMP(0);
@@ -313,15 +338,19 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
       for (int rr = 0; rr < RPW; ++rr) {
         const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_inv), rr));
         const float invn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r_invn), rr));
-        const float win[5] = {w[rr].x, w[rr].y, w[rr].z, w[rr].w, dpp_next_lane(w[rr].x)};
-        float xv[4], xnv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          xv[j] = isp[j] ? feat_price(win[j], inv, FEAT) : 0.f;
-          xnv[j] = isp[j] ? feat_price(win[j + 1], invn, FEAT) : 0.f;
+        const float w4 = dpp_next_lane(w[rr].x);
+        // packed fp32 (v_pk_mul_f32 / v_pk_add_f32): same IEEE rounding as feat_price, half the VALU ops
+        f32x2_t x01 = {w[rr].x, w[rr].y}, x23 = {w[rr].z, w[rr].w};
+        f32x2_t n01 = {w[rr].y, w[rr].z}, n23 = {w[rr].w, w4};
+        if (FEAT) {
+          const f32x2_t iv = {inv, inv}, ivn = {invn, invn}, one = {1.0f, 1.0f};
+          x01 = x01 * iv - one; x23 = x23 * iv - one;
+          n01 = n01 * ivn - one; n23 = n23 * ivn - one;
         }
-        lds_st4(px + rr * G::SX, xv[0], xv[1], xv[2], xv[3]);
-        lds_st4(pxn + rr * G::SX, xnv[0], xnv[1], xnv[2], xnv[3]);
+        lds_st4(px + rr * G::SX, isp[0] ? x01.x : 0.f, isp[1] ? x01.y : 0.f, isp[2] ? x23.x : 0.f,
+                isp[3] ? x23.y : 0.f);
+        lds_st4(pxn + rr * G::SX, isp[0] ? n01.x : 0.f, isp[1] ? n01.y : 0.f, isp[2] ? n23.x : 0.f,
+                isp[3] ? n23.y : 0.f);
       }
     }
     if (lane < RPW) {   // x tail: (budget, shares, 1) features (same wave, after its row stores)
@@ -330,12 +359,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
       xt[1] = f2bf(feat_shares(eA_sh, wl, p.inv_b0, FEAT));
       xt[2] = f2bf(1.0f);
     }
-    {
-      const int nxt = chunk + gridDim.x;
-      STW_LOAD_PRICES(nxt, eB_pos)
-      eA_pos = eB_pos; eA_b = eB_b; eA_sh = eB_sh; eA_val = eB_val; eA_rs = eB_rs; eA_ep = eB_ep;
-      STW_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
-    }
+    if constexpr (!PF_LATE) STW_PREFETCH_NEXT();
     __syncthreads();
     STW_STAMP(1);
     // ------------------------------------------------------------ P1-P2: hidden layers of Q(x)
@@ -474,6 +498,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     __syncthreads();
     STW_STAMP(6);
     // ------------------------------------------------------------ P9: weight gradients (sum over the chunk's envs)
+    if constexpr (PF_LATE) STW_PREFETCH_NEXT();
 #pragma unroll
     for (int ks = 0; ks < C / 32; ++ks) {
       const int k0 = 32 * ks;
@@ -511,8 +536,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   }
 #undef STW_LOAD_ENV
 #undef STW_LOAD_PRICES
+#undef STW_PREFETCH_NEXT
 #undef STW_STAMP
 
+  STW_STAMPX(2);
   // ---------------------------------------------------------------- gradient slab write-out
   float* sl = p.slab + (size_t)blockIdx.x * p.P;
 #pragma unroll
@@ -536,6 +563,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) sl[p.off_b2 + 4 * g4 + j] = gB2[j];
 
+  STW_STAMPX(3);
   if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;  // 1-based update count for the optimizer
   // ---------------------------------------------------------------- per-workgroup stats (waves -> LDS -> slab)
   {
@@ -553,6 +581,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     for (int k = 0; k < NW; ++k) t += sQ[k * NSTAT + tid];
     p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
   }
+  STW_STAMPX(4);
+#undef STW_STAMPX
 }
 
 template <int INP, int H1P, int H2P, int FEAT>
@@ -569,23 +599,23 @@ static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
   return hipGetLastError();
 }
 
-}  // namespace wide
+}  // namespace ST_WIDE_NS
 }  // namespace st
 
-extern "C" int st_qstep_wide_lds_bytes(int inp, int h1p, int h2p) {
-  if (inp == 224 && h1p == 128 && h2p == 128) return st::wide::Geo<224, 128, 128>::BYTES;
+extern "C" int ST_WIDE_API(st_qstep_wide_lds_bytes)(int inp, int h1p, int h2p) {
+  if (inp == 224 && h1p == 128 && h2p == 128) return st::ST_WIDE_NS::Geo<224, 128, 128>::BYTES;
   return -1;
 }
 
 // Preconditions (checked here and by the host, sharetrade/trainer/engine.py): E % 64 == 0,
 // 1 <= grid <= E / 64, H + 3 <= inp - 16, 8-element aligned weight offsets (16-byte fragment loads).
-extern "C" hipError_t st_qstep_wide_launch(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
+extern "C" hipError_t ST_WIDE_API(st_qstep_wide_launch)(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
                                            hipStream_t stream) {
-  if (p->E % st::wide::C != 0 || grid < 1 || grid > p->E / st::wide::C) return hipErrorInvalidValue;
+  if (p->E % st::ST_WIDE_NS::C != 0 || grid < 1 || grid > p->E / st::ST_WIDE_NS::C) return hipErrorInvalidValue;
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->H + 3 > inp - 16) return hipErrorInvalidValue;
   if (inp == 224 && h1p == 128 && h2p == 128)
-    return p->feat_mode ? st::wide::launch_f<224, 128, 128, 1>(*p, grid, stream)
-                        : st::wide::launch_f<224, 128, 128, 0>(*p, grid, stream);
+    return p->feat_mode ? st::ST_WIDE_NS::launch_f<224, 128, 128, 1>(*p, grid, stream)
+                        : st::ST_WIDE_NS::launch_f<224, 128, 128, 0>(*p, grid, stream);
   return hipErrorInvalidValue;
 }

@@ -141,6 +141,7 @@ class EngineConfig:
     # envs per LDS chunk of the fused bf16 step kernel: 0 = auto (64 when E % 64 == 0, else 32);
     # 64 = csrc/qstep_wide.hip (layer-1 weights in VGPRs), 32 = csrc/qstep_fused.hip (weights in LDS)
     chunk: int = 0
+    step_waves: int = 8             # 64-env-chunk kernel: 8 waves (two per SIMD, measured fastest) or 4
     graph: bool = True              # capture the step in a HIP graph
     backend: str = "auto"           # auto | native | torch
     bucket_mb: float = 4.0          # DP gradient all-reduce bucket (one call below this size)

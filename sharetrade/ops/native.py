@@ -78,6 +78,8 @@ def lib() -> C.CDLL:
     L.st_qstep_wide_launch.restype = C.c_int
     L.st_qstep_wide_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
     L.st_qstep_wide_lds_bytes.restype = C.c_int
+    L.st_qstep_wide_launch_w8.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_qstep_wide_launch_w8.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
     L.st_reduce_optim.restype = C.c_int
     L.st_advance.argtypes = [C.c_void_p, C.c_void_p]

@@ -120,6 +120,8 @@ class VectorEngine:
             if want == 64 and not wide_ok:
                 raise NotImplementedError(f"engine.chunk=64 needs E % 64 == 0 and padded dims (224, 128, 128); "
                                           f"got E={self.E}, dims {L.pdims}")
+            if cfg.engine.step_waves not in (4, 8):
+                raise ValueError(f"engine.step_waves must be 4 or 8, got {cfg.engine.step_waves}")
             if want not in (0, 32, 64):
                 raise ValueError(f"engine.chunk must be 0 (auto), 32 or 64, got {want}")
             self.chunk = 64 if (want in (0, 64) and wide_ok) else 32
@@ -259,7 +261,10 @@ class VectorEngine:
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
 
     def _launch_qstep(self, L, sh) -> None:
-        fn = L.st_qstep_wide_launch if self.chunk == 64 else L.st_qstep_launch
+        if self.chunk == 64:
+            fn = L.st_qstep_wide_launch_w8 if self.cfg.engine.step_waves == 8 else L.st_qstep_wide_launch
+        else:
+            fn = L.st_qstep_launch
         d = self.layout.pdims
         native.check(fn(self._qp, d[0], d[1], d[2], self.grid, sh), f"qstep(chunk={self.chunk})")
 

@@ -94,8 +94,9 @@ def test_qstep_matches_oracle(native_built, compat, E):
     assert _rel(grad, g32) < 0.1
 
 
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("compat", [False, True])
-def test_wide_and_narrow_kernels_agree(native_built, compat):
+def test_wide_and_narrow_kernels_agree(native_built, compat, waves):
     """csrc/qstep_wide.hip (64-env chunks) vs csrc/qstep_fused.hip (32-env chunks) on the same state:
     identical env transitions, gradients equal up to fp32 summation order."""
     from sharetrade.trainer.engine import VectorEngine
@@ -108,6 +109,7 @@ def test_wide_and_narrow_kernels_agree(native_built, compat):
         cfg = _cfg(compat)
         cfg.agent.epsilon = 0.5
         cfg.engine.chunk = chunk
+        cfg.engine.step_waves = waves
         eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
         assert eng.chunk == chunk
         eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)

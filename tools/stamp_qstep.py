@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--out", default="")
     ap.add_argument("--chunk", type=int, default=0, help="0 = engine default, 32 or 64")
+    ap.add_argument("--waves", type=int, default=8, help="64-env-chunk kernel: 4 or 8 waves")
     a = ap.parse_args()
     import build
 
@@ -33,6 +34,7 @@ def main():
 
     cfg = preset_config("flagship")
     cfg.engine.chunk = a.chunk
+    cfg.engine.step_waves = a.waves
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=a.envs)
     eng.run(3)
@@ -57,7 +59,12 @@ def main():
     for n, v in rows:
         lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
     lines.append(f"| chunk loop (stamp0->stamp0) | {loop:.0f} | |")
-    if eng.chunk != 32:   # the P0 sub-stamps exist in the 32-env kernel only
+    if eng.chunk != 32:   # the P0 sub-stamps exist in the 32-env kernel only; it stamps prologue / epilogue
+        x = st.cpu().view(-1, 16)[iters, 8:13].double()
+        lines.append(f"| prologue (W0 fragments, W1/W2 -> LDS, first gather) | {float(x[1] - x[0]):.0f} | |")
+        lines.append(f"| chunk loop, all chunks | {float(x[2] - x[1]):.0f} | |")
+        lines.append(f"| gradient slab write-out | {float(x[3] - x[2]):.0f} | |")
+        lines.append(f"| stats + exit | {float(x[4] - x[3]):.0f} | |")
         txt = "\n".join(lines) + "\n"
         print(txt)
         if a.out:
