@@ -45,6 +45,7 @@ def main() -> int:
                     help="all ranks on cuda:0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
     ap.add_argument("--step-waves", type=int, default=8, help="64-env-chunk kernel: waves per workgroup (4 or 8)")
+    ap.add_argument("--step-variant", default="", help="tuning build of the 64-env-chunk kernel (suffix)")
     ap.add_argument("--chunk", type=int, default=0,
                     help="envs per chunk of the fused step kernel: 0 = auto (64 when envs %% 64 == 0), 32, 64")
     ap.add_argument("--sync-dp", action="store_true",
@@ -85,6 +86,7 @@ def main() -> int:
     cfg.engine.dp_overlap = not args.sync_dp
     cfg.engine.chunk = args.chunk
     cfg.engine.step_waves = args.step_waves
+    cfg.engine.step_variant = args.step_variant
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 

@@ -30,105 +30,156 @@ struct OptimParams {
   int nstat;
   float lr, beta1, beta2, eps, scale;
   int tdelay;              // updates lagging the step counter (overlapped DP applies step t-1's gradient at t)
+  int slab_bf16;           // slabs are bf16, column-blocked [ceil(P/128)][G][128] (P % 8 == 0), else fp32 [G][P]
 };
 
-constexpr int RT = 256;   // threads per workgroup
-constexpr int CW = 16;    // float4 columns per workgroup (256 B of every slab row)
-constexpr int RG = RT / CW;  // row groups per workgroup: 16 independent partial sums per column
+constexpr int CW = 16;    // 16-byte slab columns per workgroup (256 B of every slab row)
+constexpr int SLAB_BLK = 128;   // bf16 slabs: parameters per column block (= CW x 8)
 
+// NV parameters per thread column: 4 (fp32 slabs [G][P], one float4 per row) or 8 (bf16 slabs: the
+// step kernel rounds each workgroup's fp32 partial sum once and stores it column-BLOCKED,
+// [P/128][G][128], so this workgroup's 128 columns of all G rows are one contiguous 64 KB run
+// instead of G strided 256-byte pieces; 8 bf16 = one 16-byte load per row).  The sums are fp32.
+// tools/ubench/slab_reduce.hip measured the layouts / shapes (profiles/r1_slab_reduce.md).
+template <int NV, int RT>
 __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
-  __shared__ float4 part[RG][CW];
+  constexpr int NQ = NV / 4;   // float4 groups per thread column
+  constexpr int RG = RT / CW;  // row groups per workgroup: independent partial sums per column
+  __shared__ float4 part[RG][CW][NQ];
   const int tid = threadIdx.x, rg = tid / CW, c = tid % CW;
-  const int col4 = blockIdx.x * CW + c;  // float4 column index
-  const int P4 = p.P >> 2;
-  if (p.mode != 2 && p.stats && blockIdx.x == gridDim.x - 1) {
-    // step statistics folded into this pass (no extra launches): 32 row groups x 8 stats
-    __shared__ double sred[RT / 8][8];
-    const int j = tid & 7, grp = tid >> 3;
+  const int colv = blockIdx.x * CW + c;  // NV-parameter column index
+  const int PV = p.P / NV;
+  if (p.mode != 2 && p.stats && blockIdx.x == 0) {
+    // step statistics folded into this pass (no extra launches; block 0 is dispatched first): thread t
+    // sums stat (t & 7) over rows t/8, t/8 + RT/8, ...; then a shuffle fold over the 8 lanes of a
+    // wave that share the stat, and one LDS slot per wave (all in fp64)
+    __shared__ double sred[RT / 64][8];
+    const int j = tid & 7, grp = tid >> 3, lane = tid & 63, w = tid >> 6;
     double acc = 0.0;
     if (j < p.nstat)
       for (int r = grp; r < p.G; r += RT / 8) acc += (double)p.stats[r * p.nstat + j];
-    sred[grp][j] = acc;
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane < 8) sred[w][lane] = acc;
     __syncthreads();
     if (tid < p.nstat) {
       double t = 0.0;
-      for (int k = 0; k < RT / 8; ++k) t += sred[k][tid];
+#pragma unroll
+      for (int k = 0; k < RT / 64; ++k) t += sred[k][tid];
       p.stat_acc[tid] += t;
     }
   }
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the updating lanes (row group 0) fetch their optimizer operands BEFORE the slab pass, so their
+  // latency hides under it instead of trailing the reduction
+  const bool upd = p.mode != 1 && rg == 0 && colv < PV;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 w4[NQ], m4[NQ], s1v[NQ], s2v[NQ], g[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    w4[q] = m4[q] = s1v[q] = s2v[q] = g[q] = z4;
+    if (upd) {
+      const int col4 = colv * NQ + q;
+      w4[q] = reinterpret_cast<const float4*>(p.params)[col4];
+      m4[q] = reinterpret_cast<const float4*>(p.mask)[col4];
+      if (p.kind >= 1) s1v[q] = reinterpret_cast<const float4*>(p.s1)[col4];
+      if (p.kind == 2) s2v[q] = reinterpret_cast<const float4*>(p.s2)[col4];
+    }
+  }
   if (p.mode != 2) {
-    if (col4 < P4) {
-      const float4* s = reinterpret_cast<const float4*>(p.slab) + col4;
+    if (colv < PV) {
+      if constexpr (NV == 4) {
+        const float4* sp = reinterpret_cast<const float4*>(p.slab) + colv;
 #pragma unroll 8
-      for (int r = rg; r < p.G; r += RG) {
-        const float4 v = s[(size_t)r * P4];
-        g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+        for (int r = rg; r < p.G; r += RG) {
+          const float4 v = sp[(size_t)r * PV];
+          g[0].x += v.x; g[0].y += v.y; g[0].z += v.z; g[0].w += v.w;
+        }
+      } else {
+        const uint4* sp = reinterpret_cast<const uint4*>(p.slab) + (size_t)blockIdx.x * p.G * CW + c;
+#pragma unroll 8
+        for (int r = rg; r < p.G; r += RG) {
+          const uint4 v = sp[(size_t)r * CW];
+          g[0].x += __uint_as_float(v.x << 16); g[0].y += __uint_as_float(v.x & 0xFFFF0000u);
+          g[0].z += __uint_as_float(v.y << 16); g[0].w += __uint_as_float(v.y & 0xFFFF0000u);
+          g[1].x += __uint_as_float(v.z << 16); g[1].y += __uint_as_float(v.z & 0xFFFF0000u);
+          g[1].z += __uint_as_float(v.w << 16); g[1].w += __uint_as_float(v.w & 0xFFFF0000u);
+        }
       }
     }
-    part[rg][c] = g;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) part[rg][c][q] = g[q];
     __syncthreads();
     if (rg != 0) return;
-    for (int k = 1; k < RG; ++k) {
-      const float4 v = part[k][c];
-      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
-    }
-    g.x *= p.scale; g.y *= p.scale; g.z *= p.scale; g.w *= p.scale;
+    for (int k = 1; k < RG; ++k)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const float4 v = part[k][c][q];
+        g[q].x += v.x; g[q].y += v.y; g[q].z += v.z; g[q].w += v.w;
+      }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) { g[q].x *= p.scale; g[q].y *= p.scale; g[q].z *= p.scale; g[q].w *= p.scale; }
     if (p.mode == 1) {
-      if (col4 < P4) reinterpret_cast<float4*>(p.grad)[col4] = g;
+      if (colv < PV)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) reinterpret_cast<float4*>(p.grad)[colv * NQ + q] = g[q];
       return;
     }
   } else {
     if (rg != 0) return;
-    if (col4 < P4) {
-      g = reinterpret_cast<const float4*>(p.grad)[col4];
-      g.x *= p.scale; g.y *= p.scale; g.z *= p.scale; g.w *= p.scale;
-    }
+    if (colv < PV)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float4 v = reinterpret_cast<const float4*>(p.grad)[colv * NQ + q];
+        v.x *= p.scale; v.y *= p.scale; v.z *= p.scale; v.w *= p.scale;
+        g[q] = v;
+      }
   }
   const unsigned long long tstep = p.ctrl[1];
   if (blockIdx.x == 0 && tid == 0) p.ctrl[0] = tstep;  // next step index (read by the next step kernel)
   const unsigned long long t = tstep - (unsigned long long)p.tdelay;   // 1-based optimizer update count
-  if (col4 >= P4) return;
-  float gg[4] = {g.x, g.y, g.z, g.w};
-  const float4 m4 = reinterpret_cast<const float4*>(p.mask)[col4];
-  const float mm[4] = {m4.x, m4.y, m4.z, m4.w};
-  float4 w4 = reinterpret_cast<float4*>(p.params)[col4];
-  float w[4] = {w4.x, w4.y, w4.z, w4.w};
-  if (p.kind == 1) {  // AdaGrad (TF ApplyAdagrad)
-    float4 a4 = reinterpret_cast<float4*>(p.s1)[col4];
-    float a[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = gg[k] * mm[k];
-      a[k] += gk * gk;
-      w[k] -= p.lr * gk * rsqrtf(a[k]);
-    }
-    reinterpret_cast<float4*>(p.s1)[col4] = make_float4(a[0], a[1], a[2], a[3]);
-  } else if (p.kind == 2) {  // Adam
-    const float c1 = 1.f - powf(p.beta1, (float)t), c2 = 1.f - powf(p.beta2, (float)t);
-    const float ic1 = 1.f / c1, ic2 = 1.f / c2;
-    float4 m4v = reinterpret_cast<float4*>(p.s1)[col4];
-    float4 v4v = reinterpret_cast<float4*>(p.s2)[col4];
-    float m[4] = {m4v.x, m4v.y, m4v.z, m4v.w}, v[4] = {v4v.x, v4v.y, v4v.z, v4v.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = gg[k] * mm[k];
-      m[k] = p.beta1 * m[k] + (1.f - p.beta1) * gk;
-      v[k] = p.beta2 * v[k] + (1.f - p.beta2) * gk * gk;
-      w[k] -= p.lr * (m[k] * ic1) / (sqrtf(v[k] * ic2) + p.eps) * mm[k];
-    }
-    reinterpret_cast<float4*>(p.s1)[col4] = make_float4(m[0], m[1], m[2], m[3]);
-    reinterpret_cast<float4*>(p.s2)[col4] = make_float4(v[0], v[1], v[2], v[3]);
-  } else {  // SGD
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] -= p.lr * gg[k] * mm[k];
+  if (colv >= PV) return;
+  float ic1 = 1.f, ic2 = 1.f;
+  if (p.kind == 2) {
+    ic1 = 1.f / (1.f - powf(p.beta1, (float)t));
+    ic2 = 1.f / (1.f - powf(p.beta2, (float)t));
   }
-  reinterpret_cast<float4*>(p.params)[col4] = make_float4(w[0], w[1], w[2], w[3]);
-  if (p.params_bf) {
-    uint2 o;
-    o.x = pack_bf2(w[0], w[1]);
-    o.y = pack_bf2(w[2], w[3]);
-    reinterpret_cast<uint2*>(p.params_bf)[col4] = o;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int col4 = colv * NQ + q;
+    const float gg[4] = {g[q].x, g[q].y, g[q].z, g[q].w};
+    const float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
+    float w[4] = {w4[q].x, w4[q].y, w4[q].z, w4[q].w};
+    if (p.kind == 1) {  // AdaGrad (TF ApplyAdagrad)
+      float a[4] = {s1v[q].x, s1v[q].y, s1v[q].z, s1v[q].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gk = gg[k] * mm[k];
+        a[k] += gk * gk;
+        w[k] -= p.lr * gk * rsqrtf(a[k]);
+      }
+      reinterpret_cast<float4*>(p.s1)[col4] = make_float4(a[0], a[1], a[2], a[3]);
+    } else if (p.kind == 2) {  // Adam
+      float m[4] = {s1v[q].x, s1v[q].y, s1v[q].z, s1v[q].w}, v[4] = {s2v[q].x, s2v[q].y, s2v[q].z, s2v[q].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gk = gg[k] * mm[k];
+        m[k] = p.beta1 * m[k] + (1.f - p.beta1) * gk;
+        v[k] = p.beta2 * v[k] + (1.f - p.beta2) * gk * gk;
+        w[k] -= p.lr * (m[k] * ic1) / (sqrtf(v[k] * ic2) + p.eps) * mm[k];
+      }
+      reinterpret_cast<float4*>(p.s1)[col4] = make_float4(m[0], m[1], m[2], m[3]);
+      reinterpret_cast<float4*>(p.s2)[col4] = make_float4(v[0], v[1], v[2], v[3]);
+    } else {  // SGD
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] -= p.lr * gg[k] * mm[k];
+    }
+    reinterpret_cast<float4*>(p.params)[col4] = make_float4(w[0], w[1], w[2], w[3]);
+    if (p.params_bf) {
+      uint2 o;
+      o.x = pack_bf2(w[0], w[1]);
+      o.y = pack_bf2(w[2], w[3]);
+      reinterpret_cast<uint2*>(p.params_bf)[col4] = o;
+    }
   }
 }
 
@@ -145,9 +196,16 @@ __global__ void to_bf16_kernel(const float* __restrict__ in, bf16_t* __restrict_
 }  // namespace st
 
 extern "C" hipError_t st_reduce_optim(const st::OptimParams* p, hipStream_t stream) {
-  const int P4 = p->P >> 2;
-  const int grid = (P4 + st::CW - 1) / st::CW;   // ~740 workgroups for the 2x128 net: fills 256 CUs
-  hipLaunchKernelGGL(st::reduce_optim_kernel, dim3(grid), dim3(st::RT), 0, stream, *p);
+  if (p->stats && (p->nstat < 1 || p->nstat > 8)) return hipErrorInvalidValue;
+  if (p->slab_bf16 && p->mode != 2) {
+    if (p->P % 8 != 0) return hipErrorInvalidValue;
+    const int grid = (p->P + st::SLAB_BLK - 1) / st::SLAB_BLK;   // one 128-column block each
+    hipLaunchKernelGGL((st::reduce_optim_kernel<8, 512>), dim3(grid), dim3(512), 0, stream, *p);
+  } else {
+    if (p->P % 4 != 0) return hipErrorInvalidValue;
+    const int grid = (p->P / 4 + st::CW - 1) / st::CW;   // ~740 workgroups for the 2x128 net: fills 256 CUs
+    hipLaunchKernelGGL((st::reduce_optim_kernel<4, 256>), dim3(grid), dim3(256), 0, stream, *p);
+  }
   return hipGetLastError();
 }
 

@@ -27,6 +27,9 @@ struct QStepParams {
   uint32_t key0, key1;
   int env_offset;
   unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][16]) or null
+  int slab_bf16;            // slabs written as bf16, column-blocked [ceil(P/128)][slab_rows][128]
+                            // (64-env-chunk kernel only; csrc/optim.hip reads them)
+  int slab_rows;            // G: workgroups of the launch (= slab rows)
 };
 
 // rows of QStepParams::env
@@ -49,6 +52,30 @@ ST_DEV s8v frag_tr(const bf16_t* img, int S, int k0, int c0, int l16, int g4) {
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
+}
+
+// frag_tr with the k (row) order permuted for bank-conflict-free reads: lane (g4, l16) element j =
+// img[k0 + 4*g4 + j][c0 + l16] for j < 4 and img[k0 + 16 + 4*g4 + j - 4][c0 + l16] for j >= 4, so
+// each ds_read_b64_tr_b16 lane group of 32 reads 8 consecutive rows (one 8-dword bank window per row
+// when the row stride is an odd multiple of 8 dwords: 144 / 240 bf16).  Valid wherever BOTH operands
+// of the MFMA are read with it (k runs over a sum index, e.g. envs in a weight gradient).
+ST_DEV s8v frag_trp(const bf16_t* img, int S, int k0, int c0, int l16, int g4) {
+  const bf16_t* p = img + (k0 + 4 * g4 + (l16 >> 2)) * S + c0 + 4 * (l16 & 3);
+  s4v lo = lds_tr4(p);
+  s4v hi = lds_tr4(p + 16 * S);
+  s8v r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// inclusive sum over each 16-lane DPP row (lane 15 of a row holds the row total): 4 row_shr adds
+ST_DEV float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x111, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x112, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x114, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x118, 0xF, 0xF, true));
+  return v;
 }
 
 // value of lane+1 (lane 63 gets 0): DPP wave_shl:1 — one VALU op instead of a ds_bpermute

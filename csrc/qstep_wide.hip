@@ -44,6 +44,15 @@ constexpr int RPW = C / NW;    // gather rows per wave
 #define ST_WIDE_PF_LATE 1
 #endif
 constexpr bool PF_LATE = ST_WIDE_PF_LATE;
+#ifndef ST_WIDE_PF_AFTER_DW0
+#define ST_WIDE_PF_AFTER_DW0 0
+#endif
+#ifndef ST_WIDE_GTILE
+#define ST_WIDE_GTILE 0
+#endif
+#ifndef ST_WIDE_STATW
+#define ST_WIDE_STATW 1
+#endif
 constexpr int SQ = OUTP + 8;
 constexpr int ENVF = 6;        // fp32 words per env in sEnv
 static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w < NET");
@@ -67,7 +76,8 @@ struct Geo {
   static constexpr int fENVI = fENV + C * ENVF * 4;  // [C][4] ints
   static constexpr int fB1 = fENVI + C * 4 * 4;      // b1 [H2P]
   static constexpr int fB2 = fB1 + H2P * 4;          // b2 [16]
-  static constexpr int BYTES = fB2 + OUTP * 4;
+  static constexpr int fST = fB2 + OUTP * 4;          // step statistics [NSTAT] fp32 (end of launch)
+  static constexpr int BYTES = fST + NSTAT * 4;
   static_assert(BYTES <= 163840, "LDS budget exceeded");
   static_assert(H1P % (16 * NW) == 0 && H2P % (16 * NW) == 0 && H1P == H2P, "m-tiles per wave");
   static_assert(INP % 32 == 0 && H1P % 32 == 0, "padding");
@@ -192,6 +202,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   int* sEnvI = reinterpret_cast<int*>(smem + G::fENVI);
   float* sB1 = reinterpret_cast<float*>(smem + G::fB1);
   float* sB2 = reinterpret_cast<float*>(smem + G::fB2);
+  float* sSt = reinterpret_cast<float*>(smem + G::fST);
 
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -230,25 +241,49 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   }
 
   // ---------------------------------------------------------------- gradient accumulators
-  constexpr int NT0 = G::NT0, NT1 = G::NT1;
-  f4v gW0[MT][NT0];
-  f4v gW1[MT][NT1];
-  f4v gB1[MT], gW2[MT];
+  // Weight-gradient tiling (independent of the forward split): wave w owns GA0 row tiles (h1) x B0
+  // column tiles of dW0^T and GA1 x B1 of dW1^T.  ST_WIDE_GTILE=1 splits dW0 of the 8-wave build in 2
+  // column groups (a 2x7 block: 9 fragment reads per k-step instead of 1+13): P9 drops ~15 %, but the
+  // extra live registers slow P3 / P6 and the whole step measured 2-3 % slower
+  // (profiles/r1_wide_step_variants.md), so the default is the 1x13 strip.
+  constexpr int GA0 = ST_WIDE_GTILE ? 2 : G::MT;       // dW0 row tiles per wave
+  constexpr int GC0 = NW / (H1P / 16 / GA0);           // dW0 column groups
+  constexpr int GA1 = (NW >= 8) ? 1 : 2;               // dW1 row tiles per wave (registers: 8 waves)
+  constexpr int GC1 = NW / (H2P / 16 / GA1);
+  static_assert(GC0 >= 1 && (H1P / 16 / GA0) * GC0 == NW && (H2P / 16 / GA1) * GC1 == NW, "gradient tiling");
+  static_assert(GC0 == 1 || (INP / 16) % GC0 == 0, "dW0 column groups");
+  constexpr int B0 = (GC0 == 1) ? G::NT0 : (INP / 16) / GC0;
+  constexpr int B1 = (H1P / 16) / GC1;
+  const int ghb0 = GA0 * (wave / GC0), gcg0 = wave % GC0;   // row-tile base, column group
+  const int ghb1 = GA1 * (wave / GC1), gcg1 = wave % GC1;
+  f4v gW0[GA0][B0];
+  f4v gW1[GA1][B1];
+  f4v gB1[GA1], gW2[MT];
   f4v gB2 = zero4();
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
+  for (int i = 0; i < GA0; ++i)
 #pragma unroll
-    for (int n = 0; n < NT0; ++n) gW0[i][n] = zero4();
+    for (int n = 0; n < B0; ++n) gW0[i][n] = zero4();
 #pragma unroll
-    for (int n = 0; n < NT1; ++n) gW1[i][n] = zero4();
+  for (int i = 0; i < GA1; ++i) {
+#pragma unroll
+    for (int n = 0; n < B1; ++n) gW1[i][n] = zero4();
     gB1[i] = zero4();
-    gW2[i] = zero4();
   }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) gW2[i] = zero4();
   // ones fragment for bias gradients: B[k][n] = (n == 0)
   s8v ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (l16 == 0) ? (short)0x3F80 : (short)0;
 
+  // step statistics.  8-wave build (STATW): the Q-holding lanes (waves < NET) leave their per-env
+  // values in LDS at the end of P6 and the waves that idle through P3 / P6 (NET..2*NET-1) fold them
+  // into two lane accumulators at the start of P7 -- 2 live registers instead of 7 (those were the
+  // spill victims of the 256-register build) and no reduction work on the P6 critical path.
+  // 4-wave build: per-lane accumulators in the Q-holding lanes (512 registers).
+  constexpr bool STATW = ST_WIDE_STATW && NW >= 2 * NET;
+  float sa0 = 0.f, sa1 = 0.f;
   float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
         st_qslot = 0.f;
 
@@ -412,12 +447,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         sEnv[r * ENVF + 3] = b2;
         sEnv[r * ENVF + 4] = rew;
         sEnvI[r * 4 + 1] = s2;
-        sEnvI[r * 4 + 2] = a;
+        sEnvI[r * 4 + 2] = STATW ? (a | (exploit ? 0 : 4)) : a;   // (8-wave: explore flag in bit 2)
         bf16_t* xn = sR0 + r * G::SX;
         xn[H] = f2bf(feat_budget(b2, p.inv_b0, FEAT));
         xn[H + 1] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
         xn[H + 2] = f2bf(1.0f);
-        st_explore += exploit ? 0.f : 1.f;
+        if constexpr (!STATW) st_explore += exploit ? 0.f : 1.f;
         ENV_I(ER_ACTION, e) = a;
         ENV_F(ER_REWARD, e) = rew;
       }
@@ -445,7 +480,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         float mx = n[0];
         if (n[1] > mx) { mx = n[1]; am = 1; }
         if (n[2] > mx) { mx = n[2]; am = 2; }
-        const int a = sEnvI[r * 4 + 2];
+        const int araw = sEnvI[r * 4 + 2], a = araw & 3;
         const float rew = sEnv[r * ENVF + 4];
         const int slot = p.target_compat ? am : a;
         const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
@@ -454,20 +489,17 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         float dq = p.loss_coef * diff;
         if (p.output_relu && !(qs > 0.f)) dq = 0.f;
         // dQ row: one nonzero at `slot`, written as two 16-byte stores
+        // (slot < 3: only the first two words can be nonzero)
         const uint32_t dqb = (uint32_t)f2bf(dq);
-        uint32_t wd[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) wd[k] = (slot == 2 * k) ? dqb : (slot == 2 * k + 1) ? (dqb << 16) : 0u;
+        const uint32_t wd0 = (slot == 0) ? dqb : (slot == 1) ? (dqb << 16) : 0u, wd1 = (slot == 2) ? dqb : 0u;
         uint4* dqr = reinterpret_cast<uint4*>(sDQ + r * SQ);
-        dqr[0] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-        dqr[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
-        st_loss += diff * diff;
-        st_reward += rew;
-        st_qslot += qs;
+        dqr[0] = make_uint4(wd0, wd1, 0u, 0u);
+        dqr[1] = make_uint4(0u, 0u, 0u, 0u);
         const float b2 = sEnv[r * ENVF + 3], vnew = sEnv[r * ENVF + 2];
         const int s2 = sEnvI[r * 4 + 1];
         const int np = sEnvI[r * 4 + 0] + 1;
         const float rs = sEnv[r * ENVF + 5] + rew;
+        float fdone = 0.f, ndone = 0.f;
         if (np >= p.T - H) {
           const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
           ENV_F(ER_LAST_FINAL, e) = fin;
@@ -477,9 +509,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
           ENV_F(ER_VALUE, e) = 0.f;
           ENV_I(ER_POS, e) = 0;
           ENV_F(ER_RET_SUM, e) = 0.f;
-          st_done += 1.f;
-          st_fsum += fin;
-          st_fsq += fin * fin;
+          fdone = fin;
+          ndone = 1.f;
         } else {
           ENV_F(ER_BUDGET, e) = b2;
           ENV_I(ER_SHARES, e) = s2;
@@ -487,47 +518,84 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
           ENV_I(ER_POS, e) = np;
           ENV_F(ER_RET_SUM, e) = rs;
         }
+        if constexpr (STATW) {
+          // per-env stats for the idle waves (sQ / sEnv[0..1] are dead until the next chunk's P0 / P3)
+          sQ[r * 4 + 0] = rew;
+          sQ[r * 4 + 1] = diff * diff;
+          sQ[r * 4 + 2] = qs;
+          sQ[r * 4 + 3] = (araw >> 2) ? 1.f : 0.f;
+          sEnv[r * ENVF + 0] = fdone;
+          sEnv[r * ENVF + 1] = ndone;
+        } else {
+          st_reward += rew;
+          st_loss += diff * diff;
+          st_qslot += qs;
+          st_done += ndone;
+          st_fsum += fdone;
+          st_fsq += fdone * fdone;
+        }
       }
     }
     __syncthreads();
     STW_STAMP(5);
     // ------------------------------------------------------------ P7-P8: backward (data)
+    if constexpr (STATW) {
+      // stats fold (lane = env row of the chunk): wave NET: reward, loss; +1: qslot, explore;
+      // +2: final portfolio sum, sum of squares; +3: episodes done
+      // (row index re-derived from tid behind an opaque move: a loop-invariant address kept live
+      // across the chunk would cost a register of the 256-register build)
+      const int sw = wave - NET;
+      int ln = tid;
+      asm volatile("" : "+v"(ln));
+      ln &= 63;
+      if (sw == 0) { sa0 += sQ[ln * 4 + 0]; sa1 += sQ[ln * 4 + 1]; }
+      else if (sw == 1) { sa0 += sQ[ln * 4 + 2]; sa1 += sQ[ln * 4 + 3]; }
+      else if (sw == 2) { const float f = sEnv[ln * ENVF + 0]; sa0 += f; sa1 += f * f; }
+      else if (sw == 3) { sa0 += sEnv[ln * ENVF + 1]; }
+    }
     bwd_data<MT, OUTP, G::SW2, SQ, G::SH2, G::SH2>(sW2, sDQ, sH2, sR0, m0, l16, g4);
     __syncthreads();
     bwd_data<MT, H2P, G::SW1, G::SH2, G::SH1, G::SH1>(sW1, sR0, sH1, sR1, m0, l16, g4);
     __syncthreads();
     STW_STAMP(6);
     // ------------------------------------------------------------ P9: weight gradients (sum over the chunk's envs)
-    if constexpr (PF_LATE) STW_PREFETCH_NEXT();
+    if constexpr (PF_LATE && !ST_WIDE_PF_AFTER_DW0) STW_PREFETCH_NEXT();
 #pragma unroll
     for (int ks = 0; ks < C / 32; ++ks) {
       const int k0 = 32 * ks;
       // dW0^T[h1][in] += dZ1^T . X
-      s8v a1[MT];
+      s8v a1[GA0];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) a1[i] = frag_tr(sR1, G::SH1, k0, m0 + 16 * i, l16, g4);
+      for (int i = 0; i < GA0; ++i) a1[i] = frag_trp(sR1, G::SH1, k0, (ghb0 + i) * 16, l16, g4);
 #pragma unroll
-      for (int n = 0; n < NT0; ++n) {
-        const s8v bx = frag_tr(sX, G::SX, k0, n * 16, l16, g4);
+      for (int n = 0; n < B0; ++n) {
+        const s8v bx = frag_trp(sX, G::SX, k0, (gcg0 * B0 + n) * 16, l16, g4);
 #pragma unroll
-        for (int i = 0; i < MT; ++i) gW0[i][n] = mfma32(a1[i], bx, gW0[i][n]);
+        for (int i = 0; i < GA0; ++i) gW0[i][n] = mfma32(a1[i], bx, gW0[i][n]);
       }
+    }
+    // the next chunk's windows land during the dW1 / dW2 half, the barrier and the next gather's
+    // row-owner work; their registers are not live across the forward / backward / dW0 phases
+    if constexpr (PF_LATE && ST_WIDE_PF_AFTER_DW0) STW_PREFETCH_NEXT();
+#pragma unroll
+    for (int ks = 0; ks < C / 32; ++ks) {
+      const int k0 = 32 * ks;
       // dW1^T[h2][h1] += dZ2^T . H1 ; db1 += dZ2^T . 1
-      s8v a2[MT];
+      s8v a2[GA1];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) a2[i] = frag_tr(sR0, G::SH2, k0, m0 + 16 * i, l16, g4);
+      for (int i = 0; i < GA1; ++i) a2[i] = frag_trp(sR0, G::SH2, k0, (ghb1 + i) * 16, l16, g4);
 #pragma unroll
-      for (int n = 0; n < NT1; ++n) {
-        const s8v bh = frag_tr(sH1, G::SH1, k0, n * 16, l16, g4);
+      for (int n = 0; n < B1; ++n) {
+        const s8v bh = frag_trp(sH1, G::SH1, k0, (gcg1 * B1 + n) * 16, l16, g4);
 #pragma unroll
-        for (int i = 0; i < MT; ++i) gW1[i][n] = mfma32(a2[i], bh, gW1[i][n]);
+        for (int i = 0; i < GA1; ++i) gW1[i][n] = mfma32(a2[i], bh, gW1[i][n]);
       }
 #pragma unroll
-      for (int i = 0; i < MT; ++i) gB1[i] = mfma32(a2[i], ones, gB1[i]);
+      for (int i = 0; i < GA1; ++i) gB1[i] = mfma32(a2[i], ones, gB1[i]);
       // dW2^T[out][h2] += dQ^T . H2 ; db2 += dQ^T . 1
-      const s8v aq = frag_tr(sDQ, SQ, k0, 0, l16, g4);
+      const s8v aq = frag_trp(sDQ, SQ, k0, 0, l16, g4);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, frag_tr(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
+      for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, frag_trp(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
       gB2 = mfma32(aq, ones, gB2);   // every wave (branch-free accumulators); wave 0 writes it
     }
     __syncthreads();
@@ -541,45 +609,79 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 
   STW_STAMPX(2);
   // ---------------------------------------------------------------- gradient slab write-out
-  float* sl = p.slab + (size_t)blockIdx.x * p.P;
+  // (bf16 slabs: each workgroup's fp32 partial is rounded once; csrc/optim.hip sums them in fp32)
+  auto write_slab = [&](auto put) {
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int h = m0 + 16 * i + 4 * g4;
+    for (int i = 0; i < GA0; ++i) {
+      const int h = (ghb0 + i) * 16 + 4 * g4;
 #pragma unroll
-    for (int n = 0; n < NT0; ++n)
+      for (int n = 0; n < B0; ++n)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sl[p.off_w0 + (h + j) * INP + n * 16 + l16] = gW0[i][n][j];
+        for (int j = 0; j < 4; ++j) put(p.off_w0 + (h + j) * INP + (gcg0 * B0 + n) * 16 + l16, gW0[i][n][j]);
+    }
 #pragma unroll
-    for (int n = 0; n < NT1; ++n)
+    for (int i = 0; i < GA1; ++i) {
+      const int h = (ghb1 + i) * 16 + 4 * g4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sl[p.off_w1 + (h + j) * H1P + n * 16 + l16] = gW1[i][n][j];
-    if (l16 == 0)
+      for (int n = 0; n < B1; ++n)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sl[p.off_b1 + h + j] = gB1[i][j];
+        for (int j = 0; j < 4; ++j) put(p.off_w1 + (h + j) * H1P + (gcg1 * B1 + n) * 16 + l16, gW1[i][n][j]);
+      if (gcg1 == 0 && l16 == 0)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sl[p.off_w2 + (4 * g4 + j) * H2P + m0 + 16 * i + l16] = gW2[i][j];
+        for (int j = 0; j < 4; ++j) put(p.off_b1 + h + j, gB1[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) put(p.off_w2 + (4 * g4 + j) * H2P + m0 + 16 * i + l16, gW2[i][j]);
+    if (wave == 0 && l16 == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
+  };
+  if (p.slab_bf16) {
+    // column-blocked [ceil(P/128)][G][128] (csrc/optim.hip reads one contiguous block per workgroup)
+    bf16_t* const sb = reinterpret_cast<bf16_t*>(p.slab) + (size_t)blockIdx.x * 128;
+    const size_t bstride = (size_t)p.slab_rows * 128;
+    write_slab([&](int i, float v) { sb[(size_t)(i >> 7) * bstride + (i & 127)] = f2bf(v); });
+  } else {
+    float* const sf = p.slab + (size_t)blockIdx.x * p.P;
+    write_slab([&](int i, float v) { sf[i] = v; });
   }
-  if (wave == 0 && l16 == 0)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) sl[p.off_b2 + 4 * g4 + j] = gB2[j];
 
   STW_STAMPX(3);
   if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;  // 1-based update count for the optimizer
-  // ---------------------------------------------------------------- per-workgroup stats (waves -> LDS -> slab)
-  {
-    const float v0 = wave_sum(st_reward), v1 = wave_sum(st_loss), v2 = wave_sum(st_explore),
-                v3 = wave_sum(st_done), v4 = wave_sum(st_fsum), v5 = wave_sum(st_fsq), v6 = wave_sum(st_qslot);
-    if (lane == 0) {
-      float* so = sQ + wave * NSTAT;
-      so[0] = v0; so[1] = v1; so[2] = v2; so[3] = v3; so[4] = v4; so[5] = v5; so[6] = v6; so[7] = 0.f;
+  // ---------------------------------------------------------------- per-workgroup stats (-> LDS -> slab)
+  // (the chunk loop ends on a barrier; sSt is outside every chunk buffer)
+  if constexpr (STATW) {
+    const int sw = wave - NET;
+    if (tid < NSTAT) sSt[tid] = 0.f;
+    __syncthreads();
+    if (sw >= 0 && sw < 4) {
+      const float v0 = wave_sum(sa0), v1 = wave_sum(sa1);
+      if (lane == 0) {
+        constexpr int k0[4] = {0, 6, 4, 3}, k1[4] = {1, 2, 5, 7};
+        sSt[k0[sw]] = v0;
+        if (sw < 3) sSt[k1[sw]] = v1;
+      }
     }
-  }
-  __syncthreads();
-  if (tid < NSTAT) {
-    float t = 0.f;
+    __syncthreads();
+    if (tid < NSTAT) p.stats[(size_t)blockIdx.x * NSTAT + tid] = sSt[tid];
+  } else {
+    const float v[NSTAT - 1] = {st_reward, st_loss, st_explore, st_done, st_fsum, st_fsq, st_qslot};
+    float* so = sQ + wave * NSTAT;   // waves -> LDS, then a fixed-order fold (deterministic)
 #pragma unroll
-    for (int k = 0; k < NW; ++k) t += sQ[k * NSTAT + tid];
-    p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
+    for (int k = 0; k < NSTAT - 1; ++k) {
+      const float t = wave_sum(v[k]);
+      if (lane == 0) so[k] = t;
+    }
+    if (lane == 0) so[NSTAT - 1] = 0.f;
+    __syncthreads();
+    if (tid < NSTAT) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) t += sQ[k * NSTAT + tid];
+      p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
+    }
   }
   STW_STAMPX(4);
 #undef STW_STAMPX
@@ -614,6 +716,7 @@ extern "C" hipError_t ST_WIDE_API(st_qstep_wide_launch)(const st::QStepParams* p
   if (p->E % st::ST_WIDE_NS::C != 0 || grid < 1 || grid > p->E / st::ST_WIDE_NS::C) return hipErrorInvalidValue;
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->H + 3 > inp - 16) return hipErrorInvalidValue;
+  if (p->slab_bf16 && (p->slab_rows != grid || p->P % 8 != 0)) return hipErrorInvalidValue;
   if (inp == 224 && h1p == 128 && h2p == 128)
     return p->feat_mode ? st::ST_WIDE_NS::launch_f<224, 128, 128, 1>(*p, grid, stream)
                         : st::ST_WIDE_NS::launch_f<224, 128, 128, 0>(*p, grid, stream);

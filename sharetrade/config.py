@@ -142,10 +142,12 @@ class EngineConfig:
     # 64 = csrc/qstep_wide.hip (layer-1 weights in VGPRs), 32 = csrc/qstep_fused.hip (weights in LDS)
     chunk: int = 0
     step_waves: int = 8             # 64-env-chunk kernel: 8 waves (two per SIMD, measured fastest) or 4
+    step_variant: str = ""          # tuning builds of the 64-env-chunk kernel (st_qstep_wide_launch_<v>); "" = default
     graph: bool = True              # capture the step in a HIP graph
     backend: str = "auto"           # auto | native | torch
     bucket_mb: float = 4.0          # DP gradient all-reduce bucket (one call below this size)
     grad_compress: str = ""         # "" | "bf16" (wire format of the DP all-reduce)
+    slab_dtype: str = "bf16"        # per-workgroup gradient partials of the 64-env-chunk kernel: "bf16" | "fp32"
     # DP gradient all-reduce overlapped with the next step's fused kernel: the gradient of step t
     # is applied after step t+1's kernel (one-step delay, identical on every rank).  The reference
     # applies updates asynchronously through one mailbox; False = strict sync DP (bit-equal to one

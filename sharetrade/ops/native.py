@@ -40,6 +40,7 @@ class QStepParams(C.Structure):
         ("key0", C.c_uint32), ("key1", C.c_uint32),
         ("env_offset", C.c_int),
         ("stamps", C.c_void_p),
+        ("slab_bf16", C.c_int), ("slab_rows", C.c_int),
     ]
 
 
@@ -50,12 +51,20 @@ class OptimParams(C.Structure):
         ("stats", C.c_void_p), ("stat_acc", C.c_void_p),
         ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int), ("nstat", C.c_int),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
-        ("tdelay", C.c_int),
+        ("tdelay", C.c_int), ("slab_bf16", C.c_int),
     ]
 
 
 # rows of QStepParams::env (csrc/qstep_fused.hip EnvRow): int32 / fp32 words
 ENV_ROWS = ("pos", "budget", "shares", "value", "ret_sum", "episodes", "last_final", "actions_out", "rewards_out")
+
+
+def variant_launch(suffix: str):
+    """``st_qstep_wide_launch_<suffix>`` of a tuning build of the 64-env-chunk kernel (same params)."""
+    fn = getattr(lib(), "st_qstep_wide_launch_" + suffix)
+    fn.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    fn.restype = C.c_int
+    return fn
 
 
 def available() -> bool:

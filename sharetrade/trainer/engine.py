@@ -195,7 +195,12 @@ class VectorEngine:
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
         self.grid = max(1, min(props.multi_processor_count, self.E // self.chunk))
-        self.slab = torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev)
+        # per-workgroup gradient partials: bf16 rows for the 64-env-chunk kernel by default (the slab
+        # pass of reduce_optim reads half the bytes; each partial is rounded once, summed in fp32)
+        self.slab_bf16 = (self.chunk == 64 and self.cfg.engine.slab_dtype == "bf16" and L.numel % 8 == 0)
+        # (bf16 slabs are column-blocked [ceil(P/128)][grid][128]; padding columns stay zero)
+        self.slab = (torch.zeros((L.numel + 127) // 128 * 128 * self.grid, dtype=torch.bfloat16, device=dev)
+                     if self.slab_bf16 else torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev))
         self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)
         self._build_structs()
 
@@ -207,6 +212,7 @@ class VectorEngine:
         q.prices, q.env = native.ptr(self.prices), native.ptr(self.env_soa)
         q.wq, q.wf = native.ptr(self.params_bf), native.ptr(self.params)
         q.slab, q.stats = native.ptr(self.slab), native.ptr(self.stat_slab)
+        q.slab_bf16, q.slab_rows = int(self.slab_bf16), self.grid
         q.ctrl = native.ptr(self.ctrl)
         q.T, q.E, q.H, q.P = self.T, self.E, self.H, L.numel
         q.off_w0, q.off_w1, q.off_b1 = seg["W0"].offset, seg["W1"].offset, seg["b1"].offset
@@ -231,6 +237,7 @@ class VectorEngine:
         o.s1 = native.ptr(self.opt.s1) if self.opt.s1.numel() else None
         o.s2 = native.ptr(self.opt.s2) if self.opt.s2.numel() else None
         o.slab, o.grad, o.ctrl = native.ptr(self.slab), native.ptr(self.grad), native.ptr(self.ctrl)
+        o.slab_bf16 = int(self.slab_bf16)
         o.G, o.P, o.kind = self.grid, L.numel, OPT_KIND[a.optimizer]
         o.stats, o.stat_acc, o.nstat = native.ptr(self.stat_slab), native.ptr(self.stat_acc), NSTAT
         o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
@@ -263,6 +270,8 @@ class VectorEngine:
     def _launch_qstep(self, L, sh) -> None:
         if self.chunk == 64:
             fn = L.st_qstep_wide_launch_w8 if self.cfg.engine.step_waves == 8 else L.st_qstep_wide_launch
+            if self.cfg.engine.step_variant:   # tuning builds (csrc/qstep_wide8_<v>.hip), same contract
+                fn = native.variant_launch(self.cfg.engine.step_variant)
         else:
             fn = L.st_qstep_launch
         d = self.layout.pdims

@@ -110,6 +110,7 @@ def test_wide_and_narrow_kernels_agree(native_built, compat, waves):
         cfg.agent.epsilon = 0.5
         cfg.engine.chunk = chunk
         cfg.engine.step_waves = waves
+        cfg.engine.slab_dtype = "fp32"   # summation-order-only comparison (bf16 slabs: next test)
         eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
         assert eng.chunk == chunk
         eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
@@ -125,6 +126,35 @@ def test_wide_and_narrow_kernels_agree(native_built, compat, waves):
         assert torch.equal(s32[k].nan_to_num(-1.0), s64[k].nan_to_num(-1.0)), k
     assert _rel(g64, g32) < 1e-4, _rel(g64, g32)
     assert torch.allclose(st64, st32, rtol=1e-4, atol=1e-3)
+
+
+def test_bf16_gradient_slabs_match_fp32(native_built):
+    """64-env-chunk kernel: bf16 per-workgroup gradient partials (the default) vs fp32 partials on
+    the same state -- identical transitions, gradients equal up to one bf16 rounding per partial."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 4096
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for sd in ("fp32", "bf16"):
+        cfg = _cfg(False)
+        cfg.agent.epsilon = 0.5
+        cfg.engine.chunk = 64
+        cfg.engine.slab_dtype = sd
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.slab_bf16 == (sd == "bf16")
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 150)
+        eng.ctrl.fill_(7)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        out[sd] = (g, eng.actions_out.cpu().clone(), eng.stat_slab.sum(0).cpu())
+    g32, a32, st32 = out["fp32"]
+    g16, a16, st16 = out["bf16"]
+    assert torch.equal(a32, a16)
+    assert torch.equal(st32, st16)
+    assert _rel(g16, g32) < 4e-3, _rel(g16, g32)
+    assert _rel(g16, g32) > 0.0   # the bf16 path really ran
 
 
 @pytest.mark.parametrize("opt", ["adam", "adagrad", "sgd"])

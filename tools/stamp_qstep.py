@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--out", default="")
     ap.add_argument("--chunk", type=int, default=0, help="0 = engine default, 32 or 64")
+    ap.add_argument("--variant", default="", help="tuning build suffix (st_qstep_wide_launch_<v>)")
     ap.add_argument("--waves", type=int, default=8, help="64-env-chunk kernel: 4 or 8 waves")
     a = ap.parse_args()
     import build
@@ -35,6 +36,7 @@ def main():
     cfg = preset_config("flagship")
     cfg.engine.chunk = a.chunk
     cfg.engine.step_waves = a.waves
+    cfg.engine.step_variant = a.variant
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=a.envs)
     eng.run(3)
