@@ -51,6 +51,8 @@ def main() -> int:
     ap.add_argument("--sync-dp", action="store_true",
                     help="N>1: strict sync DP (all-reduce exposed) instead of the all-reduce overlapped with the "
                          "next step's kernel (one-step delayed gradient, identical on every rank)")
+    ap.add_argument("--chunk-schedule", default="auto",
+                    help="step-kernel chunk schedule: auto (dynamic for overlapped DP) | static | dynamic")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,6 +89,7 @@ def main() -> int:
     cfg.engine.chunk = args.chunk
     cfg.engine.step_waves = args.step_waves
     cfg.engine.step_variant = args.step_variant
+    cfg.engine.chunk_schedule = args.chunk_schedule
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 
@@ -169,6 +172,7 @@ def main() -> int:
                 "envs_per_gpu": eng.E,
                 "hip_graph": use_graph,
                 "kernel_chunk": eng.chunk,
+                "chunk_schedule": getattr(eng, "chunk_schedule", "static"),
             },
             "episode_return_mean": round(float(ret[0] / ret[1]), 4),
             "episode_return_window_steps": args.steps,

@@ -31,6 +31,8 @@ struct OptimParams {
   float lr, beta1, beta2, eps, scale;
   int tdelay;              // updates lagging the step counter (overlapped DP applies step t-1's gradient at t)
   int slab_bf16;           // slabs are bf16, column-blocked [ceil(P/128)][G][128] (P % 8 == 0), else fp32 [G][P]
+  unsigned* chunk_heads;   // the step kernel's 8 per-XCD chunk-claim heads (stride 32 words) or null:
+                           // re-zeroed by the slab pass (it runs after the step kernel, before the next)
 };
 
 constexpr int CW = 16;    // 16-byte slab columns per workgroup (256 B of every slab row)
@@ -49,6 +51,7 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
   const int tid = threadIdx.x, rg = tid / CW, c = tid % CW;
   const int colv = blockIdx.x * CW + c;  // NV-parameter column index
   const int PV = p.P / NV;
+  if (p.mode != 2 && p.chunk_heads && blockIdx.x == 0 && tid < 8) p.chunk_heads[32 * tid] = 0u;
   if (p.mode != 2 && p.stats && blockIdx.x == 0) {
     // step statistics folded into this pass (no extra launches; block 0 is dispatched first): thread t
     // sums stat (t & 7) over rows t/8, t/8 + RT/8, ...; then a shuffle fold over the 8 lanes of a

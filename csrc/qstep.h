@@ -30,6 +30,9 @@ struct QStepParams {
   int slab_bf16;            // slabs written as bf16, column-blocked [ceil(P/128)][slab_rows][128]
                             // (64-env-chunk kernel only; csrc/optim.hip reads them)
   int slab_rows;            // G: workgroups of the launch (= slab rows)
+  // dynamic chunk schedule (64-env-chunk kernel): 8 per-XCD claim heads, one per 128-byte line
+  // (heads[32 * x]), zero at launch; null = static schedule.  csrc/optim.hip re-zeroes them.
+  unsigned* chunk_heads;
 };
 
 // rows of QStepParams::env

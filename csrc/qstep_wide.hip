@@ -77,7 +77,8 @@ struct Geo {
   static constexpr int fB1 = fENVI + C * 4 * 4;      // b1 [H2P]
   static constexpr int fB2 = fB1 + H2P * 4;          // b2 [16]
   static constexpr int fST = fB2 + OUTP * 4;          // step statistics [NSTAT] fp32 (end of launch)
-  static constexpr int BYTES = fST + NSTAT * 4;
+  static constexpr int fCL = fST + NSTAT * 4;         // dynamic schedule: claimed chunk (broadcast slot)
+  static constexpr int BYTES = fCL + 16;
   static_assert(BYTES <= 163840, "LDS budget exceeded");
   static_assert(H1P % (16 * NW) == 0 && H2P % (16 * NW) == 0 && H1P == H2P, "m-tiles per wave");
   static_assert(INP % 32 == 0 && H1P % 32 == 0, "padding");
@@ -183,7 +184,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
   }
 }
 
-template <int INP, int H1P, int H2P, int FEAT>
+template <int INP, int H1P, int H2P, int FEAT, bool DYN>
 __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   using G = Geo<INP, H1P, H2P>;
   constexpr int MT = G::MT;
@@ -214,6 +215,23 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 #define STW_STAMPX(I) \
   if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[nmy * 16 + 8 + (I)] = __builtin_amdgcn_s_memtime();
   STW_STAMPX(0);
+
+  // ---------------------------------------------------------------- chunk schedule
+  // static: chunk k of this workgroup = blockIdx.x + k * gridDim.x.  dynamic (p.chunk_heads): the
+  // chunks of XCD x (chunk % 8 == x; workgroup i runs on XCD i % 8) are handed out by that XCD's
+  // claim head -- a workgroup's first chunk is fixed, later ones are claimed (one returning atomic by
+  // thread 0, two chunks ahead, broadcast through LDS).  Workgroups that start late (their CU still
+  // held by a concurrent RCCL kernel in overlapped DP) then take fewer chunks instead of stretching
+  // the launch's tail.  Per-XCD heads: one device-scope word serves ~88 claims/us.
+  constexpr bool dyn = DYN;   // (a template flag: the static build keeps its scalar registers)
+  int* sCl = reinterpret_cast<int*>(smem + G::fCL);
+  const int xcd = blockIdx.x & 7;
+  unsigned* const head = dyn ? p.chunk_heads + 32 * xcd : nullptr;
+  const int gx = (int)gridDim.x >> 3;   // workgroups per XCD (dynamic mode: grid % 8 == 0)
+  unsigned claim_v = 0u;                // thread 0: the claim in flight (consumed at the next publish)
+  if (dyn && tid == 0) claim_v = atomicAdd(head, 1u);
+  // k-th chunk of a sequence: static = blockIdx.x + k * grid; dynamic = xcd + 8 * j
+  auto dyn_chunk = [&](unsigned j) { return (int)min(j * 8u + (unsigned)xcd, 0x7FFFFFF0u); };
 
   // ---------------------------------------------------------------- weights (once per launch)
   // W0^T rows m0 + 16i + l16 -> MT x KS0 A fragments in VGPRs (global dwordx4; the 57 KB image is
@@ -290,7 +308,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   const int nchunks = p.E / C;
   int iter = 0;
 #define STW_STAMP(I) \
-  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0) p.stamps[iter * 16 + (I)] = __builtin_amdgcn_s_memtime();
+  if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0 && (!dyn || iter < nmy)) p.stamps[iter * 16 + (I)] = __builtin_amdgcn_s_memtime();
 
   // ---------------------------------------------------------------- software-pipelined gather
   // (same scheme as qstep_fused.hip: env state two chunks ahead, price windows one chunk ahead,
@@ -331,19 +349,28 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 // weight-gradient phase, so the window registers are live only from there to the next gather)
 #define STW_PREFETCH_NEXT()                                                \
   {                                                                        \
-    const int nxt = chunk + gridDim.x;                                     \
-    STW_LOAD_PRICES(nxt, eB_pos)                                           \
+    const int nxt_ = dyn ? c1 : chunk + (int)gridDim.x;                    \
+    STW_LOAD_PRICES(nxt_, eB_pos)                                          \
     eA_pos = eB_pos; eA_b = eB_b; eA_sh = eB_sh; eA_val = eB_val; eA_rs = eB_rs; eA_ep = eB_ep; \
-    STW_LOAD_ENV(nxt + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep) \
+    if constexpr (dyn) c2 = __builtin_amdgcn_readfirstlane(sCl[0]);        \
+    STW_LOAD_ENV(dyn ? c2 : nxt_ + (int)gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep) \
   }
-  STW_LOAD_ENV(blockIdx.x, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
-  STW_LOAD_PRICES(blockIdx.x, eA_pos)
-  STW_LOAD_ENV(blockIdx.x + gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
+  // chunk = the chunk being computed, c1 = the next one (env state loaded), c2 = the one after
+  int chunk = blockIdx.x, c1 = blockIdx.x + gridDim.x, c2 = c1;
+  STW_LOAD_ENV(chunk, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
+  STW_LOAD_PRICES(chunk, eA_pos)
+  if (dyn) {
+    if (tid == 0) sCl[0] = dyn_chunk((unsigned)gx + claim_v);
+    __syncthreads();
+    c1 = __builtin_amdgcn_readfirstlane(sCl[0]);
+  }
+  STW_LOAD_ENV(dyn ? c1 : chunk + (int)gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep)
   __syncthreads();
   STW_STAMPX(1);
 
-  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+  while (chunk < nchunks) {
     STW_STAMP(0);
+    if (dyn && tid == 0) claim_v = atomicAdd(head, 1u);   // the chunk after c1 (published after P1)
     const int ebase = chunk * C;
     // ------------------------------------------------------------ P0: windows -> feature rows
     // row-owner lanes (lane rr < RPW owns row wave*RPW + rr): env scalars -> LDS, 1/last, 1/new
@@ -401,6 +428,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     auto a_w0 = [&](int i, int ks) { return aW0[i][ks]; };
     auto a_w1 = [&](int i, int ks) { return frag_row(sW1, G::SW1, m0 + 16 * i, ks * 32, l16, g4); };
     fwd_hidden<MT, INP, G::SX, G::SH1>(a_w0, sX, sH1, nullptr, m0, l16, g4);
+    if (dyn && tid == 0) sCl[0] = dyn_chunk((unsigned)gx + claim_v);   // read in P9
     __syncthreads();
     fwd_hidden<MT, H1P, G::SH1, G::SH2>(a_w1, sH1, sH2, sB1, m0, l16, g4);
     __syncthreads();
@@ -601,6 +629,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     __syncthreads();
     STW_STAMP(7);
     ++iter;
+    if constexpr (dyn) {
+      chunk = c1;
+      c1 = c2;
+    } else {
+      chunk += gridDim.x;
+    }
   }
 #undef STW_LOAD_ENV
 #undef STW_LOAD_PRICES
@@ -687,18 +721,24 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 #undef STW_STAMPX
 }
 
-template <int INP, int H1P, int H2P, int FEAT>
-static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
+template <int INP, int H1P, int H2P, int FEAT, bool DYN>
+static hipError_t launch_fd(const QStepParams& p, int grid, hipStream_t stream) {
   using G = Geo<INP, H1P, H2P>;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)qstep_wide_kernel<INP, H1P, H2P, FEAT>,
+    hipError_t e = hipFuncSetAttribute((const void*)qstep_wide_kernel<INP, H1P, H2P, FEAT, DYN>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((qstep_wide_kernel<INP, H1P, H2P, FEAT>), dim3(grid), dim3(NT), G::BYTES, stream, p);
+  hipLaunchKernelGGL((qstep_wide_kernel<INP, H1P, H2P, FEAT, DYN>), dim3(grid), dim3(NT), G::BYTES, stream, p);
   return hipGetLastError();
+}
+
+template <int INP, int H1P, int H2P, int FEAT>
+static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
+  return p.chunk_heads ? launch_fd<INP, H1P, H2P, FEAT, true>(p, grid, stream)
+                       : launch_fd<INP, H1P, H2P, FEAT, false>(p, grid, stream);
 }
 
 }  // namespace ST_WIDE_NS
@@ -717,6 +757,7 @@ extern "C" hipError_t ST_WIDE_API(st_qstep_wide_launch)(const st::QStepParams* p
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->H + 3 > inp - 16) return hipErrorInvalidValue;
   if (p->slab_bf16 && (p->slab_rows != grid || p->P % 8 != 0)) return hipErrorInvalidValue;
+  if (p->chunk_heads && (!st::ST_WIDE_NS::PF_LATE || grid % 8 != 0 || (p->E / st::ST_WIDE_NS::C) % 8 != 0)) return hipErrorInvalidValue;
   if (inp == 224 && h1p == 128 && h2p == 128)
     return p->feat_mode ? st::ST_WIDE_NS::launch_f<224, 128, 128, 1>(*p, grid, stream)
                         : st::ST_WIDE_NS::launch_f<224, 128, 128, 0>(*p, grid, stream);

@@ -153,6 +153,12 @@ class EngineConfig:
     # applies updates asynchronously through one mailbox; False = strict sync DP (bit-equal to one
     # process holding all envs).
     dp_overlap: bool = False
+    # chunk schedule of the 64-env-chunk step kernel: "static" (chunk k of workgroup i = i + k*grid,
+    # bit-reproducible), "dynamic" (per-XCD claim heads: workgroups whose CU is still held by the
+    # overlapped RCCL all-reduce take fewer chunks instead of stretching the launch), or "auto"
+    # (dynamic for overlapped DP with world_size > 1, else static)
+    chunk_schedule: str = "auto"
+    grid: int = 0                   # step-kernel workgroups: 0 = one per CU (capped at the chunk count)
 
 
 @dataclass

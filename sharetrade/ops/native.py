@@ -41,6 +41,7 @@ class QStepParams(C.Structure):
         ("env_offset", C.c_int),
         ("stamps", C.c_void_p),
         ("slab_bf16", C.c_int), ("slab_rows", C.c_int),
+        ("chunk_heads", C.c_void_p),
     ]
 
 
@@ -52,6 +53,7 @@ class OptimParams(C.Structure):
         ("G", C.c_int), ("P", C.c_int), ("kind", C.c_int), ("mode", C.c_int), ("nstat", C.c_int),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
         ("tdelay", C.c_int), ("slab_bf16", C.c_int),
+        ("chunk_heads", C.c_void_p),
     ]
 
 
@@ -109,6 +111,9 @@ def lib() -> C.CDLL:
 
 def _bind_optional(L: C.CDLL) -> None:
     """Entry points of the fp32 small-batch path (csrc/mlp_f32.hip)."""
+    if hasattr(L, "st_occupy"):   # csrc/diag.hip
+        L.st_occupy.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.st_occupy.restype = C.c_int
     if hasattr(L, "st_mlp_fwd_f32"):
         L.st_mlp_fwd_f32.restype = C.c_int
         L.st_td_update_f32.restype = C.c_int

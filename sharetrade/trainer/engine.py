@@ -194,7 +194,7 @@ class VectorEngine:
         self.prices4 = native.replicate4(self.prices)   # aligned-gather replicas (4 x bank, HBM is plentiful)
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
-        self.grid = max(1, min(props.multi_processor_count, self.E // self.chunk))
+        self.grid = max(1, min(self.cfg.engine.grid or props.multi_processor_count, self.E // self.chunk))
         # per-workgroup gradient partials: bf16 rows for the 64-env-chunk kernel by default (the slab
         # pass of reduce_optim reads half the bytes; each partial is rounded once, summed in fp32)
         self.slab_bf16 = (self.chunk == 64 and self.cfg.engine.slab_dtype == "bf16" and L.numel % 8 == 0)
@@ -202,6 +202,17 @@ class VectorEngine:
         self.slab = (torch.zeros((L.numel + 127) // 128 * 128 * self.grid, dtype=torch.bfloat16, device=dev)
                      if self.slab_bf16 else torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev))
         self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)
+        sched = self.cfg.engine.chunk_schedule
+        if sched == "auto":
+            sched = "dynamic" if (self.world_size > 1 and self.cfg.engine.dp_overlap) else "static"
+        if sched not in ("static", "dynamic"):
+            raise ValueError(f"engine.chunk_schedule: {sched!r}")
+        # dynamic: 8 per-XCD claim heads, one per 128-byte line (csrc/qstep_wide.hip); needs the
+        # 64-env-chunk kernel, grid % 8 == 0 and (E / 64) % 8 == 0, else the static schedule is used
+        dyn_ok = self.chunk == 64 and self.grid % 8 == 0 and (self.E // 64) % 8 == 0
+        self.chunk_schedule = "dynamic" if (sched == "dynamic" and dyn_ok) else "static"
+        self.chunk_heads = (torch.zeros(8 * 32, dtype=torch.int32, device=dev)
+                            if self.chunk_schedule == "dynamic" else None)
         self._build_structs()
 
     def _build_structs(self):
@@ -230,6 +241,7 @@ class VectorEngine:
         q.feat_mode = tr.FEATURES[cfg.env.features]
         q.key0, q.key1 = int(self.key0), int(self.key1)
         q.env_offset = self.env_offset
+        q.chunk_heads = native.ptr(self.chunk_heads) if self.chunk_heads is not None else None
         self._qp = q
         a = cfg.agent
         o = native.OptimParams()
@@ -241,6 +253,7 @@ class VectorEngine:
         o.G, o.P, o.kind = self.grid, L.numel, OPT_KIND[a.optimizer]
         o.stats, o.stat_acc, o.nstat = native.ptr(self.stat_slab), native.ptr(self.stat_acc), NSTAT
         o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+        o.chunk_heads = q.chunk_heads   # re-zeroed by every slab pass (modes 0 / 1)
         self._op = o
 
     # ---------------------------------------------------------------- stepping

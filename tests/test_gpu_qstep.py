@@ -241,3 +241,41 @@ def test_compat_env_rewards_zero(native_built):
     assert s["episodes_done"] == E
     fin = eng.final_portfolios().cpu()
     assert torch.all(fin == cfg.env.budget)
+
+
+def test_dynamic_chunk_schedule_matches_static(native_built):
+    """csrc/qstep_wide.hip dynamic schedule (per-XCD claim heads): every chunk is stepped exactly once
+    per launch (positions advance by one, heads re-zeroed by the slab pass), transitions equal the
+    static schedule's and gradients agree up to the bf16 rounding of differently-grouped partials."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 64 * 8 * 6   # 48 chunks over a grid of 16: 3 per workgroup on average
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for sched in ("static", "dynamic"):
+        cfg = _cfg(False)
+        cfg.agent.epsilon = 0.5
+        cfg.engine.chunk = 64
+        cfg.engine.chunk_schedule = sched
+        cfg.engine.grid = 16
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.chunk_schedule == sched and eng.grid == 16
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 150)
+        pos0 = eng.state.pos.clone()
+        eng.ctrl.fill_(7)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        assert torch.equal(eng.state.pos, pos0 + 1), "a chunk was skipped or stepped twice"
+        out[sched] = (g, eng.actions_out.cpu().clone(), eng.stat_slab.sum(0).cpu())
+        if sched == "dynamic":
+            assert int(eng.chunk_heads.abs().sum()) == 0, "claim heads not re-zeroed"
+            g2 = eng.native_grad().detach().cpu().clone()   # second launch: heads reset worked
+            torch.cuda.synchronize()
+            assert torch.equal(eng.state.pos, pos0 + 2)
+            assert torch.isfinite(g2).all()
+    gs, as_, sts = out["static"]
+    gd, ad, std_ = out["dynamic"]
+    assert torch.equal(ad, as_)
+    assert _rel(gd, gs) < 4e-3, _rel(gd, gs)
+    assert torch.allclose(std_, sts, rtol=1e-4, atol=1e-3)
