@@ -60,6 +60,8 @@ struct F32Rows {
   int T, H, compat_env, target_compat, feat_mode, s0, env_offset;
   float eps, inv_ramp, b0, inv_b0;
   uint32_t key0, key1;
+  int reward_mode;               // engine mode: 1 = reward is the portfolio's one-step return
+  float td_clip;                 // > 0: TD error clamped to [-td_clip, td_clip] (Huber loss)
 };
 
 // out[n] = act(sum_k W^T[n][k] * in[k] + b[n]) for n < N (padded N); rows of W^T are contiguous.
@@ -192,7 +194,8 @@ __global__ void __launch_bounds__(F_NT) f32_rows_kernel(F32Net net, F32Rows r) {
       const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
       const float cur = __fadd_rn(b, __fmul_rn((float)s, vprev));
       const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
-      const float rew = __fsub_rn(nw, cur);
+      float rew = __fsub_rn(nw, cur);
+      if (r.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
       s_env[3] = b2;
       s_env[4] = rew;
       s_envi[1] = s2;
@@ -225,7 +228,7 @@ __global__ void __launch_bounds__(F_NT) f32_rows_kernel(F32Net net, F32Rows r) {
     const float y = __fadd_rn(rew, __fmul_rn(r.gamma, mx));
     const float qs = Q[slot];
     const float diff = __fsub_rn(qs, y);
-    float dq = r.coef * diff;
+    float dq = r.coef * (r.td_clip > 0.f ? fminf(fmaxf(diff, -r.td_clip), r.td_clip) : diff);
     if (net.output_relu && !(qs > 0.f)) dq = 0.f;
     s_slot = slot;
     D0[0] = dq;

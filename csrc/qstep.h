@@ -33,6 +33,8 @@ struct QStepParams {
   // dynamic chunk schedule (64-env-chunk kernel): 8 per-XCD claim heads, one per 128-byte line
   // (heads[32 * x]), zero at launch; null = static schedule.  csrc/optim.hip re-zeroes them.
   unsigned* chunk_heads;
+  int reward_mode;          // 0: reward = change of portfolio value; 1: its one-step return (change / previous)
+  float td_clip;            // > 0: the TD error fed back is clamped to [-td_clip, td_clip] (Huber loss)
 };
 
 // rows of QStepParams::env

@@ -57,6 +57,10 @@ struct QStepParams {
   uint32_t key0, key1;
   int env_offset;
   unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][16]) or null
+  int slab_bf16, slab_rows;    // (64-env-chunk kernel fields, csrc/qstep.h: same layout)
+  unsigned* chunk_heads;
+  int reward_mode;             // 0: reward = change of portfolio value; 1: its one-step return
+  float td_clip;               // > 0: TD error clamped to [-td_clip, td_clip] (Huber loss)
 };
 
 // rows of QStepParams::env
@@ -458,7 +462,8 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
       const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
       const float cur = __fadd_rn(b, __fmul_rn((float)s, vprev));
       const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
-      const float rew = __fsub_rn(nw, cur);
+      float rew = __fsub_rn(nw, cur);
+      if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
       sEnv[r * 8 + 3] = b2;
       sEnv[r * 8 + 4] = rew;
       sEnvI[r * 4 + 1] = s2;
@@ -495,7 +500,7 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
       const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
       const float qs = sQ[r * 4 + slot];
       const float diff = __fsub_rn(qs, y);
-      float dq = p.loss_coef * diff;
+      float dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
       if (p.output_relu && !(qs > 0.f)) dq = 0.f;
       bf16_t* dqr = sDQ + r * SQ;
 #pragma unroll

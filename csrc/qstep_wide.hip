@@ -471,7 +471,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
         const float cur = __fadd_rn(b, __fmul_rn((float)s, vprev));
         const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
-        const float rew = __fsub_rn(nw, cur);
+        float rew = __fsub_rn(nw, cur);
+        if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
         sEnv[r * ENVF + 3] = b2;
         sEnv[r * ENVF + 4] = rew;
         sEnvI[r * 4 + 1] = s2;
@@ -514,7 +515,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
         const float qs = sQ[r * 4 + slot];
         const float diff = __fsub_rn(qs, y);
-        float dq = p.loss_coef * diff;
+        float dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
         if (p.output_relu && !(qs > 0.f)) dq = 0.f;
         // dQ row: one nonzero at `slot`, written as two 16-byte stores
         // (slot < 3: only the first two words can be nonzero)

@@ -74,6 +74,11 @@ class AgentConfig:
     # "action": TD target written at the taken action (the intended semantics)
     target_slot: str = "compat"
     loss_reduction: str = "sum"     # "sum" over the batch (reference, B=1) | "mean"
+    # "absolute": reward = change of portfolio value in $ (TrainerChildActor.scala:142-143);
+    # "relative": the portfolio's one-step return (change / previous value) -- scale-free across
+    # envs whose prices drift apart (bf16 engine kernels and the torch oracle)
+    reward_mode: str = "absolute"
+    td_clip: float = 0.0            # > 0: clamp the TD error fed back (Huber loss); 0 = squared error
     snapshot_interval: int = 500    # QDecisionPolicyActor.scala:74
     seed: int = 1234
 
@@ -93,7 +98,7 @@ class EnvConfig:
 
 @dataclass
 class DataConfig:
-    source: str = "csv"             # csv | linear | random_walk
+    source: str = "csv"             # csv | linear | random_walk | ar1 (momentum walk: a learnable signal)
     ticker: str = "MSFT"
     start: str = "1992-01-01"
     end: str = "2015-01-01"
@@ -102,6 +107,7 @@ class DataConfig:
     length: int = 6047              # synthetic series length
     start_price: float = 50.0
     volatility: float = 0.02
+    ar_phi: float = 0.3             # ar1 source: log-return autocorrelation
     seed: int = 7
 
 
@@ -276,7 +282,8 @@ def preset_config(name: str = "reference_compat") -> Config:
         cfg.agent.optimizer = "adam"
         cfg.agent.lr = 1e-3
         cfg.agent.loss_reduction = "mean"
-        cfg.agent.gamma = 0.99
+        cfg.agent.gamma = 0.9            # tools/learning_curve.py: stable and learns (0.99 drifts)
+        cfg.agent.reward_mode = "relative"
         cfg.data.source = "random_walk"
         cfg.engine.dtype = "bf16"
         cfg.engine.envs_per_rank = 65536

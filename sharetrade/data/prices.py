@@ -90,6 +90,22 @@ def random_walk(length: int, start_price: float = 50.0, volatility: float = 0.02
     return start_price * np.exp(logp)
 
 
+def ar1_walk(length: int, start_price: float = 50.0, volatility: float = 0.02, phi: float = 0.3,
+             seed: int = 7, n_series: int = 1) -> np.ndarray:
+    """Seeded geometric walk(s) whose log-returns follow AR(1): r_t = phi * r_{t-1} + vol * eps_t,
+    shape ``[n_series, length]`` (float64).  phi > 0 is momentum: yesterday's move predicts today's,
+    a signal a Q-learner can exploit (a plain random walk has none)."""
+    rng = np.random.default_rng(seed)
+    eps = rng.standard_normal((n_series, length - 1)) * volatility
+    r = np.empty_like(eps)
+    prev = np.zeros(n_series)
+    for t in range(length - 1):
+        prev = phi * prev + eps[:, t]
+        r[:, t] = prev
+    logp = np.concatenate([np.zeros((n_series, 1)), np.cumsum(r, axis=1)], axis=1)
+    return start_price * np.exp(logp)
+
+
 def random_walk_dates(length: int, start: Date = _dt.date(2000, 1, 3)) -> List[Date]:
     return [start + _dt.timedelta(days=i) for i in range(length)]
 

@@ -96,8 +96,9 @@ def gather_windows(prices: torch.Tensor, pos: torch.Tensor, H: int, shift: int =
 
 
 def env_transition(a: torch.Tensor, b: torch.Tensor, s: torch.Tensor, v_prev: torch.Tensor,
-                   v_new: torch.Tensor, compat: bool, b0: float, s0: int):
-    """Apply actions; returns (b', s', reward).  fp32 arithmetic, no FMA contraction."""
+                   v_new: torch.Tensor, compat: bool, b0: float, s0: int, relative: bool = False):
+    """Apply actions; returns (b', s', reward).  fp32 arithmetic, no FMA contraction.
+    ``relative``: reward = change / previous portfolio value (0 where that value is not positive)."""
     if compat:
         bd = torch.full_like(b, float(b0))
         sd = torch.full_like(s, int(s0))
@@ -109,7 +110,10 @@ def env_transition(a: torch.Tensor, b: torch.Tensor, s: torch.Tensor, v_prev: to
     s2 = torch.where(buy, sd + 1, torch.where(sell, sd - 1, sd)).to(torch.int32)
     cur = b + s.float() * v_prev
     new = b2 + s2.float() * v_new
-    return b2, s2, new - cur
+    r = new - cur
+    if relative:
+        r = torch.where(cur > 0, r / torch.where(cur > 0, cur, torch.ones_like(cur)), torch.zeros_like(r))
+    return b2, s2, r
 
 
 def select_actions(q: torch.Tensor, pos: torch.Tensor, env_ids: np.ndarray, step: int, seed: int,
@@ -128,7 +132,8 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
                     history: int, feature_mode: str, budget0: float, shares0: int, compat_env: bool,
                     target_slot: str, gamma: float, output_relu: bool, epsilon: float, ramp: float,
                     seed: int, rank: int, step: int, loss_coef: float, env_offset: int = 0,
-                    emulate_bf16: bool = False, forced_actions: Optional[torch.Tensor] = None):
+                    emulate_bf16: bool = False, forced_actions: Optional[torch.Tensor] = None,
+                    reward_mode: str = "absolute", td_clip: float = 0.0):
     """One fused engine step for all envs.  Returns ``(new_state, grad, info)``.
 
     ``loss_coef`` multiplies ``(q_slot - y)`` (2.0 for the reference's summed
@@ -144,7 +149,8 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
     a, exploit = select_actions(q, pos, env_ids, step, seed, rank, epsilon, ramp, layout.n_actions)
     if forced_actions is not None:
         a = forced_actions.to(torch.int32)
-    b2, s2, r = env_transition(a, st.budget, st.shares, st.value, v_new, compat_env, budget0, shares0)
+    b2, s2, r = env_transition(a, st.budget, st.shares, st.value, v_new, compat_env, budget0, shares0,
+                               relative=(reward_mode == "relative"))
     win2 = gather_windows(prices, pos, H, shift=1)
     x2 = features(win2, b2, s2, feature_mode, budget0)
     q2, _, _ = qn.forward(params, layout, x2, output_relu, emulate_bf16)
@@ -157,7 +163,10 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
         y = r + gamma * qa.max(dim=1).values
     qs = q.gather(1, slot[:, None])[:, 0]
     dq = torch.zeros_like(q)
-    dq.scatter_(1, slot[:, None], (loss_coef * (qs - y))[:, None])
+    d = qs - y
+    if td_clip > 0:
+        d = d.clamp(-td_clip, td_clip)
+    dq.scatter_(1, slot[:, None], (loss_coef * d)[:, None])
     grad = qn.backward(params, layout, xp, acts, q, dq, output_relu, emulate_bf16)
     loss = ((qs - y) ** 2).sum()
 

@@ -45,6 +45,7 @@ class F32Rows(C.Structure):
         ("feat_mode", C.c_int), ("s0", C.c_int), ("env_offset", C.c_int),
         ("eps", C.c_float), ("inv_ramp", C.c_float), ("b0", C.c_float), ("inv_b0", C.c_float),
         ("key0", C.c_uint32), ("key1", C.c_uint32),
+        ("reward_mode", C.c_int), ("td_clip", C.c_float),
     ]
 
 
@@ -150,6 +151,7 @@ class F32Learner:
         r.q_out, r.qn_out, r.acts, r.dz, r.loss = (s.q.data_ptr(), s.qn.data_ptr(), s.acts.data_ptr(),
                                                    s.dz.data_ptr(), s.loss.data_ptr())
         r.B, r.mode, r.gamma, r.coef = B, 1, float(a.gamma), float(coef)
+        r.td_clip = float(a.td_clip)
         sh = native.stream_handle()
         native.check(self.L.st_f32_rows(self.net, r, sh), "st_f32_rows(td)")
         opt = self.l.opt
@@ -182,6 +184,8 @@ class F32EngineStep:
         r.q_out, r.qn_out, r.acts, r.dz, r.loss = (self.s.q.data_ptr(), None, self.s.acts.data_ptr(),
                                                    self.s.dz.data_ptr(), self.s.loss.data_ptr())
         r.B, r.mode, r.gamma, r.coef = E, 2, float(cfg.agent.gamma), float(eng.loss_coef)
+        r.reward_mode = int(cfg.agent.reward_mode == "relative")
+        r.td_clip = float(cfg.agent.td_clip)
         r.prices = eng.prices.data_ptr()
         r.budget, r.shares, r.value, r.pos = (st.budget.data_ptr(), st.shares.data_ptr(), st.value.data_ptr(),
                                               st.pos.data_ptr())

@@ -42,6 +42,7 @@ class QStepParams(C.Structure):
         ("stamps", C.c_void_p),
         ("slab_bf16", C.c_int), ("slab_rows", C.c_int),
         ("chunk_heads", C.c_void_p),
+        ("reward_mode", C.c_int), ("td_clip", C.c_float),
     ]
 
 

@@ -132,7 +132,8 @@ class QLearner:
         qs = q.gather(1, slot[:, None])[:, 0]
         diff = qs - target
         dq = torch.zeros_like(q)
-        dq.scatter_(1, slot[:, None], (coef * diff)[:, None])
+        fb = diff.clamp(-a.td_clip, a.td_clip) if a.td_clip > 0 else diff   # Huber (agent.td_clip)
+        dq.scatter_(1, slot[:, None], (coef * fb)[:, None])
         grad = qn.backward(self.params, L, xp, acts, q, dq, m.output_relu)
         qn.optimizer_step_ref(self.params, grad, self.opt, self.mask, a.lr, a.adam_betas, a.adam_eps)
         return float((diff * diff).sum())

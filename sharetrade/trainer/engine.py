@@ -67,6 +67,21 @@ def make_price_bank(cfg: Config, E: int, device: torch.device, seed: int = 0) ->
             return out
         arr = tr_random_walk(E, d.length, d.start_price, d.volatility, d.seed + 7919 * seed)
         return torch.from_numpy(arr).to(device)
+    if d.source == "ar1":
+        # momentum walk, generated on the device: one [E] recurrence step per day
+        g = torch.Generator(device=device)
+        g.manual_seed(d.seed + 7919 * seed)
+        out = padded_bank(E, d.length, device)
+        eps = torch.empty(E, device=device)
+        r = torch.zeros(E, device=device)
+        logp = torch.zeros(E, device=device)
+        out[:, 0] = d.start_price
+        for t in range(1, d.length):
+            eps.normal_(0.0, d.volatility, generator=g)
+            r.mul_(d.ar_phi).add_(eps)
+            logp.add_(r)
+            out[:, t] = d.start_price * torch.exp(logp)
+        return out
     from ..data import prices as pr
 
     src = pr.make_source(d)
@@ -242,6 +257,8 @@ class VectorEngine:
         q.key0, q.key1 = int(self.key0), int(self.key1)
         q.env_offset = self.env_offset
         q.chunk_heads = native.ptr(self.chunk_heads) if self.chunk_heads is not None else None
+        q.reward_mode = {"absolute": 0, "relative": 1}[cfg.agent.reward_mode]
+        q.td_clip = float(cfg.agent.td_clip)
         self._qp = q
         a = cfg.agent
         o = native.OptimParams()
@@ -365,7 +382,8 @@ class VectorEngine:
             target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
             epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0,
             step=self.step_count, loss_coef=self.loss_coef, env_offset=self.env_offset,
-            emulate_bf16=(cfg.engine.dtype == "bf16"))
+            emulate_bf16=(cfg.engine.dtype == "bf16"), reward_mode=cfg.agent.reward_mode,
+            td_clip=cfg.agent.td_clip)
         if self.world_size > 1:
             self._sync.all_reduce(grad)
         qn.optimizer_step_ref(self.params, grad, self.opt, self.mask, cfg.agent.lr, cfg.agent.adam_betas,

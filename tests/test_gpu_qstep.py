@@ -64,7 +64,7 @@ def test_qstep_matches_oracle(native_built, compat, E):
         budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
         target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
         epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
-        loss_coef=eng.loss_coef, emulate_bf16=True)
+        loss_coef=eng.loss_coef, reward_mode=cfg.agent.reward_mode, td_clip=cfg.agent.td_clip, emulate_bf16=True)
     mism = (info0["actions"].cpu() != acts).float().mean().item()
     assert mism <= 0.05, f"action mismatch rate {mism}"
 
@@ -73,7 +73,7 @@ def test_qstep_matches_oracle(native_built, compat, E):
         budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
         target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
         epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
-        loss_coef=eng.loss_coef, emulate_bf16=True, forced_actions=acts)
+        loss_coef=eng.loss_coef, reward_mode=cfg.agent.reward_mode, td_clip=cfg.agent.td_clip, emulate_bf16=True, forced_actions=acts)
     assert torch.equal(info["reward"], rew)
     for k in ("budget", "shares", "value", "pos", "episodes"):
         assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), k
@@ -90,7 +90,7 @@ def test_qstep_matches_oracle(native_built, compat, E):
         budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
         target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
         epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
-        loss_coef=eng.loss_coef, emulate_bf16=False, forced_actions=acts)
+        loss_coef=eng.loss_coef, reward_mode=cfg.agent.reward_mode, td_clip=cfg.agent.td_clip, emulate_bf16=False, forced_actions=acts)
     assert _rel(grad, g32) < 0.1
 
 
@@ -279,3 +279,43 @@ def test_dynamic_chunk_schedule_matches_static(native_built):
     assert torch.equal(ad, as_)
     assert _rel(gd, gs) < 4e-3, _rel(gd, gs)
     assert torch.allclose(std_, sts, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("chunk", [32, 64])
+def test_reward_modes_and_td_clip_match_oracle(native_built, chunk):
+    """agent.reward_mode = relative / absolute and agent.td_clip (Huber) in both step kernels vs the
+    torch oracle: identical rewards and transitions, gradients within the bf16 tolerance."""
+    from sharetrade.env import trading as tr
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 128
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    for mode, clip in (("absolute", 0.0), ("relative", 0.0), ("absolute", 0.5)):
+        cfg = _cfg(False)
+        cfg.agent.epsilon = 0.5
+        cfg.agent.reward_mode, cfg.agent.td_clip = mode, clip
+        cfg.engine.chunk = chunk
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.chunk == chunk
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 3 % 150)
+        eng.state.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
+        eng.state.value.copy_(prices[:, 0].to(dev))
+        st0 = eng.state.clone().to("cpu")
+        eng.ctrl.fill_(5)
+        params = eng.params.detach().cpu().clone()
+        grad = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        acts, rew = eng.actions_out.cpu().clone(), eng.rewards_out.cpu().clone()
+        ns, g_ref, info = tr.engine_step_ref(
+            prices, st0, params, eng.layout, history=cfg.model.history, feature_mode=cfg.env.features,
+            budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
+            target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
+            epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5,
+            loss_coef=eng.loss_coef, reward_mode=mode, td_clip=clip, emulate_bf16=True, forced_actions=acts)
+        assert torch.equal(info["reward"], rew), mode
+        if mode == "relative":
+            assert float(rew.abs().max()) < 0.5   # one-step returns, not dollars
+        for k in ("budget", "shares", "value", "pos"):
+            assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (mode, k)
+        assert _rel(grad, g_ref) < 3e-2, (mode, clip, _rel(grad, g_ref))

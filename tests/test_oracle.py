@@ -94,3 +94,22 @@ def test_compat_msft_run_reproduces_reference_portfolio():
     s = eng.stats_dict()
     assert s["reward_sum"] == 0.0
     assert torch.all(eng.current_portfolios() == 2400.0)
+
+
+def test_ar1_price_bank_has_momentum():
+    """data.source = "ar1": log-returns with lag-1 autocorrelation ~phi (the learnable signal of
+    tools/learning_curve.py); prices positive, first column the start price."""
+    import torch
+
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.engine import make_price_bank
+
+    cfg = preset_config("flagship")
+    cfg.data.source, cfg.data.ar_phi, cfg.data.length = "ar1", 0.3, 2000
+    bank = make_price_bank(cfg, 128, torch.device("cpu"))
+    assert bank.shape == (128, 2000) and bool((bank > 0).all())
+    assert torch.allclose(bank[:, 0], torch.full((128,), cfg.data.start_price))
+    r = torch.log(bank[:, 1:].double() / bank[:, :-1].double())
+    a, b = r[:, 1:] - r[:, 1:].mean(), r[:, :-1] - r[:, :-1].mean()
+    rho = float((a * b).sum() / (a.norm() * b.norm()))
+    assert abs(rho - 0.3) < 0.03, rho
