@@ -122,9 +122,14 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) { g[q].x *= p.scale; g[q].y *= p.scale; g[q].z *= p.scale; g[q].w *= p.scale; }
     if (p.mode == 1) {
+      // masked like the update (padding entries of the 64-env-chunk kernel's slabs are not zero)
       if (colv < PV)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) reinterpret_cast<float4*>(p.grad)[colv * NQ + q] = g[q];
+        for (int q = 0; q < NQ; ++q) {
+          const float4 m = reinterpret_cast<const float4*>(p.mask)[colv * NQ + q];
+          reinterpret_cast<float4*>(p.grad)[colv * NQ + q] =
+              make_float4(g[q].x * m.x, g[q].y * m.y, g[q].z * m.z, g[q].w * m.w);
+        }
       return;
     }
   } else {
@@ -200,6 +205,7 @@ __global__ void to_bf16_kernel(const float* __restrict__ in, bf16_t* __restrict_
 
 extern "C" hipError_t st_reduce_optim(const st::OptimParams* p, hipStream_t stream) {
   if (p->stats && (p->nstat < 1 || p->nstat > 8)) return hipErrorInvalidValue;
+  if (!p->mask || !p->params) return hipErrorInvalidValue;   // every mode reads the trainable mask
   if (p->slab_bf16 && p->mode != 2) {
     if (p->P % 8 != 0) return hipErrorInvalidValue;
     const int grid = (p->P + st::SLAB_BLK - 1) / st::SLAB_BLK;   // one 128-column block each

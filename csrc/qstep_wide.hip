@@ -387,13 +387,14 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
       r_inv = __fdiv_rn(1.0f, wl);
       r_invn = __fdiv_rn(1.0f, wv);
     }
-    // lane L < INP/4 owns window columns k = 4L..4L+3 of every row: price features, 0 for k >= H
-    // (the budget / shares / ones tail of x is written below by the row owners, the one of x' by
-    // the env step); one 8-byte LDS store per row for x and one for x'
+    // lane L < INP/4 owns window columns k = 4L..4L+3 of every row: price features; one 8-byte LDS
+    // store per row for x and one for x'.  Columns H..H+2 are overwritten with the (budget, shares, 1)
+    // tail (x: below, by the row owners of this wave; x': by the env step in P3).  Columns >= H+3 keep
+    // the (finite) features of the prices past the window: the layer-1 weights of those padding
+    // columns are zero (engine invariant, re-applied on load; the optimizer masks them), so they add
+    // exactly 0 to Q -- no per-element select (64 VALU per wave and chunk).  Their weight gradient is
+    // masked in the slab pass.
     if (lane < INP / 4) {
-      bool isp[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) isp[j] = 4 * lane + j < H;
       bf16_t* px = sX + (wave * RPW) * G::SX + 4 * lane;
       bf16_t* pxn = sR0 + (wave * RPW) * G::SX + 4 * lane;
 #pragma unroll
@@ -409,10 +410,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
           x01 = x01 * iv - one; x23 = x23 * iv - one;
           n01 = n01 * ivn - one; n23 = n23 * ivn - one;
         }
-        lds_st4(px + rr * G::SX, isp[0] ? x01.x : 0.f, isp[1] ? x01.y : 0.f, isp[2] ? x23.x : 0.f,
-                isp[3] ? x23.y : 0.f);
-        lds_st4(pxn + rr * G::SX, isp[0] ? n01.x : 0.f, isp[1] ? n01.y : 0.f, isp[2] ? n23.x : 0.f,
-                isp[3] ? n23.y : 0.f);
+        lds_st4(px + rr * G::SX, x01.x, x01.y, x23.x, x23.y);
+        lds_st4(pxn + rr * G::SX, n01.x, n01.y, n23.x, n23.y);
       }
     }
     if (lane < RPW) {   // x tail: (budget, shares, 1) features (same wave, after its row stores)

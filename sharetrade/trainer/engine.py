@@ -157,6 +157,10 @@ class VectorEngine:
         m, a = cfg.model, cfg.agent
         p0 = params.clone().float() if params is not None else qn.init_params(L, m, seed=a.seed)
         self.params = p0.to(self.device)
+        # padding entries of the flat layout are exactly zero (csrc/qstep_wide.hip relies on the layer-1
+        # padding columns: the gathered rows carry finite non-zero values there)
+        self._real = L.trainable_mask(True).to(self.device)
+        self.params.mul_(self._real)
         self.mask = L.trainable_mask(m.train_bias).to(self.device)
         self.opt = qn.OptimState(a.optimizer, L.numel, a.adagrad_init_acc, device=self.device)
         self.state = tr.EnvState.create(self.E, cfg.env.budget, cfg.env.shares, device=self.device)
@@ -468,6 +472,7 @@ class VectorEngine:
 
     def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
         self.params.copy_(d["params"].to(self.device))
+        self.params.mul_(self._real)
         if self.opt.s1.numel():
             self.opt.s1.copy_(d["opt_s1"].to(self.device))
         if self.opt.s2.numel():
