@@ -53,6 +53,14 @@ constexpr bool PF_LATE = ST_WIDE_PF_LATE;
 #ifndef ST_WIDE_STATW
 #define ST_WIDE_STATW 1
 #endif
+#ifndef ST_WIDE_GRAD_EARLY
+#define ST_WIDE_GRAD_EARLY 1
+#endif
+constexpr bool GRAD_EARLY = ST_WIDE_GRAD_EARLY;
+#ifndef ST_WIDE_DW0_PIPE
+#define ST_WIDE_DW0_PIPE 3
+#endif
+constexpr int DW0_PIPE = ST_WIDE_DW0_PIPE;   // X fragments in flight in the dW0 strip (0 = compiler's order)
 constexpr int SQ = OUTP + 8;
 constexpr int ENVF = 6;        // fp32 words per env in sEnv
 static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w < NET");
@@ -581,50 +589,95 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
       else if (sw == 2) { const float f = sEnv[ln * ENVF + 0]; sa0 += f; sa1 += f * f; }
       else if (sw == 3) { sa0 += sEnv[ln * ENVF + 1]; }
     }
+    // dW2^T[out][h2] += dQ^T . H2, db2 += dQ^T . 1  (reads dQ, H2)
+    auto grad_w2 = [&]() {
+#pragma unroll
+      for (int ks = 0; ks < C / 32; ++ks) {
+        const int k0 = 32 * ks;
+        const s8v aq = frag_trp(sDQ, SQ, k0, 0, l16, g4);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, frag_trp(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
+        gB2 = mfma32(aq, ones, gB2);   // every wave (branch-free accumulators); wave 0 writes it
+      }
+    };
+    // dW1^T[h2][h1] += dZ2^T . H1, db1 += dZ2^T . 1  (reads dZ2 = R0, H1)
+    auto grad_w1 = [&]() {
+#pragma unroll
+      for (int ks = 0; ks < C / 32; ++ks) {
+        const int k0 = 32 * ks;
+        s8v a2[GA1];
+#pragma unroll
+        for (int i = 0; i < GA1; ++i) a2[i] = frag_trp(sR0, G::SH2, k0, (ghb1 + i) * 16, l16, g4);
+#pragma unroll
+        for (int n = 0; n < B1; ++n) {
+          const s8v bh = frag_trp(sH1, G::SH1, k0, (gcg1 * B1 + n) * 16, l16, g4);
+#pragma unroll
+          for (int i = 0; i < GA1; ++i) gW1[i][n] = mfma32(a2[i], bh, gW1[i][n]);
+        }
+#pragma unroll
+        for (int i = 0; i < GA1; ++i) gB1[i] = mfma32(a2[i], ones, gB1[i]);
+      }
+    };
+    // dW0^T[h1][in] += dZ1^T . X  (reads dZ1 = R1, X)
+    auto grad_w0 = [&]() {
+      if constexpr (DW0_PIPE > 0 && GA0 == 1) {
+        // software-pipelined strip: DW0_PIPE X fragments in flight ahead of the MFMA that consumes
+        // them, order pinned with sched_group_barrier (hipcc otherwise reuses ONE fragment buffer:
+        // read, wait, MFMA, read, ... -- the LDS latency of all 2 x 13 reads in series)
+#pragma unroll
+        for (int ks = 0; ks < C / 32; ++ks) {
+          const int k0 = 32 * ks;
+          const s8v a1 = frag_trp(sR1, G::SH1, k0, ghb0 * 16, l16, g4);
+          s8v bq[DW0_PIPE > 0 ? DW0_PIPE : 1];
+#pragma unroll
+          for (int d = 0; d < DW0_PIPE; ++d) bq[d] = frag_trp(sX, G::SX, k0, (gcg0 * B0 + d) * 16, l16, g4);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * (DW0_PIPE + 1), 0);
+#pragma unroll
+          for (int n = 0; n < B0; ++n) {
+            const s8v bx = bq[n % DW0_PIPE];
+            gW0[0][n] = mfma32(a1, bx, gW0[0][n]);
+            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+            if (n + DW0_PIPE < B0) {
+              bq[n % DW0_PIPE] = frag_trp(sX, G::SX, k0, (gcg0 * B0 + n + DW0_PIPE) * 16, l16, g4);
+              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+          }
+        }
+        return;
+      }
+#pragma unroll
+      for (int ks = 0; ks < C / 32; ++ks) {
+        const int k0 = 32 * ks;
+        s8v a1[GA0];
+#pragma unroll
+        for (int i = 0; i < GA0; ++i) a1[i] = frag_trp(sR1, G::SH1, k0, (ghb0 + i) * 16, l16, g4);
+#pragma unroll
+        for (int n = 0; n < B0; ++n) {
+          const s8v bx = frag_trp(sX, G::SX, k0, (gcg0 * B0 + n) * 16, l16, g4);
+#pragma unroll
+          for (int i = 0; i < GA0; ++i) gW0[i][n] = mfma32(a1[i], bx, gW0[i][n]);
+        }
+      }
+    };
+    // GRAD_EARLY: each weight gradient runs in the first phase where its operands are final -- dW2 beside
+    // the layer-2 data backward (P7), dW1 beside the layer-1 data backward (P8) -- filling those
+    // latency-bound phases; P9 keeps dW0 only.  (P7 writes only R0, P8 only R1: no read hazards.)
     bwd_data<MT, OUTP, G::SW2, SQ, G::SH2, G::SH2>(sW2, sDQ, sH2, sR0, m0, l16, g4);
+    if constexpr (GRAD_EARLY) grad_w2();
     __syncthreads();
     bwd_data<MT, H2P, G::SW1, G::SH2, G::SH1, G::SH1>(sW1, sR0, sH1, sR1, m0, l16, g4);
+    if constexpr (GRAD_EARLY) grad_w1();
     __syncthreads();
     STW_STAMP(6);
     // ------------------------------------------------------------ P9: weight gradients (sum over the chunk's envs)
     if constexpr (PF_LATE && !ST_WIDE_PF_AFTER_DW0) STW_PREFETCH_NEXT();
-#pragma unroll
-    for (int ks = 0; ks < C / 32; ++ks) {
-      const int k0 = 32 * ks;
-      // dW0^T[h1][in] += dZ1^T . X
-      s8v a1[GA0];
-#pragma unroll
-      for (int i = 0; i < GA0; ++i) a1[i] = frag_trp(sR1, G::SH1, k0, (ghb0 + i) * 16, l16, g4);
-#pragma unroll
-      for (int n = 0; n < B0; ++n) {
-        const s8v bx = frag_trp(sX, G::SX, k0, (gcg0 * B0 + n) * 16, l16, g4);
-#pragma unroll
-        for (int i = 0; i < GA0; ++i) gW0[i][n] = mfma32(a1[i], bx, gW0[i][n]);
-      }
-    }
-    // the next chunk's windows land during the dW1 / dW2 half, the barrier and the next gather's
+    grad_w0();
+    // the next chunk's windows land during the rest of the phase, the barrier and the next gather's
     // row-owner work; their registers are not live across the forward / backward / dW0 phases
     if constexpr (PF_LATE && ST_WIDE_PF_AFTER_DW0) STW_PREFETCH_NEXT();
-#pragma unroll
-    for (int ks = 0; ks < C / 32; ++ks) {
-      const int k0 = 32 * ks;
-      // dW1^T[h2][h1] += dZ2^T . H1 ; db1 += dZ2^T . 1
-      s8v a2[GA1];
-#pragma unroll
-      for (int i = 0; i < GA1; ++i) a2[i] = frag_trp(sR0, G::SH2, k0, (ghb1 + i) * 16, l16, g4);
-#pragma unroll
-      for (int n = 0; n < B1; ++n) {
-        const s8v bh = frag_trp(sH1, G::SH1, k0, (gcg1 * B1 + n) * 16, l16, g4);
-#pragma unroll
-        for (int i = 0; i < GA1; ++i) gW1[i][n] = mfma32(a2[i], bh, gW1[i][n]);
-      }
-#pragma unroll
-      for (int i = 0; i < GA1; ++i) gB1[i] = mfma32(a2[i], ones, gB1[i]);
-      // dW2^T[out][h2] += dQ^T . H2 ; db2 += dQ^T . 1
-      const s8v aq = frag_trp(sDQ, SQ, k0, 0, l16, g4);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, frag_trp(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
-      gB2 = mfma32(aq, ones, gB2);   // every wave (branch-free accumulators); wave 0 writes it
+    if constexpr (!GRAD_EARLY) {
+      grad_w1();
+      grad_w2();
     }
     __syncthreads();
     STW_STAMP(7);
