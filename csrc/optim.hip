@@ -30,13 +30,14 @@ struct OptimParams {
   int nstat;
   float lr, beta1, beta2, eps, scale;
   int tdelay;              // updates lagging the step counter (overlapped DP applies step t-1's gradient at t)
-  int slab_bf16;           // slabs are bf16, column-blocked [ceil(P/128)][G][128] (P % 8 == 0), else fp32 [G][P]
+  int slab_bf16;           // slabs are bf16, column-blocked [P/32][G][32] (P % 32 == 0), else fp32 [G][P]
   unsigned* chunk_heads;   // the step kernel's 8 per-XCD chunk-claim heads (stride 32 words) or null:
                            // re-zeroed by the slab pass (it runs after the step kernel, before the next)
 };
 
 constexpr int CW = 16;    // 16-byte slab columns per workgroup (256 B of every slab row)
-constexpr int SLAB_BLK = 128;   // bf16 slabs: parameters per column block (= CW x 8)
+constexpr int SLAB_BLK = 128;   // bf16 slabs: parameters per reduce workgroup (= CW x 8) = 4 column blocks
+constexpr int SLAB_CB = 32;     // bf16 slabs: parameters per column block of the slab layout
 
 // NV parameters per thread column: 4 (fp32 slabs [G][P], one float4 per row) or 8 (bf16 slabs: the
 // step kernel rounds each workgroup's fp32 partial sum once and stores it column-BLOCKED,
@@ -98,10 +99,13 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
           g[0].x += v.x; g[0].y += v.y; g[0].z += v.z; g[0].w += v.w;
         }
       } else {
-        const uint4* sp = reinterpret_cast<const uint4*>(p.slab) + (size_t)blockIdx.x * p.G * CW + c;
+        // column c of this workgroup: block 4 * blockIdx.x + c / 4, 16-byte piece c % 4 of its 64-byte rows
+        constexpr int PPB = SLAB_CB / 8;   // 16-byte pieces per block row
+        const uint4* sp = reinterpret_cast<const uint4*>(p.slab) +
+                          (size_t)(blockIdx.x * (CW / PPB) + c / PPB) * p.G * PPB + c % PPB;
 #pragma unroll 8
         for (int r = rg; r < p.G; r += RG) {
-          const uint4 v = sp[(size_t)r * CW];
+          const uint4 v = sp[(size_t)r * PPB];
           g[0].x += __uint_as_float(v.x << 16); g[0].y += __uint_as_float(v.x & 0xFFFF0000u);
           g[0].z += __uint_as_float(v.y << 16); g[0].w += __uint_as_float(v.y & 0xFFFF0000u);
           g[1].x += __uint_as_float(v.z << 16); g[1].y += __uint_as_float(v.z & 0xFFFF0000u);
@@ -207,8 +211,8 @@ extern "C" hipError_t st_reduce_optim(const st::OptimParams* p, hipStream_t stre
   if (p->stats && (p->nstat < 1 || p->nstat > 8)) return hipErrorInvalidValue;
   if (!p->mask || !p->params) return hipErrorInvalidValue;   // every mode reads the trainable mask
   if (p->slab_bf16 && p->mode != 2) {
-    if (p->P % 8 != 0) return hipErrorInvalidValue;
-    const int grid = (p->P + st::SLAB_BLK - 1) / st::SLAB_BLK;   // one 128-column block each
+    if (p->P % st::SLAB_CB != 0) return hipErrorInvalidValue;
+    const int grid = (p->P + st::SLAB_BLK - 1) / st::SLAB_BLK;   // 128 parameters (4 column blocks) each
     hipLaunchKernelGGL((st::reduce_optim_kernel<8, 512>), dim3(grid), dim3(512), 0, stream, *p);
   } else {
     if (p->P % 4 != 0) return hipErrorInvalidValue;

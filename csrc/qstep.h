@@ -27,7 +27,7 @@ struct QStepParams {
   uint32_t key0, key1;
   int env_offset;
   unsigned long long* stamps;  // debug: s_memtime per phase of workgroup 0 ([iter][16]) or null
-  int slab_bf16;            // slabs written as bf16, column-blocked [ceil(P/128)][slab_rows][128]
+  int slab_bf16;            // slabs written as bf16, column-blocked [P/32][slab_rows][32]
                             // (64-env-chunk kernel only; csrc/optim.hip reads them)
   int slab_rows;            // G: workgroups of the launch (= slab rows)
   // dynamic chunk schedule (64-env-chunk kernel): 8 per-XCD claim heads, one per 128-byte line

@@ -697,42 +697,56 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   STW_STAMPX(2);
   // ---------------------------------------------------------------- gradient slab write-out
   // (bf16 slabs: each workgroup's fp32 partial is rounded once; csrc/optim.hip sums them in fp32)
-  auto write_slab = [&](auto put) {
+  // rowp(row): this lane's pointer for the weight row whose first parameter index is `row`;
+  // put_w(rp, cb, v): weight (row, cb + l16) with a wave-uniform column tile base cb (multiple of 16);
+  // put_b(i, v): bias parameter i
+  auto write_slab = [&](auto rowp, auto put_w, auto put_b) {
 #pragma unroll
     for (int i = 0; i < GA0; ++i) {
       const int h = (ghb0 + i) * 16 + 4 * g4;
 #pragma unroll
-      for (int n = 0; n < B0; ++n)
+      for (int j = 0; j < 4; ++j) {
+        const auto rp = rowp(p.off_w0 + (h + j) * INP);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) put(p.off_w0 + (h + j) * INP + (gcg0 * B0 + n) * 16 + l16, gW0[i][n][j]);
+        for (int n = 0; n < B0; ++n) put_w(rp, (gcg0 * B0 + n) * 16, gW0[i][n][j]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < GA1; ++i) {
       const int h = (ghb1 + i) * 16 + 4 * g4;
 #pragma unroll
-      for (int n = 0; n < B1; ++n)
+      for (int j = 0; j < 4; ++j) {
+        const auto rp = rowp(p.off_w1 + (h + j) * H1P);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) put(p.off_w1 + (h + j) * H1P + (gcg1 * B1 + n) * 16 + l16, gW1[i][n][j]);
+        for (int n = 0; n < B1; ++n) put_w(rp, (gcg1 * B1 + n) * 16, gW1[i][n][j]);
+      }
       if (gcg1 == 0 && l16 == 0)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) put(p.off_b1 + h + j, gB1[i][j]);
+        for (int j = 0; j < 4; ++j) put_b(p.off_b1 + h + j, gB1[i][j]);
     }
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) put(p.off_w2 + (4 * g4 + j) * H2P + m0 + 16 * i + l16, gW2[i][j]);
+      for (int j = 0; j < 4; ++j) put_w(rowp(p.off_w2 + (4 * g4 + j) * H2P), m0 + 16 * i, gW2[i][j]);
     if (wave == 0 && l16 == 0)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
+      for (int j = 0; j < 4; ++j) put_b(p.off_b2 + 4 * g4 + j, gB2[j]);
   };
   if (p.slab_bf16) {
-    // column-blocked [ceil(P/128)][G][128] (csrc/optim.hip reads one contiguous block per workgroup)
-    bf16_t* const sb = reinterpret_cast<bf16_t*>(p.slab) + (size_t)blockIdx.x * 128;
-    const size_t bstride = (size_t)p.slab_rows * 128;
-    write_slab([&](int i, float v) { sb[(size_t)(i >> 7) * bstride + (i & 127)] = f2bf(v); });
+    // column-blocked [P/32][G][32] (csrc/optim.hip): parameter i of this workgroup at
+    // ((i >> 5) * G + blockIdx.x) * 32 + (i & 31).  Weight rows start on 32-parameter boundaries
+    // (segment offsets and padded row lengths are multiples of 32; checked by the launcher), so a
+    // lane's row costs one multiply and each column tile is a scalar offset from it (the 128-wide
+    // blocks this replaced took a shift / mask / multiply per element: ~1,170 VALU per wave)
+    bf16_t* const sb = reinterpret_cast<bf16_t*>(p.slab) + (size_t)blockIdx.x * 32 + l16;
+    const size_t BS = (size_t)p.slab_rows * 32;
+    write_slab([&](int row) { return sb + (size_t)(row >> 5) * BS; },
+               [&](bf16_t* rp, int cb, float v) { rp[(size_t)(cb >> 5) * BS + (cb & 31)] = f2bf(v); },
+               [&](int i, float v) { sb[(size_t)(i >> 5) * BS + (i & 31) - l16] = f2bf(v); });
   } else {
-    float* const sf = p.slab + (size_t)blockIdx.x * p.P;
-    write_slab([&](int i, float v) { sf[i] = v; });
+    float* const sf = p.slab + (size_t)blockIdx.x * p.P + l16;
+    write_slab([&](int row) { return sf + row; }, [&](float* rp, int cb, float v) { rp[cb] = v; },
+               [&](int i, float v) { sf[i - l16] = v; });
   }
 
   STW_STAMPX(3);
@@ -809,7 +823,9 @@ extern "C" hipError_t ST_WIDE_API(st_qstep_wide_launch)(const st::QStepParams* p
   if (p->E % st::ST_WIDE_NS::C != 0 || grid < 1 || grid > p->E / st::ST_WIDE_NS::C) return hipErrorInvalidValue;
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->H + 3 > inp - 16) return hipErrorInvalidValue;
-  if (p->slab_bf16 && (p->slab_rows != grid || p->P % 8 != 0)) return hipErrorInvalidValue;
+  if (p->slab_bf16 && (p->slab_rows != grid || p->P % 32 != 0 || ((p->off_w0 | p->off_w1 | p->off_w2) & 31) ||
+                       inp % 32 || h1p % 32 || h2p % 32))
+    return hipErrorInvalidValue;   // 32-parameter column blocks, weight rows block-aligned
   if (p->chunk_heads && (!st::ST_WIDE_NS::PF_LATE || grid % 8 != 0 || (p->E / st::ST_WIDE_NS::C) % 8 != 0)) return hipErrorInvalidValue;
   if (inp == 224 && h1p == 128 && h2p == 128)
     return p->feat_mode ? st::ST_WIDE_NS::launch_f<224, 128, 128, 1>(*p, grid, stream)

@@ -216,8 +216,9 @@ class VectorEngine:
         self.grid = max(1, min(self.cfg.engine.grid or props.multi_processor_count, self.E // self.chunk))
         # per-workgroup gradient partials: bf16 rows for the 64-env-chunk kernel by default (the slab
         # pass of reduce_optim reads half the bytes; each partial is rounded once, summed in fp32)
-        self.slab_bf16 = (self.chunk == 64 and self.cfg.engine.slab_dtype == "bf16" and L.numel % 8 == 0)
-        # (bf16 slabs are column-blocked [ceil(P/128)][grid][128]; padding columns stay zero)
+        self.slab_bf16 = (self.chunk == 64 and self.cfg.engine.slab_dtype == "bf16" and L.numel % 32 == 0
+                          and all(seg.offset % 32 == 0 for seg in L.segments.values()))
+        # (bf16 slabs are column-blocked [P/32][grid][32])
         self.slab = (torch.zeros((L.numel + 127) // 128 * 128 * self.grid, dtype=torch.bfloat16, device=dev)
                      if self.slab_bf16 else torch.zeros(self.grid, L.numel, dtype=torch.float32, device=dev))
         self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)

@@ -26,8 +26,7 @@ for sd in ("fp32", "bf16"):
     if sd == "fp32":
         slab = eng.slab.cpu().float()
     else:
-        Pp = (P + 127) // 128 * 128
-        slab = eng.slab.cpu().float().view(Pp // 128, G, 128).permute(1, 0, 2).reshape(G, Pp)[:, :P]
+        slab = eng.slab.cpu().float()[: P * G].view(P // 32, G, 32).permute(1, 0, 2).reshape(G, P)
     res[sd] = slab
     w = ~torch.isnan(slab)
     print(sd, "grid", G, "P", P, "written per row", w.sum(1).tolist(), "segments", {k: (v.offset, v.numel) for k, v in eng.layout.segments.items()})
