@@ -241,6 +241,46 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   // k-th chunk of a sequence: static = blockIdx.x + k * grid; dynamic = xcd + 8 * j
   auto dyn_chunk = [&](unsigned j) { return (int)min(j * 8u + (unsigned)xcd, 0x7FFFFFF0u); };
 
+  // ---------------------------------------------------------------- gather state + first env loads
+  // (issued before the weight loads: the first chunk's price windows depend on its env positions,
+  // two dependent HBM round trips that now overlap the weight traffic of the prologue)
+  const int nchunks = p.E / C;
+  int eA_pos = 0, eA_sh = 0, eA_ep = 0, eB_pos = 0, eB_sh = 0, eB_ep = 0;
+  float eA_b = 0.f, eA_val = 0.f, eA_rs = 0.f, eB_b = 0.f, eB_val = 0.f, eB_rs = 0.f;
+  float4 w[RPW];
+  float wl = 0.f, wv = 0.f;
+#define STW_LOAD_ENV(CH, POS, B, SH, VAL, RS, EP)                          \
+  {                                                                        \
+    const int ch_ = min((CH), nchunks - 1);                                \
+    const int e_ = ch_ * C + wave * RPW + min(lane, RPW - 1);              \
+    POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                  \
+    VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);            \
+  }
+#define STW_LOAD_PRICES(CH, POS)                                           \
+  {                                                                        \
+    const int ch_ = min((CH), nchunks - 1);                                \
+    const int sh_ = (POS) & 3;                                             \
+    const size_t off_ = ((size_t)sh_ * p.E + (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1))) \
+        * p.T4 + (size_t)((POS) - sh_);                                    \
+    const unsigned long long a_ = (unsigned long long)(p.prices4 + off_);  \
+    const unsigned alo_ = (unsigned)a_, ahi_ = (unsigned)(a_ >> 32);       \
+    _Pragma("unroll") for (int rr = 0; rr < RPW; ++rr) {                   \
+      const unsigned long long b_ =                                        \
+          ((unsigned long long)__builtin_amdgcn_readlane(ahi_, rr) << 32) | \
+          (unsigned)__builtin_amdgcn_readlane(alo_, rr);                   \
+      typedef float f4g_ __attribute__((ext_vector_type(4)));              \
+      const f4g_ v_ = reinterpret_cast<const __attribute__((address_space(1))) f4g_*>(b_)[lane]; \
+      w[rr] = make_float4(v_.x, v_.y, v_.z, v_.w);                         \
+    }                                                                      \
+    const float* pl_ = p.prices +                                          \
+        (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1)) * p.T + (POS) + H; \
+    wl = pl_[-1];                                                          \
+    wv = pl_[0];                                                           \
+  }
+  // chunk = the chunk being computed, c1 = the next one (env state loaded), c2 = the one after
+  int chunk = blockIdx.x, c1 = blockIdx.x + gridDim.x, c2 = c1;
+  STW_LOAD_ENV(chunk, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
+
   // ---------------------------------------------------------------- weights (once per launch)
   // W0^T rows m0 + 16i + l16 -> MT x KS0 A fragments in VGPRs (global dwordx4; the 57 KB image is
   // L2-resident across the workgroups of an XCD)
@@ -313,7 +353,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
         st_qslot = 0.f;
 
-  const int nchunks = p.E / C;
   int iter = 0;
 #define STW_STAMP(I) \
   if (p.stamps != nullptr && blockIdx.x == 0 && tid == 0 && (!dyn || iter < nmy)) p.stamps[iter * 16 + (I)] = __builtin_amdgcn_s_memtime();
@@ -321,38 +360,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   // ---------------------------------------------------------------- software-pipelined gather
   // (same scheme as qstep_fused.hip: env state two chunks ahead, price windows one chunk ahead,
   // every load unconditional with clamped indices; lanes rr < RPW own one row each)
-  int eA_pos = 0, eA_sh = 0, eA_ep = 0, eB_pos = 0, eB_sh = 0, eB_ep = 0;
-  float eA_b = 0.f, eA_val = 0.f, eA_rs = 0.f, eB_b = 0.f, eB_val = 0.f, eB_rs = 0.f;
-  float4 w[RPW];
-  float wl = 0.f, wv = 0.f;
-#define STW_LOAD_ENV(CH, POS, B, SH, VAL, RS, EP)                          \
-  {                                                                        \
-    const int ch_ = min((CH), nchunks - 1);                                \
-    const int e_ = ch_ * C + wave * RPW + min(lane, RPW - 1);              \
-    POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                  \
-    VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);            \
-  }
-#define STW_LOAD_PRICES(CH, POS)                                           \
-  {                                                                        \
-    const int ch_ = min((CH), nchunks - 1);                                \
-    const int sh_ = (POS) & 3;                                             \
-    const size_t off_ = ((size_t)sh_ * p.E + (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1))) \
-        * p.T4 + (size_t)((POS) - sh_);                                    \
-    const unsigned long long a_ = (unsigned long long)(p.prices4 + off_);  \
-    const unsigned alo_ = (unsigned)a_, ahi_ = (unsigned)(a_ >> 32);       \
-    _Pragma("unroll") for (int rr = 0; rr < RPW; ++rr) {                   \
-      const unsigned long long b_ =                                        \
-          ((unsigned long long)__builtin_amdgcn_readlane(ahi_, rr) << 32) | \
-          (unsigned)__builtin_amdgcn_readlane(alo_, rr);                   \
-      typedef float f4g_ __attribute__((ext_vector_type(4)));              \
-      const f4g_ v_ = reinterpret_cast<const __attribute__((address_space(1))) f4g_*>(b_)[lane]; \
-      w[rr] = make_float4(v_.x, v_.y, v_.z, v_.w);                         \
-    }                                                                      \
-    const float* pl_ = p.prices +                                          \
-        (size_t)(ch_ * C + wave * RPW + min(lane, RPW - 1)) * p.T + (POS) + H; \
-    wl = pl_[-1];                                                          \
-    wv = pl_[0];                                                           \
-  }
 // next chunk's price windows + the env state of the one after (PF_LATE: issued at the start of the
 // weight-gradient phase, so the window registers are live only from there to the next gather)
 #define STW_PREFETCH_NEXT()                                                \
@@ -363,9 +370,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     if constexpr (dyn) c2 = __builtin_amdgcn_readfirstlane(sCl[0]);        \
     STW_LOAD_ENV(dyn ? c2 : nxt_ + (int)gridDim.x, eB_pos, eB_b, eB_sh, eB_val, eB_rs, eB_ep) \
   }
-  // chunk = the chunk being computed, c1 = the next one (env state loaded), c2 = the one after
-  int chunk = blockIdx.x, c1 = blockIdx.x + gridDim.x, c2 = c1;
-  STW_LOAD_ENV(chunk, eA_pos, eA_b, eA_sh, eA_val, eA_rs, eA_ep)
   STW_LOAD_PRICES(chunk, eA_pos)
   if (dyn) {
     if (tid == 0) sCl[0] = dyn_chunk((unsigned)gx + claim_v);
