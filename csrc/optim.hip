@@ -73,23 +73,26 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
       p.stat_acc[tid] += t;
     }
   }
-  // the updating lanes (row group 0) fetch their optimizer operands BEFORE the slab pass, so their
-  // latency hides under it instead of trailing the reduction
-  const bool upd = p.mode != 1 && rg == 0 && colv < PV;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 w4[NQ], m4[NQ], s1v[NQ], s2v[NQ], g[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    w4[q] = m4[q] = s1v[q] = s2v[q] = g[q] = z4;
-    if (upd) {
-      const int col4 = colv * NQ + q;
-      w4[q] = reinterpret_cast<const float4*>(p.params)[col4];
-      m4[q] = reinterpret_cast<const float4*>(p.mask)[col4];
-      if (p.kind >= 1) s1v[q] = reinterpret_cast<const float4*>(p.s1)[col4];
-      if (p.kind == 2) s2v[q] = reinterpret_cast<const float4*>(p.s2)[col4];
+  // one thread per parameter of this workgroup's NP = CW * NV columns does the update (was: the 16
+  // lanes of row group 0 with NV parameters each -- a one-wave tail per workgroup).  Its operands are
+  // fetched BEFORE the slab pass, so their latency hides under it.
+  constexpr int NP = CW * NV;
+  static_assert(NP <= RT, "one updating thread per parameter");
+  const int pidx = blockIdx.x * NP + tid;
+  const bool own = tid < NP && pidx < p.P;
+  float w = 0.f, mk = 0.f, s1 = 0.f, s2 = 0.f, gsum = 0.f;
+  if (own) {
+    mk = p.mask[pidx];
+    if (p.mode != 1) {
+      w = p.params[pidx];
+      if (p.kind >= 1) s1 = p.s1[pidx];
+      if (p.kind == 2) s2 = p.s2[pidx];
     }
   }
   if (p.mode != 2) {
+    float4 g[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) g[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (colv < PV) {
       if constexpr (NV == 4) {
         const float4* sp = reinterpret_cast<const float4*>(p.slab) + colv;
@@ -113,86 +116,49 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
         }
       }
     }
+    // partials [RG][NP] in LDS (part[rg][c][q] as floats: parameter c * NV + 4q + k of row group rg)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) part[rg][c][q] = g[q];
     __syncthreads();
-    if (rg != 0) return;
-    for (int k = 1; k < RG; ++k)
+    if (!own) return;
+    const float* pf = reinterpret_cast<const float*>(&part[0][0][0]);
+    float a0 = 0.f, a1 = 0.f;   // two chains: fixed order, deterministic
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const float4 v = part[k][c][q];
-        g[q].x += v.x; g[q].y += v.y; g[q].z += v.z; g[q].w += v.w;
-      }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) { g[q].x *= p.scale; g[q].y *= p.scale; g[q].z *= p.scale; g[q].w *= p.scale; }
+    for (int k = 0; k < RG; k += 2) {
+      a0 += pf[k * NP + tid];
+      a1 += pf[(k + 1) * NP + tid];
+    }
+    gsum = (a0 + a1) * p.scale;
     if (p.mode == 1) {
       // masked like the update (padding entries of the 64-env-chunk kernel's slabs are not zero)
-      if (colv < PV)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const float4 m = reinterpret_cast<const float4*>(p.mask)[colv * NQ + q];
-          reinterpret_cast<float4*>(p.grad)[colv * NQ + q] =
-              make_float4(g[q].x * m.x, g[q].y * m.y, g[q].z * m.z, g[q].w * m.w);
-        }
+      p.grad[pidx] = gsum * mk;
       return;
     }
   } else {
-    if (rg != 0) return;
-    if (colv < PV)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float4 v = reinterpret_cast<const float4*>(p.grad)[colv * NQ + q];
-        v.x *= p.scale; v.y *= p.scale; v.z *= p.scale; v.w *= p.scale;
-        g[q] = v;
-      }
+    if (!own) return;
+    gsum = p.grad[pidx] * p.scale;
   }
   const unsigned long long tstep = p.ctrl[1];
   if (blockIdx.x == 0 && tid == 0) p.ctrl[0] = tstep;  // next step index (read by the next step kernel)
   const unsigned long long t = tstep - (unsigned long long)p.tdelay;   // 1-based optimizer update count
-  if (colv >= PV) return;
-  float ic1 = 1.f, ic2 = 1.f;
-  if (p.kind == 2) {
-    ic1 = 1.f / (1.f - powf(p.beta1, (float)t));
-    ic2 = 1.f / (1.f - powf(p.beta2, (float)t));
+  const float gk = gsum * mk;
+  if (p.kind == 1) {  // AdaGrad (TF ApplyAdagrad)
+    s1 += gk * gk;
+    w -= p.lr * gk * rsqrtf(s1);
+    p.s1[pidx] = s1;
+  } else if (p.kind == 2) {  // Adam
+    const float ic1 = 1.f / (1.f - powf(p.beta1, (float)t));
+    const float ic2 = 1.f / (1.f - powf(p.beta2, (float)t));
+    s1 = p.beta1 * s1 + (1.f - p.beta1) * gk;
+    s2 = p.beta2 * s2 + (1.f - p.beta2) * gk * gk;
+    w -= p.lr * (s1 * ic1) / (sqrtf(s2 * ic2) + p.eps) * mk;
+    p.s1[pidx] = s1;
+    p.s2[pidx] = s2;
+  } else {  // SGD
+    w -= p.lr * gk;
   }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int col4 = colv * NQ + q;
-    const float gg[4] = {g[q].x, g[q].y, g[q].z, g[q].w};
-    const float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
-    float w[4] = {w4[q].x, w4[q].y, w4[q].z, w4[q].w};
-    if (p.kind == 1) {  // AdaGrad (TF ApplyAdagrad)
-      float a[4] = {s1v[q].x, s1v[q].y, s1v[q].z, s1v[q].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float gk = gg[k] * mm[k];
-        a[k] += gk * gk;
-        w[k] -= p.lr * gk * rsqrtf(a[k]);
-      }
-      reinterpret_cast<float4*>(p.s1)[col4] = make_float4(a[0], a[1], a[2], a[3]);
-    } else if (p.kind == 2) {  // Adam
-      float m[4] = {s1v[q].x, s1v[q].y, s1v[q].z, s1v[q].w}, v[4] = {s2v[q].x, s2v[q].y, s2v[q].z, s2v[q].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float gk = gg[k] * mm[k];
-        m[k] = p.beta1 * m[k] + (1.f - p.beta1) * gk;
-        v[k] = p.beta2 * v[k] + (1.f - p.beta2) * gk * gk;
-        w[k] -= p.lr * (m[k] * ic1) / (sqrtf(v[k] * ic2) + p.eps) * mm[k];
-      }
-      reinterpret_cast<float4*>(p.s1)[col4] = make_float4(m[0], m[1], m[2], m[3]);
-      reinterpret_cast<float4*>(p.s2)[col4] = make_float4(v[0], v[1], v[2], v[3]);
-    } else {  // SGD
-#pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] -= p.lr * gg[k] * mm[k];
-    }
-    reinterpret_cast<float4*>(p.params)[col4] = make_float4(w[0], w[1], w[2], w[3]);
-    if (p.params_bf) {
-      uint2 o;
-      o.x = pack_bf2(w[0], w[1]);
-      o.y = pack_bf2(w[2], w[3]);
-      reinterpret_cast<uint2*>(p.params_bf)[col4] = o;
-    }
-  }
+  p.params[pidx] = w;
+  if (p.params_bf) p.params_bf[pidx] = f2bf(w);
 }
 
 // ctrl[1] = ctrl[0] + 1 : the 1-based update count of the step about to run.
