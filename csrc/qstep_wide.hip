@@ -60,7 +60,11 @@ constexpr bool GRAD_EARLY = ST_WIDE_GRAD_EARLY;
 #ifndef ST_WIDE_DW0_PIPE
 #define ST_WIDE_DW0_PIPE 3
 #endif
-constexpr int DW0_PIPE = ST_WIDE_DW0_PIPE;   // X fragments in flight in the dW0 strip (0 = compiler's order)
+constexpr int DW0_PIPE = ST_WIDE_DW0_PIPE;   // X fragments in flight in the dW0 strip (0 = compiler order)
+#ifndef ST_WIDE_KPIPE
+#define ST_WIDE_KPIPE 0
+#endif
+constexpr int KPIPE = ST_WIDE_KPIPE;   // double-buffered k-loops (bits): 1 layer-1 forward, 2 layer-2 forward, 4 data backward
 constexpr int SQ = OUTP + 8;
 constexpr int ENVF = 6;        // fp32 words per env in sEnv
 static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w < NET");
@@ -99,13 +103,44 @@ struct Geo {
 // out^T[m][env] for this wave's MT m-tiles and the chunk's NET env tiles; A fragments given per
 // (m-tile, k-step) by the functor, B = activation rows.  Epilogue: + bias, ReLU, bf16 store into
 // out image [env][m].
-template <int MT, int K, int SB, int SO, typename AFrag>
+template <int MT, int K, int SB, int SO, bool ALDS, typename AFrag>
 ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* bias, int m0, int l16, int g4) {
   f4v acc[MT][NET];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int n = 0; n < NET; ++n) acc[i][n] = zero4();
+  if constexpr ((KPIPE & (ALDS ? 2 : 1)) != 0) {
+    // double-buffered k-loop: k-step ks+1's fragments are read while ks's MFMAs issue (order pinned;
+    // hipcc's own order waits lgkmcnt(0) for each k-step's reads right before its MFMAs)
+    constexpr int KS = K / 32, NR = NET + (ALDS ? MT : 0);
+    s8v b[2][NET], a[2][MT];
+#pragma unroll
+    for (int n = 0; n < NET; ++n) b[0][n] = frag_row(sB, SB, 16 * n, 0, l16, g4);
+    if constexpr (ALDS)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[0][i] = afrag(i, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c = ks & 1;
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int n = 0; n < NET; ++n) b[c ^ 1][n] = frag_row(sB, SB, 16 * n, (ks + 1) * 32, l16, g4);
+        if constexpr (ALDS)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) a[c ^ 1][i] = afrag(i, ks + 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const s8v aa = ALDS ? a[c][i] : afrag(i, ks);
+#pragma unroll
+        for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(aa, b[c][n], acc[i][n]);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x8, MT * NET, 0);
+    }
+  } else
 #pragma unroll
   for (int ks = 0; ks < K / 32; ++ks) {
     s8v b[NET];
@@ -163,6 +198,30 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
       const s4v a = lds_tr4(sWT + (4 * g4 + (l16 >> 2)) * SW + m0 + 16 * i + 4 * (l16 & 3));
 #pragma unroll
       for (int n = 0; n < NET; ++n) acc[i][n] = mfma16(a, b[n], acc[i][n]);
+    }
+  } else if constexpr ((KPIPE & 4) != 0) {
+    constexpr int KS = K / 32, NR = NET + 2 * MT;   // frag_tr = 2 reads
+    s8v b[2][NET], a[2][MT];
+#pragma unroll
+    for (int n = 0; n < NET; ++n) b[0][n] = frag_row(sDZ, SD, 16 * n, 0, l16, g4);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) a[0][i] = frag_tr(sWT, SW, 0, m0 + 16 * i, l16, g4);
+    __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c = ks & 1;
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int n = 0; n < NET; ++n) b[c ^ 1][n] = frag_row(sDZ, SD, 16 * n, (ks + 1) * 32, l16, g4);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a[c ^ 1][i] = frag_tr(sWT, SW, (ks + 1) * 32, m0 + 16 * i, l16, g4);
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(a[c][i], b[c][n], acc[i][n]);
+      __builtin_amdgcn_sched_group_barrier(0x8, MT * NET, 0);
     }
   } else {
 #pragma unroll
@@ -438,10 +497,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     // ------------------------------------------------------------ P1-P2: hidden layers of Q(x)
     auto a_w0 = [&](int i, int ks) { return aW0[i][ks]; };
     auto a_w1 = [&](int i, int ks) { return frag_row(sW1, G::SW1, m0 + 16 * i, ks * 32, l16, g4); };
-    fwd_hidden<MT, INP, G::SX, G::SH1>(a_w0, sX, sH1, nullptr, m0, l16, g4);
+    fwd_hidden<MT, INP, G::SX, G::SH1, false>(a_w0, sX, sH1, nullptr, m0, l16, g4);
     if (dyn && tid == 0) sCl[0] = dyn_chunk((unsigned)gx + claim_v);   // read in P9
     __syncthreads();
-    fwd_hidden<MT, H1P, G::SH1, G::SH2>(a_w1, sH1, sH2, sB1, m0, l16, g4);
+    fwd_hidden<MT, H1P, G::SH1, G::SH2, true>(a_w1, sH1, sH2, sB1, m0, l16, g4);
     __syncthreads();
     STW_STAMP(2);
     // ------------------------------------------------------------ P3: Q(x), epsilon-greedy, env step
@@ -500,9 +559,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     __syncthreads();
     STW_STAMP(3);
     // ------------------------------------------------------------ P4-P5: hidden layers of Q(x')
-    fwd_hidden<MT, INP, G::SX, G::SH1>(a_w0, sR0, sR1, nullptr, m0, l16, g4);
+    fwd_hidden<MT, INP, G::SX, G::SH1, false>(a_w0, sR0, sR1, nullptr, m0, l16, g4);
     __syncthreads();
-    fwd_hidden<MT, H1P, G::SH1, G::SH2>(a_w1, sR1, sR0, sB1, m0, l16, g4);
+    fwd_hidden<MT, H1P, G::SH1, G::SH2, true>(a_w1, sR1, sR0, sB1, m0, l16, g4);
     __syncthreads();
     STW_STAMP(4);
     // ------------------------------------------------------------ P6: Q(x'), TD target, dQ, state write-back
