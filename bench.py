@@ -53,6 +53,8 @@ def main() -> int:
                          "next step's kernel (one-step delayed gradient, identical on every rank)")
     ap.add_argument("--chunk-schedule", default="auto",
                     help="step-kernel chunk schedule: auto (dynamic for overlapped DP) | static | dynamic")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps per HIP-graph replay in the timed loop (0 = engine.graph_steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,14 +92,15 @@ def main() -> int:
     cfg.engine.step_waves = args.step_waves
     cfg.engine.step_variant = args.step_variant
     cfg.engine.chunk_schedule = args.chunk_schedule
+    if args.graph_steps:
+        cfg.engine.graph_steps = args.graph_steps
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 
     use_graph = (world == 1) and not args.no_graph
     if use_graph:
         eng.capture_graph(warmup=2)
-    for _ in range(args.warmup):
-        eng.step()
+    eng.run(args.warmup)
     eng.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -110,8 +113,7 @@ def main() -> int:
                                                   torch.profiler.ProfilerActivity.CUDA])
         prof.__enter__()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
+    eng.run(args.steps)   # whole multi-step graph replays (engine.graph_steps) + single steps
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -171,6 +173,7 @@ def main() -> int:
                                      "all-reduce overlapped with next step (1-step delayed)"),
                 "envs_per_gpu": eng.E,
                 "hip_graph": use_graph,
+                "graph_steps": cfg.engine.graph_steps if use_graph else None,
                 "kernel_chunk": eng.chunk,
                 "chunk_schedule": getattr(eng, "chunk_schedule", "static"),
             },

@@ -105,6 +105,11 @@ struct Geo {
 // out image [env][m].
 template <int MT, int K, int SB, int SO, bool ALDS, typename AFrag>
 ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* bias, int m0, int l16, int g4) {
+  float bb[MT][4];   // bias read up front (its LDS latency under the MFMAs)
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bb[i][j] = bias ? bias[m0 + 16 * i + 4 * g4 + j] : 0.f;
   f4v acc[MT][NET];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -156,13 +161,11 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int m = m0 + 16 * i + 4 * g4;
-    float bb[4] = {0.f, 0.f, 0.f, 0.f};
-    if (bias) { bb[0] = bias[m]; bb[1] = bias[m + 1]; bb[2] = bias[m + 2]; bb[3] = bias[m + 3]; }
 #pragma unroll
     for (int n = 0; n < NET; ++n) {
       const f4v v = acc[i][n];
-      lds_st4(sO + (16 * n + l16) * SO + m, fmaxf(v[0] + bb[0], 0.f), fmaxf(v[1] + bb[1], 0.f),
-              fmaxf(v[2] + bb[2], 0.f), fmaxf(v[3] + bb[3], 0.f));
+      lds_st4(sO + (16 * n + l16) * SO + m, fmaxf(v[0] + bb[i][0], 0.f), fmaxf(v[1] + bb[i][1], 0.f),
+              fmaxf(v[2] + bb[i][2], 0.f), fmaxf(v[3] + bb[i][3], 0.f));
     }
   }
 }
@@ -184,6 +187,14 @@ ST_DEV f4v fwd_out(const bf16_t* sA, const bf16_t* sB, int nt, int l16, int g4) 
 // masked by (act[env][m] > 0), bf16 store into out image [env][m].
 template <int MT, int K, int SW, int SD, int SACT, int SO>
 ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, bf16_t* sO, int m0, int l16, int g4) {
+  // ReLU masks (forward activations) read up front: their LDS latency hides under the MFMAs, and the
+  // epilogue has no load between its stores (hipcc kept each mask read right before its store:
+  // one LDS round trip per tile)
+  s4v hm[MT][NET];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < NET; ++n) hm[i][n] = lds_ld4(sAct + (16 * n + l16) * SACT + m0 + 16 * i + 4 * g4);
   f4v acc[MT][NET];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -243,7 +254,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
 #pragma unroll
     for (int n = 0; n < NET; ++n) {
       const int env = 16 * n + l16;
-      const s4v h = lds_ld4(sAct + env * SACT + m);
+      const s4v h = hm[i][n];
       const f4v v = acc[i][n];
       lds_st4(sO + env * SO + m, h[0] > 0 ? v[0] : 0.f, h[1] > 0 ? v[1] : 0.f, h[2] > 0 ? v[2] : 0.f,
               h[3] > 0 ? v[3] : 0.f);

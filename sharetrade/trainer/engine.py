@@ -414,11 +414,22 @@ class VectorEngine:
         self.step_count += 1
 
     def run(self, n: int) -> None:
+        """``n`` steps; with captured graphs, whole multi-step graphs first (one replay per
+        ``graph_steps`` steps: fewer graph-launch boundaries on the GPU), then single steps."""
+        gk = getattr(self, "_graph_k", None)
+        if gk is not None:
+            g, k = gk
+            for _ in range(n // k):
+                g.replay()
+                self.step_count += k
+            n -= (n // k) * k
         for _ in range(n):
             self.step()
 
-    def capture_graph(self, warmup: int = 2) -> bool:
-        """Capture one native step in a HIP graph (single-rank only)."""
+    def capture_graph(self, warmup: int = 2, graph_steps: Optional[int] = None) -> bool:
+        """Capture one native step in a HIP graph (single-rank only), plus a ``graph_steps``-step
+        graph for :meth:`run` (``engine.graph_steps``; the step index lives in device memory, so
+        the captured steps replay correctly back to back)."""
         if self.backend != "native" or self.world_size > 1:
             return False
         s = torch.cuda.Stream(device=self.device)
@@ -432,6 +443,14 @@ class VectorEngine:
         with torch.cuda.graph(g):
             self._native_step()
         self._graph = g
+        k = int(self.cfg.engine.graph_steps if graph_steps is None else graph_steps)
+        self._graph_k = None
+        if k > 1:
+            gk = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gk):
+                for _ in range(k):
+                    self._native_step()
+            self._graph_k = (gk, k)
         return True
 
     # ---------------------------------------------------------------- metrics

@@ -226,6 +226,29 @@ def test_graph_replay_matches_eager(native_built):
     assert int(a.ctrl[0]) == int(b.ctrl[0]) == 7
 
 
+def test_multi_step_graph_matches_eager(native_built):
+    """engine.graph_steps: run(n) replays k-step graphs then single steps -- bit-identical to n
+    eager steps (the step index lives in device memory)."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg()
+    E = 128
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    a = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    b = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    b.capture_graph(warmup=2, graph_steps=4)
+    a.run(2)
+    a.run(11)          # no graph: 11 eager steps
+    b.run(11)          # 2 x 4-step graph + 3 single-step replays
+    torch.cuda.synchronize()
+    assert a.step_count == b.step_count == 13
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.state.budget, b.state.budget)
+    assert torch.equal(a.state.pos, b.state.pos)
+    assert int(a.ctrl[0]) == int(b.ctrl[0]) == 13
+
+
 def test_compat_env_rewards_zero(native_built):
     """Quirk Q1 on the GPU path: decisions from constructor budget/shares => reward 0."""
     from sharetrade.trainer.engine import VectorEngine
