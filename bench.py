@@ -35,8 +35,8 @@ REFERENCE_FLOOR = 58.0  # derived minimum throughput of the reference app (BASEL
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 65536)),
                     help="vectorised envs per GPU")
     ap.add_argument("--no-graph", action="store_true")

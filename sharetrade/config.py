@@ -150,7 +150,7 @@ class EngineConfig:
     step_waves: int = 8             # 64-env-chunk kernel: 8 waves (two per SIMD, measured fastest) or 4
     step_variant: str = ""          # tuning builds of the 64-env-chunk kernel (st_qstep_wide_launch_<v>); "" = default
     graph: bool = True              # capture the step in a HIP graph
-    graph_steps: int = 8            # steps per graph replay in VectorEngine.run (fewer launch boundaries)
+    graph_steps: int = 16           # steps per graph replay in VectorEngine.run (fewer launch boundaries)
     backend: str = "auto"           # auto | native | torch
     bucket_mb: float = 4.0          # DP gradient all-reduce bucket (one call below this size)
     grad_compress: str = ""         # "" | "bf16" (wire format of the DP all-reduce)
