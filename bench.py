@@ -48,9 +48,11 @@ def main() -> int:
     ap.add_argument("--step-variant", default="", help="tuning build of the 64-env-chunk kernel (suffix)")
     ap.add_argument("--chunk", type=int, default=0,
                     help="envs per chunk of the fused step kernel: 0 = auto (64 when envs %% 64 == 0), 32, 64")
-    ap.add_argument("--sync-dp", action="store_true",
-                    help="N>1: strict sync DP (all-reduce exposed) instead of the all-reduce overlapped with the "
-                         "next step's kernel (one-step delayed gradient, identical on every rank)")
+    ap.add_argument("--dp-overlap", action="store_true",
+                    help="N>1: all-reduce of step t on RCCL's stream under step t+1's kernel (one-step delayed "
+                         "gradient, eager launches) instead of sync DP captured in HIP graphs (the default: "
+                         "measured faster, tools/dp_host_overhead.py)")
+    ap.add_argument("--sync-dp", action="store_true", help="(default) strict synchronous DP")
     ap.add_argument("--chunk-schedule", default="auto",
                     help="step-kernel chunk schedule: auto (dynamic for overlapped DP) | static | dynamic")
     ap.add_argument("--graph-steps", type=int, default=0,
@@ -87,7 +89,7 @@ def main() -> int:
 
     cfg = preset_config("flagship")
     cfg.engine.envs_per_rank = args.envs
-    cfg.engine.dp_overlap = not args.sync_dp
+    cfg.engine.dp_overlap = bool(args.dp_overlap) and world > 1
     cfg.engine.chunk = args.chunk
     cfg.engine.step_waves = args.step_waves
     cfg.engine.step_variant = args.step_variant
@@ -97,9 +99,17 @@ def main() -> int:
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 
-    use_graph = (world == 1) and not args.no_graph
+    use_graph = not args.no_graph and not cfg.engine.dp_overlap
     if use_graph:
-        eng.capture_graph(warmup=2)
+        try:
+            use_graph = eng.capture_graph(warmup=2)
+        except Exception as e:  # noqa: BLE001 -- fall back to eager launches, same math
+            print(f"bench: HIP graph capture failed ({str(e).splitlines()[0]}); running eagerly", file=sys.stderr)
+            from sharetrade.ops import native as _native
+
+            _native.clear_last_error()
+            torch.cuda.synchronize()
+            eng._graph, eng._graph_k, use_graph = None, None, False
     eng.run(args.warmup)
     eng.synchronize()
     if world > 1:
@@ -169,8 +179,8 @@ def main() -> int:
                 "seq_len": cfg.model.history,
                 "parallelism": f"dp{world}",
                 "dp_gradient_sync": ("none" if world == 1 else
-                                     "sync all-reduce" if args.sync_dp else
-                                     "all-reduce overlapped with next step (1-step delayed)"),
+                                     "all-reduce overlapped with next step (1-step delayed)" if cfg.engine.dp_overlap
+                                     else "sync all-reduce every step"),
                 "envs_per_gpu": eng.E,
                 "hip_graph": use_graph,
                 "graph_steps": cfg.engine.graph_steps if use_graph else None,

@@ -120,6 +120,12 @@ def _bind_optional(L: C.CDLL) -> None:
         L.st_td_update_f32.restype = C.c_int
 
 
+def clear_last_error() -> int:
+    """Read and reset the HIP runtime's sticky last error (e.g. the hipErrorStreamCaptureInvalidated
+    a failed graph capture leaves behind, which the next launcher's hipGetLastError would report)."""
+    return int(C.CDLL("libamdhip64.so").hipGetLastError())
+
+
 def check(err: int, what: str) -> None:
     if err != 0:
         raise RuntimeError(f"HIP error {err} in {what}")

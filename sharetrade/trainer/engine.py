@@ -427,11 +427,23 @@ class VectorEngine:
             self.step()
 
     def capture_graph(self, warmup: int = 2, graph_steps: Optional[int] = None) -> bool:
-        """Capture one native step in a HIP graph (single-rank only), plus a ``graph_steps``-step
-        graph for :meth:`run` (``engine.graph_steps``; the step index lives in device memory, so
-        the captured steps replay correctly back to back)."""
-        if self.backend != "native" or self.world_size > 1:
+        """Capture one native step in a HIP graph, plus a ``graph_steps``-step graph for :meth:`run`
+        (``engine.graph_steps``; the step index lives in device memory, so the captured steps replay
+        correctly back to back).
+
+        DP (world_size > 1): the synchronous step -- slab reduce, RCCL all-reduce of the flat
+        gradient, optimizer -- is captured with its collective (every rank captures the same
+        sequence).  On one MI355X that removes the per-step cross-stream event handshakes of the
+        eager path: a 1-rank RCCL group measured 69.0 us/step eager, 61.1 us/step replayed, against
+        58.8 us without DP (tools/dp_host_overhead.py).  The overlapped-DP path (``dp_overlap``)
+        keeps Python-side pending state between steps and is not captured."""
+        if self.backend != "native" or (self.world_size > 1 and self.cfg.engine.dp_overlap):
             return False
+        if self.world_size > 1:
+            import torch.distributed as dist
+
+            if dist.get_backend(self.group) != "nccl":   # gloo collectives run on the host: not capturable
+                return False
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

@@ -92,3 +92,42 @@ def test_overlapped_dp_is_rank_consistent_and_one_step_delayed(native_built):
     p_sync = out[False][0]["params"]
     rel = float((a["params"] - p_sync).norm() / p_sync.norm())
     assert 0.0 < rel < 5e-2, rel
+
+
+def _rccl_capture_worker(_rank, port, out):
+    """One rank over a real RCCL group: the sync-DP step (slab reduce -> all-reduce -> optimizer)
+    captured in a multi-step HIP graph vs the same step launched eagerly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from sharetrade.parallel.dist import DistContext, GradSync
+    from sharetrade.trainer.engine import VectorEngine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    res = {}
+    for mode in ("eager", "graph"):
+        cfg = _cfg("bf16")
+        eng = VectorEngine(cfg, prices=_bank(256), device=dev, envs=256)
+        # the DP code path (world_size > 1) over the 1-rank RCCL group
+        eng.world_size = 2
+        eng._sync = GradSync(DistContext(0, 2, 0, "nccl", dev, dist.group.WORLD), eng.layout.numel)
+        if mode == "graph":
+            assert eng.capture_graph(warmup=2, graph_steps=4)
+            eng.run(9)                   # 2 x 4-step graph + 1 single-step graph
+        else:
+            eng.run(11)
+        torch.cuda.synchronize()
+        res[mode] = {"params": eng.params.cpu(), "budget": eng.state.budget.cpu(), "step": eng.step_count}
+    torch.save(res, os.path.join(out, "cap.pt"))
+    dist.destroy_process_group()
+
+
+def test_sync_dp_step_captured_with_rccl_matches_eager(native_built):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rccl_capture_worker, args=(_port(), d), nprocs=1, join=True, start_method="spawn")
+        res = torch.load(os.path.join(d, "cap.pt"), weights_only=True)
+    assert res["eager"]["step"] == res["graph"]["step"] == 11
+    assert torch.equal(res["eager"]["params"], res["graph"]["params"])
+    assert torch.equal(res["eager"]["budget"], res["graph"]["budget"])
