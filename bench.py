@@ -73,6 +73,9 @@ def main() -> int:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # the DP step is captured in HIP graphs with its RCCL all-reduce: no user-buffer registration
+        # of captured collectives (it goes through IPC handles; the pool's driver is dmabuf-only)
+        os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
         kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
         dist.init_process_group(args.dist_backend, rank=rank, world_size=world, **kw)
         group = dist.group.WORLD
