@@ -769,6 +769,38 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 #undef STW_STAMP
 
   STW_STAMPX(2);
+  // ---------------------------------------------------------------- per-workgroup stats (-> LDS -> slab)
+  // (before the slab write-out, so its barrier does not wait for the slab stores; the chunk loop
+  // ends on a barrier; sSt is outside every chunk buffer)
+  if constexpr (STATW) {
+    const int sw = wave - NET;
+    if (sw >= 0 && sw < 4) {   // the four folding waves write all NSTAT slots (slot 7 is unused: 0)
+      const float v0 = wave_sum(sa0), v1 = wave_sum(sa1);
+      if (lane == 0) {
+        constexpr int k0[4] = {0, 6, 4, 3}, k1[4] = {1, 2, 5, 7};
+        sSt[k0[sw]] = v0;
+        sSt[k1[sw]] = sw < 3 ? v1 : 0.f;
+      }
+    }
+    __syncthreads();
+    if (tid < NSTAT) p.stats[(size_t)blockIdx.x * NSTAT + tid] = sSt[tid];
+  } else {
+    const float v[NSTAT - 1] = {st_reward, st_loss, st_explore, st_done, st_fsum, st_fsq, st_qslot};
+    float* so = sQ + wave * NSTAT;   // waves -> LDS, then a fixed-order fold (deterministic)
+#pragma unroll
+    for (int k = 0; k < NSTAT - 1; ++k) {
+      const float t = wave_sum(v[k]);
+      if (lane == 0) so[k] = t;
+    }
+    if (lane == 0) so[NSTAT - 1] = 0.f;
+    __syncthreads();
+    if (tid < NSTAT) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) t += sQ[k * NSTAT + tid];
+      p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
+    }
+  }
   // ---------------------------------------------------------------- gradient slab write-out
   // (bf16 slabs: each workgroup's fp32 partial is rounded once; csrc/optim.hip sums them in fp32)
   // rowp(row): this lane's pointer for the weight row whose first parameter index is `row`;
@@ -825,39 +857,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 
   STW_STAMPX(3);
   if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;  // 1-based update count for the optimizer
-  // ---------------------------------------------------------------- per-workgroup stats (-> LDS -> slab)
-  // (the chunk loop ends on a barrier; sSt is outside every chunk buffer)
-  if constexpr (STATW) {
-    const int sw = wave - NET;
-    if (tid < NSTAT) sSt[tid] = 0.f;
-    __syncthreads();
-    if (sw >= 0 && sw < 4) {
-      const float v0 = wave_sum(sa0), v1 = wave_sum(sa1);
-      if (lane == 0) {
-        constexpr int k0[4] = {0, 6, 4, 3}, k1[4] = {1, 2, 5, 7};
-        sSt[k0[sw]] = v0;
-        if (sw < 3) sSt[k1[sw]] = v1;
-      }
-    }
-    __syncthreads();
-    if (tid < NSTAT) p.stats[(size_t)blockIdx.x * NSTAT + tid] = sSt[tid];
-  } else {
-    const float v[NSTAT - 1] = {st_reward, st_loss, st_explore, st_done, st_fsum, st_fsq, st_qslot};
-    float* so = sQ + wave * NSTAT;   // waves -> LDS, then a fixed-order fold (deterministic)
-#pragma unroll
-    for (int k = 0; k < NSTAT - 1; ++k) {
-      const float t = wave_sum(v[k]);
-      if (lane == 0) so[k] = t;
-    }
-    if (lane == 0) so[NSTAT - 1] = 0.f;
-    __syncthreads();
-    if (tid < NSTAT) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < NW; ++k) t += sQ[k * NSTAT + tid];
-      p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
-    }
-  }
   STW_STAMPX(4);
 #undef STW_STAMPX
 }

@@ -65,8 +65,8 @@ def main():
         x = st.cpu().view(-1, 16)[iters, 8:13].double()
         lines.append(f"| prologue (W0 fragments, W1/W2 -> LDS, first gather) | {float(x[1] - x[0]):.0f} | |")
         lines.append(f"| chunk loop, all chunks | {float(x[2] - x[1]):.0f} | |")
-        lines.append(f"| gradient slab write-out | {float(x[3] - x[2]):.0f} | |")
-        lines.append(f"| stats + exit | {float(x[4] - x[3]):.0f} | |")
+        lines.append(f"| step statistics + gradient slab write-out | {float(x[3] - x[2]):.0f} | |")
+        lines.append(f"| exit | {float(x[4] - x[3]):.0f} | |")
         txt = "\n".join(lines) + "\n"
         print(txt)
         if a.out:
