@@ -65,6 +65,32 @@ constexpr int DW0_PIPE = ST_WIDE_DW0_PIPE;   // X fragments in flight in the dW0
 #define ST_WIDE_KPIPE 0
 #endif
 constexpr int KPIPE = ST_WIDE_KPIPE;   // double-buffered k-loops (bits): 1 layer-1 forward, 2 layer-2 forward, 4 data backward
+#ifndef ST_WIDE_ASWZ
+#define ST_WIDE_ASWZ 1
+#endif
+// Activation images (rows = envs: X, X', H1, H2, H1', H2', dZ1, dZ2) store the 16-byte unit of
+// column c of row r at c ^ 8 * bit2(r).  Fragment reads stay conflict-free (tools/lds_bank_sim.py);
+// the epilogue ds_write_b64 of 16 env rows at one column drops from 4-way to 2-way bank conflicts
+// (rows r and r + 4 no longer share banks).  Weight images and the dQ rows are not swizzled.
+constexpr bool ASWZ = ST_WIDE_ASWZ;
+// asw(r, lo): the swizzled offset of column base + lo for a base that is a multiple of 16 and lo < 16
+// (then (base + lo) ^ 8 bit2(r) = base + (lo ^ 8 bit2(r)): the base stays an immediate offset)
+ST_DEV int asw(int r, int lo) { return ASWZ ? (lo ^ ((r & 4) << 1)) : lo; }
+// frag_row / frag_trp (csrc/qstep.h) on a swizzled activation image (k0, c0: multiples of 16)
+ST_DEV s8v afrag_row(const bf16_t* img, int S, int r0, int k0, int l16, int g4) {
+  const int r = r0 + l16;
+  return lds_ld8(img + r * S + k0 + asw(r, 8 * g4));
+}
+ST_DEV s8v afrag_trp(const bf16_t* img, int S, int k0, int c0, int l16, int g4) {
+  const int r = k0 + 4 * g4 + (l16 >> 2);   // the second read is row r + 16: same bit 2
+  const bf16_t* q = img + r * S + c0 + asw(r, 4 * (l16 & 3));
+  s4v lo = lds_tr4(q);
+  s4v hi = lds_tr4(q + 16 * S);
+  s8v v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
 constexpr int SQ = OUTP + 8;
 constexpr int ENVF = 6;        // fp32 words per env in sEnv
 static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w < NET");
@@ -121,7 +147,7 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
     constexpr int KS = K / 32, NR = NET + (ALDS ? MT : 0);
     s8v b[2][NET], a[2][MT];
 #pragma unroll
-    for (int n = 0; n < NET; ++n) b[0][n] = frag_row(sB, SB, 16 * n, 0, l16, g4);
+    for (int n = 0; n < NET; ++n) b[0][n] = afrag_row(sB, SB, 16 * n, 0, l16, g4);
     if constexpr (ALDS)
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[0][i] = afrag(i, 0);
@@ -131,7 +157,7 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
       const int c = ks & 1;
       if (ks + 1 < KS) {
 #pragma unroll
-        for (int n = 0; n < NET; ++n) b[c ^ 1][n] = frag_row(sB, SB, 16 * n, (ks + 1) * 32, l16, g4);
+        for (int n = 0; n < NET; ++n) b[c ^ 1][n] = afrag_row(sB, SB, 16 * n, (ks + 1) * 32, l16, g4);
         if constexpr (ALDS)
 #pragma unroll
           for (int i = 0; i < MT; ++i) a[c ^ 1][i] = afrag(i, ks + 1);
@@ -150,7 +176,7 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
   for (int ks = 0; ks < K / 32; ++ks) {
     s8v b[NET];
 #pragma unroll
-    for (int n = 0; n < NET; ++n) b[n] = frag_row(sB, SB, 16 * n, ks * 32, l16, g4);
+    for (int n = 0; n < NET; ++n) b[n] = afrag_row(sB, SB, 16 * n, ks * 32, l16, g4);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const s8v a = afrag(i, ks);
@@ -164,7 +190,7 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
 #pragma unroll
     for (int n = 0; n < NET; ++n) {
       const f4v v = acc[i][n];
-      lds_st4(sO + (16 * n + l16) * SO + m, fmaxf(v[0] + bb[i][0], 0.f), fmaxf(v[1] + bb[i][1], 0.f),
+      lds_st4(sO + (16 * n + l16) * SO + m0 + 16 * i + asw(l16, 4 * g4), fmaxf(v[0] + bb[i][0], 0.f), fmaxf(v[1] + bb[i][1], 0.f),
               fmaxf(v[2] + bb[i][2], 0.f), fmaxf(v[3] + bb[i][3], 0.f));
     }
   }
@@ -177,7 +203,7 @@ ST_DEV f4v fwd_out(const bf16_t* sA, const bf16_t* sB, int nt, int l16, int g4) 
 #pragma unroll
   for (int ks = 0; ks < K / 32; ++ks) {
     const s8v a = frag_row(sA, SA, 0, ks * 32, l16, g4);
-    const s8v b = frag_row(sB, SB, 16 * nt, ks * 32, l16, g4);
+    const s8v b = afrag_row(sB, SB, 16 * nt, ks * 32, l16, g4);
     acc = mfma32(a, b, acc);
   }
   return acc;
@@ -194,7 +220,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int n = 0; n < NET; ++n) hm[i][n] = lds_ld4(sAct + (16 * n + l16) * SACT + m0 + 16 * i + 4 * g4);
+    for (int n = 0; n < NET; ++n) hm[i][n] = lds_ld4(sAct + (16 * n + l16) * SACT + m0 + 16 * i + asw(l16, 4 * g4));
   f4v acc[MT][NET];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -214,7 +240,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
     constexpr int KS = K / 32, NR = NET + 2 * MT;   // frag_tr = 2 reads
     s8v b[2][NET], a[2][MT];
 #pragma unroll
-    for (int n = 0; n < NET; ++n) b[0][n] = frag_row(sDZ, SD, 16 * n, 0, l16, g4);
+    for (int n = 0; n < NET; ++n) b[0][n] = afrag_row(sDZ, SD, 16 * n, 0, l16, g4);
 #pragma unroll
     for (int i = 0; i < MT; ++i) a[0][i] = frag_tr(sWT, SW, 0, m0 + 16 * i, l16, g4);
     __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
@@ -223,7 +249,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
       const int c = ks & 1;
       if (ks + 1 < KS) {
 #pragma unroll
-        for (int n = 0; n < NET; ++n) b[c ^ 1][n] = frag_row(sDZ, SD, 16 * n, (ks + 1) * 32, l16, g4);
+        for (int n = 0; n < NET; ++n) b[c ^ 1][n] = afrag_row(sDZ, SD, 16 * n, (ks + 1) * 32, l16, g4);
 #pragma unroll
         for (int i = 0; i < MT; ++i) a[c ^ 1][i] = frag_tr(sWT, SW, (ks + 1) * 32, m0 + 16 * i, l16, g4);
         __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
@@ -239,7 +265,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
     for (int ks = 0; ks < K / 32; ++ks) {
       s8v b[NET];
 #pragma unroll
-      for (int n = 0; n < NET; ++n) b[n] = frag_row(sDZ, SD, 16 * n, ks * 32, l16, g4);
+      for (int n = 0; n < NET; ++n) b[n] = afrag_row(sDZ, SD, 16 * n, ks * 32, l16, g4);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const s8v a = frag_tr(sWT, SW, ks * 32, m0 + 16 * i, l16, g4);
@@ -256,7 +282,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
       const int env = 16 * n + l16;
       const s4v h = hm[i][n];
       const f4v v = acc[i][n];
-      lds_st4(sO + env * SO + m, h[0] > 0 ? v[0] : 0.f, h[1] > 0 ? v[1] : 0.f, h[2] > 0 ? v[2] : 0.f,
+      lds_st4(sO + env * SO + m0 + 16 * i + asw(l16, 4 * g4), h[0] > 0 ? v[0] : 0.f, h[1] > 0 ? v[1] : 0.f, h[2] > 0 ? v[2] : 0.f,
               h[3] > 0 ? v[3] : 0.f);
     }
   }
@@ -492,15 +518,17 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
           x01 = x01 * iv - one; x23 = x23 * iv - one;
           n01 = n01 * ivn - one; n23 = n23 * ivn - one;
         }
-        lds_st4(px + rr * G::SX, x01.x, x01.y, x23.x, x23.y);
-        lds_st4(pxn + rr * G::SX, n01.x, n01.y, n23.x, n23.y);
+        const int cw = asw(wave * RPW + rr, (4 * lane) & 15) - ((4 * lane) & 15);   // swizzle shift of this row
+        lds_st4(px + rr * G::SX + cw, x01.x, x01.y, x23.x, x23.y);
+        lds_st4(pxn + rr * G::SX + cw, n01.x, n01.y, n23.x, n23.y);
       }
     }
     if (lane < RPW) {   // x tail: (budget, shares, 1) features (same wave, after its row stores)
-      bf16_t* xt = sX + (wave * RPW + lane) * G::SX + H;
-      xt[0] = f2bf(feat_budget(eA_b, p.inv_b0, FEAT));
-      xt[1] = f2bf(feat_shares(eA_sh, wl, p.inv_b0, FEAT));
-      xt[2] = f2bf(1.0f);
+      const int rw = wave * RPW + lane;
+      bf16_t* xt = sX + rw * G::SX;
+      xt[(H & ~15) + asw(rw, H & 15)] = f2bf(feat_budget(eA_b, p.inv_b0, FEAT));
+      xt[((H + 1) & ~15) + asw(rw, (H + 1) & 15)] = f2bf(feat_shares(eA_sh, wl, p.inv_b0, FEAT));
+      xt[((H + 2) & ~15) + asw(rw, (H + 2) & 15)] = f2bf(1.0f);
     }
     if constexpr (!PF_LATE) STW_PREFETCH_NEXT();
     __syncthreads();
@@ -559,9 +587,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         sEnvI[r * 4 + 1] = s2;
         sEnvI[r * 4 + 2] = STATW ? (a | (exploit ? 0 : 4)) : a;   // (8-wave: explore flag in bit 2)
         bf16_t* xn = sR0 + r * G::SX;
-        xn[H] = f2bf(feat_budget(b2, p.inv_b0, FEAT));
-        xn[H + 1] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
-        xn[H + 2] = f2bf(1.0f);
+        xn[(H & ~15) + asw(r, H & 15)] = f2bf(feat_budget(b2, p.inv_b0, FEAT));
+        xn[((H + 1) & ~15) + asw(r, (H + 1) & 15)] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
+        xn[((H + 2) & ~15) + asw(r, (H + 2) & 15)] = f2bf(1.0f);
         if constexpr (!STATW) st_explore += exploit ? 0.f : 1.f;
         ENV_I(ER_ACTION, e) = a;
         ENV_F(ER_REWARD, e) = rew;
@@ -670,7 +698,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         const int k0 = 32 * ks;
         const s8v aq = frag_trp(sDQ, SQ, k0, 0, l16, g4);
 #pragma unroll
-        for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, frag_trp(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
+        for (int i = 0; i < MT; ++i) gW2[i] = mfma32(aq, afrag_trp(sH2, G::SH2, k0, m0 + 16 * i, l16, g4), gW2[i]);
         gB2 = mfma32(aq, ones, gB2);   // every wave (branch-free accumulators); wave 0 writes it
       }
     };
@@ -681,10 +709,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         const int k0 = 32 * ks;
         s8v a2[GA1];
 #pragma unroll
-        for (int i = 0; i < GA1; ++i) a2[i] = frag_trp(sR0, G::SH2, k0, (ghb1 + i) * 16, l16, g4);
+        for (int i = 0; i < GA1; ++i) a2[i] = afrag_trp(sR0, G::SH2, k0, (ghb1 + i) * 16, l16, g4);
 #pragma unroll
         for (int n = 0; n < B1; ++n) {
-          const s8v bh = frag_trp(sH1, G::SH1, k0, (gcg1 * B1 + n) * 16, l16, g4);
+          const s8v bh = afrag_trp(sH1, G::SH1, k0, (gcg1 * B1 + n) * 16, l16, g4);
 #pragma unroll
           for (int i = 0; i < GA1; ++i) gW1[i][n] = mfma32(a2[i], bh, gW1[i][n]);
         }
@@ -701,10 +729,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 #pragma unroll
         for (int ks = 0; ks < C / 32; ++ks) {
           const int k0 = 32 * ks;
-          const s8v a1 = frag_trp(sR1, G::SH1, k0, ghb0 * 16, l16, g4);
+          const s8v a1 = afrag_trp(sR1, G::SH1, k0, ghb0 * 16, l16, g4);
           s8v bq[DW0_PIPE > 0 ? DW0_PIPE : 1];
 #pragma unroll
-          for (int d = 0; d < DW0_PIPE; ++d) bq[d] = frag_trp(sX, G::SX, k0, (gcg0 * B0 + d) * 16, l16, g4);
+          for (int d = 0; d < DW0_PIPE; ++d) bq[d] = afrag_trp(sX, G::SX, k0, (gcg0 * B0 + d) * 16, l16, g4);
           __builtin_amdgcn_sched_group_barrier(0x100, 2 * (DW0_PIPE + 1), 0);
 #pragma unroll
           for (int n = 0; n < B0; ++n) {
@@ -712,7 +740,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
             gW0[0][n] = mfma32(a1, bx, gW0[0][n]);
             __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
             if (n + DW0_PIPE < B0) {
-              bq[n % DW0_PIPE] = frag_trp(sX, G::SX, k0, (gcg0 * B0 + n + DW0_PIPE) * 16, l16, g4);
+              bq[n % DW0_PIPE] = afrag_trp(sX, G::SX, k0, (gcg0 * B0 + n + DW0_PIPE) * 16, l16, g4);
               __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             }
           }
@@ -724,10 +752,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         const int k0 = 32 * ks;
         s8v a1[GA0];
 #pragma unroll
-        for (int i = 0; i < GA0; ++i) a1[i] = frag_trp(sR1, G::SH1, k0, (ghb0 + i) * 16, l16, g4);
+        for (int i = 0; i < GA0; ++i) a1[i] = afrag_trp(sR1, G::SH1, k0, (ghb0 + i) * 16, l16, g4);
 #pragma unroll
         for (int n = 0; n < B0; ++n) {
-          const s8v bx = frag_trp(sX, G::SX, k0, (gcg0 * B0 + n) * 16, l16, g4);
+          const s8v bx = afrag_trp(sX, G::SX, k0, (gcg0 * B0 + n) * 16, l16, g4);
 #pragma unroll
           for (int i = 0; i < GA0; ++i) gW0[i][n] = mfma32(a1[i], bx, gW0[i][n]);
         }
