@@ -5,7 +5,9 @@ BASELINE.json config 2/3: a 2-layer 128-hidden MLP Q-network in bf16, online
 Q-learning (select -> env step -> TD update -> Adam) over ``--envs`` vectorised
 Buy/Sell/Hold trading envs per GPU on synthetic random-walk price series
 (6,047 days each, like the reference's MSFT file) with random-init weights;
-one process per GPU, gradients all-reduced every step with RCCL.
+one process per GPU, gradients all-reduced every step with RCCL.  Default
+1,048,576 envs per GPU (weak scaling: per-GPU work fixed as N grows); the env
+state, the per-env price banks and their aligned replicas stay resident in HBM.
 
 Single GPU:   python bench.py --steps 200 --warmup 20
 N GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -37,8 +39,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 65536)),
-                    help="vectorised envs per GPU")
+    ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 1 << 20)),
+                    help="vectorised envs per GPU (default 1,048,576: ~127 GB of HBM-resident price banks "
+                         "per GPU; fixed per-step costs amortised, profiles/r1_env_sweep.md)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) | gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
