@@ -342,3 +342,46 @@ def test_reward_modes_and_td_clip_match_oracle(native_built, chunk):
         for k in ("budget", "shares", "value", "pos"):
             assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (mode, k)
         assert _rel(grad, g_ref) < 3e-2, (mode, clip, _rel(grad, g_ref))
+
+
+def test_large_bank_gather_matches_oracle(native_built):
+    """131,072 envs x 6,047 days: the 4 aligned replicas hold 3.2e9 floats, so replica offsets of the
+    upper envs pass 2^31 elements (the bench runs 1,048,576 envs per GPU).  The last 512 envs
+    (windows spread over the whole series) must select the same greedy actions as the fp32 oracle on
+    their own rows and make bit-identical env transitions."""
+    from sharetrade.env import trading as tr
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg()
+    cfg.agent.epsilon, cfg.agent.ramp = 1.0, 1.0   # exploit whenever pos >= 1: actions = argmax Q(x)
+    cfg.data.source, cfg.data.length = "random_walk", 6047
+    E, S = 131072, 512
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, device=dev, envs=E)
+    assert eng.chunk == 64 and eng.prices4.numel() > 2 ** 31
+    idx = torch.arange(E, dtype=torch.int32, device=dev)
+    eng.state.pos.copy_(1 + idx * 37 % (eng.T - cfg.model.history - 3))
+    eng.state.shares.copy_(idx % 3)
+    eng.state.value.copy_(eng.prices[:, 0])
+    st0 = eng.state.clone()
+    eng.ctrl.fill_(5)
+    params = eng.params.detach().cpu().clone()
+    eng.native_grad()
+    torch.cuda.synchronize()
+    sub = slice(E - S, E)
+    acts = eng.actions_out[sub].cpu().clone()
+    prices = eng.prices[sub].cpu().clone()
+    st_sub = tr.EnvState(**{k: v[sub].cpu().clone() for k, v in st0.as_dict().items()})
+    kw = dict(history=cfg.model.history, feature_mode=cfg.env.features, budget0=cfg.env.budget,
+              shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions, target_slot=cfg.agent.target_slot,
+              gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu, epsilon=cfg.agent.epsilon,
+              ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=5, loss_coef=eng.loss_coef,
+              env_offset=E - S, reward_mode=cfg.agent.reward_mode, td_clip=cfg.agent.td_clip, emulate_bf16=True)
+    _, _, info0 = tr.engine_step_ref(prices, st_sub, params, eng.layout, **kw)
+    assert bool(info0["exploit"].all())
+    mism = (info0["actions"].cpu() != acts).float().mean().item()
+    assert mism <= 0.05, f"action mismatch rate {mism}"
+    ns, _, info = tr.engine_step_ref(prices, st_sub, params, eng.layout, forced_actions=acts, **kw)
+    assert torch.equal(info["reward"], eng.rewards_out[sub].cpu())
+    for k in ("budget", "shares", "value", "pos"):
+        assert torch.equal(getattr(ns, k), getattr(eng.state, k)[sub].cpu()), k
