@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=64, help="acting steps to pre-fill the replay ring")
     ap.add_argument("--updates", type=int, default=1)
+    ap.add_argument("--dw-gemm", default="auto", help="weight-gradient GEMMs: auto | hip | hipblaslt")
     a = ap.parse_args()
     import build
 
@@ -38,7 +39,7 @@ def main():
     cfg.model.hidden = [int(x) for x in a.hidden.split(",")]
     cfg.agent.lr = 1e-4
     dev = torch.device("cuda", 0)
-    d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay)
+    d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay, dw_gemm=a.dw_gemm)
     for _ in range(a.warmup):
         d.act_step()
     d.capture()

@@ -92,11 +92,17 @@ class DeepDQN:
 
     def __init__(self, cfg: Config, device: torch.device, envs: int = 16384, batch: int = 4096,
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
-                 prices: Optional[torch.Tensor] = None, seed: Optional[int] = None):
+                 prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto"):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
         self.E, self.B, self.cap = int(envs), int(batch), int(replay_capacity)
+        # weight-gradient GEMMs (plain bf16 -> fp32 products, no epilogue): "hip" = csrc/gemm_bf16.hip
+        # split-K, "hipblaslt" = torch.mm(out_dtype=fp32), "auto" = hipBLASLt where it measured faster
+        # (both dims >= 1024: 19 vs 30 us at 1024x1024x4096, tools/bench_dw.py / profiles/r1_dw_gemm.md)
+        if dw_gemm not in ("auto", "hip", "hipblaslt"):
+            raise ValueError(f"dw_gemm: {dw_gemm!r}")
+        self.dw_gemm = dw_gemm
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -296,8 +302,12 @@ class DeepDQN:
         for l in reversed(range(self.L)):
             # weight / bias gradients of layer l: dW = G_l^T . A_l
             # long-K, few-tile product: 128x128 tiles split over K (atomic fp32 accumulation)
-            wt = (128, 128) if self.pdims[l + 1] % 128 == 0 and self.pdims[l] % 128 == 0 else None
-            gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=wt, splitk="auto")
+            o, i = self.pdims[l + 1], self.pdims[l]
+            if self.dw_gemm == "hipblaslt" or (self.dw_gemm == "auto" and o >= 1024 and i >= 1024):
+                torch.mm(self.GT[l], actsT[l].t(), out_dtype=torch.float32, out=self.dW[l])
+            else:
+                wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else None
+                gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=wt, splitk="auto")
             native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
                                            self.db[l].data_ptr(), sh), "bias grad")
             if l > 0:

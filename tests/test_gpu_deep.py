@@ -17,12 +17,12 @@ def _cfg():
     return cfg
 
 
-def _dqn(E=256, B=256, cap=4096):
+def _dqn(E=256, B=256, cap=4096, **kw):
     from sharetrade.data.prices import random_walk
     from sharetrade.trainer.deep import DeepDQN
 
     prices = torch.from_numpy(random_walk(400, 50.0, 0.02, 4, n_series=E).astype(np.float32))
-    return DeepDQN(_cfg(), torch.device("cuda", 0), envs=E, batch=B, replay_capacity=cap, prices=prices)
+    return DeepDQN(_cfg(), torch.device("cuda", 0), envs=E, batch=B, replay_capacity=cap, prices=prices, **kw)
 
 
 def test_replay_ring_and_env_step(native_built):
@@ -43,8 +43,9 @@ def test_replay_ring_and_env_step(native_built):
     assert int(d.rp_ctrl[1]) == d.cap and int(d.rp["pos"][0]) == 16
 
 
-def test_update_gradients_match_torch(native_built):
-    d = _dqn()
+@pytest.mark.parametrize("dw_gemm", ["hip", "hipblaslt"])
+def test_update_gradients_match_torch(native_built, dw_gemm):
+    d = _dqn(dw_gemm=dw_gemm)
     for _ in range(8):
         d.act_step()
     d.update_step()
@@ -53,7 +54,7 @@ def test_update_gradients_match_torch(native_built):
     W = [w.float() for w in d.Wb]  # note: Adam already updated d.W; grads are from the pre-update copies
     # recompute with the weights used by the update: undo nothing — compare grads against autograd on a
     # network whose bf16 weights are the *pre-update* ones, captured before the step below
-    d2 = _dqn()
+    d2 = _dqn(dw_gemm=dw_gemm)
     for _ in range(8):
         d2.act_step()
     Wpre = [w.float().clone().requires_grad_(True) for w in d2.Wb]
@@ -87,8 +88,9 @@ def test_update_gradients_match_torch(native_built):
     assert abs(float(d2.loss) / d2.B - float(loss)) < 1e-2 * float(loss) + 1e-6
 
 
-def test_graph_iteration_runs(native_built):
-    d = _dqn()
+@pytest.mark.parametrize("dw_gemm", ["hip", "hipblaslt"])
+def test_graph_iteration_runs(native_built, dw_gemm):
+    d = _dqn(dw_gemm=dw_gemm)
     for _ in range(4):
         d.act_step()
     d.capture()
