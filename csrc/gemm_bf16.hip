@@ -52,19 +52,22 @@ struct GemmGeo {
   static constexpr int KLOOP_BYTES = 2 * BUF_EL * 2;
   static constexpr int EPI_BYTES = (BM * (BN + 8) + BN * (BM + 8)) * 2;
   static constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
-  static constexpr int WM = BM / 2, WN = BN / 2;    // per-wave output tile
+  // waves: 2 x 2 (256 threads, two blocks per CU) or, for BM = 256, 4 x 2 (512 threads, one block
+  // per CU: 1.33x fewer L2 bytes per MFMA than 128 x 128)
+  static constexpr int NWM = BM >= 256 ? 4 : 2, NWN = 2, NT = 64 * NWM * NWN, MINB = NT > 256 ? 1 : 2;
+  static constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
   static constexpr int TM = WM / 16, TN = WN / 16;  // 16x16 MFMA tiles per wave
   static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
-  static_assert(LDS_BYTES * 2 <= 163840, "two blocks per CU");
+  static_assert(LDS_BYTES * MINB <= 163840, "LDS per CU");
 };
 
 // stage one operand tile (ROWS x 64 bf16) of K-tile k0 into a linear LDS image with the
 // chunk swizzle moved to the source address.  ROWS*8 16-B pieces, 64 per wave-instruction.
-template <int ROWS>
+template <int ROWS, int NWAVE = GT / 64>
 ST_DEV void stage_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, bf16_t* lds, int wave, int lane) {
   constexpr int INSTR = ROWS / 8;        // wave-instructions per tile
 #pragma unroll
-  for (int j = wave; j < INSTR; j += GT / 64) {
+  for (int j = wave; j < INSTR; j += NWAVE) {
     const int r = j * 8 + (lane >> 3);
     const int c = lane & 7;
     const int g = c ^ (r & 7);
@@ -79,9 +82,14 @@ ST_DEV s8v frag_sw(const bf16_t* lds, int r, int g) {
   return lds_ld8(lds + r * GBK + ((g ^ (r & 7)) << 3));
 }
 
+template <int BM> constexpr int gemm_threads() { return BM >= 256 ? 512 : 256; }
+template <int BM> constexpr int gemm_min_blocks() { return BM >= 256 ? 1 : 2; }
+
 template <int BM, int BN, int EPI>
-__global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
+__global__ void __launch_bounds__(gemm_threads<BM>(), gemm_min_blocks<BM>()) gemm_nt_kernel(GemmArgs p) {
   using G = GemmGeo<BM, BN>;
+  constexpr int NW = G::NT / 64;
+  static_assert(G::NT == gemm_threads<BM>() && G::MINB == gemm_min_blocks<BM>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
@@ -97,7 +105,7 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
   bid -= ks * nwg;
   const int tm = bid / ntn, tn = bid % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / G::NWN, wn = wave % G::NWN;
 
   f4v acc[G::TM][G::TN];
 #pragma unroll
@@ -107,16 +115,16 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
 
   const int nk = p.K / GBK / nsplit;
   const int kb = ks * nk * GBK;
-  stage_tile<BM>(p.A, p.lda, m0, kb, buf, wave, lane);
-  stage_tile<BN>(p.B, p.ldb, n0, kb, buf + G::A_EL, wave, lane);
+  stage_tile<BM, NW>(p.A, p.lda, m0, kb, buf, wave, lane);
+  stage_tile<BN, NW>(p.B, p.ldb, n0, kb, buf + G::A_EL, wave, lane);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     bf16_t* cur = buf + (t & 1) * G::BUF_EL;
     if (t + 1 < nk) {
       bf16_t* nxt = buf + ((t + 1) & 1) * G::BUF_EL;
-      stage_tile<BM>(p.A, p.lda, m0, kb + (t + 1) * GBK, nxt, wave, lane);
-      stage_tile<BN>(p.B, p.ldb, n0, kb + (t + 1) * GBK, nxt + G::A_EL, wave, lane);
+      stage_tile<BM, NW>(p.A, p.lda, m0, kb + (t + 1) * GBK, nxt, wave, lane);
+      stage_tile<BN, NW>(p.B, p.ldb, n0, kb + (t + 1) * GBK, nxt + G::A_EL, wave, lane);
     }
     const bf16_t* cA = cur;
     const bf16_t* cB = cur + G::A_EL;
@@ -190,14 +198,14 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs p) {
     __syncthreads();
     bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
     constexpr int CPR = BN / 8;   // 16-byte chunks per C row
-    for (int c = tid; c < BM * CPR; c += GT) {
+    for (int c = tid; c < BM * CPR; c += G::NT) {
       const int r = c / CPR, k = (c % CPR) * 8;
       *reinterpret_cast<uint4*>(out + (size_t)(m0 + r) * p.ldo + n0 + k) =
           *reinterpret_cast<const uint4*>(sC + r * SC + k);
     }
     if (p.outT) {
       constexpr int CPRT = BM / 8;
-      for (int c = tid; c < BN * CPRT; c += GT) {
+      for (int c = tid; c < BN * CPRT; c += G::NT) {
         const int r = c / CPRT, k = (c % CPRT) * 8;
         *reinterpret_cast<uint4*>(p.outT + (size_t)(n0 + r) * p.ldoT + m0 + k) =
             *reinterpret_cast<const uint4*>(sCT + r * SCT + k);
@@ -217,16 +225,17 @@ static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
     attr = true;
   }
   const int nwg = (p.M / BM) * (p.N / BN) * (p.splitk > 1 ? p.splitk : 1);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI>), dim3(nwg), dim3(GT), G::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
   return hipGetLastError();
 }
 
 }  // namespace st
 
-// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64 (BM x BN)
+// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves)
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
-  const int bm = tile == 0 ? 128 : (tile == 1 ? 64 : 128);
-  const int bn = tile == 0 ? 128 : 64;
+  if (tile < 0 || tile > 3) return hipErrorInvalidValue;
+  const int bm = tile == 3 ? 256 : (tile == 1 ? 64 : 128);
+  const int bn = (tile == 0 || tile == 3) ? 128 : 64;
   if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
   if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
   if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
@@ -242,6 +251,7 @@ extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipSt
   if (tile == 0) { ST_G(128, 128) }
   if (tile == 1) { ST_G(64, 64) }
   if (tile == 2) { ST_G(128, 64) }
+  if (tile == 3) { ST_G(256, 128) }
 #undef ST_G
   return hipErrorInvalidValue;
 }

@@ -12,7 +12,7 @@ def _bf(shape, seed, scale=1.0):
 
 @pytest.mark.parametrize("M,N,K,tile", [(256, 256, 128, (128, 128)), (512, 1024, 1024, (128, 128)),
                                         (128, 192, 64, (64, 64)), (4096, 64, 1024, (128, 64)),
-                                        (1024, 1024, 4096, (64, 64))])
+                                        (1024, 1024, 4096, (64, 64)), (512, 256, 256, (256, 128))])
 def test_gemm_f32_epilogue(native_built, M, N, K, tile):
     from sharetrade.ops.gemm import EPI_F32, gemm_nt
 
@@ -28,7 +28,7 @@ def test_gemm_f32_epilogue(native_built, M, N, K, tile):
     assert torch.allclose(out, 2 * ref, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("tile", [(128, 128), (64, 64)])
+@pytest.mark.parametrize("tile", [(128, 128), (64, 64), (256, 128)])
 def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     from sharetrade.ops.gemm import EPI_BF16, gemm_nt
 
@@ -44,7 +44,8 @@ def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     assert torch.equal(outT, out.t().contiguous())
 
 
-def test_gemm_relu_grad_epilogue(native_built):
+@pytest.mark.parametrize("tile", [(64, 64), (256, 128)])
+def test_gemm_relu_grad_epilogue(native_built, tile):
     from sharetrade.ops.gemm import EPI_RELU_GRAD, gemm_nt
 
     M, N, K = 256, 128, 64
@@ -52,7 +53,7 @@ def test_gemm_relu_grad_epilogue(native_built):
     act = torch.relu(torch.randn(M, N, device="cuda")).to(torch.bfloat16)
     out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     outT = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
-    gemm_nt(A, B, out, EPI_RELU_GRAD, tile=(64, 64), outT=outT, auxT=act.t().contiguous())
+    gemm_nt(A, B, out, EPI_RELU_GRAD, tile=tile, outT=outT, auxT=act.t().contiguous())
     ref = (A.float() @ B.float().t()) * (act.float() > 0)
     torch.cuda.synchronize()
     assert torch.allclose(out.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))

@@ -21,6 +21,9 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t0) / iters
 
 
+TILES_AB = [(128, 128), (256, 128)]
+
+
 def main():
     import build
 
@@ -35,11 +38,13 @@ def main():
         o16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         o32 = torch.empty(M, N, device="cuda", dtype=torch.float32)
         fl = 2.0 * M * N * K
-        t16 = timeit(lambda: gemm_nt(A, B, o16, EPI_BF16, relu=True))
-        t32 = timeit(lambda: gemm_nt(A, B, o32, EPI_F32))
         tt = timeit(lambda: torch.matmul(A, B.t()))
-        rows.append(f"| {M} | {N} | {K} | {pick_tile(M, N)} | {fl / t16 / 1e12:.0f} | {fl / t32 / 1e12:.0f} | "
-                    f"{fl / tt / 1e12:.0f} |")
+        tiles = [pick_tile(M, N)] + [t for t in TILES_AB if t != pick_tile(M, N) and M % t[0] == 0 and N % t[1] == 0]
+        for t in tiles:
+            t16 = timeit(lambda: gemm_nt(A, B, o16, EPI_BF16, relu=True, tile=t))
+            t32 = timeit(lambda: gemm_nt(A, B, o32, EPI_F32, tile=t))
+            rows.append(f"| {M} | {N} | {K} | {t} | {fl / t16 / 1e12:.0f} | {fl / t32 / 1e12:.0f} | "
+                        f"{fl / tt / 1e12:.0f} |")
     txt = "\n".join(rows) + "\n"
     print(txt)
     if len(sys.argv) > 1:
