@@ -45,16 +45,18 @@ struct GemmArgs {
                          // added into out (which then holds the prior value / zeros)
 };
 
-template <int BM, int BN>
+template <int BM, int BN, int S = 2>
 struct GemmGeo {
   static constexpr int A_EL = BM * GBK, B_EL = BN * GBK;
   static constexpr int BUF_EL = A_EL + B_EL;
-  static constexpr int KLOOP_BYTES = 2 * BUF_EL * 2;
+  static constexpr int KLOOP_BYTES = S * BUF_EL * 2;   // S-stage LDS ring
   static constexpr int EPI_BYTES = (BM * (BN + 8) + BN * (BM + 8)) * 2;
   static constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
   // waves: 2 x 2 (256 threads, two blocks per CU) or, for BM = 256, 4 x 2 (512 threads, one block
   // per CU: 1.33x fewer L2 bytes per MFMA than 128 x 128)
-  static constexpr int NWM = BM >= 256 ? 4 : 2, NWN = 2, NT = 64 * NWM * NWN, MINB = NT > 256 ? 1 : 2;
+  static constexpr int NWM = BM >= 256 ? 4 : 2, NWN = 2, NT = 64 * NWM * NWN, MINB = (NT > 256 || S > 2) ? 1 : 2;
+  // LDS-DMA instructions per wave per K-tile (vmcnt budget of the S-stage ring)
+  static constexpr int LPT = (BM / 8 + NT / 64 - 1) / (NT / 64) + (BN / 8 + NT / 64 - 1) / (NT / 64);
   static constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
   static constexpr int TM = WM / 16, TN = WN / 16;  // 16x16 MFMA tiles per wave
   static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
@@ -83,13 +85,20 @@ ST_DEV s8v frag_sw(const bf16_t* lds, int r, int g) {
 }
 
 template <int BM> constexpr int gemm_threads() { return BM >= 256 ? 512 : 256; }
-template <int BM> constexpr int gemm_min_blocks() { return BM >= 256 ? 1 : 2; }
+template <int BM, int S> constexpr int gemm_min_blocks() { return (BM >= 256 || S > 2) ? 1 : 2; }
 
-template <int BM, int BN, int EPI>
-__global__ void __launch_bounds__(gemm_threads<BM>(), gemm_min_blocks<BM>()) gemm_nt_kernel(GemmArgs p) {
-  using G = GemmGeo<BM, BN>;
+// s_waitcnt immediate: vmcnt = N (gfx9 split field), expcnt / lgkmcnt not waited on
+template <int N>
+ST_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <int BM, int BN, int EPI, int S = 2>
+__global__ void __launch_bounds__(gemm_threads<BM>(), (gemm_min_blocks<BM, S>())) gemm_nt_kernel(GemmArgs p) {
+  using G = GemmGeo<BM, BN, S>;
   constexpr int NW = G::NT / 64;
-  static_assert(G::NT == gemm_threads<BM>() && G::MINB == gemm_min_blocks<BM>(), "launch bounds");
+  static_assert(G::NT == gemm_threads<BM>() && G::MINB == gemm_min_blocks<BM, S>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
@@ -115,6 +124,43 @@ __global__ void __launch_bounds__(gemm_threads<BM>(), gemm_min_blocks<BM>()) gem
 
   const int nk = p.K / GBK / nsplit;
   const int kb = ks * nk * GBK;
+  if constexpr (S > 2) {
+    // S-stage ring: tiles t+1 .. t+S-2 stay in flight while tile t is multiplied; one barrier per
+    // K-tile (it also retires every wave's reads of tile t-1, whose buffer the next load refills)
+#pragma unroll
+    for (int s0 = 0; s0 < S - 1; ++s0)
+      if (s0 < nk) {
+        stage_tile<BM, NW>(p.A, p.lda, m0, kb + s0 * GBK, buf + s0 * G::BUF_EL, wave, lane);
+        stage_tile<BN, NW>(p.B, p.ldb, n0, kb + s0 * GBK, buf + s0 * G::BUF_EL + G::A_EL, wave, lane);
+      }
+    int slot = 0;
+    for (int t = 0; t < nk; ++t) {
+      if (t + S - 2 < nk) wait_vmcnt<(S - 2) * G::LPT>();   // tile t landed, later ones may fly
+      else __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      if (t + S - 1 < nk) {
+        const int ls = slot == 0 ? S - 1 : slot - 1;        // (t + S - 1) % S: tile t-1's buffer
+        stage_tile<BM, NW>(p.A, p.lda, m0, kb + (t + S - 1) * GBK, buf + ls * G::BUF_EL, wave, lane);
+        stage_tile<BN, NW>(p.B, p.ldb, n0, kb + (t + S - 1) * GBK, buf + ls * G::BUF_EL + G::A_EL, wave, lane);
+      }
+      const bf16_t* cA = buf + slot * G::BUF_EL;
+      const bf16_t* cB = cA + G::A_EL;
+#pragma unroll
+      for (int kk = 0; kk < GBK / 32; ++kk) {
+        s8v a[G::TM], b[G::TN];
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i) a[i] = frag_sw(cA, wm * G::WM + 16 * i + l16, kk * 4 + g4);
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j) b[j] = frag_sw(cB, wn * G::WN + 16 * j + l16, kk * 4 + g4);
+#pragma unroll
+        for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < G::TN; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+      }
+      slot = slot == S - 1 ? 0 : slot + 1;
+    }
+    __syncthreads();   // every wave's last reads retired before the epilogue reuses the ring
+  } else {
   stage_tile<BM, NW>(p.A, p.lda, m0, kb, buf, wave, lane);
   stage_tile<BN, NW>(p.B, p.ldb, n0, kb, buf + G::A_EL, wave, lane);
   __builtin_amdgcn_s_waitcnt(0);
@@ -142,6 +188,7 @@ __global__ void __launch_bounds__(gemm_threads<BM>(), gemm_min_blocks<BM>()) gem
     }
     __builtin_amdgcn_s_waitcnt(0);   // next tile landed (and this tile's reads retired)
     __syncthreads();
+  }
   }
 
   // ------------------------------------------------------------------ epilogues
@@ -214,44 +261,47 @@ __global__ void __launch_bounds__(gemm_threads<BM>(), gemm_min_blocks<BM>()) gem
   }
 }
 
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, int S = 2>
 static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
-  using G = GemmGeo<BM, BN>;
+  using G = GemmGeo<BM, BN, S>;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, EPI, S>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int nwg = (p.M / BM) * (p.N / BN) * (p.splitk > 1 ? p.splitk : 1);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI, S>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
   return hipGetLastError();
 }
 
 }  // namespace st
 
-// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves)
+// tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
+//       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU)
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
-  if (tile < 0 || tile > 3) return hipErrorInvalidValue;
+  if (tile < 0 || tile > 5) return hipErrorInvalidValue;
   const int bm = tile == 3 ? 256 : (tile == 1 ? 64 : 128);
-  const int bn = (tile == 0 || tile == 3) ? 128 : 64;
+  const int bn = (tile == 1 || tile == 2) ? 64 : 128;
   if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
   if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
   if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
   if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return hipErrorInvalidValue;
   if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return hipErrorInvalidValue;
-#define ST_G(BM_, BN_)                                                                   \
+#define ST_G(BM_, BN_, S_)                                                               \
   switch (epi) {                                                                         \
-    case 0: return st::launch_gemm<BM_, BN_, 0>(*p, stream);                             \
-    case 1: return st::launch_gemm<BM_, BN_, 1>(*p, stream);                             \
-    case 2: return st::launch_gemm<BM_, BN_, 2>(*p, stream);                             \
+    case 0: return st::launch_gemm<BM_, BN_, 0, S_>(*p, stream);                         \
+    case 1: return st::launch_gemm<BM_, BN_, 1, S_>(*p, stream);                         \
+    case 2: return st::launch_gemm<BM_, BN_, 2, S_>(*p, stream);                         \
     default: return hipErrorInvalidValue;                                                \
   }
-  if (tile == 0) { ST_G(128, 128) }
-  if (tile == 1) { ST_G(64, 64) }
-  if (tile == 2) { ST_G(128, 64) }
-  if (tile == 3) { ST_G(256, 128) }
+  if (tile == 0) { ST_G(128, 128, 2) }
+  if (tile == 1) { ST_G(64, 64, 2) }
+  if (tile == 2) { ST_G(128, 64, 2) }
+  if (tile == 3) { ST_G(256, 128, 2) }
+  if (tile == 4) { ST_G(128, 128, 3) }
+  if (tile == 5) { ST_G(128, 128, 4) }
 #undef ST_G
   return hipErrorInvalidValue;
 }

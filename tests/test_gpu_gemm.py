@@ -12,7 +12,9 @@ def _bf(shape, seed, scale=1.0):
 
 @pytest.mark.parametrize("M,N,K,tile", [(256, 256, 128, (128, 128)), (512, 1024, 1024, (128, 128)),
                                         (128, 192, 64, (64, 64)), (4096, 64, 1024, (128, 64)),
-                                        (1024, 1024, 4096, (64, 64)), (512, 256, 256, (256, 128))])
+                                        (1024, 1024, 4096, (64, 64)), (512, 256, 256, (256, 128)),
+                                        (256, 256, 128, (128, 128, 4)), (512, 1024, 1024, (128, 128, 3)),
+                                        (256, 512, 64, (128, 128, 3)), (512, 256, 1024, (128, 128, 4))])
 def test_gemm_f32_epilogue(native_built, M, N, K, tile):
     from sharetrade.ops.gemm import EPI_F32, gemm_nt
 
@@ -28,7 +30,7 @@ def test_gemm_f32_epilogue(native_built, M, N, K, tile):
     assert torch.allclose(out, 2 * ref, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("tile", [(128, 128), (64, 64), (256, 128)])
+@pytest.mark.parametrize("tile", [(128, 128), (64, 64), (256, 128), (128, 128, 3), (128, 128, 4)])
 def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     from sharetrade.ops.gemm import EPI_BF16, gemm_nt
 
@@ -44,7 +46,7 @@ def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     assert torch.equal(outT, out.t().contiguous())
 
 
-@pytest.mark.parametrize("tile", [(64, 64), (256, 128)])
+@pytest.mark.parametrize("tile", [(64, 64), (256, 128), (128, 128, 4)])
 def test_gemm_relu_grad_epilogue(native_built, tile):
     from sharetrade.ops.gemm import EPI_RELU_GRAD, gemm_nt
 
@@ -69,7 +71,8 @@ def test_gemm_rejects_bad_shapes(native_built):
 
 
 @pytest.mark.parametrize("M,N,K,tile,sk", [(1024, 1024, 4096, (128, 128), "auto"), (768, 256, 16384, (64, 64), 8),
-                                           (768, 64, 16384, (64, 64), "auto")])
+                                           (768, 64, 16384, (64, 64), "auto"),
+                                           (1024, 1024, 4096, (128, 128, 3), "auto")])
 def test_gemm_split_k(native_built, M, N, K, tile, sk):
     from sharetrade.ops.gemm import EPI_F32, gemm_nt, pick_splitk
 
