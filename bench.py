@@ -108,7 +108,9 @@ def main() -> int:
     use_graph = not args.no_graph and not cfg.engine.dp_overlap
     if use_graph:
         try:
-            use_graph = eng.capture_graph(warmup=2)
+            # 2 eager steps before capture, then one replay of each captured graph (graph upload);
+            # all of them untimed and reported as "graph_prime_steps"
+            use_graph = eng.capture_graph(warmup=2, prime=True)
         except Exception as e:  # noqa: BLE001 -- fall back to eager launches, same math
             print(f"bench: HIP graph capture failed ({str(e).splitlines()[0]}); running eagerly", file=sys.stderr)
             from sharetrade.ops import native as _native
@@ -116,6 +118,7 @@ def main() -> int:
             _native.clear_last_error()
             torch.cuda.synchronize()
             eng._graph, eng._graph_k, use_graph = None, None, False
+    prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()
     if world > 1:
@@ -165,7 +168,7 @@ def main() -> int:
     value = total_steps / el
     if rank == 0:
         st = stats.cpu().tolist()
-        n_trans = eng.E * world * (args.warmup + args.steps + (2 if use_graph else 0))
+        n_trans = eng.E * world * eng.step_count   # every step taken (prime + warmup + timed)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -193,6 +196,7 @@ def main() -> int:
                 "kernel_chunk": eng.chunk,
                 "chunk_schedule": getattr(eng, "chunk_schedule", "static"),
             },
+            "graph_prime_steps": prime_steps,
             "episode_return_mean": round(float(ret[0] / ret[1]), 4),
             "episode_return_window_steps": args.steps,
             "mean_reward_per_step": st[0] / max(n_trans, 1),

@@ -43,6 +43,31 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+_INC = None
+
+
+def _includes(path: str, seen=None):
+    """Every local ``#include "..."`` reachable from ``path`` (recursively), so an edit to
+    ``qstep_wide.hip`` rebuilds ``qstep_wide8.hip`` and its tuning variants that include it."""
+    import re
+
+    global _INC
+    if _INC is None:
+        _INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+    seen = set() if seen is None else seen
+    try:
+        with open(path) as f:
+            txt = f.read()
+    except OSError:
+        return seen
+    for name in _INC.findall(txt):
+        dep = os.path.normpath(os.path.join(os.path.dirname(path), name))
+        if dep not in seen and os.path.exists(dep):
+            seen.add(dep)
+            _includes(dep, seen)
+    return seen
+
+
 def _run(cmd):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
@@ -61,7 +86,7 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
     for s in srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(o, [s] + hdrs):
+        if force or _newer(o, [s] + hdrs + sorted(_includes(s))):
             todo.append((s, o))
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(lambda so: _run([HIPCC] + HIP_FLAGS + ["-c", so[0], "-o", so[1]]), todo))

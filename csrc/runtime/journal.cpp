@@ -25,6 +25,7 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -109,6 +110,24 @@ uint32_t record_crc(uint64_t seq, uint8_t type, const void* payload, size_t n) {
   return crc_mask(c);
 }
 
+// Exact snapshot file name "snapshot-<pid>-<seq:020>-<ts:020>.snap" (no extra characters): a plain
+// prefix match would let pid "x" claim the snapshots of pid "x-1".
+bool parse_snap_name(const std::string& nm, const std::string& prefix, long long* seq, long long* ts) {
+  constexpr size_t kW = 20;
+  if (nm.size() != prefix.size() + kW + 1 + kW + 5) return false;
+  if (nm.compare(0, prefix.size(), prefix) != 0) return false;
+  const char* p = nm.c_str() + prefix.size();
+  for (size_t i = 0; i < kW; ++i)
+    if (p[i] < '0' || p[i] > '9') return false;
+  if (p[kW] != '-') return false;
+  for (size_t i = 0; i < kW; ++i)
+    if (p[kW + 1 + i] < '0' || p[kW + 1 + i] > '9') return false;
+  if (std::memcmp(p + 2 * kW + 1, ".snap", 5) != 0) return false;
+  *seq = std::strtoll(std::string(p, kW).c_str(), nullptr, 10);
+  *ts = std::strtoll(std::string(p + kW + 1, kW).c_str(), nullptr, 10);
+  return true;
+}
+
 struct Record {
   uint64_t seq;
   uint8_t type;
@@ -188,6 +207,20 @@ void* st_journal_open(const char* dir, const char* pid, int fsync_mode) {
   return j;
 }
 
+// Write one framed buffer at the journal's end.  A failed write (e.g. ENOSPC part-way) is rolled
+// back -- the file is truncated to the offset before the append and the position reset -- so a later
+// successful append is never written behind a torn record (which recovery would truncate away).
+static bool write_or_rollback(Journal* j, const void* buf, size_t n) {
+  using namespace strt;
+  const off_t at = ::lseek(j->fd, 0, SEEK_CUR);
+  if (at < 0) return false;
+  if (write_all(j->fd, buf, n) && (j->fsync_mode != 1 || fdatasync(j->fd) == 0)) return true;
+  const int saved = errno;
+  if (ftruncate(j->fd, at) == 0) ::lseek(j->fd, at, SEEK_SET);
+  errno = saved;
+  return false;
+}
+
 static int64_t append_record(Journal* j, uint8_t type, uint64_t seq, const void* payload, size_t n) {
   using namespace strt;
   std::vector<uint8_t> buf(kRecHeader + n);
@@ -196,8 +229,7 @@ static int64_t append_record(Journal* j, uint8_t type, uint64_t seq, const void*
   put_u64(&buf[8], seq);
   buf[16] = type;
   if (n) std::memcpy(&buf[kRecHeader], payload, n);
-  if (!write_all(j->fd, buf.data(), buf.size())) return -1;
-  if (j->fsync_mode == 1 && fdatasync(j->fd) != 0) return -1;
+  if (!write_or_rollback(j, buf.data(), buf.size())) return -1;
   return (int64_t)seq;
 }
 
@@ -228,8 +260,7 @@ int64_t st_journal_append_batch(void* h, int count, const void* const* payloads,
     buf[o + 16] = 0;
     if (n) std::memcpy(&buf[o + kRecHeader], payloads[i], n);
   }
-  if (!write_all(j->fd, buf.data(), buf.size())) return -1;
-  if (j->fsync_mode == 1 && fdatasync(j->fd) != 0) return -1;
+  if (!write_or_rollback(j, buf.data(), buf.size())) return -1;
   j->highest = seq;
   return (int64_t)seq;
 }
@@ -339,10 +370,8 @@ int st_snapshot_latest(const char* dir, const char* pid, int64_t max_seq, int64_
   long long best_seq = -1, best_ts = -1;
   while (dirent* e = readdir(d)) {
     std::string nm = e->d_name;
-    if (nm.compare(0, prefix.size(), prefix) != 0) continue;
-    if (nm.size() < 5 || nm.compare(nm.size() - 5, 5, ".snap") != 0) continue;
     long long s = -1, t = -1;
-    if (std::sscanf(nm.c_str() + prefix.size(), "%lld-%lld", &s, &t) != 2) continue;
+    if (!parse_snap_name(nm, prefix, &s, &t)) continue;
     if (max_seq >= 0 && s > max_seq) continue;
     if (s > best_seq || (s == best_seq && t > best_ts)) {
       std::vector<uint8_t> img;
@@ -387,9 +416,8 @@ int st_snapshot_delete_to(const char* dir, const char* pid, int64_t max_seq) {
   std::vector<std::string> victims;
   while (dirent* e = readdir(d)) {
     std::string nm = e->d_name;
-    if (nm.compare(0, prefix.size(), prefix) != 0) continue;
     long long s = -1, t = -1;
-    if (std::sscanf(nm.c_str() + prefix.size(), "%lld-%lld", &s, &t) != 2) continue;
+    if (!strt::parse_snap_name(nm, prefix, &s, &t)) continue;
     if (s <= max_seq) victims.push_back(std::string(dir) + "/" + nm);
   }
   closedir(d);

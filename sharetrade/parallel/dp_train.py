@@ -20,7 +20,7 @@ import torch
 from ..config import Config
 from ..persist import checkpoint as ck
 from . import dist as D
-from .elastic import Heartbeat, fail_point
+from .elastic import Heartbeat, fail_point, heartbeat_store
 
 
 def committed_steps(ckpt_dir: str):
@@ -59,7 +59,7 @@ def dp_worker(rank: int, world: int, generation: int, cfg_dict: Dict[str, Any], 
     ctx = D.init(backend=backend or ("gloo" if device == "cpu" else None), device=device)
     hb = None
     try:
-        store = torch.distributed.distributed_c10d._get_default_store() if ctx.is_distributed else None
+        store = heartbeat_store()   # hosted by ElasticRunner's watchdog
         hb = Heartbeat(store, rank, generation).start() if store is not None else None
     except Exception:  # noqa: BLE001
         hb = None
@@ -77,6 +77,8 @@ def dp_worker(rank: int, world: int, generation: int, cfg_dict: Dict[str, Any], 
         eng.load_state_dict(state)
     eng.sync_params_from(0)        # re-dispatch: every rank continues from rank 0's learner state
     for step in range(start, steps):
+        if hb is not None:
+            hb.progress(step)
         fail_point(rank, step, generation)
         eng.step()
         s = step + 1

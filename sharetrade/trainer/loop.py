@@ -21,11 +21,17 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
           ckpt_every: int = 0, resume: bool = False, trace_path: Optional[str] = None, graph: bool = True,
           rank: int = 0, world_size: int = 1, group=None) -> Dict[str, Any]:
     eng = VectorEngine(cfg, device=device, envs=envs, rank=rank, world_size=world_size, group=group)
-    mgr = CheckpointManager(ckpt_dir, interval=ckpt_every) if ckpt_dir else None
-    if mgr and resume:
-        p = mgr.latest()
-        if p:
-            st, _ = load_ckpt(p)
+    # one process: CheckpointManager files; several ranks: one shard per rank per step, committed by
+    # rank 0 after a barrier (parallel/dp_train.py) -- every rank owns different envs / price banks
+    sharded = world_size > 1
+    mgr = CheckpointManager(ckpt_dir, interval=ckpt_every) if ckpt_dir and not sharded else None
+    if ckpt_dir and resume:
+        if sharded:
+            st = _load_committed_shard(ckpt_dir, rank, eng.device, group)
+            if st is not None:
+                eng.load_state_dict(st)
+        elif mgr.latest():
+            st, _ = load_ckpt(mgr.latest())
             eng.load_state_dict(st)
     eng.sync_params_from(0)
     if graph and eng.backend == "native" and world_size == 1:
@@ -55,9 +61,11 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
                 if ms is not None:
                     rec["allreduce_ms"] = ms
             ml.log(rec)
-        if mgr and mgr.should_save(s) and rank == 0:
+        if mgr and mgr.should_save(s):
             eng.synchronize()
             mgr.save(s, eng.state_dict(), {"kind": "VectorEngine"})
+        elif sharded and ckpt_dir and ckpt_every and s % ckpt_every == 0:
+            _save_sharded(ckpt_dir, s, rank, world_size, eng, group)
     eng.synchronize()
     dt = time.perf_counter() - t0
     if prof is not None:
@@ -68,3 +76,40 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
     return {"backend": eng.backend, "kernel": eng.kernel, "envs": eng.E, "steps": steps,
             "env_steps_per_s": eng.E * world_size * steps / dt, "seconds": dt, **eng.stats_dict(),
             **eng.portfolio_summary()}
+
+
+def _save_sharded(ckpt_dir: str, step: int, rank: int, world: int, eng: VectorEngine, group, keep: int = 3) -> None:
+    """Every rank writes its shard (``state_dict`` -- and so ``flush_pending`` -- runs on every rank,
+    keeping the overlapped-DP schedule identical across ranks); rank 0 commits after a barrier."""
+    import shutil
+
+    import torch.distributed as dist
+
+    from ..parallel.dp_train import commit, committed_steps, save_shard
+
+    eng.synchronize()
+    save_shard(ckpt_dir, step, rank, eng)
+    dist.barrier(group=group)
+    if rank == 0:
+        commit(ckpt_dir, step, world)
+        for old in committed_steps(ckpt_dir)[:-keep]:
+            shutil.rmtree(os.path.join(ckpt_dir, f"step-{old:09d}"), ignore_errors=True)
+    dist.barrier(group=group)
+
+
+def _load_committed_shard(ckpt_dir: str, rank: int, device: torch.device, group):
+    """This rank's shard of the newest step every rank sees committed (MIN over ranks)."""
+    import torch.distributed as dist
+
+    from ..parallel.dp_train import committed_steps
+
+    done = committed_steps(ckpt_dir)
+    t = torch.tensor([done[-1] if done else -1], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    step = int(t[0])
+    if step < 0:
+        return None
+    st, meta = load_ckpt(os.path.join(ckpt_dir, f"step-{step:09d}", f"rank-{rank}.stck"))
+    if int(meta.get("rank", rank)) != rank:
+        raise RuntimeError(f"shard for rank {rank} holds rank {meta.get('rank')}")
+    return st

@@ -66,3 +66,37 @@ def test_heartbeat_watchdog_flags_stale_rank():
     wd.stop()
     hb0.stop()
     assert dead == [1]
+
+
+def test_hung_rank_is_detected_by_watchdog_and_recovered():
+    """A rank that hangs (alive, heartbeat thread beating, main loop stuck) is flagged by the
+    launcher's progress watchdog within seconds -- not the generation timeout -- and the
+    respawned generation finishes bit-identically to an uninterrupted run."""
+    import time
+
+    ref, ref_f = _run(2, 8)
+    d = tempfile.mkdtemp()
+    t0 = time.monotonic()
+    r = ElasticRunner(dp_worker, 2, args=(_cfg(), 8, os.path.join(d, "ckpt"), 3, 3, os.path.join(d, "out")),
+                      max_restarts=2, env={"SHARETRADE_HANG_AT": "0:4"}, stall_timeout_s=3.0,
+                      gen_timeout_s=300.0).run()
+    assert r.ok and r.restarts == 1
+    assert (0, 0) in r.flagged or (0, 1) in r.flagged   # rank 0 hung; rank 1 blocks in its collective
+    assert time.monotonic() - t0 < 120
+    got_f = [ck.load(os.path.join(d, "out", f"final-rank-{k}.stck"))[0] for k in range(2)]
+    for a, b in zip(ref_f, got_f):
+        assert torch.equal(a["params"], b["params"])
+        assert torch.equal(a["env_pos"], b["env_pos"])
+
+
+def test_watchdog_flags_stalled_progress():
+    import time
+
+    store = torch.distributed.HashStore()
+    hb = Heartbeat(store, 0, interval_s=0.05).start()    # alive ...
+    hb.progress(3)                                        # ... but never advances past step 3
+    wd = Watchdog(store, 1, timeout_s=5.0, poll_s=0.05, stall_timeout_s=0.3).start()
+    time.sleep(0.8)
+    wd.stop()
+    hb.stop()
+    assert wd.dead == [0]

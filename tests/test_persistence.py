@@ -230,3 +230,56 @@ def test_price_getter_file_journal_recovery(tmp_path):
 
 def _true(c):
     assert c
+
+
+def test_snapshot_names_do_not_collide_across_pids(tmp_path):
+    """pid "x" must not load or delete the snapshots of pid "x-1" (exact name match)."""
+    s = LocalSnapshotStore(str(tmp_path / "snaps"))
+    s.save("x-1", 7, {"who": "x-1"}, timestamp=10)
+    assert s.load_latest("x") is None
+    s.save("x", 3, {"who": "x"}, timestamp=11)
+    assert s.load_latest("x").snapshot == {"who": "x"}
+    assert s.delete_to("x", 100) == 1
+    assert s.load_latest("x-1").snapshot == {"who": "x-1"}
+
+
+_FSIZE_CHILD = r"""
+import os, resource, signal, sys
+sys.path.insert(0, sys.argv[2])
+from sharetrade import protocol as P
+from sharetrade.persist.journal import FileJournal
+d = sys.argv[1]
+j = FileJournal(d)
+j.append("p", [P.Event("S0", {})])
+size = os.path.getsize(os.path.join(d, "p.journal"))
+signal.signal(signal.SIGXFSZ, signal.SIG_IGN)
+soft, hard = resource.getrlimit(resource.RLIMIT_FSIZE)
+resource.setrlimit(resource.RLIMIT_FSIZE, (size + 40, hard))   # the next big record is cut part-way (EFBIG)
+import datetime as dt
+try:
+    j.append("p", [P.Event("BIG", {dt.date(2000, 1, 1) + dt.timedelta(days=i): float(i) for i in range(200)})])
+    print("no-error")
+except Exception:
+    print("append-failed")
+assert os.path.getsize(os.path.join(d, "p.journal")) == size, "torn bytes left behind"
+resource.setrlimit(resource.RLIMIT_FSIZE, (soft, hard))
+j.append("p", [P.Event("S1", {})])
+j.close()
+"""
+
+
+def test_failed_append_is_rolled_back(tmp_path):
+    """A write that fails part-way (file-size limit ~ ENOSPC) leaves no torn record: the next
+    acknowledged append survives recovery."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = str(tmp_path / "j")
+    r = subprocess.run([sys.executable, "-c", _FSIZE_CHILD, d, root], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "append-failed" in r.stdout
+    j = FileJournal(d)
+    assert [e.stock_name for _, e in j.replay("p")] == ["S0", "S1"]
+    assert j.truncated_bytes("p") == 0
+    j.close()
