@@ -47,6 +47,8 @@ def main() -> int:
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on cuda:0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
+    ap.add_argument("--step-kernel", default="auto",
+                    help="fused step kernel: auto | wide (64-env chunks) | pair (two 32-env slots in flight) | narrow")
     ap.add_argument("--step-waves", type=int, default=8, help="64-env-chunk kernel: waves per workgroup (4 or 8)")
     ap.add_argument("--step-variant", default="", help="tuning build of the 64-env-chunk kernel (suffix)")
     ap.add_argument("--chunk", type=int, default=0,
@@ -98,6 +100,7 @@ def main() -> int:
     cfg.engine.dp_overlap = bool(args.dp_overlap) and world > 1
     cfg.engine.chunk = args.chunk
     cfg.engine.step_waves = args.step_waves
+    cfg.engine.step_kernel = args.step_kernel
     cfg.engine.step_variant = args.step_variant
     cfg.engine.chunk_schedule = args.chunk_schedule
     if args.graph_steps:
@@ -194,6 +197,7 @@ def main() -> int:
                 "hip_graph": use_graph,
                 "graph_steps": cfg.engine.graph_steps if use_graph else None,
                 "kernel_chunk": eng.chunk,
+                "step_kernel": getattr(eng, "step_kernel", None),
                 "chunk_schedule": getattr(eng, "chunk_schedule", "static"),
             },
             "graph_prime_steps": prime_steps,

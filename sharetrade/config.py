@@ -148,6 +148,10 @@ class EngineConfig:
     # 64 = csrc/qstep_wide.hip (layer-1 weights in VGPRs), 32 = csrc/qstep_fused.hip (weights in LDS)
     chunk: int = 0
     step_waves: int = 8             # 64-env-chunk kernel: 8 waves (two per SIMD, measured fastest) or 4
+    # fused bf16 step kernel: "auto" (by chunk), "wide" (csrc/qstep_wide.hip, 64-env chunks),
+    # "narrow" (csrc/qstep_fused.hip, 32-env chunks) or "pair" (csrc/qstep_pair.hip: two 32-env chunks
+    # in flight per workgroup, five phases apart; E % 64 == 0, static schedule)
+    step_kernel: str = "auto"
     step_variant: str = ""          # tuning builds of the 64-env-chunk kernel (st_qstep_wide_launch_<v>); "" = default
     graph: bool = True              # capture the step in a HIP graph
     graph_steps: int = 16           # steps per graph replay in VectorEngine.run (fewer launch boundaries)

@@ -92,6 +92,10 @@ def lib() -> C.CDLL:
     L.st_qstep_wide_lds_bytes.restype = C.c_int
     L.st_qstep_wide_launch_w8.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_qstep_wide_launch_w8.restype = C.c_int
+    L.st_qstep_pair_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_qstep_pair_launch.restype = C.c_int
+    L.st_qstep_pair_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.st_qstep_pair_lds_bytes.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
     L.st_reduce_optim.restype = C.c_int
     L.st_advance.argtypes = [C.c_void_p, C.c_void_p]
@@ -152,6 +156,13 @@ def qstep_wide_supported(inp: int, h1p: int, h2p: int) -> bool:
     if not available():
         return False
     return lib().st_qstep_wide_lds_bytes(inp, h1p, h2p) > 0
+
+
+def qstep_pair_supported(inp: int, h1p: int, h2p: int) -> bool:
+    """Two-slot pipelined variant (csrc/qstep_pair.hip: two 32-env chunks in flight per workgroup)."""
+    if not available():
+        return False
+    return lib().st_qstep_pair_lds_bytes(inp, h1p, h2p) > 0
 
 
 def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float, key0: int, key1: int) -> None:

@@ -127,9 +127,20 @@ class VectorEngine:
             # bf16: the fused MFMA step kernel (csrc/qstep_fused.hip);
             # fp32: the exact-fp32 row kernels (csrc/mlp_f32.hip) — any MLP up to 6 layers x 1024
             self.kernel = "bf16_fused" if fused_ok else "fp32_rows"
-        # envs per chunk of the fused kernel: 64 -> csrc/qstep_wide.hip, 32 -> csrc/qstep_fused.hip
+        # envs per chunk of the fused kernel: 64 -> csrc/qstep_wide.hip, 32 -> csrc/qstep_fused.hip;
+        # step_kernel "pair" -> csrc/qstep_pair.hip (two 32-env slots per workgroup: chunk = 64 envs of
+        # work per workgroup and cycle)
         self.chunk = 32
-        if self.kernel == "bf16_fused":
+        self.step_kernel = "narrow"
+        sk = cfg.engine.step_kernel
+        if sk not in ("auto", "wide", "narrow", "pair"):
+            raise ValueError(f"engine.step_kernel: {sk!r}")
+        if self.kernel == "bf16_fused" and sk == "pair":
+            if not (self.E % 64 == 0 and native.qstep_pair_supported(L.pdims[0], L.pdims[1], L.pdims[2])):
+                raise NotImplementedError(f"engine.step_kernel='pair' needs E % 64 == 0 and padded dims "
+                                          f"(224, 128, 128); got E={self.E}, dims {L.pdims}")
+            self.chunk, self.step_kernel = 64, "pair"
+        elif self.kernel == "bf16_fused":
             want = int(cfg.engine.chunk)
             wide_ok = self.E % 64 == 0 and native.qstep_wide_supported(L.pdims[0], L.pdims[1], L.pdims[2])
             if want == 64 and not wide_ok:
@@ -139,7 +150,15 @@ class VectorEngine:
                 raise ValueError(f"engine.step_waves must be 4 or 8, got {cfg.engine.step_waves}")
             if want not in (0, 32, 64):
                 raise ValueError(f"engine.chunk must be 0 (auto), 32 or 64, got {want}")
+            if sk == "wide":
+                want = 64
+            elif sk == "narrow":
+                want = 32
+            if want == 64 and not wide_ok:
+                raise NotImplementedError(f"the 64-env-chunk kernel needs E % 64 == 0 and padded dims "
+                                          f"(224, 128, 128); got E={self.E}, dims {L.pdims}")
             self.chunk = 64 if (want in (0, 64) and wide_ok) else 32
+            self.step_kernel = "wide" if self.chunk == 64 else "narrow"
         # ------------------------------------------------------------ data
         if prices is not None:
             bank = padded_bank(prices.shape[0], prices.shape[1], self.device)
@@ -229,7 +248,7 @@ class VectorEngine:
             raise ValueError(f"engine.chunk_schedule: {sched!r}")
         # dynamic: 8 per-XCD claim heads, one per 128-byte line (csrc/qstep_wide.hip); needs the
         # 64-env-chunk kernel, grid % 8 == 0 and (E / 64) % 8 == 0, else the static schedule is used
-        dyn_ok = self.chunk == 64 and self.grid % 8 == 0 and (self.E // 64) % 8 == 0
+        dyn_ok = self.step_kernel == "wide" and self.grid % 8 == 0 and (self.E // 64) % 8 == 0
         self.chunk_schedule = "dynamic" if (sched == "dynamic" and dyn_ok) else "static"
         self.chunk_heads = (torch.zeros(8 * 32, dtype=torch.int32, device=dev)
                             if self.chunk_schedule == "dynamic" else None)
@@ -303,7 +322,9 @@ class VectorEngine:
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
 
     def _launch_qstep(self, L, sh) -> None:
-        if self.chunk == 64:
+        if self.step_kernel == "pair":
+            fn = L.st_qstep_pair_launch
+        elif self.chunk == 64:
             fn = L.st_qstep_wide_launch_w8 if self.cfg.engine.step_waves == 8 else L.st_qstep_wide_launch
             if self.cfg.engine.step_variant:   # tuning builds (csrc/qstep_wide8_<v>.hip), same contract
                 fn = native.variant_launch(self.cfg.engine.step_variant)

@@ -385,3 +385,64 @@ def test_large_bank_gather_matches_oracle(native_built):
     assert torch.equal(info["reward"], eng.rewards_out[sub].cpu())
     for k in ("budget", "shares", "value", "pos"):
         assert torch.equal(getattr(ns, k), getattr(eng.state, k)[sub].cpu()), k
+
+
+@pytest.mark.parametrize("compat", [False, True])
+@pytest.mark.parametrize("E,grid", [(512, 0), (448, 3), (64 * 20, 4), (4096, 0)])
+def test_pair_kernel_matches_wide(native_built, compat, E, grid):
+    """csrc/qstep_pair.hip (two 32-env chunk slots in flight, five phases apart) vs csrc/qstep_wide.hip
+    on the same state: identical env transitions, actions and rewards, gradients and statistics equal
+    up to fp32 summation order.  Small grids give several pipeline cycles per workgroup and slots
+    with unequal chunk counts (pipeline fill and drain)."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for sk in ("wide", "pair"):
+        cfg = _cfg(compat)
+        cfg.agent.epsilon = 0.5
+        cfg.engine.step_kernel = sk
+        cfg.engine.grid = grid
+        cfg.engine.slab_dtype = "fp32"
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.step_kernel == sk
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
+        eng.state.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
+        eng.state.pos[::97] = prices.shape[1] - cfg.model.history - 1    # some episodes end this step
+        eng.ctrl.fill_(9)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        out[sk] = (g, eng.actions_out.cpu().clone(), eng.rewards_out.cpu().clone(),
+                   {k: v.cpu().clone() for k, v in eng.state.as_dict().items()}, eng.stat_slab.sum(0).cpu())
+    gw, aw, rw, sw, stw = out["wide"]
+    gp, ap, rp, sp, stp = out["pair"]
+    assert torch.equal(aw, ap) and torch.equal(rw, rp)
+    for k in sw:
+        assert torch.equal(sw[k].nan_to_num(-1.0), sp[k].nan_to_num(-1.0)), k
+    assert _rel(gp, gw) < 1e-4, _rel(gp, gw)
+    assert torch.allclose(stp, stw, rtol=1e-4, atol=1e-3), (stp, stw)
+
+
+def test_pair_kernel_multi_step_bf16_slabs(native_built):
+    """Pair kernel through the default bf16 slabs and the optimizer over several graph-replayed steps:
+    tracks the wide kernel (same actions every step while the parameters agree to bf16 rounding)."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 64 * 64
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    res = {}
+    for sk in ("wide", "pair"):
+        cfg = _cfg(False)
+        cfg.engine.step_kernel = sk
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        eng.capture_graph(warmup=1, graph_steps=4)
+        eng.run(9)
+        torch.cuda.synchronize()
+        res[sk] = (eng.params.cpu().clone(), eng.state.pos.cpu().clone(), eng.stats_dict())
+    pw, posw, stw = res["wide"]
+    pp, posp, stp = res["pair"]
+    assert torch.equal(posw, posp)
+    assert _rel(pp, pw) < 1e-3, _rel(pp, pw)
+    assert abs(stp["explore"] - stw["explore"]) <= 0.01 * max(1.0, stw["explore"])
