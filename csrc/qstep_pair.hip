@@ -21,9 +21,10 @@
 // the same registers.  Per-slot LDS: the activation images of one 32-env chunk (~60 KB); two slots
 // + weights = 163,168 of the 163,840 bytes a workgroup may declare.
 //
-// The epsilon-greedy draw (Philox) is computed in P0 by the row-owner lanes (it depends only on the
-// env id, the step and the env position), taking ~60 dependent VALU ops off the P3 critical path;
-// P3 only resolves exploit ? argmax : random action.  Same draws, same actions as the other kernels.
+// The epsilon-greedy draw (Philox) is computed in P1 by one wave for the whole chunk (it depends only
+// on the env id, the step and the env position), taking ~60 dependent VALU ops off the P3 critical
+// path; P3 only resolves exploit ? argmax : random action.  Same draws, same actions as the other
+// kernels.
 //
 // Pipeline fill / drain: every interval runs both slots unconditionally (one basic block per
 // interval, no uniform branches around the phases); a slot without a chunk computes on a clamped
@@ -45,6 +46,12 @@ constexpr int ENVF = 6;          // fp32 words per env in sEnv
 #define ST_PAIR_DW0_PIPE 3
 #endif
 constexpr int DW0_PIPE = ST_PAIR_DW0_PIPE;
+#ifndef ST_PAIR_STAGGER
+#define ST_PAIR_STAGGER 0   // 1: duplicated phase code per wave half -- 134 VGPR spills, not usable
+#endif
+#ifndef ST_PAIR_PRIO
+#define ST_PAIR_PRIO 0      // 1: waves 4-7 at s_setprio 1 through the chunk loop -- measured no gain
+#endif
 
 // activation images: 16-byte unit of column c of row r stored at c ^ 8 * bit2(r) (see qstep_wide.hip)
 ST_DEV int asw(int r, int lo) { return lo ^ ((r & 4) << 1); }
@@ -184,18 +191,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
   float* const sB2 = reinterpret_cast<float*>(smem + G::fB2);
   float* const sSt = reinterpret_cast<float*>(smem + G::fST);
 
-  const int tid = threadIdx.x;
-  int lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
-  // lane ids re-derived behind an opaque move at every barrier interval: without it hipcc hoists every
-  // lane-dependent LDS address of both slots out of the chunk loop (slot 1 lies past the 64 KB
-  // ds-offset reach, so each needs its own register) and spills them across the loop
-  auto refresh = [&]() {
-    int t = tid;
-    asm volatile("" : "+v"(t));
-    lane = t & 63;
-    l16 = lane & 15;
-    g4 = lane >> 4;
-  };
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.H;
   const unsigned long long step = p.ctrl[0];
@@ -286,20 +282,30 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
   STP_STAMPX(1);
 
   // ================================================================ phases (slot S = compile time)
-  auto sbf = [&](auto s) { return reinterpret_cast<bf16_t*>(smem + G::SLOT0 + decltype(s)::v * G::SLOT_BYTES); };
-  auto sfl = [&](auto s, int off) { return reinterpret_cast<float*>(smem + G::SLOT0 + decltype(s)::v * G::SLOT_BYTES + off); };
+  // Slot base: an opaque scalar, re-materialised once per phase.  Every lane-dependent LDS address is
+  // then (lane part, loop-invariant and shared by both slots) + (slot base, SGPR) + (immediate < 64 KB);
+  // with compile-time slot bases hipcc hoisted a separate address register per image, pattern and slot
+  // out of the chunk loop (slot 1 lies past the 64 KB ds-offset reach) and spilled them.
+  auto slot_base = [&](auto s) {
+    int o = G::SLOT0 + decltype(s)::v * G::SLOT_BYTES;
+    asm volatile("" : "+s"(o));
+    return smem + o;
+  };
 
-  // P0: windows -> feature rows x, x'; env scalars -> LDS; epsilon-greedy draw (row-owner lanes)
-  auto P0 = [&](auto s, int ch) {
+#define SB_BF(SB, OFF) (reinterpret_cast<bf16_t*>(SB) + (OFF))
+#define SB_FL(SB, OFF) (reinterpret_cast<float*>((SB) + (OFF)))
+#define SB_IN(SB, OFF) (reinterpret_cast<int*>((SB) + (OFF)))
+  // P0: windows -> feature rows x, x'; env scalars -> LDS (row-owner lanes)
+  auto P0 = [&](auto s) {
     constexpr int S = decltype(s)::v;
-    bf16_t* sX = sbf(s) + G::oX;
-    bf16_t* sR0 = sbf(s) + G::oR0;
-    float* sEnv = sfl(s, G::fENV);
-    int* sEnvI = reinterpret_cast<int*>(sfl(s, G::fENVI));
+    char* const sb = slot_base(s);
+    bf16_t* sX = SB_BF(sb, G::oX);
+    bf16_t* sR0 = SB_BF(sb, G::oR0);
+    float* sEnv = SB_FL(sb, G::fENV);
+    int* sEnvI = SB_IN(sb, G::fENVI);
     float r_inv = 0.f, r_invn = 0.f;
     if (lane < RPW) {
       const int r = wave * RPW + lane;
-      const int e = min(ch, nch - 1) * C + r;
       sEnv[r * ENVF + 0] = e_b[S];
       sEnv[r * ENVF + 1] = e_val[S];
       sEnv[r * ENVF + 2] = wv[S];
@@ -309,15 +315,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
       sEnvI[r * 4 + 3] = e_ep[S];
       r_inv = __fdiv_rn(1.0f, wl[S]);
       r_invn = __fdiv_rn(1.0f, wv[S]);
-      // epsilon-greedy draw: exploit flag (bit 3) + random action (bits 0-1)
-      uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
-               c2 = (uint32_t)(step >> 32), c3 = 0u;
-      philox4x32(c0, c1, c2, c3, p.key0, p.key1);
-      const float u1 = u24(c0), u2 = u24(c1);
-      const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)e_pos[S], p.inv_ramp));
-      int rnd = (int)(u2 * 3.0f);
-      rnd = rnd > 2 ? 2 : rnd;
-      sEnvI[r * 4 + 2] = rnd | (exploit ? 8 : 0);
     }
     if (lane < INP / 4) {
       bf16_t* px = sX + (wave * RPW) * G::SX + 4 * lane;
@@ -349,18 +346,47 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
   };
   auto a_w0 = [&](int ks) { return aW0[ks]; };
   auto a_w1 = [&](int ks) { return frag_row(sW1, G::SW1, m0, ks * 32, l16, g4); };
-  // P1 / P2: hidden layers of Q(x); P4 / P5: of Q(x')
-  auto P1 = [&](auto s) { fwd_hidden<INP, G::SX, G::SH1>(a_w0, sbf(s) + G::oX, sbf(s) + G::oH1, nullptr, m0, l16, g4); };
-  auto P2 = [&](auto s) { fwd_hidden<H1P, G::SH1, G::SH2>(a_w1, sbf(s) + G::oH1, sbf(s) + G::oH2, sB1, m0, l16, g4); };
-  auto P4 = [&](auto s) { fwd_hidden<INP, G::SX, G::SH1>(a_w0, sbf(s) + G::oR0, sbf(s) + G::oR1, nullptr, m0, l16, g4); };
-  auto P5 = [&](auto s) { fwd_hidden<H1P, G::SH1, G::SH2>(a_w1, sbf(s) + G::oR1, sbf(s) + G::oR0, sB1, m0, l16, g4); };
+  // P1 / P2: hidden layers of Q(x); P4 / P5: of Q(x').  P1 also draws the chunk's epsilon-greedy
+  // decisions on ONE wave (DRAW_WAVE, lanes = the 32 envs; its SIMD partner is not a P3 / P6 wave):
+  // Philox is ~60 dependent VALU ops with quarter-rate multiplies, paid once per chunk instead of by
+  // every wave's row-owner lanes; P3 reads the result two intervals later.
+  constexpr int DRAW_WAVE = 2;
+  auto P1 = [&](auto s, int ch) {
+    char* const sb = slot_base(s);
+    if (wave == DRAW_WAVE && lane < C) {
+      int* sEnvI = SB_IN(sb, G::fENVI);
+      const int pos = sEnvI[lane * 4 + 0];
+      uint32_t c0 = (uint32_t)(p.env_offset + ch * C + lane), c1 = (uint32_t)(step & 0xFFFFFFFFull),
+               c2 = (uint32_t)(step >> 32), c3 = 0u;
+      philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+      const float u1 = u24(c0), u2 = u24(c1);
+      const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
+      int rnd = (int)(u2 * 3.0f);
+      rnd = rnd > 2 ? 2 : rnd;
+      sEnvI[lane * 4 + 2] = rnd | (exploit ? 8 : 0);   // exploit flag (bit 3) + random action
+    }
+    fwd_hidden<INP, G::SX, G::SH1>(a_w0, SB_BF(sb, G::oX), SB_BF(sb, G::oH1), nullptr, m0, l16, g4);
+  };
+  auto P2 = [&](auto s) {
+    char* const sb = slot_base(s);
+    fwd_hidden<H1P, G::SH1, G::SH2>(a_w1, SB_BF(sb, G::oH1), SB_BF(sb, G::oH2), sB1, m0, l16, g4);
+  };
+  auto P4 = [&](auto s) {
+    char* const sb = slot_base(s);
+    fwd_hidden<INP, G::SX, G::SH1>(a_w0, SB_BF(sb, G::oR0), SB_BF(sb, G::oR1), nullptr, m0, l16, g4);
+  };
+  auto P5 = [&](auto s) {
+    char* const sb = slot_base(s);
+    fwd_hidden<H1P, G::SH1, G::SH2>(a_w1, SB_BF(sb, G::oR1), SB_BF(sb, G::oR0), sB1, m0, l16, g4);
+  };
   // P3: Q(x), action, Buy/Sell/Hold env step, x' tail (waves < NET; lanes g4 == 0 own env 16w + l16)
   auto P3 = [&](auto s, int ch, bool valid) {
     if (wave >= NET) return;
-    float* sQ = sfl(s, G::fQ);
-    float* sEnv = sfl(s, G::fENV);
-    int* sEnvI = reinterpret_cast<int*>(sfl(s, G::fENVI));
-    const f4v qa = fwd_out<H2P, G::SW2, G::SH2>(sW2, sbf(s) + G::oH2, wave, l16, g4);
+    char* const sb = slot_base(s);
+    float* sQ = SB_FL(sb, G::fQ);
+    float* sEnv = SB_FL(sb, G::fENV);
+    int* sEnvI = SB_IN(sb, G::fENVI);
+    const f4v qa = fwd_out<H2P, G::SW2, G::SH2>(sW2, SB_BF(sb, G::oH2), wave, l16, g4);
     if (g4 == 0) {
       const int r = 16 * wave + l16, e = ch * C + r;
       float q[3];
@@ -395,7 +421,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
       sEnv[r * ENVF + 4] = rew;
       sEnvI[r * 4 + 1] = s2;
       sEnvI[r * 4 + 2] = a | (exploit ? 0 : 4);
-      bf16_t* xn = sbf(s) + G::oR0 + r * G::SX;
+      bf16_t* xn = SB_BF(sb, G::oR0) + r * G::SX;
       xn[(H & ~15) + asw(r, H & 15)] = f2bf(feat_budget(b2, p.inv_b0, FEAT));
       xn[((H + 1) & ~15) + asw(r, (H + 1) & 15)] = f2bf(feat_shares(s2, vnew, p.inv_b0, FEAT));
       xn[((H + 2) & ~15) + asw(r, (H + 2) & 15)] = f2bf(1.0f);
@@ -408,10 +434,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
   // P6: Q(x'), TD target, dQ row, env state write-back, per-env statistics -> LDS
   auto P6 = [&](auto s, int ch, bool valid) {
     if (wave >= NET) return;
-    float* sQ = sfl(s, G::fQ);
-    float* sEnv = sfl(s, G::fENV);
-    int* sEnvI = reinterpret_cast<int*>(sfl(s, G::fENVI));
-    const f4v qn = fwd_out<H2P, G::SW2, G::SH2>(sW2, sbf(s) + G::oR0, wave, l16, g4);
+    char* const sb = slot_base(s);
+    float* sQ = SB_FL(sb, G::fQ);
+    float* sEnv = SB_FL(sb, G::fENV);
+    int* sEnvI = SB_IN(sb, G::fENVI);
+    const f4v qn = fwd_out<H2P, G::SW2, G::SH2>(sW2, SB_BF(sb, G::oR0), wave, l16, g4);
     if (g4 == 0) {
       const int r = 16 * wave + l16, e = ch * C + r;
       float n[3];
@@ -434,7 +461,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
       if ((p.output_relu && !(qs > 0.f)) || !valid) dq = 0.f;
       const uint32_t dqb = (uint32_t)f2bf(dq);
       const uint32_t wd0 = (slot == 0) ? dqb : (slot == 1) ? (dqb << 16) : 0u, wd1 = (slot == 2) ? dqb : 0u;
-      uint4* dqr = reinterpret_cast<uint4*>(sbf(s) + G::oDQ + r * SQ);
+      uint4* dqr = reinterpret_cast<uint4*>(SB_BF(sb, G::oDQ) + r * SQ);
       dqr[0] = make_uint4(wd0, wd1, 0u, 0u);
       dqr[1] = make_uint4(0u, 0u, 0u, 0u);
       const float b2 = sEnv[r * ENVF + 3], vnew = sEnv[r * ENVF + 2];
@@ -476,42 +503,40 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
   };
   // P7: statistics fold (waves NET..NET+3), layer-2 data backward + dW2 / db2
   auto P7 = [&](auto s) {
+    char* const sb = slot_base(s);
     {
       const int sw = wave - NET;
-      int ln = tid;
-      asm volatile("" : "+v"(ln));
-      ln &= 63;
-      const float* sQ = sfl(s, G::fQ);
-      const float* sEnv = sfl(s, G::fENV);
       // selects, not branches on the accumulators (a branch per accumulator made hipcc address
       // sa0 / sa1 through the stack)
       float x0 = 0.f, x1 = 0.f;
-      if (sw >= 0 && sw < 4 && ln < C) {
-        const f4v q = *reinterpret_cast<const f4v*>(sQ + ln * 4);
-        const float f0 = sEnv[ln * ENVF + 0], f1 = sEnv[ln * ENVF + 1];
+      if (sw >= 0 && sw < 4 && lane < C) {
+        const f4v q = *reinterpret_cast<const f4v*>(SB_FL(sb, G::fQ) + lane * 4);
+        const float f0 = SB_FL(sb, G::fENV)[lane * ENVF + 0], f1 = SB_FL(sb, G::fENV)[lane * ENVF + 1];
         x0 = sw == 0 ? q[0] : sw == 1 ? q[2] : sw == 2 ? f0 : f1;
         x1 = sw == 0 ? q[1] : sw == 1 ? q[3] : sw == 2 ? f0 * f0 : 0.f;
       }
       sa0 += x0;
       sa1 += x1;
     }
-    bwd_data<OUTP, G::SW2, SQ, G::SH2, G::SH2>(sW2, sbf(s) + G::oDQ, sbf(s) + G::oH2, sbf(s) + G::oR0, m0, l16, g4);
-    const s8v aq = frag_trp(sbf(s) + G::oDQ, SQ, 0, 0, l16, g4);
-    gW2 = mfma32(aq, afrag_trp(sbf(s) + G::oH2, G::SH2, 0, m0, l16, g4), gW2);
+    bwd_data<OUTP, G::SW2, SQ, G::SH2, G::SH2>(sW2, SB_BF(sb, G::oDQ), SB_BF(sb, G::oH2), SB_BF(sb, G::oR0), m0, l16, g4);
+    const s8v aq = frag_trp(SB_BF(sb, G::oDQ), SQ, 0, 0, l16, g4);
+    gW2 = mfma32(aq, afrag_trp(SB_BF(sb, G::oH2), G::SH2, 0, m0, l16, g4), gW2);
     gB2 = mfma32(aq, ones, gB2);
   };
   // P8: layer-1 data backward + dW1 / db1 (dZ2 = R0, H1)
   auto P8 = [&](auto s) {
-    bwd_data<H2P, G::SW1, G::SH2, G::SH1, G::SH1>(sW1, sbf(s) + G::oR0, sbf(s) + G::oH1, sbf(s) + G::oR1, m0, l16, g4);
-    const s8v a2 = afrag_trp(sbf(s) + G::oR0, G::SH2, 0, m0, l16, g4);
+    char* const sb = slot_base(s);
+    bwd_data<H2P, G::SW1, G::SH2, G::SH1, G::SH1>(sW1, SB_BF(sb, G::oR0), SB_BF(sb, G::oH1), SB_BF(sb, G::oR1), m0, l16, g4);
+    const s8v a2 = afrag_trp(SB_BF(sb, G::oR0), G::SH2, 0, m0, l16, g4);
 #pragma unroll
-    for (int n = 0; n < B1; ++n) gW1[n] = mfma32(a2, afrag_trp(sbf(s) + G::oH1, G::SH1, 0, 16 * n, l16, g4), gW1[n]);
+    for (int n = 0; n < B1; ++n) gW1[n] = mfma32(a2, afrag_trp(SB_BF(sb, G::oH1), G::SH1, 0, 16 * n, l16, g4), gW1[n]);
     gB1 = mfma32(a2, ones, gB1);
   };
   // P9: dW0^T[h1][in] += dZ1^T . X over the chunk's 32 envs (one k-step), software-pipelined strip
   auto P9 = [&](auto s) {
-    const bf16_t* sX = sbf(s) + G::oX;
-    const s8v a1 = afrag_trp(sbf(s) + G::oR1, G::SH1, 0, m0, l16, g4);
+    char* const sb = slot_base(s);
+    const bf16_t* sX = SB_BF(sb, G::oX);
+    const s8v a1 = afrag_trp(SB_BF(sb, G::oR1), G::SH1, 0, m0, l16, g4);
     s8v bq[DW0_PIPE];
 #pragma unroll
     for (int d = 0; d < DW0_PIPE; ++d) bq[d] = afrag_trp(sX, G::SX, 0, 16 * d, l16, g4);
@@ -527,87 +552,87 @@ __global__ void __launch_bounds__(NT, 1) qstep_pair_kernel(QStepParams p) {
       }
     }
   };
+#undef SB_BF
+#undef SB_FL
+#undef SB_IN
 
+  // Stagger (ST_PAIR_STAGGER): the two waves sharing a SIMD (w and w + 4) run an interval's two phases
+  // in opposite orders, so while one issues one phase's MFMAs the other is in the other phase's
+  // LDS / VALU work instead of both contending for the same pipe at the same time.
+  auto both = [&](auto&& x, auto&& y) {
+    if (ST_PAIR_STAGGER && wave >= 4) {
+      y();
+      x();
+    } else {
+      x();
+      y();
+    }
+  };
   constexpr SlotT<0> A{};
   constexpr SlotT<1> B{};
   int iter = 0;
 #define STP_STAMP(I) \
   if (p.stamps != nullptr && bid == 0 && tid == 0) p.stamps[iter * 16 + (I)] = __builtin_amdgcn_s_memtime();
+  if (ST_PAIR_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   for (int k = 0;; ++k) {
     const int ca = bid + 2 * k * grid;         // slot A: P0..P9 in intervals 0..9
     const int cbp = ca - grid;                 // slot B, second half (P5..P9 in intervals 0..4)
     const int cb = ca + grid;                  // slot B, first half (P0..P4 in intervals 5..9)
     const bool va = ca < nch, vbp = k > 0 && cbp < nch, vb = cb < nch;
     if (!va && !vbp) break;
-    refresh();
-    const int cac = min(ca, nch - 1), cbpc = min(max(cbp, 0), nch - 1), cbc = min(cb, nch - 1);
     STP_STAMP(0);
-    // I0: A.P0 | B.P5
-    P0(A, cac);
-    P5(B);
-    __syncthreads();
-    refresh();
-    // I1: B.P6 (waves < NET, latency chain first) | A.P1
-    P6(B, cbpc, vbp);
-    P1(A);
-    __syncthreads();
-    refresh();
-    STP_STAMP(1);
-    // I2: A.P2 | B.P7 (+ env state of B's next chunk)
-    P7(B);
-    P2(A);
+    const int cac = min(ca, nch - 1), cbpc = min(max(cbp, 0), nch - 1), cbc = min(cb, nch - 1);
+    // I0: A.P0 | B.P5 (+ env state of B's next chunk: three intervals ahead of its window loads' use)
     STP_LOAD_ENV(1, cb)
+    both([&] { P0(A); }, [&] { P5(B); });
     __syncthreads();
-    refresh();
-    // I3: A.P3 | B.P8
-    P3(A, cac, va);
-    P8(B);
+    STP_STAMP(1);
+    // I1: B.P6 (waves < NET, latency chain first) | A.P1
+    both([&] { P6(B, cbpc, vbp); }, [&] { P1(A, cac); });
     __syncthreads();
-    refresh();
     STP_STAMP(2);
-    // I4: A.P4 | B.P9 (+ price windows of B's next chunk)
+    // I2: A.P2 | B.P7 (+ price windows of B's next chunk, used in I5)
     STP_LOAD_PRICES(1, cb)
-    P9(B);
-    P4(A);
+    both([&] { P7(B); }, [&] { P2(A); });
     __syncthreads();
-    refresh();
-    if (!va) break;   // drain: the rest of this cycle would be slot A's and slot B's empty phases
     STP_STAMP(3);
-    // I5: A.P5 | B.P0
-    P0(B, cbc);
-    P5(A);
+    // I3: A.P3 | B.P8
+    both([&] { P3(A, cac, va); }, [&] { P8(B); });
     __syncthreads();
-    refresh();
-    // I6: A.P6 | B.P1
-    P6(A, cac, va);
-    P1(B);
-    __syncthreads();
-    refresh();
     STP_STAMP(4);
-    // I7: A.P7 | B.P2 (+ env state of A's next chunk)
-    P7(A);
-    P2(B);
-    STP_LOAD_ENV(0, ca + 2 * grid)
+    // I4: A.P4 | B.P9
+    both([&] { P9(B); }, [&] { P4(A); });
     __syncthreads();
-    refresh();
-    // I8: A.P8 | B.P3
-    P3(B, cbc, vb);
-    P8(A);
-    __syncthreads();
-    refresh();
     STP_STAMP(5);
-    // I9: A.P9 | B.P4 (+ price windows of A's next chunk)
-    STP_LOAD_PRICES(0, ca + 2 * grid)
-    P9(A);
-    P4(B);
+    if (!va) break;   // drain: the rest of this cycle would be slot A's and slot B's empty phases
+    // I5: A.P5 | B.P0 (+ env state of A's next chunk)
+    STP_LOAD_ENV(0, ca + 2 * grid)
+    both([&] { P0(B); }, [&] { P5(A); });
     __syncthreads();
-    refresh();
     STP_STAMP(6);
+    // I6: A.P6 | B.P1
+    both([&] { P6(A, cac, va); }, [&] { P1(B, cbc); });
+    __syncthreads();
+    STP_STAMP(7);
+    // I7: A.P7 | B.P2 (+ price windows of A's next chunk, used in I0)
+    STP_LOAD_PRICES(0, ca + 2 * grid)
+    both([&] { P7(A); }, [&] { P2(B); });
+    __syncthreads();
+    STP_STAMP(8);
+    // I8: A.P8 | B.P3
+    both([&] { P3(B, cbc, vb); }, [&] { P8(A); });
+    __syncthreads();
+    STP_STAMP(9);
+    // I9: A.P9 | B.P4
+    both([&] { P9(A); }, [&] { P4(B); });
+    __syncthreads();
+    STP_STAMP(10);
     ++iter;
   }
 #undef STP_LOAD_ENV
 #undef STP_LOAD_PRICES
 #undef STP_STAMP
+  if (ST_PAIR_PRIO) __builtin_amdgcn_s_setprio(0);
 
   STP_STAMPX(2);
   // ---------------------------------------------------------------- per-workgroup stats (-> LDS -> slab)

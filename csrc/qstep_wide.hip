@@ -73,6 +73,13 @@ constexpr int KPIPE = ST_WIDE_KPIPE;   // double-buffered k-loops (bits): 1 laye
 // the epilogue ds_write_b64 of 16 env rows at one column drops from 4-way to 2-way bank conflicts
 // (rows r and r + 4 no longer share banks).  Weight images and the dQ rows are not swizzled.
 constexpr bool ASWZ = ST_WIDE_ASWZ;
+#ifndef ST_WIDE_DRAW_EARLY
+#define ST_WIDE_DRAW_EARLY 0
+#endif
+// DRAW_EARLY (off: A/B in profiles/r2_pair_kernel.md, P3 -330 ticks but P1-2 / P6 +600): the chunk's epsilon-greedy draws (Philox: ~60 dependent VALU ops with quarter-rate
+// multiplies) are computed in P1 by the last wave for all 64 envs (lane = env row) and left in
+// sEnvI[.][2]; P3 only resolves exploit ? argmax : random action.  Same draws, same actions.
+constexpr bool DRAW_EARLY = ST_WIDE_DRAW_EARLY;
 // asw(r, lo): the swizzled offset of column base + lo for a base that is a multiple of 16 and lo < 16
 // (then (base + lo) ^ 8 bit2(r) = base + (lo ^ 8 bit2(r)): the base stays an immediate offset)
 ST_DEV int asw(int r, int lo) { return ASWZ ? (lo ^ ((r & 4) << 1)) : lo; }
@@ -536,6 +543,17 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     // ------------------------------------------------------------ P1-P2: hidden layers of Q(x)
     auto a_w0 = [&](int i, int ks) { return aW0[i][ks]; };
     auto a_w1 = [&](int i, int ks) { return frag_row(sW1, G::SW1, m0 + 16 * i, ks * 32, l16, g4); };
+    if (DRAW_EARLY && wave == NW - 1) {
+      const int pos = sEnvI[lane * 4 + 0];
+      uint32_t c0 = (uint32_t)(p.env_offset + ebase + lane), c1 = (uint32_t)(step & 0xFFFFFFFFull),
+               c2 = (uint32_t)(step >> 32), c3 = 0u;
+      philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+      const float u1 = u24(c0), u2 = u24(c1);
+      const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
+      int rnd = (int)(u2 * 3.0f);
+      rnd = rnd > 2 ? 2 : rnd;
+      sEnvI[lane * 4 + 2] = rnd | (exploit ? 8 : 0);   // exploit flag (bit 3) + random action
+    }
     fwd_hidden<MT, INP, G::SX, G::SH1, false>(a_w0, sX, sH1, nullptr, m0, l16, g4);
     if (dyn && tid == 0) sCl[0] = dyn_chunk((unsigned)gx + claim_v);   // read in P9
     __syncthreads();
@@ -561,14 +579,22 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         float best = q[0];
         if (q[1] > best) { best = q[1]; greedy = 1; }
         if (q[2] > best) { best = q[2]; greedy = 2; }
-        const int ps = sEnvI[r * 4 + 0];
-        uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
-                 c2 = (uint32_t)(step >> 32), c3 = 0u;
-        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
-        const float u1 = u24(c0), u2 = u24(c1);
-        const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)ps, p.inv_ramp));
-        int rnd = (int)(u2 * 3.0f);
-        rnd = rnd > 2 ? 2 : rnd;
+        bool exploit;
+        int rnd;
+        if constexpr (DRAW_EARLY) {
+          const int draw = sEnvI[r * 4 + 2];
+          exploit = (draw & 8) != 0;
+          rnd = draw & 3;
+        } else {
+          const int ps = sEnvI[r * 4 + 0];
+          uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
+                   c2 = (uint32_t)(step >> 32), c3 = 0u;
+          philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+          const float u1 = u24(c0), u2 = u24(c1);
+          exploit = u1 < fminf(p.eps, __fmul_rn((float)ps, p.inv_ramp));
+          rnd = (int)(u2 * 3.0f);
+          rnd = rnd > 2 ? 2 : rnd;
+        }
         const int a = exploit ? greedy : rnd;
         const float b = sEnv[r * ENVF + 0], vprev = sEnv[r * ENVF + 1], vnew = sEnv[r * ENVF + 2];
         const int s = sEnvI[r * 4 + 1];
