@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=64, help="acting steps to pre-fill the replay ring")
     ap.add_argument("--updates", type=int, default=1)
     ap.add_argument("--dw-gemm", default="auto", help="weight-gradient GEMMs: auto | hip | hipblaslt")
+    ap.add_argument("--serial", action="store_true", help="one stream (no concurrent GEMM chains in the update)")
+    ap.add_argument("--unfused-adam", action="store_true", help="per-layer Adam + row-sum + counter launches")
     a = ap.parse_args()
     import build
 
@@ -39,7 +41,8 @@ def main():
     cfg.model.hidden = [int(x) for x in a.hidden.split(",")]
     cfg.agent.lr = 1e-4
     dev = torch.device("cuda", 0)
-    d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay, dw_gemm=a.dw_gemm)
+    d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay, dw_gemm=a.dw_gemm,
+                concurrent=not a.serial, fused_adam=not a.unfused_adam)
     for _ in range(a.warmup):
         d.act_step()
     d.capture()
@@ -77,6 +80,7 @@ def main():
         "act_ms": round(t_act * 1e3, 4), "update_ms": round(t_upd * 1e3, 4),
         "update_tflops": round(upd_flop / t_upd / 1e12, 1), "replay_size": s["replay_size"],
         "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
+        "concurrent_update": d.concurrent, "fused_adam": d.fused_adam,
     }
     print(json.dumps(out))
 

@@ -45,6 +45,12 @@ struct DeepGather {
   float* r_out;               // [B]
   int* a_out;                 // [B]
   float* done_out;            // [B]
+  // replay mode: fp32 buffers zeroed on the way (split-K weight-gradient outputs, accumulated with
+  // atomics later in the same update) -- replaces two fill launches
+  float* zero0;
+  int zero0_n;
+  float* zero1;
+  int zero1_n;
 };
 
 ST_DEV float dfeat_price(float w, float inv, int mode) { return mode ? (w * inv - 1.0f) : w; }
@@ -53,6 +59,11 @@ ST_DEV float dfeat_price(float w, float inv, int mode) { return mode ? (w * inv 
 __global__ void __launch_bounds__(256) deep_gather_kernel(DeepGather g) {
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
+  if (g.mode == 1) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+    for (int i = gid; i < g.zero0_n; i += gs) g.zero0[i] = 0.f;
+    for (int i = gid; i < g.zero1_n; i += gs) g.zero1[i] = 0.f;
+  }
   if (row >= g.B) return;
   int e, ps, s, s2 = 0;
   float b, b2 = 0.f;
@@ -210,6 +221,8 @@ struct DeepTD {
   float* loss;          // [1] (atomic)
   int B, ldq, n_actions;
   float gamma, coef;
+  unsigned long long* t;   // update counter: advanced here (after this update's replay gather read it,
+                           // before its Adam reads it as the 1-based step)
 };
 
 __global__ void __launch_bounds__(256) deep_td_kernel(DeepTD p) {
@@ -231,6 +244,7 @@ __global__ void __launch_bounds__(256) deep_td_kernel(DeepTD p) {
   }
   l = wave_sum(l);
   if ((threadIdx.x & 63) == 0) atomicAdd(p.loss, l);
+  if (p.t && blockIdx.x == 0 && threadIdx.x == 0) p.t[0] += 1ull;
 }
 
 // bias gradient: db[o] = sum_b dZT[o][b]  (one workgroup per output row)
@@ -269,7 +283,7 @@ struct AdamLayer {
   const float* mask;    // [O, I] trainable mask (null = all trainable)
   bf16_t* wb;           // [O, I] bf16 copy
   bf16_t* wbT;          // [I, O] bf16 transposed copy
-  const unsigned long long* t;   // device update counter (1-based t = *t + 1): graph-replay safe
+  const unsigned long long* t;   // device update counter, already advanced by deep_td (1-based t = *t)
   int O, I;
   float lr, beta1, beta2, eps;
 };
@@ -279,7 +293,7 @@ struct AdamLayer {
 __global__ void __launch_bounds__(256) adam_tile_kernel(AdamLayer p) {
   __shared__ bf16_t t[32][34];
   const int o0 = blockIdx.y * 32, i0 = blockIdx.x * 32;
-  const float tt = (float)(*p.t + 1ull);
+  const float tt = (float)(*p.t);
   const float c1 = 1.f / (1.f - powf(p.beta1, tt)), c2 = 1.f / (1.f - powf(p.beta2, tt));
   for (int k = threadIdx.x; k < 32 * 32; k += 256) {
     const int oo = k / 32, ii = k % 32;
@@ -311,7 +325,124 @@ __global__ void __launch_bounds__(256) adam_tile_kernel(AdamLayer p) {
   }
 }
 
+// ---------------------------------------------------------------- multi-tensor Adam (one launch)
+// Every weight matrix and bias of the MLP in one launch: weight segments in 32x32 tiles (the bf16
+// copy and, through LDS, its transpose, as adam_tile_kernel); bias segments in blocks of 32 entries
+// whose gradient is reduced here from the transposed layer gradient GT [O][B] (bf16) -- the bias
+// gradient row sums need no launch of their own.  The update counter was advanced by deep_td (a
+// last-block counter here cost ~40 us: 3.5k device-scope atomics on one word).  Replaces 2L Adam +
+// L row-sum + 1 counter launches.
+constexpr int ADAM_MAX_SEG = 16;
+struct AdamSeg {
+  float* w;
+  float* g;              // weights: gradient (read); biases: gradient (written here, from gT)
+  float* m;
+  float* v;
+  const float* mask;     // trainable mask (null = all trainable)
+  bf16_t* wb;            // weights: bf16 copy [O][I]
+  bf16_t* wbT;           // weights: bf16 transposed copy [I][O]
+  const bf16_t* gT;      // biases: layer gradient transposed [I][ldg] (bf16); row sums over nb columns
+  int O, I;              // weights: [O][I]; biases: O = 1, I = n
+  int ldg, nb;
+  int bias;
+  int blocks;            // tiles (weights) or 32-entry blocks (biases)
+};
+struct AdamMulti {
+  AdamSeg seg[ADAM_MAX_SEG];
+  int nseg;
+  const unsigned long long* t;   // update counter, already advanced by deep_td (1-based t = *t)
+  int total;
+  float lr, beta1, beta2, eps;
+};
+
+__global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
+  __shared__ bf16_t tl[32][34];
+  __shared__ float red[32];
+  int b = blockIdx.x, si = 0;
+  while (si + 1 < p.nseg && b >= p.seg[si].blocks) b -= p.seg[si++].blocks;
+  const AdamSeg& S = p.seg[si];
+  const float tt = (float)(*p.t);
+  const float c1 = 1.f / (1.f - powf(p.beta1, tt)), c2 = 1.f / (1.f - powf(p.beta2, tt));
+  auto upd = [&](size_t idx, float g) {
+    float w = S.w[idx];
+    const float mk = S.mask ? S.mask[idx] : 1.f;
+    if (mk != 0.f) {
+      g *= mk;
+      const float m = p.beta1 * S.m[idx] + (1.f - p.beta1) * g;
+      const float v = p.beta2 * S.v[idx] + (1.f - p.beta2) * g * g;
+      S.m[idx] = m;
+      S.v[idx] = v;
+      w -= p.lr * (m * c1) / (sqrtf(v * c2) + p.eps);
+      S.w[idx] = w;
+    }
+    return w;
+  };
+  if (S.bias) {
+    // 32 entries: wave w reduces rows 8w..8w+7 of gT (nb bf16 each, 16-byte loads)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i0 = b * 32;
+#pragma unroll 1
+    for (int r = 0; r < 8; ++r) {
+      const int i = i0 + 8 * wave + r;
+      float acc = 0.f;
+      if (i < S.I) {
+        const bf16_t* row = S.gT + (size_t)i * S.ldg;
+        for (int c = 8 * lane; c < S.nb; c += 512) {
+          const uint4 q = *reinterpret_cast<const uint4*>(row + c);
+          const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc += bf2f((bf16_t)(u[k] & 0xFFFF)) + bf2f((bf16_t)(u[k] >> 16));
+        }
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) red[8 * wave + r] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int i = i0 + threadIdx.x;
+      if (i < S.I) {
+        const float g = red[threadIdx.x];
+        S.g[i] = g;
+        upd((size_t)i, g);
+      }
+    }
+  } else {
+    const int tiles_i = (S.I + 31) / 32;
+    const int o0 = (b / tiles_i) * 32, i0 = (b % tiles_i) * 32;
+    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+      const int oo = k / 32, ii = k % 32;
+      const int o = o0 + oo, i = i0 + ii;
+      bf16_t wb = 0;
+      if (o < S.O && i < S.I) {
+        const size_t idx = (size_t)o * S.I + i;
+        wb = f2bf(upd(idx, S.g[idx]));
+        S.wb[idx] = wb;
+      }
+      tl[oo][ii] = wb;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+      const int ii = k / 32, oo = k % 32;
+      const int o = o0 + oo, i = i0 + ii;
+      if (S.wbT && o < S.O && i < S.I) S.wbT[(size_t)i * S.O + o] = tl[oo][ii];
+    }
+  }
+}
+
 }  // namespace st
+
+extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
+  if (p->nseg < 1 || p->nseg > st::ADAM_MAX_SEG) return hipErrorInvalidValue;
+  int total = 0;
+  for (int i = 0; i < p->nseg; ++i) {
+    const st::AdamSeg& g = p->seg[i];
+    const int want = g.bias ? (g.I + 31) / 32 : ((g.I + 31) / 32) * ((g.O + 31) / 32);
+    if (g.blocks != want || (g.bias && (g.nb % 8 || g.ldg % 8 || !g.gT))) return hipErrorInvalidValue;
+    total += g.blocks;
+  }
+  if (total != p->total) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::adam_multi_kernel, dim3(total), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t st_deep_gather(const st::DeepGather* g, hipStream_t s) {
   if (g->in_p > 256 || g->in_p % 4 || g->H + 2 > g->in_p) return hipErrorInvalidValue;

@@ -98,9 +98,10 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_
     few-tile products (weight gradients) over extra workgroups with atomic accumulation."""
     t = tile or pick_tile(A.shape[0], B.shape[0])
     sk = kw.pop("splitk", 1)
+    prezeroed = kw.pop("prezeroed", False)   # split-K output already zeroed by an earlier kernel
     if sk == "auto":
         sk = pick_splitk(A.shape[0], B.shape[0], A.shape[1], t) if epi == EPI_F32 else 1
-    if sk > 1 and not kw.get("accumulate", False):
+    if sk > 1 and not kw.get("accumulate", False) and not prezeroed:
         out.zero_()
     g = make_args(A, B, out, epi, splitk=sk, **kw)
     if g.M % t[0] or g.N % t[1] or g.K % 64:

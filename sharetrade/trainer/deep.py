@@ -41,7 +41,8 @@ class _Gather(C.Structure):
                 ("inv_b0", C.c_float), ("mode", C.c_int), ("B", C.c_int), ("pos", C.c_void_p),
                 ("budget", C.c_void_p), ("shares", C.c_void_p), ("rp", _Replay), ("key0", C.c_uint32),
                 ("key1", C.c_uint32), ("step", C.c_void_p), ("X", C.c_void_p), ("Xn", C.c_void_p),
-                ("r_out", C.c_void_p), ("a_out", C.c_void_p), ("done_out", C.c_void_p)]
+                ("r_out", C.c_void_p), ("a_out", C.c_void_p), ("done_out", C.c_void_p),
+                ("zero0", C.c_void_p), ("zero0_n", C.c_int), ("zero1", C.c_void_p), ("zero1_n", C.c_int)]
 
 
 class _Env(C.Structure):
@@ -56,13 +57,27 @@ class _Env(C.Structure):
 class _TD(C.Structure):
     _fields_ = [("q", C.c_void_p), ("qt", C.c_void_p), ("r", C.c_void_p), ("a", C.c_void_p), ("done", C.c_void_p),
                 ("dq", C.c_void_p), ("dqT", C.c_void_p), ("loss", C.c_void_p), ("B", C.c_int), ("ldq", C.c_int),
-                ("n_actions", C.c_int), ("gamma", C.c_float), ("coef", C.c_float)]
+                ("n_actions", C.c_int), ("gamma", C.c_float), ("coef", C.c_float), ("t", C.c_void_p)]
 
 
 class _Adam(C.Structure):
     _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("mask", C.c_void_p),
                 ("wb", C.c_void_p), ("wbT", C.c_void_p), ("t", C.c_void_p), ("O", C.c_int), ("I", C.c_int),
                 ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float)]
+
+
+ADAM_MAX_SEG = 16
+
+
+class _AdamSeg(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("mask", C.c_void_p),
+                ("wb", C.c_void_p), ("wbT", C.c_void_p), ("gT", C.c_void_p), ("O", C.c_int), ("I", C.c_int),
+                ("ldg", C.c_int), ("nb", C.c_int), ("bias", C.c_int), ("blocks", C.c_int)]
+
+
+class _AdamMulti(C.Structure):
+    _fields_ = [("seg", _AdamSeg * ADAM_MAX_SEG), ("nseg", C.c_int), ("t", C.c_void_p), ("total", C.c_int), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
+                ("eps", C.c_float)]
 
 
 def _bind():
@@ -75,6 +90,7 @@ def _bind():
                          ("st_transpose_bf16", [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                 C.c_void_p]),
                          ("st_adam_tile", [C.POINTER(_Adam), C.c_void_p]),
+                         ("st_adam_multi", [C.POINTER(_AdamMulti), C.c_void_p]),
                          ("st_counter_inc", [C.c_void_p, C.c_void_p])):
             f = getattr(L, fn)
             f.argtypes = args
@@ -92,7 +108,8 @@ class DeepDQN:
 
     def __init__(self, cfg: Config, device: torch.device, envs: int = 16384, batch: int = 4096,
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
-                 prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto"):
+                 prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
+                 concurrent: bool = True, fused_adam: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -103,6 +120,12 @@ class DeepDQN:
         if dw_gemm not in ("auto", "hip", "hipblaslt"):
             raise ValueError(f"dw_gemm: {dw_gemm!r}")
         self.dw_gemm = dw_gemm
+        # concurrent: the independent GEMM chains of an update (online / target forward; weight
+        # gradients / data backward) on two streams inside the captured graph -- each 4096-row GEMM
+        # fills only one 128x128 tile per CU, two chains at once give every CU two.
+        # fused_adam: one multi-tensor Adam launch that also reduces the bias gradients and advances
+        # the update counter (was 2L Adam + L row-sum + 1 counter launches).
+        self.concurrent, self.fused_adam = bool(concurrent), bool(fused_adam)
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -146,10 +169,31 @@ class DeepDQN:
             self.WbT.append(self.W[l].t().contiguous().to(b16))
             self.Wt.append(self.Wb[l].clone())
             self.bt.append(self.b[l].clone())
-            self.dW.append(torch.zeros(o, i, device=dev))
             self.db.append(torch.zeros(1, o, device=dev))
+        # weight gradients: views of one flat fp32 buffer (the replay gather zeroes the split-K span)
+        sizes = [self.pdims[l + 1] * self.pdims[l] for l in range(self.L)]
+        self._dW_flat = torch.zeros(sum(sizes), device=dev)
+        off = 0
+        for l in range(self.L):
+            self.dW.append(self._dW_flat[off:off + sizes[l]].view(self.pdims[l + 1], self.pdims[l]))
+            off += sizes[l]
+        self._dw_plan = []   # per layer: ("blaslt", None) or ("hip", (tile, splitk))
+        for l in range(self.L):
+            o, i = self.pdims[l + 1], self.pdims[l]
+            if self.dw_gemm == "hipblaslt" or (self.dw_gemm == "auto" and o >= 1024 and i >= 1024):
+                self._dw_plan.append(("blaslt", None))
+            else:
+                wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else gm.pick_tile(o, i)
+                self._dw_plan.append(("hip", (wt, gm.pick_splitk(o, self.pdims[l], self.B, wt))))
+        sk_layers = [l for l, (k, a) in enumerate(self._dw_plan) if k == "hip" and a[1] > 1]
+        self._zero_span = (0, 0)
+        if sk_layers:
+            lo = sum(sizes[:sk_layers[0]])
+            hi = sum(sizes[:sk_layers[-1] + 1])
+            self._zero_span = (lo, hi - lo)
         self._bT_scratch = torch.zeros(max(self.pdims), 1, dtype=b16, device=dev)
         self.t_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._side = torch.cuda.Stream(device=dev) if self.concurrent else None
         # ------------------------------------------------------------ data, envs, replay
         from .engine import make_price_bank, padded_bank
 
@@ -228,6 +272,9 @@ class DeepDQN:
         gr.mode, gr.B = 1, self.B
         gr.X, gr.Xn = self.X.data_ptr(), self.Xn.data_ptr()
         gr.r_out, gr.a_out, gr.done_out = self.r_b.data_ptr(), self.a_b.data_ptr(), self.d_b.data_ptr()
+        z0, zn = self._zero_span
+        gr.zero0 = self._dW_flat.data_ptr() + 4 * z0 if zn else None
+        gr.zero0_n, gr.zero1, gr.zero1_n = zn, None, 0
         self._gather_rp = gr
         ev = _Env()
         ev.prices, ev.T, ev.H, ev.E = self.prices.data_ptr(), self.T, self.H, self.E
@@ -245,6 +292,7 @@ class DeepDQN:
         td.dq, td.dqT, td.loss = self.G[-1].data_ptr(), self.GT[-1].data_ptr(), self.loss.data_ptr()
         td.B, td.ldq, td.n_actions = self.B, ACT_PAD, self.n_act
         td.gamma, td.coef = float(cfg.agent.gamma), 2.0 / self.B
+        td.t = self.t_ctr.data_ptr()   # the update counter advances in the TD kernel
         self._td = td
         a = cfg.agent
         self._adam = []
@@ -261,6 +309,33 @@ class DeepDQN:
                 ad.lr, ad.beta1, ad.beta2, ad.eps = float(a.lr), float(a.adam_betas[0]), float(a.adam_betas[1]), \
                     float(a.adam_eps)
                 self._adam.append(ad)
+        am = _AdamMulti()
+        segs = []
+        for l in range(self.L):
+            O, I = self.pdims[l + 1], self.pdims[l]
+            w = _AdamSeg()
+            w.w, w.g, w.m, w.v, w.mask = (self.W[l].data_ptr(), self.dW[l].data_ptr(), self.Wm[l].data_ptr(),
+                                          self.Wv[l].data_ptr(), self.Wmask[l].data_ptr())
+            w.wb, w.wbT, w.gT = self.Wb[l].data_ptr(), self.WbT[l].data_ptr(), None
+            w.O, w.I, w.ldg, w.nb, w.bias = O, I, 0, 0, 0
+            w.blocks = ((I + 31) // 32) * ((O + 31) // 32)
+            b = _AdamSeg()
+            b.w, b.g, b.m, b.v, b.mask = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
+                                          self.bv[l].data_ptr(), self.bmask[l].data_ptr())
+            b.wb, b.wbT, b.gT = None, None, self.GT[l].data_ptr()
+            b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
+            b.blocks = (O + 31) // 32
+            segs += [w, b]
+        if len(segs) > ADAM_MAX_SEG:
+            self.fused_adam = False
+        else:
+            for k, sg in enumerate(segs):
+                am.seg[k] = sg
+            am.nseg, am.t = len(segs), self.t_ctr.data_ptr()
+            am.total = sum(sg.blocks for sg in segs)
+            am.lr, am.beta1, am.beta2, am.eps = (float(a.lr), float(a.adam_betas[0]), float(a.adam_betas[1]),
+                                                 float(a.adam_eps))
+        self._adam_multi = am
 
     def _bscratch(self, l: int) -> torch.Tensor:
         if not hasattr(self, "_bias_bf"):
@@ -287,36 +362,62 @@ class DeepDQN:
         self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe)
         native.check(self.k.st_deep_env_step(self._env, sh), "deep_env_step")
 
+    def _dw(self, l: int, actsT) -> None:
+        """Weight gradient of layer l: dW = G_l^T . A_l (long-K, few-tile product)."""
+        kind, arg = self._dw_plan[l]
+        if kind == "blaslt":
+            torch.mm(self.GT[l], actsT[l].t(), out_dtype=torch.float32, out=self.dW[l])
+        else:
+            tile, sk = arg
+            gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=tile, splitk=sk,
+                       prezeroed=sk > 1)   # zeroed by this update's replay gather
+
     def update_step(self) -> None:
-        """One DQN update: sample B transitions, Q(x) online / Q(x') target, TD, backward, Adam."""
+        """One DQN update: sample B transitions, Q(x) online / Q(x') target, TD, backward, Adam.
+
+        With ``concurrent``: the target-network forward runs beside the online forward, and each
+        layer's weight gradient beside the next data-backward GEMM, on a second stream (fork / join
+        with stream waits, so the whole update still captures into one HIP graph)."""
         sh = native.stream_handle()
         k = self.k
+        main = torch.cuda.current_stream(self.dev)
+        side = self._side
         native.check(k.st_deep_gather(self._gather_rp, sh), "deep_gather(replay)")
         native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
                                          self.in_p, sh), "transpose X")
         acts = [self.X] + self.Act[1:]
         actsT = [self.XT] + self.ActT[1:]
-        self._forward(self.X, acts, actsT, self.Wb, self.b, self.Q)
-        self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)
+            self._forward(self.X, acts, actsT, self.Wb, self.b, self.Q)
+            main.wait_stream(side)
+        else:
+            self._forward(self.X, acts, actsT, self.Wb, self.b, self.Q)
+            self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)
         native.check(k.st_deep_td(self._td, sh), "deep_td")
         for l in reversed(range(self.L)):
-            # weight / bias gradients of layer l: dW = G_l^T . A_l
-            # long-K, few-tile product: 128x128 tiles split over K (atomic fp32 accumulation)
-            o, i = self.pdims[l + 1], self.pdims[l]
-            if self.dw_gemm == "hipblaslt" or (self.dw_gemm == "auto" and o >= 1024 and i >= 1024):
-                torch.mm(self.GT[l], actsT[l].t(), out_dtype=torch.float32, out=self.dW[l])
+            if side is not None:
+                side.wait_stream(main)        # G_l is ready
+                with torch.cuda.stream(side):
+                    self._dw(l, actsT)
             else:
-                wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else None
-                gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=wt, splitk="auto")
-            native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
-                                           self.db[l].data_ptr(), sh), "bias grad")
+                self._dw(l, actsT)
+            if not self.fused_adam:
+                native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
+                                               self.db[l].data_ptr(), sh), "bias grad")
             if l > 0:
                 # G_{l-1} = (G_l . W_l) * (A_l > 0)
                 gm.gemm_nt(self.G[l], self.WbT[l], self.G[l - 1], gm.EPI_RELU_GRAD, outT=self.GT[l - 1],
                            auxT=actsT[l])
-        for ad in self._adam:
-            native.check(k.st_adam_tile(ad, sh), "adam")
-        native.check(k.st_counter_inc(self.t_ctr.data_ptr(), sh), "t++")
+        if side is not None:
+            main.wait_stream(side)
+        if self.fused_adam:
+            native.check(k.st_adam_multi(self._adam_multi, sh), "adam_multi")
+        else:
+            for ad in self._adam:
+                native.check(k.st_adam_tile(ad, sh), "adam")
 
     def sync_target(self) -> None:
         for l in range(self.L):

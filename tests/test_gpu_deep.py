@@ -43,9 +43,11 @@ def test_replay_ring_and_env_step(native_built):
     assert int(d.rp_ctrl[1]) == d.cap and int(d.rp["pos"][0]) == 16
 
 
-@pytest.mark.parametrize("dw_gemm", ["hip", "hipblaslt"])
-def test_update_gradients_match_torch(native_built, dw_gemm):
-    d = _dqn(dw_gemm=dw_gemm)
+@pytest.mark.parametrize("dw_gemm,concurrent,fused", [("hip", True, True), ("hipblaslt", True, True),
+                                                       ("hip", False, False), ("hipblaslt", False, True)])
+def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused):
+    kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused)
+    d = _dqn(**kw)
     for _ in range(8):
         d.act_step()
     d.update_step()
@@ -54,11 +56,12 @@ def test_update_gradients_match_torch(native_built, dw_gemm):
     W = [w.float() for w in d.Wb]  # note: Adam already updated d.W; grads are from the pre-update copies
     # recompute with the weights used by the update: undo nothing — compare grads against autograd on a
     # network whose bf16 weights are the *pre-update* ones, captured before the step below
-    d2 = _dqn(dw_gemm=dw_gemm)
+    d2 = _dqn(**kw)
     for _ in range(8):
         d2.act_step()
     Wpre = [w.float().clone().requires_grad_(True) for w in d2.Wb]
     bpre = [b.float().clone().view(-1).requires_grad_(True) for b in d2.b]
+    W32, b32 = [w.clone() for w in d2.W], [b.clone().view(-1) for b in d2.b]   # fp32 masters
     Wt = [w.float() for w in d2.Wt]
     bt = [b.float().view(-1) for b in d2.bt]
     d2.update_step()
@@ -87,11 +90,22 @@ def test_update_gradients_match_torch(native_built, dw_gemm):
         assert relb < 3e-2, (l, relb)
     lv = float(loss.detach()) if torch.is_tensor(loss) else float(loss)
     assert abs(float(d2.loss) / d2.B - lv) < 1e-2 * lv + 1e-6
+    assert int(d2.t_ctr) == 1                                  # one update counted (by deep_td)
+    # the optimizer step itself: Adam (t = 1) on the gradients just checked
+    a = d2.cfg.agent
+    for l in range(d2.L):
+        for p0, g, p1, msk in ((W32[l], d2.dW[l], d2.W[l], d2.Wmask[l]),
+                               (b32[l], d2.db[l].view(-1), d2.b[l].view(-1), d2.bmask[l].view(-1))):
+            g = g * msk
+            m = (1 - a.adam_betas[0]) * g / (1 - a.adam_betas[0])
+            v = (1 - a.adam_betas[1]) * g * g / (1 - a.adam_betas[1])
+            want = (p0 - a.lr * m / (v.sqrt() + a.adam_eps)) * msk + p0 * (1 - msk)
+            assert torch.allclose(p1.view_as(want), want, rtol=1e-5, atol=1e-6 * a.lr), l
 
 
-@pytest.mark.parametrize("dw_gemm", ["hip", "hipblaslt"])
-def test_graph_iteration_runs(native_built, dw_gemm):
-    d = _dqn(dw_gemm=dw_gemm)
+@pytest.mark.parametrize("dw_gemm,concurrent", [("hip", True), ("hipblaslt", True), ("hipblaslt", False)])
+def test_graph_iteration_runs(native_built, dw_gemm, concurrent):
+    d = _dqn(dw_gemm=dw_gemm, concurrent=concurrent)
     for _ in range(4):
         d.act_step()
     d.capture()
@@ -100,4 +114,5 @@ def test_graph_iteration_runs(native_built, dw_gemm):
     torch.cuda.synchronize()
     s = d.stats_dict()
     assert s["updates"] == 6 and np.isfinite(s["loss_sum"])
+    assert int(d.t_ctr) == 6
     assert all(torch.isfinite(w).all() for w in d.W)
