@@ -109,7 +109,7 @@ class DeepDQN:
     def __init__(self, cfg: Config, device: torch.device, envs: int = 16384, batch: int = 4096,
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
-                 concurrent: bool = True, fused_adam: bool = True):
+                 concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -126,6 +126,12 @@ class DeepDQN:
         # fused_adam: one multi-tensor Adam launch that also reduces the bias gradients and advances
         # the update counter (was 2L Adam + L row-sum + 1 counter launches).
         self.concurrent, self.fused_adam = bool(concurrent), bool(fused_adam)
+        # overlap_act: one captured graph per iteration in which the update first samples its batch,
+        # then the act step (gather -> 5 GEMMs -> env step -> replay insert) runs on a third stream
+        # beside the update's GEMM chains; Adam waits for both (the act step reads the pre-update
+        # weights, as in the serial order).  Only difference from the serial order: the update samples
+        # the ring as it was BEFORE this iteration's 16k inserts (one act step older).
+        self.overlap_act = bool(overlap_act)
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -194,6 +200,7 @@ class DeepDQN:
         self._bT_scratch = torch.zeros(max(self.pdims), 1, dtype=b16, device=dev)
         self.t_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self._side = torch.cuda.Stream(device=dev) if self.concurrent else None
+        self._act_stream = torch.cuda.Stream(device=dev) if self.overlap_act else None
         # ------------------------------------------------------------ data, envs, replay
         from .engine import make_price_bank, padded_bank
 
@@ -372,7 +379,7 @@ class DeepDQN:
             gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=tile, splitk=sk,
                        prezeroed=sk > 1)   # zeroed by this update's replay gather
 
-    def update_step(self) -> None:
+    def update_step(self, with_act: bool = False) -> None:
         """One DQN update: sample B transitions, Q(x) online / Q(x') target, TD, backward, Adam.
 
         With ``concurrent``: the target-network forward runs beside the online forward, and each
@@ -383,6 +390,13 @@ class DeepDQN:
         main = torch.cuda.current_stream(self.dev)
         side = self._side
         native.check(k.st_deep_gather(self._gather_rp, sh), "deep_gather(replay)")
+        act = self._act_stream if with_act else None
+        if with_act:
+            if act is None:
+                raise RuntimeError("update_step(with_act=True) needs overlap_act=True")
+            act.wait_stream(main)              # the batch is sampled: the act step may insert now
+            with torch.cuda.stream(act):
+                self.act_step()
         native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
                                          self.in_p, sh), "transpose X")
         acts = [self.X] + self.Act[1:]
@@ -413,6 +427,8 @@ class DeepDQN:
                            auxT=actsT[l])
         if side is not None:
             main.wait_stream(side)
+        if act is not None:
+            main.wait_stream(act)              # the act step's GEMMs read the pre-update weights
         if self.fused_adam:
             native.check(k.st_adam_multi(self._adam_multi, sh), "adam_multi")
         else:
@@ -430,8 +446,11 @@ class DeepDQN:
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
-            self.act_step()
-            self.update_step()
+            if self.overlap_act:
+                self.update_step(with_act=True)   # same op order as the captured iteration
+            else:
+                self.act_step()
+                self.update_step()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         self.env_steps += 1
         self.updates += 1
@@ -441,13 +460,29 @@ class DeepDQN:
         self._g_upd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_upd):
             self.update_step()
+        self._g_iter = None
+        if self.overlap_act:
+            self._g_iter = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_iter):
+                self.update_step(with_act=True)
 
     def iteration(self, updates_per_step: int = 1) -> None:
-        if self._g_act is not None:
-            self._g_act.replay()
+        if self.overlap_act and updates_per_step >= 1:
+            if getattr(self, "_g_iter", None) is not None:
+                self._g_iter.replay()
+            else:
+                self.update_step(with_act=True)
+            self.env_steps += 1
+            self.updates += 1
+            if self.target_every and self.updates % self.target_every == 0:
+                self.sync_target()
+            updates_per_step -= 1
         else:
-            self.act_step()
-        self.env_steps += 1
+            if self._g_act is not None:
+                self._g_act.replay()
+            else:
+                self.act_step()
+            self.env_steps += 1
         for _ in range(updates_per_step):
             if self._g_upd is not None:
                 self._g_upd.replay()

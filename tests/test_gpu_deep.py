@@ -116,3 +116,34 @@ def test_graph_iteration_runs(native_built, dw_gemm, concurrent):
     assert s["updates"] == 6 and np.isfinite(s["loss_sum"])
     assert int(d.t_ctr) == 6
     assert all(torch.isfinite(w).all() for w in d.W)
+
+
+def test_overlapped_act_matches_same_order_serial(native_built):
+    """overlap_act: the act step on its own stream beside the update's GEMM chains (captured graph)
+    equals the same sequence run on one stream -- update gather, act step, rest of the update -- up to
+    fp32 atomic summation order: identical env state and replay contents, same weights within 1e-5."""
+    res = []
+    for serial in (False, True):
+        d = _dqn(dw_gemm="hipblaslt", overlap_act=True)
+        for _ in range(6):
+            d.act_step()
+        if serial:
+            d._act_stream = torch.cuda.current_stream()   # same op order, one stream, eager
+            for _ in range(4):
+                d.iteration()
+        else:
+            d.capture()            # warm-up iteration (serial act + update), then graphs
+            for _ in range(3):
+                d.iteration()
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    if a.updates != b.updates:
+        pytest.fail(f"update count {a.updates} vs {b.updates}")
+    assert int(a.t_ctr) == int(b.t_ctr) == 4 and int(a.rp_ctrl[0]) == int(b.rp_ctrl[0]) == 10 * a.E
+    for k in ("pos", "budget", "shares", "episodes"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    for k in a.rp:
+        assert torch.equal(a.rp[k], b.rp[k]), k
+    for wa, wb in zip(a.W, b.W):
+        assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
