@@ -50,11 +50,16 @@ struct GemmGeo {
   static constexpr int A_EL = BM * GBK, B_EL = BN * GBK;
   static constexpr int BUF_EL = A_EL + B_EL;
   static constexpr int KLOOP_BYTES = S * BUF_EL * 2;   // S-stage LDS ring
-  static constexpr int EPI_BYTES = (BM * (BN + 8) + BN * (BM + 8)) * 2;
+  // 256 x 256 tiles stage only C for the epilogue (C and C^T would need 270 KB): no transposed output
+  static constexpr bool HAS_T = !(BM >= 256 && BN >= 256);
+  static constexpr int EPI_BYTES = (BM * (BN + 8) + (HAS_T ? BN * (BM + 8) : 0)) * 2;
   static constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
-  // waves: 2 x 2 (256 threads, two blocks per CU) or, for BM = 256, 4 x 2 (512 threads, one block
-  // per CU: 1.33x fewer L2 bytes per MFMA than 128 x 128)
-  static constexpr int NWM = BM >= 256 ? 4 : 2, NWN = 2, NT = 64 * NWM * NWN, MINB = (NT > 256 || S > 2) ? 1 : 2;
+  // waves: 2 x 2 (256 threads, two blocks per CU); for 256 x 128, 4 x 2 (512 threads, one block per
+  // CU: 1.33x fewer L2 bytes per MFMA than 128 x 128); for 256 x 256, 2 x 2 waves of 128 x 128 each
+  // (one block per CU, 256 accumulator registers per lane: half the LDS fragment bytes per MFMA of
+  // the 64 x 64 wave tiles)
+  static constexpr int NWM = (BM >= 256 && BN < 256) ? 4 : 2, NWN = 2, NT = 64 * NWM * NWN;
+  static constexpr int MINB = (NT > 256 || S > 2 || BM * BN >= 256 * 256) ? 1 : 2;
   // LDS-DMA instructions per wave per K-tile (vmcnt budget of the S-stage ring)
   static constexpr int LPT = (BM / 8 + NT / 64 - 1) / (NT / 64) + (BN / 8 + NT / 64 - 1) / (NT / 64);
   static constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
@@ -84,8 +89,10 @@ ST_DEV s8v frag_sw(const bf16_t* lds, int r, int g) {
   return lds_ld8(lds + r * GBK + ((g ^ (r & 7)) << 3));
 }
 
-template <int BM> constexpr int gemm_threads() { return BM >= 256 ? 512 : 256; }
-template <int BM, int S> constexpr int gemm_min_blocks() { return (BM >= 256 || S > 2) ? 1 : 2; }
+template <int BM, int BN> constexpr int gemm_threads() { return (BM >= 256 && BN < 256) ? 512 : 256; }
+template <int BM, int BN, int S> constexpr int gemm_min_blocks() {
+  return ((BM >= 256 && BN < 256) || S > 2 || BM * BN >= 256 * 256) ? 1 : 2;
+}
 
 // s_waitcnt immediate: vmcnt = N (gfx9 split field), expcnt / lgkmcnt not waited on
 template <int N>
@@ -95,10 +102,10 @@ ST_DEV void wait_vmcnt() {
 }
 
 template <int BM, int BN, int EPI, int S = 2>
-__global__ void __launch_bounds__(gemm_threads<BM>(), (gemm_min_blocks<BM, S>())) gemm_nt_kernel(GemmArgs p) {
+__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_nt_kernel(GemmArgs p) {
   using G = GemmGeo<BM, BN, S>;
   constexpr int NW = G::NT / 64;
-  static_assert(G::NT == gemm_threads<BM>() && G::MINB == gemm_min_blocks<BM, S>(), "launch bounds");
+  static_assert(G::NT == gemm_threads<BM, BN>() && G::MINB == gemm_min_blocks<BM, BN, S>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
@@ -218,7 +225,7 @@ __global__ void __launch_bounds__(gemm_threads<BM>(), (gemm_min_blocks<BM, S>())
     // stage C [BM][BN+8] and C^T [BN][BM+8] in LDS (the K-loop buffers are idle now)
     constexpr int SC = BN + 8, SCT = BM + 8;
     bf16_t* sC = buf;
-    bf16_t* sCT = buf + BM * SC;
+    bf16_t* sCT = buf + BM * SC;   // (only with G::HAS_T)
 #pragma unroll
     for (int i = 0; i < G::TM; ++i)
 #pragma unroll
@@ -240,7 +247,7 @@ __global__ void __launch_bounds__(gemm_threads<BM>(), (gemm_min_blocks<BM, S>())
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) sC[(ml + r) * SC + nl] = f2bf(v[r]);
-        lds_st4(sCT + nl * SCT + ml, v[0], v[1], v[2], v[3]);
+        if constexpr (G::HAS_T) lds_st4(sCT + nl * SCT + ml, v[0], v[1], v[2], v[3]);
       }
     __syncthreads();
     bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
@@ -250,7 +257,7 @@ __global__ void __launch_bounds__(gemm_threads<BM>(), (gemm_min_blocks<BM, S>())
       *reinterpret_cast<uint4*>(out + (size_t)(m0 + r) * p.ldo + n0 + k) =
           *reinterpret_cast<const uint4*>(sC + r * SC + k);
     }
-    if (p.outT) {
+    if (G::HAS_T && p.outT) {
       constexpr int CPRT = BM / 8;
       for (int c = tid; c < BN * CPRT; c += G::NT) {
         const int r = c / CPRT, k = (c % CPRT) * 8;
@@ -279,11 +286,13 @@ static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
 }  // namespace st
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
-//       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU)
+//       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU),
+//       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output)
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
-  if (tile < 0 || tile > 5) return hipErrorInvalidValue;
-  const int bm = tile == 3 ? 256 : (tile == 1 ? 64 : 128);
-  const int bn = (tile == 1 || tile == 2) ? 64 : 128;
+  if (tile < 0 || tile > 6) return hipErrorInvalidValue;
+  const int bm = (tile == 3 || tile == 6) ? 256 : (tile == 1 ? 64 : 128);
+  const int bn = (tile == 1 || tile == 2) ? 64 : (tile == 6 ? 256 : 128);
+  if (tile == 6 && p->outT) return hipErrorInvalidValue;
   if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
   if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
   if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
@@ -302,6 +311,7 @@ extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipSt
   if (tile == 3) { ST_G(256, 128, 2) }
   if (tile == 4) { ST_G(128, 128, 3) }
   if (tile == 5) { ST_G(128, 128, 4) }
+  if (tile == 6) { ST_G(256, 256, 2) }
 #undef ST_G
   return hipErrorInvalidValue;
 }

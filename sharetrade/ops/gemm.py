@@ -12,7 +12,8 @@ from . import native
 
 EPI_BF16, EPI_RELU_GRAD, EPI_F32 = 0, 1, 2
 # (BM, BN) or (BM, BN, LDS stages) -> st_gemm_nt tile id (csrc/gemm_bf16.hip)
-TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2, (256, 128): 3, (128, 128, 3): 4, (128, 128, 4): 5}
+TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2, (256, 128): 3, (128, 128, 3): 4, (128, 128, 4): 5,
+         (256, 256): 6}
 
 
 class GemmArgs(C.Structure):

@@ -88,3 +88,30 @@ def test_gemm_split_k(native_built, M, N, K, tile, sk):
     assert err < 1e-5, err
     gemm_nt(A, B, out, EPI_F32, tile=tile, splitk=sk, accumulate=True)   # bias not re-added
     assert torch.allclose(out, 2 * ref - bias, rtol=1e-4, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 320), (1024, 512, 1024), (256, 1024, 64)])
+def test_gemm_256x256_tile(native_built, M, N, K):
+    """256x256 tile (4 waves of 128x128 accumulators): every epilogue but the transposed output,
+    which the tile refuses (its C^T staging would not fit in LDS)."""
+    from sharetrade.ops.gemm import EPI_BF16, EPI_F32, EPI_RELU_GRAD, gemm_nt
+
+    A, B = _bf((M, K), 7), _bf((N, K), 8)
+    bias = torch.randn(N, device="cuda")
+    ref = A.float() @ B.float().t()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    gemm_nt(A, B, out, EPI_BF16, tile=(256, 256), bias=bias, relu=True)
+    r = torch.relu(ref + bias)
+    torch.cuda.synchronize()
+    assert torch.allclose(out.float(), r, rtol=1e-2, atol=1e-2 * float(r.abs().max()))
+    o32 = torch.empty(M, N, device="cuda")
+    gemm_nt(A, B, o32, EPI_F32, tile=(256, 256), alpha=0.5)
+    torch.cuda.synchronize()
+    assert torch.allclose(o32, 0.5 * ref, rtol=1e-4, atol=1e-3)
+    act = torch.relu(torch.randn(M, N, device="cuda")).to(torch.bfloat16)
+    gemm_nt(A, B, out, EPI_RELU_GRAD, tile=(256, 256), auxT=act.t().contiguous())
+    r = ref * (act.float() > 0)
+    torch.cuda.synchronize()
+    assert torch.allclose(out.float(), r, rtol=1e-2, atol=1e-2 * float(r.abs().max()))
+    with pytest.raises(RuntimeError):
+        gemm_nt(A, B, out, EPI_BF16, tile=(256, 256), outT=torch.empty(N, M, dtype=torch.bfloat16, device="cuda"))

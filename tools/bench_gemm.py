@@ -21,7 +21,7 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t0) / iters
 
 
-TILES_AB = [(128, 128), (256, 128), (128, 128, 3), (128, 128, 4)]
+TILES_AB = [(128, 128), (256, 128), (256, 256), (128, 128, 3), (128, 128, 4)]
 
 
 def main():
