@@ -113,7 +113,7 @@ def main() -> int:
         try:
             # 2 eager steps before capture, then one replay of each captured graph (graph upload);
             # all of them untimed and reported as "graph_prime_steps"
-            use_graph = eng.capture_graph(warmup=2, prime=True)
+            use_graph = eng.capture_graph(warmup=2, prime=True, prime_reps=4)
         except Exception as e:  # noqa: BLE001 -- fall back to eager launches, same math
             print(f"bench: HIP graph capture failed ({str(e).splitlines()[0]}); running eagerly", file=sys.stderr)
             from sharetrade.ops import native as _native
@@ -121,6 +121,11 @@ def main() -> int:
             _native.clear_last_error()
             torch.cuda.synchronize()
             eng._graph, eng._graph_k, use_graph = None, None, False
+    # load the (lazily loaded) torch kernels of the start-of-window portfolio snapshot now: loading them
+    # between the warm-up and the timed window idles the GPU for >= 10 ms, and the clock then needs
+    # ~40 steps to settle (tools/dvfs_probe.py, profiles/r2_dvfs_probe.md)
+    eng.current_portfolios().double().clone()
+    torch.cuda.synchronize()
     prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()

@@ -447,7 +447,8 @@ class VectorEngine:
         for _ in range(n):
             self.step()
 
-    def capture_graph(self, warmup: int = 2, graph_steps: Optional[int] = None, prime: bool = False) -> bool:
+    def capture_graph(self, warmup: int = 2, graph_steps: Optional[int] = None, prime: bool = False,
+                      prime_reps: int = 1) -> bool:
         """Capture one native step in a HIP graph, plus a ``graph_steps``-step graph for :meth:`run`
         (``engine.graph_steps``; the step index lives in device memory, so the captured steps replay
         correctly back to back).
@@ -459,9 +460,11 @@ class VectorEngine:
         58.8 us without DP (tools/dp_host_overhead.py).  The overlapped-DP path (``dp_overlap``)
         keeps Python-side pending state between steps and is not captured.
 
-        ``prime``: replay each captured graph once (real, counted steps) so that the first timed
-        replay does not pay the one-time graph upload to the device (measured ~1.6 ms for the
-        16-step graph at 1M envs, i.e. +12 % on a 20-step timed window)."""
+        ``prime``: replay each captured graph (real, counted steps; the multi-step graph
+        ``prime_reps`` times) so that the first timed replay does not pay the one-time graph upload
+        to the device (~1.6 ms for the 16-step graph at 1M envs) and the clock has settled after the
+        idle of the capture itself (a >= 10 ms idle costs the next ~40 steps up to 35 %,
+        profiles/r2_dvfs_probe.md)."""
         if self.backend != "native" or (self.world_size > 1 and self.cfg.engine.dp_overlap):
             return False
         if self.world_size > 1:
@@ -492,8 +495,9 @@ class VectorEngine:
             g.replay()
             self.step_count += 1
             if self._graph_k is not None:
-                gk.replay()
-                self.step_count += k
+                for _ in range(max(1, int(prime_reps))):
+                    gk.replay()
+                    self.step_count += k
         return True
 
     # ---------------------------------------------------------------- metrics
