@@ -108,6 +108,11 @@ def main() -> int:
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
 
+    # load the (lazily loaded) torch kernels of the start-of-window portfolio snapshot before the graphs
+    # are primed: loading them between the warm-up and the timed window idled the GPU for >= 10 ms,
+    # and the clock then needs ~40 steps to settle (tools/dvfs_probe.py, profiles/r2_dvfs_probe.md)
+    eng.current_portfolios().double().clone()
+    torch.cuda.synchronize()
     use_graph = not args.no_graph and not cfg.engine.dp_overlap
     if use_graph:
         try:
@@ -121,11 +126,6 @@ def main() -> int:
             _native.clear_last_error()
             torch.cuda.synchronize()
             eng._graph, eng._graph_k, use_graph = None, None, False
-    # load the (lazily loaded) torch kernels of the start-of-window portfolio snapshot now: loading them
-    # between the warm-up and the timed window idles the GPU for >= 10 ms, and the clock then needs
-    # ~40 steps to settle (tools/dvfs_probe.py, profiles/r2_dvfs_probe.md)
-    eng.current_portfolios().double().clone()
-    torch.cuda.synchronize()
     prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()

@@ -460,8 +460,8 @@ class VectorEngine:
         58.8 us without DP (tools/dp_host_overhead.py).  The overlapped-DP path (``dp_overlap``)
         keeps Python-side pending state between steps and is not captured.
 
-        ``prime``: replay each captured graph (real, counted steps; the multi-step graph
-        ``prime_reps`` times) so that the first timed replay does not pay the one-time graph upload
+        ``prime``: replay each captured graph (real, counted steps; the multi-step graph at least
+        ``prime_reps`` times and until its replay time has settled, :meth:`prime_graph`) so that the first timed replay does not pay the one-time graph upload
         to the device (~1.6 ms for the 16-step graph at 1M envs) and the clock has settled after the
         idle of the capture itself (a >= 10 ms idle costs the next ~40 steps up to 35 %,
         profiles/r2_dvfs_probe.md)."""
@@ -495,10 +495,28 @@ class VectorEngine:
             g.replay()
             self.step_count += 1
             if self._graph_k is not None:
-                for _ in range(max(1, int(prime_reps))):
-                    gk.replay()
-                    self.step_count += k
+                self.prime_graph(prime_reps)
         return True
+
+    def prime_graph(self, min_reps: int = 1, max_reps: int = 40, tol: float = 0.015) -> int:
+        """Replay the multi-step graph at least ``min_reps`` times and until two consecutive replays
+        take the same time within ``tol`` (the clock has settled; at most ``max_reps``).  Real,
+        counted steps.  Returns the replays done."""
+        gk, k = self._graph_k
+        prev, n = None, 0
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        while n < max_reps:
+            ev[0].record()
+            gk.replay()
+            ev[1].record()
+            self.step_count += k
+            n += 1
+            ev[1].synchronize()
+            t = ev[0].elapsed_time(ev[1])
+            if n >= min_reps and prev is not None and abs(t - prev) <= tol * prev:
+                break
+            prev = t
+        return n
 
     # ---------------------------------------------------------------- metrics
     def stats_dict(self) -> Dict[str, float]:
