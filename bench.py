@@ -118,7 +118,8 @@ def main() -> int:
         try:
             # 2 eager steps before capture, then one replay of each captured graph (graph upload);
             # all of them untimed and reported as "graph_prime_steps"
-            use_graph = eng.capture_graph(warmup=2, prime=True, prime_reps=4)
+            # (N > 1: a fixed 6 replays on every rank -- each replay holds the all-reduce)
+            use_graph = eng.capture_graph(warmup=2, prime=True, prime_reps=4 if world == 1 else 6)
         except Exception as e:  # noqa: BLE001 -- fall back to eager launches, same math
             print(f"bench: HIP graph capture failed ({str(e).splitlines()[0]}); running eagerly", file=sys.stderr)
             from sharetrade.ops import native as _native

@@ -501,8 +501,17 @@ class VectorEngine:
     def prime_graph(self, min_reps: int = 1, max_reps: int = 40, tol: float = 0.015) -> int:
         """Replay the multi-step graph at least ``min_reps`` times and until two consecutive replays
         take the same time within ``tol`` (the clock has settled; at most ``max_reps``).  Real,
-        counted steps.  Returns the replays done."""
+        counted steps.  Returns the replays done.
+
+        DP (world_size > 1): exactly ``min_reps`` replays on every rank -- each replay holds the
+        gradient all-reduce, so a per-rank stopping decision could leave ranks with different
+        collective counts (a hang)."""
         gk, k = self._graph_k
+        if self.world_size > 1:
+            for _ in range(max(1, int(min_reps))):
+                gk.replay()
+                self.step_count += k
+            return max(1, int(min_reps))
         prev, n = None, 0
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         while n < max_reps:

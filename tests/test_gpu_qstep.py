@@ -446,3 +446,22 @@ def test_pair_kernel_multi_step_bf16_slabs(native_built):
     assert torch.equal(posw, posp)
     assert _rel(pp, pw) < 1e-3, _rel(pp, pw)
     assert abs(stp["explore"] - stw["explore"]) <= 0.01 * max(1.0, stw["explore"])
+
+
+def test_graph_priming_is_rank_uniform(native_built):
+    """prime_graph: one process stops once two consecutive replays agree; with world_size > 1 it
+    replays exactly min_reps times on every rank (each replay holds the DP all-reduce, so a
+    per-rank stopping decision could leave ranks with different collective counts)."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg(False)
+    cfg.engine.graph_steps = 4
+    eng = VectorEngine(cfg, prices=_prices(256), device=torch.device("cuda", 0), envs=256)
+    assert eng.capture_graph(warmup=1, prime=True, prime_reps=2)
+    s0 = eng.step_count
+    n = eng.prime_graph(3)
+    assert 3 <= n <= 40 and eng.step_count == s0 + 4 * n
+    eng.world_size = 2          # only the stopping rule is exercised (no collective in this graph)
+    s1 = eng.step_count
+    assert eng.prime_graph(5) == 5 and eng.step_count == s1 + 20
+    eng.world_size = 1
