@@ -506,6 +506,8 @@ class VectorEngine:
         DP (world_size > 1): exactly ``min_reps`` replays on every rank -- each replay holds the
         gradient all-reduce, so a per-rank stopping decision could leave ranks with different
         collective counts (a hang)."""
+        if getattr(self, "_graph_k", None) is None:
+            return 0
         gk, k = self._graph_k
         if self.world_size > 1:
             for _ in range(max(1, int(min_reps))):
