@@ -47,7 +47,8 @@ class RecurrentDQN:
     def __init__(self, cfg: Config, device: torch.device, envs: int = 65536, seq: int = 16, batch: int = 1024,
                  replay_segments: int = 1 << 17, bars: int = 4096, ep_len: int = 390, burn_in: int = 4,
                  target_every: int = 100, cost: float = 0.01, lr: float = 3e-4, seed: Optional[int] = None,
-                 bar_params: Optional[mb.BarParams] = None, actor_grid: int = 256, grad_sync=None):
+                 bar_params: Optional[mb.BarParams] = None, actor_grid: int = 256, grad_sync=None,
+                 overlap_act: bool = False):
         if device.type != "cuda":
             raise ValueError("RecurrentDQN runs on the GPU (MX-fp8 / bf16 MFMA kernels)")
         if envs % G.RN:
@@ -66,6 +67,13 @@ class RecurrentDQN:
         self.gamma = float(cfg.agent.gamma)
         self.grid = int(actor_grid)
         self.grad_sync = grad_sync
+        # overlap_act: one captured graph per iteration in which the update samples its segments first,
+        # then the actor launch runs on a side stream beside the rest of the update (unroll, BPTT,
+        # weight-gradient GEMMs, Adam); the MX-fp8 re-pack of the actor weights waits for it (the actor
+        # reads the pre-update packed weights, as in the serial order).  Only difference from the
+        # serial order: the update samples the ring as it was before this iteration's segments.
+        self.overlap_act = bool(overlap_act)
+        self._act_stream = torch.cuda.Stream(device=device) if self.overlap_act else None
         self.k = G.lib()
         self.kd = _bind_deep()
         dev, f32, b16, i32, u8 = device, torch.float32, torch.bfloat16, torch.int32, torch.uint8
@@ -247,14 +255,23 @@ class RecurrentDQN:
         native.check(self.k.st_gru_act(self._act, self.grid, native.stream_handle()), "st_gru_act")
 
     # ---------------------------------------------------------------- learner
-    def update(self) -> None:
+    def update(self, with_act: bool = False) -> None:
         """One learner update on B sampled segments: gather -> fused unroll of both nets (MX-fp8) ->
-        TD -> fused BPTT (bf16) -> split-K weight-gradient GEMMs -> Adam -> repack the actor weights."""
+        TD -> fused BPTT (bf16) -> split-K weight-gradient GEMMs -> Adam -> repack the actor weights.
+        ``with_act``: the actor launch runs on a side stream right after the gather (see overlap_act)."""
         sh = native.stream_handle()
         k, kd = self.k, self.kd
         S, B = self.S, self.B
         RS, R1 = S * B, (S + 1) * B
         native.check(k.st_gru_gather(self._gather, sh), "st_gru_gather")
+        main = torch.cuda.current_stream(self.dev)
+        act = self._act_stream if with_act else None
+        if with_act:
+            if act is None:
+                raise RuntimeError("update(with_act=True) needs overlap_act=True")
+            act.wait_stream(main)          # segments sampled: the actor may insert now
+            with torch.cuda.stream(act):
+                self.act()
         native.check(k.st_gru_seq_fwd(self._fwd, sh), "st_gru_seq_fwd")
         self.loss.zero_()
         native.check(k.st_gru_td(self._td, sh), "st_gru_td")
@@ -272,6 +289,8 @@ class RecurrentDQN:
         nl = native.lib()
         native.check(nl.st_advance(self.opt_ctrl.data_ptr(), sh), "advance")
         native.check(nl.st_reduce_optim(self._opt, sh), "adam")
+        if act is not None:
+            main.wait_stream(act)          # the actor reads the packed weights the re-pack overwrites
         self.pack("on")
 
     def sync_target(self) -> None:
@@ -284,8 +303,11 @@ class RecurrentDQN:
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
-            self.act()
-            self.update()
+            if self.overlap_act:
+                self.update(with_act=True)   # same op order as the captured iteration
+            else:
+                self.act()
+                self.update()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         self.launches += 1
         self.updates += 1
@@ -295,6 +317,11 @@ class RecurrentDQN:
         self._g_upd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_upd):
             self.update()
+        self._g_iter = None
+        if self.overlap_act:
+            self._g_iter = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_iter):
+                self.update(with_act=True)
 
     def act_step(self) -> None:
         if self._g_act is not None:
@@ -313,7 +340,18 @@ class RecurrentDQN:
             self.sync_target()
 
     def iteration(self, updates: int = 1) -> None:
-        self.act_step()
+        if self.overlap_act and updates >= 1:
+            if getattr(self, "_g_iter", None) is not None:
+                self._g_iter.replay()
+            else:
+                self.update(with_act=True)
+            self.launches += 1
+            self.updates += 1
+            if self.updates % self.target_every == 0:
+                self.sync_target()
+            updates -= 1
+        else:
+            self.act_step()
         for _ in range(updates):
             self.update_step()
 

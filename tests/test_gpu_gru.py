@@ -242,3 +242,31 @@ def test_graph_iterations_train(native_built):
     assert s["episodes"] > 0 and np.isfinite(s["episode_return_mean"])
     assert torch.isfinite(d.flat).all() and not torch.equal(w0, d.P["w_hh"])
     assert int(d.t_ctr) == 7
+
+
+def test_overlapped_actor_matches_same_order_serial(native_built):
+    """overlap_act: the actor launch on its own stream beside the update (captured graph) equals the
+    same operation order on one stream: identical env / replay state, parameters within fp32
+    atomic-order noise."""
+    res = []
+    for serial in (False, True):
+        d = _small(E=256, S=8, eps=0.9, batch=256, overlap_act=True)
+        for _ in range(2):
+            d.act()
+        if serial:
+            d._act_stream = torch.cuda.current_stream()   # same op order, one stream, eager
+            for _ in range(4):
+                d.iteration(1)
+        else:
+            d.capture()
+            for _ in range(3):
+                d.iteration(1)
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    assert a.updates == b.updates == 4 and a.launches == b.launches
+    assert int(a.t_ctr) == int(b.t_ctr) == 4
+    assert torch.equal(a.rctrl, b.rctrl)
+    assert torch.equal(a.stats, b.stats) or torch.allclose(a.stats, b.stats, rtol=1e-6)
+    rel = float((a.flat - b.flat).norm() / (b.flat.norm() + 1e-20))
+    assert rel < 1e-5, rel
