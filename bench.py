@@ -127,6 +127,10 @@ def main() -> int:
             _native.clear_last_error()
             torch.cuda.synchronize()
             eng._graph, eng._graph_k, use_graph = None, None, False
+    if not use_graph:
+        # eager launches (--no-graph, overlapped DP, or a failed capture): the same clock settling as the
+        # graph priming, a fixed 64 steps on every rank (each step holds the DP all-reduce)
+        eng.run(64)
     prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()
