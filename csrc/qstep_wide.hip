@@ -73,6 +73,9 @@ constexpr int KPIPE = ST_WIDE_KPIPE;   // double-buffered k-loops (bits): 1 laye
 // the epilogue ds_write_b64 of 16 env rows at one column drops from 4-way to 2-way bank conflicts
 // (rows r and r + 4 no longer share banks).  Weight images and the dQ rows are not swizzled.
 constexpr bool ASWZ = ST_WIDE_ASWZ;
+#ifndef ST_WIDE_PRIO
+#define ST_WIDE_PRIO 0   // 1: the second-dispatched half of the waves at s_setprio 1 through the chunk loop
+#endif
 #ifndef ST_WIDE_DRAW_EARLY
 #define ST_WIDE_DRAW_EARLY 0
 #endif
@@ -483,6 +486,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
   __syncthreads();
   STW_STAMPX(1);
 
+  if (ST_WIDE_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   while (chunk < nchunks) {
     STW_STAMP(0);
     if (dyn && tid == 0) claim_v = atomicAdd(head, 1u);   // the chunk after c1 (published after P1)
@@ -822,6 +826,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
 #undef STW_PREFETCH_NEXT
 #undef STW_STAMP
 
+  if (ST_WIDE_PRIO) __builtin_amdgcn_s_setprio(0);
   STW_STAMPX(2);
   // ---------------------------------------------------------------- per-workgroup stats (-> LDS -> slab)
   // (before the slab write-out, so its barrier does not wait for the slab stores; the chunk loop
