@@ -29,8 +29,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=4, help="actor launches to pre-fill the replay")
     ap.add_argument("--updates", type=int, default=1)
     ap.add_argument("--grid", type=int, default=0,
-                    help="actor workgroups (one per CU): 0 = auto -- all CUs, or 7/8 of them when the update runs "
-                         "beside the actor (the update's unroll / BPTT kernels take the rest)")
+                    help="actor workgroups (one per CU): 0 = auto (RecurrentDQN._auto_grid)")
+    ap.add_argument("--actor-kernel", default="auto", choices=["auto", "single", "pair"],
+                    help="single- or two-chunk actor kernel (auto: two-chunk when seq <= 32)")
     ap.add_argument("--no-overlap-act", action="store_true",
                     help="serial actor launch then update (default: the actor runs beside the update after its "
                          "segments are sampled; profiles/r2_config5_overlap.md)")
@@ -43,11 +44,9 @@ def main():
 
     cfg = preset_config("recurrent")
     dev = torch.device("cuda", 0)
-    if a.grid <= 0:
-        cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        a.grid = cus if a.no_overlap_act else cus - cus // 8
     d = RecurrentDQN(cfg, dev, envs=a.envs, seq=a.seq, batch=a.batch, bars=a.bars, replay_segments=a.replay,
-                     actor_grid=a.grid, overlap_act=not a.no_overlap_act)
+                     actor_grid=a.grid, overlap_act=not a.no_overlap_act, actor_kernel=a.actor_kernel)
+    a.grid = d.grid
     for _ in range(a.warmup):
         d.act()
     d.capture()
@@ -87,7 +86,7 @@ def main():
         "update_ms": round(t_upd * 1e3, 4), "update_tflops": round(upd_flop / t_upd / 1e12, 1),
         "episodes": s["episodes"], "episode_return_mean": s["episode_return_mean"],
         "reward_per_step": s["reward_per_step"], "loss": s["loss"], "overlap_act": d.overlap_act,
-        "actor_grid": a.grid,
+        "actor_grid": a.grid, "actor_kernel": d.actor_kernel,
     }
     print(json.dumps(out))
 

@@ -420,6 +420,8 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
       GR_STAMP(2)
       quant_h(hr, sH8 + nxt * RN * HS, sSc + nxt * RN * SCS, wave, l16, g4);
       GR_STAMP(3)
+      if (p.stamps != nullptr && blockIdx.x == 0 && chunk == 0 && lane == 0)   // every wave: arrival at barrier 1
+        p.stamps[(size_t)S * 16 + (size_t)s * RW + wave] = __builtin_amdgcn_s_memtime();
       __syncthreads();
       GR_STAMP(4)
       // ---------------------------------------------------------- env step (wave 0)
@@ -433,8 +435,9 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
           q[a] = v;
         }
         int greedy = 0;
-        if (q[1] > q[greedy]) greedy = 1;
-        if (q[2] > q[greedy]) greedy = 2;
+        const float qg = q[1] > q[0] ? q[1] : q[0];   // select chain: no stack-indexed q[greedy]
+        if (q[1] > q[0]) greedy = 1;
+        if (q[2] > qg) greedy = 2;
         const f4v u = sU[s * RN + (lane & (RN - 1))];   // (explore coin, random action, reset, step)
         const bool exploit = u[0] < fminf(p.eps, u[3] * p.inv_ramp);
         const int rnd = min((int)(u[1] * 3.0f), 2);
@@ -466,7 +469,10 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
           const size_t o = (size_t)me * p.T + t_;
           const uint4 fr = bar_feat(p, me, t_);
           const float cr = p.close[o], rr = p.ret[o];
-          fx = done ? fr : fx;
+          fx.x = done ? fr.x : fx.x;   // per component: a uint4 ternary lowers to a stack select
+      fx.y = done ? fr.y : fx.y;
+      fx.z = done ? fr.z : fx.z;
+      fx.w = done ? fr.w : fx.w;
           cx = done ? cr : cx;
           rx = done ? rr : rx;
         }
@@ -541,6 +547,425 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
   }
 }
 
+// ---------------------------------------------------------------- two-chunk actor
+// gru_act_kernel runs each env step as [MFMA phase: every wave] -> barrier -> [env phase: wave 0 alone,
+// ~1.45k of the ~8.5k cycles of a step, the other seven waves idle] -> barrier
+// (profiles/r1_stamps_gru_actor.md).  Here a workgroup holds TWO 32-env chunks (slots A, B) and
+// alternates: wave 0 runs slot A's env phase of step s while every wave runs slot B's MFMA phase of
+// step s, then slot B's env phase beside slot A's MFMA phase of step s+1 -- each barrier interval
+// pairs one chunk's serial env work with the other chunk's matrix work.  Per chunk the arithmetic
+// and its order are those of gru_act_kernel (bit-identical env / replay / h), so the same tests
+// hold.  LDS: the shared weights + two slot images (S <= 32 Philox rows each) = 146 KB.
+constexpr int PAIR_SMAX = 32;
+struct Act2Lds {
+  static constexpr int WX = 0;                                   // RW*6*64 s8v
+  static constexpr int B = WX + RW * 6 * 64 * 16;                // [4*RH] float
+  static constexpr int WQ = B + 4 * RH * 4;                      // [4*RH] float
+  static constexpr int SLOT0 = WQ + 4 * RH * 4;
+  // one slot (offsets from its base)
+  static constexpr int X = 0;                                    // [2][RN*XS] bf16
+  static constexpr int H8 = X + 2 * RN * XS * 2;                 // [2][RN*HS] bytes
+  static constexpr int SC = H8 + 2 * RN * HS;                    // [2][RN*SCS] int
+  static constexpr int QP = SC + 2 * RN * SCS * 4;               // [RW][3][RN] float
+  static constexpr int DN = QP + RW * 3 * RN * 4;                // [RN] int
+  static constexpr int U = DN + RN * 4;                          // [PAIR_SMAX][RN][4] float: Philox draws
+  static constexpr int ENV = U + PAIR_SMAX * RN * 16;            // [16][64] words: wave 0's env state
+  static constexpr int SLOT = ENV + 16 * 64 * 4;
+  static constexpr int BYTES = SLOT0 + 2 * SLOT;
+};
+static_assert(Act2Lds::BYTES <= 160 * 1024, "two-chunk actor LDS");
+static_assert(Act2Lds::SLOT0 % 16 == 0 && Act2Lds::SLOT % 16 == 0, "16-byte aligned slots");
+
+struct ActEnv {
+  int t, es, pz, eps;
+  float en, er, lr, cA, cB, rA, rB;
+  uint4 fB;
+  unsigned slot;
+};
+
+template <int V>
+struct ActSlot {
+  static constexpr int v = V;
+};
+
+__global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const s8v* sWx = reinterpret_cast<const s8v*>(lds + Act2Lds::WX);
+  float* sB = reinterpret_cast<float*>(lds + Act2Lds::B);
+  float* sWq = reinterpret_cast<float*>(lds + Act2Lds::WQ);
+
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < RW * 6 * 64; i += RT) reinterpret_cast<s8v*>(lds + Act2Lds::WX)[i] = p.wih[i];
+  for (int i = tid; i < 4 * RH; i += RT) {
+    sB[i] = p.bias4[i];
+    sWq[i] = p.wq[i];
+  }
+  i8v Wh[3][2][2];
+  int Ws4[3] = {0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int idx = (((wave * 3 + g) * 2 + m) * 2 + ks) * 64 + lane;
+        Wh[g][m][ks] = p.whh8[idx];
+        Ws4[g] |= (p.whhs[idx] & 0xFF) << (8 * (2 * m + ks));
+      }
+  const s8v* myWx = sWx + wave * 6 * 64 + lane;
+  s8v WqA;
+  {
+    const int a = l16;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int u = 32 * wave + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+      WqA[j] = (short)f2bf(a < 3 ? p.wq[a * RH + u] : 0.f);
+    }
+  }
+  const unsigned long long launch = p.ctrl[0];
+  const unsigned long long seg0 = p.rctrl[0];
+  const int nchunks = p.E / RN, S = p.S;
+  const int npairs = (nchunks + 1) / 2;
+  const bool writer = lane < RN;
+  __syncthreads();
+
+  // ---------------------------------------------------------------- per-slot state
+  // h lives in registers (every wave, both slots); wave 0's env state of the slot that is not in its
+  // env phase is parked in LDS (ActEnv) so it does not hold registers through the other slot's MFMAs
+  float hr[2][2][2][4];
+  int e0_[2] = {0, 0};
+  bool valid_[2] = {false, false};
+  float st_rew = 0.f, st_exp = 0.f, st_fin = 0.f, st_dn = 0.f;
+  auto base = [&](auto sl) { return lds + Act2Lds::SLOT0 + decltype(sl)::v * Act2Lds::SLOT; };
+  auto env_ld = [&](auto sl) {
+    const unsigned* w = reinterpret_cast<const unsigned*>(base(sl) + Act2Lds::ENV) + lane;
+    ActEnv v;
+    v.t = (int)w[0 * 64]; v.es = (int)w[1 * 64]; v.pz = (int)w[2 * 64]; v.eps = (int)w[3 * 64];
+    v.en = __uint_as_float(w[4 * 64]); v.er = __uint_as_float(w[5 * 64]); v.lr = __uint_as_float(w[6 * 64]);
+    v.cA = __uint_as_float(w[7 * 64]); v.cB = __uint_as_float(w[8 * 64]);
+    v.rA = __uint_as_float(w[9 * 64]); v.rB = __uint_as_float(w[10 * 64]);
+    v.fB = make_uint4(w[11 * 64], w[12 * 64], w[13 * 64], w[14 * 64]);
+    v.slot = w[15 * 64];
+    return v;
+  };
+  auto env_st = [&](auto sl, const ActEnv& v) {
+    unsigned* w = reinterpret_cast<unsigned*>(base(sl) + Act2Lds::ENV) + lane;
+    w[0 * 64] = (unsigned)v.t; w[1 * 64] = (unsigned)v.es; w[2 * 64] = (unsigned)v.pz; w[3 * 64] = (unsigned)v.eps;
+    w[4 * 64] = __float_as_uint(v.en); w[5 * 64] = __float_as_uint(v.er); w[6 * 64] = __float_as_uint(v.lr);
+    w[7 * 64] = __float_as_uint(v.cA); w[8 * 64] = __float_as_uint(v.cB);
+    w[9 * 64] = __float_as_uint(v.rA); w[10 * 64] = __float_as_uint(v.rB);
+    w[11 * 64] = v.fB.x; w[12 * 64] = v.fB.y; w[13 * 64] = v.fB.z; w[14 * 64] = v.fB.w;
+    w[15 * 64] = v.slot;
+  };
+
+  // load a chunk into a slot: h (fp32 registers + fp8 LDS tile 0), env state (wave 0), x_0, Philox draws
+  auto init = [&](auto sl, int chunk, bool valid) {
+    constexpr int K = decltype(sl)::v;
+    unsigned char* sb = base(sl);
+    bf16_t* sX = reinterpret_cast<bf16_t*>(sb + Act2Lds::X);
+    f4v* sU = reinterpret_cast<f4v*>(sb + Act2Lds::U);
+    const int cc = valid ? chunk : nchunks - 1;   // an empty slot computes on a clamped chunk, writes nothing
+    const int e0 = cc * RN;
+    valid_[K] = valid;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int e = e0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
+        const float4 v = *reinterpret_cast<const float4*>(p.h + (size_t)e * RH + u0);
+        hr[K][m][n][0] = v.x; hr[K][m][n][1] = v.y; hr[K][m][n][2] = v.z; hr[K][m][n][3] = v.w;
+        if (valid) {
+          const size_t slot = (size_t)((seg0 + (unsigned long long)e) % (unsigned long long)p.cap);
+          lds_st4(p.rh0 + slot * RH + u0, v.x, v.y, v.z, v.w);
+        }
+      }
+    quant_h(hr[K], sb + Act2Lds::H8, reinterpret_cast<int*>(sb + Act2Lds::SC), wave, l16, g4);
+    e0_[K] = e0;
+    if (wave == 0) {
+      const int me = e0 + (lane & (RN - 1));
+      ActEnv v;
+      v.t = p.pos[me]; v.es = p.ep_start[me]; v.pz = p.position[me]; v.en = p.entry[me];
+      v.er = p.ep_ret[me]; v.eps = p.episodes[me]; v.lr = p.last_ret[me];
+      v.slot = (unsigned)((seg0 + (unsigned long long)me) % (unsigned long long)p.cap);
+      const size_t o = (size_t)me * p.T + v.t;
+      v.cA = p.close[o];
+      v.cB = p.close[o + 1];
+      v.rA = p.ret[o];
+      v.rB = p.ret[o + 1];
+      v.fB = bar_feat(p, me, v.t + 1);
+      const uint4 f0 = bar_feat(p, me, v.t);
+      if (writer)
+        build_x(p, f0, v.cA, v.t, v.es, v.pz, v.en, sX + lane * XS,
+                valid ? p.rx + (size_t)v.slot * (size_t)(S + 1) * RF : nullptr);
+      env_st(sl, v);
+    }
+    for (int i = tid; i < S * RN; i += RT) {
+      const int ss = i / RN, e = e0 + (i % RN);
+      const unsigned long long step = launch * (unsigned long long)S + (unsigned long long)ss;
+      uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32),
+               c3 = 0x47525531u;
+      philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+      f4v u;
+      u[0] = u24(c0); u[1] = u24(c1); u[2] = u24(c2); u[3] = (float)step;
+      sU[i] = u;
+    }
+  };
+
+  // MFMA phase of one step of a slot: gates from x (bf16) and h (MX-fp8), GRU update in registers,
+  // Q partials -> LDS, h re-quantized into the other fp8 tile (reads tile `cur`, writes `cur ^ 1`)
+  auto mfma_phase = [&](auto sl, int cur) {
+    constexpr int K = decltype(sl)::v;
+    unsigned char* sb = base(sl);
+    const bf16_t* cX = reinterpret_cast<const bf16_t*>(sb + Act2Lds::X) + cur * RN * XS;
+    const unsigned char* cH = sb + Act2Lds::H8 + cur * RN * HS;
+    const int* cS = reinterpret_cast<const int*>(sb + Act2Lds::SC) + cur * RN * SCS;
+    float* sQp = reinterpret_cast<float*>(sb + Act2Lds::QP);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      f4v ar[2], az[2], anx[2], anh[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int u0 = 32 * wave + 16 * m + 4 * g4;
+        ar[m] = *reinterpret_cast<const f4v*>(sB + u0);
+        az[m] = *reinterpret_cast<const f4v*>(sB + RH + u0);
+        anx[m] = *reinterpret_cast<const f4v*>(sB + 2 * RH + u0);
+        anh[m] = *reinterpret_cast<const f4v*>(sB + 3 * RH + u0);
+      }
+      const int row = 16 * n + l16;
+      {
+        const s8v xb = lds_ld8(cX + row * XS + 8 * g4);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          ar[m] = mfma32(myWx[(0 * 2 + m) * 64], xb, ar[m]);
+          az[m] = mfma32(myWx[(1 * 2 + m) * 64], xb, az[m]);
+          anx[m] = mfma32(myWx[(2 * 2 + m) * 64], xb, anx[m]);
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 h0 = *reinterpret_cast<const uint4*>(cH + row * HS + 128 * ks + 16 * g4);
+        const uint4 h1 = *reinterpret_cast<const uint4*>(cH + row * HS + 128 * ks + 64 + 16 * g4);
+        i8v hb;
+        hb[0] = (int)h0.x; hb[1] = (int)h0.y; hb[2] = (int)h0.z; hb[3] = (int)h0.w;
+        hb[4] = (int)h1.x; hb[5] = (int)h1.y; hb[6] = (int)h1.z; hb[7] = (int)h1.w;
+        const int sc = cS[row * SCS + 4 * ks + g4];
+#define ST_MX3P(M, KS)                                                             \
+  ar[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[0][M][KS], hb, ar[M], Ws4[0], sc);          \
+  az[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[1][M][KS], hb, az[M], Ws4[1], sc);          \
+  anh[M] = mx_mfma_sel<2 * (M) + (KS)>(Wh[2][M][KS], hb, anh[M], Ws4[2], sc);
+        if (ks == 0) { ST_MX3P(0, 0) ST_MX3P(1, 0) } else { ST_MX3P(0, 1) ST_MX3P(1, 1) }
+#undef ST_MX3P
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float r = sigm2(ar[m][i]);
+          const float z = sigm2(az[m][i]);
+          const float nn = tanh2(__builtin_fmaf(r, anh[m][i], anx[m][i]));
+          hr[K][m][n][i] = __builtin_fmaf(z, hr[K][m][n][i] - nn, nn);
+        }
+      {
+        s8v hb;
+        const uint32_t p0 = pack_bf2(hr[K][0][n][0], hr[K][0][n][1]), p1 = pack_bf2(hr[K][0][n][2], hr[K][0][n][3]);
+        const uint32_t p2 = pack_bf2(hr[K][1][n][0], hr[K][1][n][1]), p3 = pack_bf2(hr[K][1][n][2], hr[K][1][n][3]);
+        hb[0] = (short)(p0 & 0xFFFF); hb[1] = (short)(p0 >> 16); hb[2] = (short)(p1 & 0xFFFF); hb[3] = (short)(p1 >> 16);
+        hb[4] = (short)(p2 & 0xFFFF); hb[5] = (short)(p2 >> 16); hb[6] = (short)(p3 & 0xFFFF); hb[7] = (short)(p3 >> 16);
+        const f4v qp = mfma32(WqA, hb, zero4());
+        if (g4 == 0) {
+          sQp[(wave * 3 + 0) * RN + row] = qp[0];
+          sQp[(wave * 3 + 1) * RN + row] = qp[1];
+          sQp[(wave * 3 + 2) * RN + row] = qp[2];
+        }
+      }
+    }
+    quant_h(hr[K], sb + Act2Lds::H8 + (cur ^ 1) * RN * HS, reinterpret_cast<int*>(sb + Act2Lds::SC) + (cur ^ 1) * RN * SCS,
+            wave, l16, g4);
+  };
+
+  // env phase of step s of a slot (wave 0): Q, epsilon-greedy, trading env, replay segment, next x
+  // into tile `nxt`, done flags (+ the next tile's h rows zeroed for finished episodes)
+  auto env_phase = [&](auto sl, int s, int nxt) {
+    constexpr int K = decltype(sl)::v;
+    unsigned char* sb = base(sl);
+    const float* sQp = reinterpret_cast<const float*>(sb + Act2Lds::QP);
+    const f4v* sU = reinterpret_cast<const f4v*>(sb + Act2Lds::U);
+    int* sDone = reinterpret_cast<int*>(sb + Act2Lds::DN);
+    const int me = e0_[K] + (lane & (RN - 1));
+    const bool valid = valid_[K];
+    ActEnv v = env_ld(sl);
+    float q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      float v = sWq[3 * RH + a];
+#pragma unroll
+      for (int w = 0; w < RW; ++w) v += sQp[(w * 3 + a) * RN + (lane & (RN - 1))];
+      q[a] = v;
+    }
+    int greedy = 0;
+    const float qg = q[1] > q[0] ? q[1] : q[0];
+    if (q[1] > q[0]) greedy = 1;
+    if (q[2] > qg) greedy = 2;
+    const f4v u = sU[s * RN + (lane & (RN - 1))];
+    const bool exploit = u[0] < fminf(p.eps, u[3] * p.inv_ramp);
+    const int rnd = min((int)(u[1] * 3.0f), 2);
+    const int a = exploit ? greedy : rnd;
+    const int np = a == 0 ? 1 : (a == 1 ? 0 : v.pz);
+    const bool trade = np != v.pz;
+    if (trade && np == 1) v.en = v.cA;
+    const float rew = (float)np * v.rA - (trade ? p.cost : 0.f);
+    v.er += rew;
+    int t1 = v.t + 1;
+    const bool done = (t1 - v.es) >= p.ep_len;
+    float fin = 0.f;
+    if (done) {
+      v.eps += 1;
+      v.lr = v.er;
+      fin = v.er;
+      v.es = min((int)(u[2] * (float)(p.T - p.ep_len - 1)), p.T - p.ep_len - 2);
+      t1 = v.es;
+      v.pz = 0;
+      v.er = 0.f;
+    } else {
+      v.pz = np;
+    }
+    v.t = t1;
+    uint4 fx = v.fB;
+    float cx = v.cB, rx = v.rB;
+    if (__builtin_amdgcn_ballot_w64(done) != 0ull) {
+      const size_t o = (size_t)me * p.T + v.t;
+      const uint4 fr = bar_feat(p, me, v.t);
+      const float cr = p.close[o], rr = p.ret[o];
+      fx.x = done ? fr.x : fx.x;   // per component: a uint4 ternary lowers to a stack select
+      fx.y = done ? fr.y : fx.y;
+      fx.z = done ? fr.z : fx.z;
+      fx.w = done ? fr.w : fx.w;
+      cx = done ? cr : cx;
+      rx = done ? rr : rx;
+    }
+    if (writer) {
+      const size_t sl_ = v.slot;
+      if (valid) {
+        p.ra[sl_ * S + s] = (unsigned char)a;
+        p.rr[sl_ * S + s] = rew;
+        p.rd[sl_ * S + s] = done ? 1 : 0;
+      }
+      build_x(p, fx, cx, v.t, v.es, v.pz, v.en,
+              reinterpret_cast<bf16_t*>(sb + Act2Lds::X) + nxt * RN * XS + lane * XS,
+              valid ? p.rx + (sl_ * (size_t)(S + 1) + (size_t)(s + 1)) * RF : nullptr);
+      sDone[lane] = done ? 1 : 0;
+      if (done) {
+        uint4* hz = reinterpret_cast<uint4*>(sb + Act2Lds::H8 + nxt * RN * HS + lane * HS);
+        const uint4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < RH / 16; ++j) hz[j] = z;
+      }
+      if (valid && p.q_out && s == S - 1) {
+        float* qo = p.q_out + (size_t)me * 4;
+        qo[0] = q[0]; qo[1] = q[1]; qo[2] = q[2]; qo[3] = (float)a;
+      }
+      if (valid) {
+        st_rew += rew;
+        st_exp += exploit ? 0.f : 1.f;
+        st_fin += fin;
+        st_dn += done ? 1.f : 0.f;
+      }
+    }
+    v.cA = cx;
+    v.rA = rx;
+    const size_t o1 = (size_t)me * p.T + min(v.t + 1, p.T - 1);
+    v.cB = p.close[o1];
+    v.rB = p.ret[o1];
+    v.fB = *reinterpret_cast<const uint4*>(p.feat + o1 * RMF);
+    env_st(sl, v);
+  };
+
+  // h of envs whose episode ended restarts from 0 (after the env phase's barrier)
+  auto reset = [&](auto sl) {
+    constexpr int K = decltype(sl)::v;
+    const int* sDone = reinterpret_cast<const int*>(base(sl) + Act2Lds::DN);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      if (sDone[16 * n + l16]) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) hr[K][m][n][i] = 0.f;
+      }
+  };
+
+  auto writeback = [&](auto sl) {
+    constexpr int K = decltype(sl)::v;
+    if (!valid_[K]) return;
+    const int e0 = e0_[K];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int e = e0 + 16 * n + l16, u0 = 32 * wave + 16 * m + 4 * g4;
+        *reinterpret_cast<float4*>(p.h + (size_t)e * RH + u0) =
+            make_float4(hr[K][m][n][0], hr[K][m][n][1], hr[K][m][n][2], hr[K][m][n][3]);
+      }
+    if (wave == 0 && writer) {
+      const int me = e0 + lane;
+      const ActEnv v = env_ld(sl);
+      p.pos[me] = v.t; p.ep_start[me] = v.es; p.position[me] = v.pz; p.entry[me] = v.en;
+      p.ep_ret[me] = v.er; p.episodes[me] = v.eps; p.last_ret[me] = v.lr;
+    }
+  };
+
+  constexpr ActSlot<0> A{};
+  constexpr ActSlot<1> Bs{};
+  for (int pr = blockIdx.x; pr < npairs; pr += gridDim.x) {
+    init(A, 2 * pr, true);
+    init(Bs, 2 * pr + 1, 2 * pr + 1 < nchunks);
+    __syncthreads();
+    mfma_phase(A, 0);                              // slot A, step 0
+    __syncthreads();
+    for (int s = 0; s < S; ++s) {
+      const int cur = s & 1, nxt = cur ^ 1;
+      // debug interval stamps (tools/stamp_gru.py --kernel pair), first pair of workgroup 0, waves 0
+      // and 4 (same SIMD): 0 start, 1 after env A, 2 after MFMA B, 3 after barrier + reset A,
+      // 4 after env B, 5 after MFMA A, 6 after barrier + reset B
+#define GP_STAMP(I)                                                                                        \
+  if (p.stamps != nullptr && blockIdx.x == 0 && pr == 0 && (wave & 3) == 0 && lane == 0)                   \
+    p.stamps[((size_t)s * 2 + (wave >> 2)) * 8 + (I)] = __builtin_amdgcn_s_memtime();
+      GP_STAMP(0)
+      if (wave == 0) env_phase(A, s, nxt);         // A: env of step s   | B: MFMA of step s
+      GP_STAMP(1)
+      mfma_phase(Bs, cur);
+      GP_STAMP(2)
+      __syncthreads();
+      reset(A);
+      GP_STAMP(3)
+      if (wave == 0) env_phase(Bs, s, nxt);        // B: env of step s   | A: MFMA of step s + 1
+      GP_STAMP(4)
+      if (s + 1 < S) mfma_phase(A, nxt);
+      GP_STAMP(5)
+      __syncthreads();
+      reset(Bs);
+      GP_STAMP(6)
+#undef GP_STAMP
+    }
+    writeback(A);
+    writeback(Bs);
+    __syncthreads();
+  }
+  if (wave == 0) {
+    st_rew = wave_sum(st_rew);
+    st_exp = wave_sum(st_exp);
+    st_fin = wave_sum(st_fin);
+    st_dn = wave_sum(st_dn);
+    if (lane == 0) {
+      atomicAdd(p.stats + 0, st_rew);
+      atomicAdd(p.stats + 1, st_exp);
+      atomicAdd(p.stats + 2, st_dn);
+      atomicAdd(p.stats + 3, st_fin);
+    }
+  }
+}
+
 __global__ void gru_advance_kernel(unsigned long long* rctrl, unsigned long long* ctrl, int E, int cap) {
   rctrl[0] += (unsigned long long)E;
   rctrl[1] = rctrl[0] < (unsigned long long)cap ? rctrl[0] : (unsigned long long)cap;
@@ -590,6 +1015,26 @@ extern "C" hipError_t st_gru_act(const st::GruAct* p, int grid, hipStream_t s) {
 
 
 
+
+extern "C" int st_gru_act_pair_smax() { return st::PAIR_SMAX; }
+
+extern "C" hipError_t st_gru_act_pair(const st::GruAct* p, int grid, hipStream_t s) {
+  if (p->E % st::RN || p->S <= 0 || p->S > st::PAIR_SMAX || p->ep_len <= 0 || p->T < p->ep_len + 3 || p->cap <= 0 ||
+      grid <= 0)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)st::gru_act_pair_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, st::Act2Lds::BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int npairs = (p->E / st::RN + 1) / 2;
+  hipLaunchKernelGGL(st::gru_act_pair_kernel, dim3(grid < npairs ? grid : npairs), dim3(st::RT), st::Act2Lds::BYTES,
+                     s, *p);
+  hipLaunchKernelGGL(st::gru_advance_kernel, dim3(1), dim3(1), 0, s, p->rctrl, p->ctrl, p->E, p->cap);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t st_mx_probe(const void* a, const void* b, const int* sa, const int* sb, float* d,
                                   hipStream_t s) {

@@ -53,6 +53,18 @@ ST_DEV float tanh2(float x) {
 }
 ST_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
 
+// max over the 4 rows of 16 lanes (lanes l, l^16, l^32, l^48) of a non-negative value: two VALU
+// row swaps (v_permlane16/32_swap) instead of two LDS round trips (ds_bpermute); unsigned max of
+// the bit patterns == float max for non-negative finite values, without NaN canonicalisation
+ST_DEV float rowmax4(float v) {
+  uint32_t b = __float_as_uint(v);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(b, b, false, false);
+  b = max((uint32_t)r16[0], (uint32_t)r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(b, b, false, false);
+  b = max((uint32_t)r32[0], (uint32_t)r32[1]);
+  return __uint_as_float(b);
+}
+
 // quantize the lane's h values (units of this wave, 2 env tiles) into an LDS fp8 tile
 ST_DEV void quant_h(const float (&hr)[2][2][4], unsigned char* sH8, int* sSc, int wave, int l16, int g4) {
 #pragma unroll
@@ -62,8 +74,7 @@ ST_DEV void quant_h(const float (&hr)[2][2][4], unsigned char* sH8, int* sSc, in
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(hr[m][n][i]));
-    amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-    amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+    amax = rowmax4(amax);
     const int e = mx_exp(amax);
     const int row = 16 * n + l16;
 #pragma unroll

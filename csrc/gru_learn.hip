@@ -404,8 +404,7 @@ ST_DEV void quant_hilo(const float (&x)[8], unsigned char* hiRow, unsigned char*
   float amax = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(x[k]));
-  amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  amax = rowmax4(amax);
   const int eh = mx_exp(amax);
   uint32_t hw[2];
   float res[8];
@@ -421,8 +420,7 @@ ST_DEV void quant_hilo(const float (&x)[8], unsigned char* hiRow, unsigned char*
   float rmax = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) rmax = fmaxf(rmax, fabsf(res[k]));
-  rmax = fmaxf(rmax, __shfl_xor(rmax, 16, 64));
-  rmax = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
+  rmax = rowmax4(rmax);
   const int el = mx_exp(rmax);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {

@@ -92,6 +92,7 @@ def lib():
         for fn, args in (("st_minute_bars", [C.POINTER(MinuteBarsArgs), vp]),
                          ("st_gru_pack", [C.POINTER(PackArgs), vp]),
                          ("st_gru_act", [C.POINTER(ActArgs), i, vp]),
+                         ("st_gru_act_pair", [C.POINTER(ActArgs), i, vp]),
                          ("st_gru_gather", [C.POINTER(GatherArgs), vp]),
                          ("st_gru_seq_fwd", [C.POINTER(SeqFwdArgs), vp]),
                          ("st_gru_td", [C.POINTER(TDArgs), vp]),
@@ -102,6 +103,7 @@ def lib():
             f.argtypes = args
             f.restype = C.c_int
         L.st_gru_act_lds_bytes.restype = C.c_int
+        L.st_gru_act_pair_smax.restype = C.c_int
         L._gru_bound = True
     return L
 

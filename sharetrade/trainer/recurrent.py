@@ -47,8 +47,8 @@ class RecurrentDQN:
     def __init__(self, cfg: Config, device: torch.device, envs: int = 65536, seq: int = 16, batch: int = 1024,
                  replay_segments: int = 1 << 17, bars: int = 4096, ep_len: int = 390, burn_in: int = 4,
                  target_every: int = 100, cost: float = 0.01, lr: float = 3e-4, seed: Optional[int] = None,
-                 bar_params: Optional[mb.BarParams] = None, actor_grid: int = 256, grad_sync=None,
-                 overlap_act: bool = False):
+                 bar_params: Optional[mb.BarParams] = None, actor_grid: int = 0, grad_sync=None,
+                 overlap_act: bool = False, actor_kernel: str = "auto"):
         if device.type != "cuda":
             raise ValueError("RecurrentDQN runs on the GPU (MX-fp8 / bf16 MFMA kernels)")
         if envs % G.RN:
@@ -65,7 +65,15 @@ class RecurrentDQN:
         self.target_every, self.cost, self.lr = int(target_every), float(cost), float(lr)
         self.seed = cfg.agent.seed if seed is None else int(seed)
         self.gamma = float(cfg.agent.gamma)
-        self.grid = int(actor_grid)
+        # actor_kernel: "single" = gru_act_kernel (one 32-env chunk per workgroup at a time), "pair" =
+        # gru_act_pair_kernel (two chunks per workgroup, one chunk's env phase beside the other's MFMA
+        # phase; needs seq <= 32), "auto" = pair when it fits.  Same results bit for bit.
+        if actor_kernel not in ("auto", "single", "pair"):
+            raise ValueError(f"actor_kernel must be auto/single/pair, got {actor_kernel!r}")
+        smax = int(G.lib().st_gru_act_pair_smax())
+        if actor_kernel == "pair" and self.S > smax:
+            raise ValueError(f"the two-chunk actor needs seq <= {smax}")
+        self.actor_kernel = ("pair" if self.S <= smax else "single") if actor_kernel == "auto" else actor_kernel
         self.grad_sync = grad_sync
         # overlap_act: one captured graph per iteration in which the update samples its segments first,
         # then the actor launch runs on a side stream beside the rest of the update (unroll, BPTT,
@@ -74,6 +82,7 @@ class RecurrentDQN:
         # serial order: the update samples the ring as it was before this iteration's segments.
         self.overlap_act = bool(overlap_act)
         self._act_stream = torch.cuda.Stream(device=device) if self.overlap_act else None
+        self.grid = int(actor_grid) if actor_grid > 0 else self._auto_grid(device)
         self.k = G.lib()
         self.kd = _bind_deep()
         dev, f32, b16, i32, u8 = device, torch.float32, torch.bfloat16, torch.int32, torch.uint8
@@ -246,13 +255,28 @@ class RecurrentDQN:
         self._opt = op
 
     # ---------------------------------------------------------------- actor
+    def _auto_grid(self, device: torch.device) -> int:
+        """Actor workgroups (one per CU): all CUs, or 7/8 of them when the update runs beside the actor
+        (its unroll / BPTT kernels take the rest) -- then trimmed to the fewest workgroups that still
+        finish the chunk (or chunk-pair) work in the same number of rounds, freeing CUs for free."""
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        avail = cus if not self.overlap_act else cus - cus // 8
+        work = self.E // G.RN
+        if self.actor_kernel == "pair":
+            work = (work + 1) // 2
+        rounds = -(-work // avail)
+        return -(-work // rounds)
+
     def pack(self, net: str = "on") -> None:
         """fp32 masters -> MX-fp8 W_hh fragments, bf16 W_ih fragments, biases, W_q (actor/learner layout)."""
         native.check(self.k.st_gru_pack(self._packs[net], native.stream_handle()), "st_gru_pack")
 
     def act(self) -> None:
         """All E envs advance S minute bars (one actor launch) and write one replay segment each."""
-        native.check(self.k.st_gru_act(self._act, self.grid, native.stream_handle()), "st_gru_act")
+        if self.actor_kernel == "pair":
+            native.check(self.k.st_gru_act_pair(self._act, self.grid, native.stream_handle()), "st_gru_act_pair")
+        else:
+            native.check(self.k.st_gru_act(self._act, self.grid, native.stream_handle()), "st_gru_act")
 
     # ---------------------------------------------------------------- learner
     def update(self, with_act: bool = False) -> None:

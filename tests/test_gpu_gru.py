@@ -121,10 +121,12 @@ def _ref_actor(d, steps, eps_exploit):
     return h, qs, acts, rews, dones, xs, states
 
 
-def test_actor_matches_reference(native_built):
+@pytest.mark.parametrize("kernel", ["single", "pair"])
+def test_actor_matches_reference(native_built, kernel):
     """eps = 0 -> every action is the Philox random draw, so env/replay must match bit for bit
     and the GRU state must match the quantization-aware fp32 reference."""
-    d = _small(eps=0.0)
+    d = _small(eps=0.0, actor_kernel=kernel)
+    assert d.actor_kernel == kernel
     q_out = torch.zeros(d.E, 4, device="cuda")
     d._act.q_out = q_out.data_ptr()
     h_ref, qs, acts, rews, dones, xs, states = _ref_actor(d, d.S, 0.0)
@@ -270,3 +272,37 @@ def test_overlapped_actor_matches_same_order_serial(native_built):
     assert torch.equal(a.stats, b.stats) or torch.allclose(a.stats, b.stats, rtol=1e-6)
     rel = float((a.flat - b.flat).norm() / (b.flat.norm() + 1e-20))
     assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("E,grid", [(96, 1), (256, 3), (1024, 0)])
+def test_pair_actor_bit_identical_to_single(native_built, E, grid):
+    """gru_act_pair_kernel (two chunks per workgroup, env phase of one beside the MFMA phase of the
+    other) == gru_act_kernel bit for bit over several launches with greedy actions: replay, env
+    state and h.  E=96 has an odd chunk count (one workgroup's second slot is empty), grid=1 and 3
+    loop a workgroup over several pairs."""
+    res = []
+    for kernel in ("single", "pair"):
+        d = _small(E=E, S=8, eps=0.9, actor_kernel=kernel, actor_grid=grid, replay_segments=4 * E)
+        q_out = torch.zeros(d.E, 4, device="cuda")
+        d._act.q_out = q_out.data_ptr()
+        for _ in range(3):
+            d.act()
+        torch.cuda.synchronize()
+        res.append((d, q_out))
+    (a, qa), (b, qb) = res
+    for n in ("ra", "rr", "rd", "rx", "rh0", "h", "pos", "ep_start", "position", "entry", "ep_ret", "episodes",
+              "last_ret", "rctrl", "ctrl"):
+        x, y = getattr(a, n), getattr(b, n)
+        if x.is_floating_point():                                     # bit patterns (last_ret starts NaN)
+            bits = {2: torch.int16, 4: torch.int32}[x.element_size()]
+            x, y = x.view(bits), y.view(bits)
+        assert torch.equal(x, y), n
+    assert torch.equal(qa, qb)
+    assert torch.allclose(a.stats, b.stats, rtol=1e-5, atol=1e-5)   # fp32 atomics: per-pair partial sums
+    assert int(b.episodes.sum()) > 0
+
+
+def test_pair_actor_rejects_long_sequences(native_built):
+    with pytest.raises(ValueError):
+        _small(S=40, actor_kernel="pair", bars=800)
+    assert _small(S=40, bars=800).actor_kernel == "single"
