@@ -109,6 +109,47 @@ class _Scratch:
         self.loss = torch.zeros(B, **f)
 
 
+class _Staging:
+    """Pinned host image of one call's inputs -- padded rows of x (and x'), rewards, actions -- and
+    its device twin: host-side inputs (the actor path's [1, 203] states) reach the GPU in ONE
+    asynchronous copy instead of a copy + three pad kernels per tensor.  The bias column and the
+    zero padding are written once; the host image is reused after the previous copy's event."""
+
+    def __init__(self, layout: qn.QNetLayout, B: int, device):
+        self.B, self.in_p = B, layout.in_p
+        self.n_x = 2 * B * self.in_p
+        n = self.n_x + 2 * B
+        self.h = torch.zeros(n, dtype=torch.float32, pin_memory=True)
+        rows = self.h[:self.n_x].view(2 * B, self.in_p)
+        rows[:, layout.bias_col] = 1.0
+        self.hn = self.h.numpy()
+        self.rows = self.hn[:self.n_x].reshape(2 * B, self.in_p)
+        self.rew = self.hn[self.n_x:self.n_x + B]
+        self.act = self.hn[self.n_x + B:].view(np.int32)
+        self.d = torch.empty(n, dtype=torch.float32, device=device)
+        self.ev = None
+        self.input_dim = layout.input_dim
+
+    def put(self, x: torch.Tensor, xn=None, r=None, act=None) -> None:
+        if self.ev is not None:
+            self.ev.synchronize()      # the previous call's copy has read the host image
+        B, D = self.B, self.input_dim
+        self.rows[:B, :D] = x.numpy()
+        if xn is not None:
+            self.rows[B:, :D] = xn.numpy()
+        if r is not None:
+            self.rew[:] = r.numpy()
+        if act is not None:
+            self.act[:] = act.numpy()
+        self.d.copy_(self.h, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def ptr(self, what: str) -> int:
+        off = {"x": 0, "xn": self.B * self.in_p, "r": self.n_x, "act": self.n_x + self.B}[what]
+        return self.d.data_ptr() + 4 * off
+
+
 class F32Learner:
     def __init__(self, learner):
         self.l = learner
@@ -116,6 +157,13 @@ class F32Learner:
         self.net = make_net(self.layout, learner.cfg.model.output_relu)
         self.L = _bind()
         self._scratch = {}
+        self._staging = {}
+
+    def _stage(self, B: int) -> _Staging:
+        st = self._staging.get(B)
+        if st is None:
+            st = self._staging[B] = _Staging(self.layout, B, self.l.device)
+        return st
 
     def _s(self, B: int) -> _Scratch:
         s = self._scratch.get(B)
@@ -132,22 +180,37 @@ class F32Learner:
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = x.shape[0]
         s = self._s(B)
-        xp = self._pad(x)
         r = F32Rows()
-        r.params, r.x, r.q_out, r.B, r.mode = self.l.params.data_ptr(), xp.data_ptr(), s.q.data_ptr(), B, 0
+        if x.device.type == "cpu":
+            st = self._stage(B)
+            st.put(x.float())
+            xptr = st.ptr("x")
+        else:
+            xp = self._pad(x)
+            xptr = xp.data_ptr()
+        r.params, r.x, r.q_out, r.B, r.mode = self.l.params.data_ptr(), xptr, s.q.data_ptr(), B, 0
         native.check(self.L.st_f32_rows(self.net, r, native.stream_handle()), "st_f32_rows(fwd)")
         return s.q.clone()
 
-    def td_update(self, x, r_, xn, act: Optional[torch.Tensor], coef: float) -> float:
+    def td_update(self, x, r_, xn, act: Optional[torch.Tensor], coef: float, want_loss: bool = True):
+        """One fused TD update; returns the loss as a float, or (``want_loss=False``) the device
+        tensor of per-row losses without waiting for the GPU."""
         B = x.shape[0]
         s = self._s(B)
-        xp, xnp = self._pad(x), self._pad(xn)
-        rew = r_.to(self.l.device, torch.float32).contiguous()
-        acti = act.to(self.l.device, torch.int32).contiguous() if act is not None else None
         a = self.l.cfg.agent
         r = F32Rows()
-        r.params, r.x, r.xn, r.reward = self.l.params.data_ptr(), xp.data_ptr(), xnp.data_ptr(), rew.data_ptr()
-        r.action = acti.data_ptr() if acti is not None else None
+        if x.device.type == "cpu" and xn.device.type == "cpu" and r_.device.type == "cpu" and \
+                (act is None or act.device.type == "cpu"):
+            st = self._stage(B)
+            st.put(x.float(), xn.float(), r_.float(), act.to(torch.int32) if act is not None else None)
+            r.params, r.x, r.xn, r.reward = self.l.params.data_ptr(), st.ptr("x"), st.ptr("xn"), st.ptr("r")
+            r.action = st.ptr("act") if act is not None else None
+        else:
+            xp, xnp = self._pad(x), self._pad(xn)
+            rew = r_.to(self.l.device, torch.float32).contiguous()
+            acti = act.to(self.l.device, torch.int32).contiguous() if act is not None else None
+            r.params, r.x, r.xn, r.reward = self.l.params.data_ptr(), xp.data_ptr(), xnp.data_ptr(), rew.data_ptr()
+            r.action = acti.data_ptr() if acti is not None else None
         r.q_out, r.qn_out, r.acts, r.dz, r.loss = (s.q.data_ptr(), s.qn.data_ptr(), s.acts.data_ptr(),
                                                    s.dz.data_ptr(), s.loss.data_ptr())
         r.B, r.mode, r.gamma, r.coef = B, 1, float(a.gamma), float(coef)
@@ -164,7 +227,7 @@ class F32Learner:
         o.mode, o.grad = 0, None
         o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
         native.check(self.L.st_f32_grad_optim(self.net, o, sh), "st_f32_grad_optim")
-        return float(s.loss.sum())
+        return float(s.loss.sum()) if want_loss else s.loss
 
 
 class F32EngineStep:

@@ -83,7 +83,7 @@ class QDecisionPolicyActor(Actor):
             ns = self._check(msg.next_state, "nextState")
             self._flush()
             it = self.learner.iteration
-            self.learner.update(s, float(msg.reward), ns, msg.action)
+            self.learner.update(s, float(msg.reward), ns, msg.action, return_loss=False)
             # QDecisionPolicyActor.scala:74 — checked on the pre-increment counter
             if it % self.cfg.agent.snapshot_interval == 0 and it != 0:
                 self.save_snapshot()

@@ -63,7 +63,8 @@ class QLearner:
         self.opt = qn.OptimState(a.optimizer, self.layout.numel, a.adagrad_init_acc, device=dev)
         self.rng = rng.PhiloxStream(self.seed, stream=3)
         self.iteration = 0
-        self.last_loss = 0.0
+        self._last_loss = 0.0
+        self._loss_dev: Optional[torch.Tensor] = None
         self._k = None
         if backend == "native":
             from ..ops import mlp_f32
@@ -72,9 +73,10 @@ class QLearner:
 
     # ------------------------------------------------------------------ inference
     def q_values(self, states: ArrayLike) -> torch.Tensor:
-        x = as_state(states, self.input_dim).to(self.device)
-        if self._k is not None:
+        x = as_state(states, self.input_dim)
+        if self._k is not None:   # host rows are staged by the kernel wrapper
             return self._k.forward(x)[:, : self.layout.n_actions]
+        x = x.to(self.device)
         q, _, _ = qn.forward(self.params, self.layout, x, self.cfg.model.output_relu)
         return q[:, : self.layout.n_actions]
 
@@ -98,27 +100,41 @@ class QLearner:
         return out
 
     # ------------------------------------------------------------------ learning
-    def update(self, states: ArrayLike, rewards, next_states: ArrayLike, actions=None) -> float:
-        """One TD update over a batch (B=1 in the reference).  Returns the loss."""
-        x = as_state(states, self.input_dim, "state").to(self.device)
-        xn = as_state(next_states, self.input_dim, "nextState").to(self.device)
+    @property
+    def last_loss(self) -> float:
+        """Loss of the last update (read back from the GPU on first access)."""
+        if self._loss_dev is not None:
+            self._last_loss, self._loss_dev = float(self._loss_dev.sum()), None
+        return self._last_loss
+
+    def update(self, states: ArrayLike, rewards, next_states: ArrayLike, actions=None,
+               return_loss: bool = True) -> Optional[float]:
+        """One TD update over a batch (B=1 in the reference).  Returns the loss; with
+        ``return_loss=False`` (the policy actor, which never reads it) the GPU path does not wait
+        for the update to finish -- ``last_loss`` still reads it back on demand."""
+        # host inputs stay on the host for the native path (one staged copy, F32Learner._stage)
+        to = (lambda t: t) if self._k is not None else (lambda t: t.to(self.device))
+        x = to(as_state(states, self.input_dim, "state"))
+        xn = to(as_state(next_states, self.input_dim, "nextState"))
         if x.shape[0] != xn.shape[0]:
             raise IllegalArgumentException("state / nextState batch mismatch")
         B = x.shape[0]
-        r = torch.as_tensor(np.broadcast_to(np.asarray(rewards, dtype=np.float32), (B,)).copy(), device=self.device)
+        r = to(torch.from_numpy(np.broadcast_to(np.asarray(rewards, dtype=np.float32), (B,)).copy()))
         act = None
         if actions is not None:
-            act = torch.as_tensor(np.broadcast_to(np.asarray(actions, dtype=np.int64), (B,)).copy(),
-                                  device=self.device)
+            act = to(torch.from_numpy(np.broadcast_to(np.asarray(actions, dtype=np.int64), (B,)).copy()))
         a = self.cfg.agent
         compat = a.target_slot == "compat" or act is None
         coef = 2.0 / B if a.loss_reduction == "mean" else 2.0
         if self._k is not None:
-            loss = self._k.td_update(x, r, xn, None if compat else act, coef)
+            loss = self._k.td_update(x, r, xn, None if compat else act, coef, want_loss=return_loss)
         else:
             loss = self._torch_update(x, r, xn, None if compat else act, coef)
         self.iteration += 1
-        self.last_loss = loss
+        if isinstance(loss, torch.Tensor):
+            self._loss_dev = loss
+            return None
+        self._last_loss, self._loss_dev = loss, None
         return loss
 
     def _torch_update(self, x, r, xn, act, coef) -> float:

@@ -65,6 +65,29 @@ def test_td_update_matches_oracle(dev, opt, slot, B):
             assert _rel(gpu.opt.s1.cpu(), cpu.opt.s1) < 1e-4
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_staged_host_inputs_match_device_inputs(dev, B):
+    """Host inputs go through the pinned staging image (one H2D copy); device inputs through the
+    pad path: identical parameters, Q values and losses; ``return_loss=False`` defers the read-back."""
+    from sharetrade.config import preset_config
+    from sharetrade.policy.learner import QLearner
+
+    cfg = preset_config("intended")
+    a, b = QLearner(cfg, device=dev), QLearner(cfg, device=dev)
+    for it in range(4):
+        x, xn = _states(B, 30 + it) / 100.0, _states(B, 40 + it) / 100.0
+        r = np.linspace(-1, 2, B).astype(np.float32)
+        acts = (np.arange(B) + it) % 3
+        la = a.update(x, r, xn, acts, return_loss=False)
+        assert la is None
+        lb = b.update(torch.as_tensor(x, device=dev), r, torch.as_tensor(xn, device=dev), acts)
+        assert a.last_loss == lb
+    assert torch.equal(a.params, b.params)
+    q_host = a.q_values(x)
+    q_dev = a.q_values(torch.as_tensor(x, device=dev))
+    assert torch.equal(q_host, q_dev)
+
+
 def test_policy_actor_on_gpu_uses_native_learner(dev):
     from sharetrade import protocol as P
     from sharetrade.actors.runtime import ActorSystem
