@@ -236,7 +236,9 @@ __global__ void __launch_bounds__(256) deep_td_kernel(DeepTD p) {
     const int a = p.a[b];
     const float diff = p.q[(size_t)b * p.ldq + a] - y;
     l = diff * diff;
-    for (int j = 0; j < p.ldq; ++j) {
+    // only the n_actions real columns: the padding columns j >= n_actions of dq / dqT are zero from
+    // allocation and nothing else writes them
+    for (int j = 0; j < p.n_actions; ++j) {
       const float v = (j == a) ? p.coef * diff : 0.f;
       p.dq[(size_t)b * p.ldq + j] = f2bf(v);
       p.dqT[(size_t)j * p.B + b] = f2bf(v);
@@ -262,16 +264,25 @@ __global__ void __launch_bounds__(256) row_sum_bf16_kernel(const bf16_t* __restr
 // bf16 transpose through LDS: out[c][r] = in[r][c], 64x64 tiles
 __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ in, int ldi, bf16_t* __restrict__ out,
                                                              int ldo, int R, int Ccols) {
-  __shared__ bf16_t t[64][66];
+  // 16-byte loads and stores (8 bf16; R, Ccols, ldi, ldo multiples of 8, checked on the host)
+  __shared__ __attribute__((aligned(16))) bf16_t t[64][72];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-    const int r = i / 64, c = i % 64;
-    if (r0 + r < R && c0 + c < Ccols) t[r][c] = in[(size_t)(r0 + r) * ldi + c0 + c];
+#pragma unroll
+  for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+    const int r = i >> 3, c = (i & 7) * 8;
+    if (r0 + r < R && c0 + c < Ccols)
+      *reinterpret_cast<uint4*>(&t[r][c]) = *reinterpret_cast<const uint4*>(in + (size_t)(r0 + r) * ldi + c0 + c);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-    const int c = i / 64, r = i % 64;
-    if (r0 + r < R && c0 + c < Ccols) out[(size_t)(c0 + c) * ldo + r0 + r] = t[r][c];
+#pragma unroll
+  for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+    const int c = i >> 3, r = (i & 7) * 8;
+    if (r0 + r < R && c0 + c < Ccols) {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = (uint32_t)t[r + 2 * k][c] | ((uint32_t)t[r + 2 * k + 1][c] << 16);
+      *reinterpret_cast<uint4*>(out + (size_t)(c0 + c) * ldo + r0 + r) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
   }
 }
 
@@ -326,8 +337,8 @@ __global__ void __launch_bounds__(256) adam_tile_kernel(AdamLayer p) {
 }
 
 // ---------------------------------------------------------------- multi-tensor Adam (one launch)
-// Every weight matrix and bias of the MLP in one launch: weight segments in 32x32 tiles (the bf16
-// copy and, through LDS, its transpose, as adam_tile_kernel); bias segments in blocks of 32 entries
+// Every weight matrix and bias of the MLP in one launch: weight segments in 64x64 tiles (the bf16
+// copy and, through LDS, its transpose, with 16-byte vector accesses); bias segments in blocks of 32 entries
 // whose gradient is reduced here from the transposed layer gradient GT [O][B] (bf16) -- the bias
 // gradient row sums need no launch of their own.  The update counter was advanced by deep_td (a
 // last-block counter here cost ~40 us: 3.5k device-scope atomics on one word).  Replaces 2L Adam +
@@ -356,7 +367,7 @@ struct AdamMulti {
 };
 
 __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
-  __shared__ bf16_t tl[32][34];
+  __shared__ __attribute__((aligned(16))) bf16_t tl[64][72];   // 144-byte rows: 16-byte aligned chunks
   __shared__ float red[32];
   int b = blockIdx.x, si = 0;
   while (si + 1 < p.nseg && b >= p.seg[si].blocks) b -= p.seg[si++].blocks;
@@ -406,24 +417,58 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
       }
     }
   } else {
-    const int tiles_i = (S.I + 31) / 32;
-    const int o0 = (b / tiles_i) * 32, i0 = (b % tiles_i) * 32;
-    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
-      const int oo = k / 32, ii = k % 32;
-      const int o = o0 + oo, i = i0 + ii;
-      bf16_t wb = 0;
+    // 64 x 64 tile: thread t owns columns i0 + 4 (t % 16) .. +3 of rows o0 + t / 16 + 16 r (r < 4) --
+    // float4 loads / stores of w, g, m, v, mask and an 8-byte store of the bf16 copy; the transposed
+    // copy leaves through LDS as 16-byte stores of 8 consecutive o of one i (I % 4 == 0 and O % 8 == 0,
+    // checked on the host).  Same per-element arithmetic as upd(); a masked element keeps w, m, v.
+    const int tiles_i = (S.I + 63) / 64;
+    const int o0 = (b / tiles_i) * 64, i0 = (b % tiles_i) * 64;
+    const int ic = 4 * (threadIdx.x & 15), orow = threadIdx.x >> 4, i = i0 + ic;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ol = orow + 16 * r, o = o0 + ol;
+      uint32_t lo = 0, hi = 0;
       if (o < S.O && i < S.I) {
         const size_t idx = (size_t)o * S.I + i;
-        wb = f2bf(upd(idx, S.g[idx]));
-        S.wb[idx] = wb;
+        float4 w = *reinterpret_cast<const float4*>(S.w + idx);
+        const float4 g4 = *reinterpret_cast<const float4*>(S.g + idx);
+        float4 m = *reinterpret_cast<const float4*>(S.m + idx);
+        float4 v = *reinterpret_cast<const float4*>(S.v + idx);
+        const float4 mk = S.mask ? *reinterpret_cast<const float4*>(S.mask + idx) : make_float4(1.f, 1.f, 1.f, 1.f);
+        auto one = [&](float& wv, float& mv, float& vv, float g, float k) {
+          if (k != 0.f) {
+            g *= k;
+            const float mn = p.beta1 * mv + (1.f - p.beta1) * g;
+            const float vn = p.beta2 * vv + (1.f - p.beta2) * g * g;
+            mv = mn;
+            vv = vn;
+            wv -= p.lr * (mn * c1) / (sqrtf(vn * c2) + p.eps);
+          }
+        };
+        one(w.x, m.x, v.x, g4.x, mk.x);
+        one(w.y, m.y, v.y, g4.y, mk.y);
+        one(w.z, m.z, v.z, g4.z, mk.z);
+        one(w.w, m.w, v.w, g4.w, mk.w);
+        *reinterpret_cast<float4*>(S.w + idx) = w;
+        *reinterpret_cast<float4*>(S.m + idx) = m;
+        *reinterpret_cast<float4*>(S.v + idx) = v;
+        lo = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
+        hi = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
+        *reinterpret_cast<uint2*>(S.wb + idx) = make_uint2(lo, hi);
       }
-      tl[oo][ii] = wb;
+      tl[ic + 0][ol] = (bf16_t)(lo & 0xFFFF);
+      tl[ic + 1][ol] = (bf16_t)(lo >> 16);
+      tl[ic + 2][ol] = (bf16_t)(hi & 0xFFFF);
+      tl[ic + 3][ol] = (bf16_t)(hi >> 16);
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
-      const int ii = k / 32, oo = k % 32;
-      const int o = o0 + oo, i = i0 + ii;
-      if (S.wbT && o < S.O && i < S.I) S.wbT[(size_t)i * S.O + o] = tl[oo][ii];
+    if (S.wbT) {
+#pragma unroll
+      for (int c = threadIdx.x; c < 64 * 8; c += 256) {
+        const int il = c >> 3, oc = (c & 7) * 8, ii = i0 + il, o = o0 + oc;
+        if (ii < S.I && o < S.O)
+          *reinterpret_cast<uint4*>(S.wbT + (size_t)ii * S.O + o) = *reinterpret_cast<const uint4*>(&tl[il][oc]);
+      }
     }
   }
 }
@@ -435,8 +480,9 @@ extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
   int total = 0;
   for (int i = 0; i < p->nseg; ++i) {
     const st::AdamSeg& g = p->seg[i];
-    const int want = g.bias ? (g.I + 31) / 32 : ((g.I + 31) / 32) * ((g.O + 31) / 32);
+    const int want = g.bias ? (g.I + 31) / 32 : ((g.I + 63) / 64) * ((g.O + 63) / 64);
     if (g.blocks != want || (g.bias && (g.nb % 8 || g.ldg % 8 || !g.gT))) return hipErrorInvalidValue;
+    if (!g.bias && (g.I % 4 || g.O % 8)) return hipErrorInvalidValue;   // vector paths of the weight tiles
     total += g.blocks;
   }
   if (total != p->total) return hipErrorInvalidValue;
@@ -458,7 +504,7 @@ extern "C" hipError_t st_deep_env_step(const st::DeepEnv* p, hipStream_t s) {
 }
 
 extern "C" hipError_t st_deep_td(const st::DeepTD* p, hipStream_t s) {
-  hipLaunchKernelGGL(st::deep_td_kernel, dim3((p->B + 255) / 256), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL(st::deep_td_kernel, dim3((p->B + 63) / 64), dim3(64), 0, s, *p);
   return hipGetLastError();
 }
 
@@ -468,6 +514,7 @@ extern "C" hipError_t st_row_sum_bf16(const bf16_t* X, int ld, int rows, int n, 
 }
 
 extern "C" hipError_t st_transpose_bf16(const bf16_t* in, int ldi, bf16_t* out, int ldo, int R, int Cc, hipStream_t s) {
+  if (R % 8 || Cc % 8 || ldi % 8 || ldo % 8) return hipErrorInvalidValue;
   hipLaunchKernelGGL(st::transpose_bf16_kernel, dim3((Cc + 63) / 64, (R + 63) / 64), dim3(256), 0, s, in, ldi, out, ldo,
                      R, Cc);
   return hipGetLastError();

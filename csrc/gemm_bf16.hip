@@ -19,6 +19,8 @@
 // through the (then idle) LDS buffers so that C and C^T leave in 16-byte stores.
 #include "common.h"
 
+#include <type_traits>
+
 namespace st {
 
 constexpr int GT = 256;   // threads
@@ -43,6 +45,14 @@ struct GemmArgs {
   float alpha;
   int splitk;            // EPI_F32 only: K split over splitk workgroups per tile, atomically
                          // added into out (which then holds the prior value / zeros)
+};
+
+// a batch of same-shape products in one launch (e.g. the online and target networks' forward
+// of one layer): workgroups [i*T, (i+1)*T) compute problem i, T = tiles x K-splits per problem
+constexpr int GEMM_MAXB = 4;
+struct GemmBatch {
+  GemmArgs a[GEMM_MAXB];
+  int n;
 };
 
 template <int BM, int BN, int S = 2>
@@ -102,21 +112,25 @@ ST_DEV void wait_vmcnt() {
 }
 
 template <int BM, int BN, int EPI, int S = 2>
-__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_nt_kernel(GemmArgs p) {
+__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_nt_kernel(GemmBatch batch) {
   using G = GemmGeo<BM, BN, S>;
   constexpr int NW = G::NT / 64;
   static_assert(G::NT == gemm_threads<BM, BN>() && G::MINB == gemm_min_blocks<BM, BN, S>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
-  // XCD-aware tile order: neighbouring tiles (sharing A rows) on one XCD's L2
-  const int ntn = p.N / BN, ntm = p.M / BM, nwg = ntn * ntm;
-  const int nsplit = p.splitk > 1 ? p.splitk : 1, ntot = nwg * nsplit;
+  // XCD-aware tile order: neighbouring tiles (sharing A rows) on one XCD's L2; every problem of a
+  // batch has the shape of the first (checked on the host)
+  const int ntn = batch.a[0].N / BN, ntm = batch.a[0].M / BM, nwg = ntn * ntm;
+  const int nsplit = batch.a[0].splitk > 1 ? batch.a[0].splitk : 1, ntot = nwg * nsplit;
   int bid = blockIdx.x;
   {
-    const int xcd = bid % 8, q = ntot / 8, r = ntot % 8;
+    const int all = ntot * batch.n, xcd = bid % 8, q = all / 8, r = all % 8;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
   }
+  const int pi = __builtin_amdgcn_readfirstlane(bid / ntot);
+  bid -= pi * ntot;
+  const GemmArgs& p = batch.a[pi];
   const int ks = bid / nwg;   // K split (split-major: one split's tiles stay on one XCD's L2)
   bid -= ks * nwg;
   const int tm = bid / ntn, tn = bid % ntn;
@@ -269,7 +283,7 @@ __global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM,
 }
 
 template <int BM, int BN, int EPI, int S = 2>
-static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
+static hipError_t launch_gemm(const GemmBatch& p, hipStream_t s) {
   using G = GemmGeo<BM, BN, S>;
   static bool attr = false;
   if (!attr) {
@@ -278,8 +292,220 @@ static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int nwg = (p.M / BM) * (p.N / BN) * (p.splitk > 1 ? p.splitk : 1);
+  const GemmArgs& a = p.a[0];
+  const int nwg = (a.M / BM) * (a.N / BN) * (a.splitk > 1 ? a.splitk : 1) * p.n;
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI, S>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- 256x256 ping-pong kernel
+// 8 waves = 2 groups (wr = M half) x 4 (wc = 64-column quarter); waves w and w + 4 share a SIMD, one
+// from each group.  The groups run one barrier interval apart: while one group issues the 64 MFMAs
+// of a K-tile (C segment) the other reads all its fragments of its next K-tile from LDS (L segment:
+// 16 A + 8 B ds_read_b128), so each SIMD's MFMA pipe is fed by one wave while the other loads.
+// Interval 2t: G0 = L(t), G1 = C(t-1); interval 2t+1: G0 = C(t), G1 = L(t).
+// LDS (160 KB): A in 2 buffers (K-tile parity; A0 = rows 0-127 read only by G0's L, A1 = rows 128-255
+// only by G1's L), B in 3 (t mod 3; B0 / B1 = columns 0-127 / 128-255, read by both groups' L), so a
+// half-tile can be restaged one interval after its last read and lands 3 intervals before it is read.
+// global_load_lds staging (2 per thread per half-tile), 4 per thread per interval:
+//   interval 2t:   A1(t+1), B0(t+2)
+//   interval 2t+1: A0(t+2), B1(t+2)
+// Every interval ends with lgkmcnt(0) (its fragment reads retired) + a counted vmcnt + a raw
+// s_barrier (a __syncthreads() fence would add vmcnt(0) and drain the staging): vmcnt(10) after even
+// intervals (A1(t) landed for G1's L(t)), vmcnt(8) after odd ones (A0(t+1), B(t+1) landed for G0's
+// L(t+1)); vmcnt(0) in the last two K-tiles, where stages are skipped.  The two groups' loops are
+// written out separately with the same stages, waits and barrier count (one loop with a role branch
+// per interval made the register allocator keep both roles' values live: 500 VGPRs of spills).
+// Epilogues: EPI_BF16 (bias / relu; no C^T) and EPI_F32 (alpha, bias, accumulate; no split-K).
+namespace pp {
+constexpr int NT = 512, HT = 128 * GBK;     // threads, elements per half-tile
+constexpr int AB = 2 * HT, BB = 2 * HT;     // one K-tile of A (A0 A1) / of B (B0 B1)
+constexpr int A_OFF = 0, B_OFF = 2 * AB;    // 2 A buffers, then 3 B buffers
+constexpr int KLOOP_BYTES = (2 * AB + 3 * BB) * 2;   // 160 KB
+constexpr int SC = 256 + 8;                 // epilogue C staging row stride (bf16)
+constexpr int EPI_BYTES = 256 * SC * 2;
+constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
+static_assert(LDS_BYTES <= 163840, "LDS");
+
+template <int N>
+ST_DEV void wait_vm_lgkm0() {   // vmcnt = N, lgkmcnt = 0, expcnt not waited on
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4));
+}
+// raw barrier that is also a compiler memory barrier (no LDS access moves across it) and emits no
+// wait of its own
+ST_DEV void barrier() { asm volatile("s_barrier" ::: "memory"); }
+}  // namespace pp
+
+template <int EPI, int PRIO = 0>
+__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntn = p.N / 256, ntm = p.M / 256, nwg = ntn * ntm;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int m0 = (bid / ntn) * 256, n0 = (bid % ntn) * 256;
+  const int nk = p.K / GBK;
+
+  auto stA = [&](int half, int kt) {   // A half-tile (rows m0 + 128 half ..) of K-tile kt
+    if (kt < nk)
+      stage_tile<128, 8>(p.A, p.lda, m0 + 128 * half, kt * GBK, buf + pp::A_OFF + (kt & 1) * pp::AB + half * pp::HT,
+                         wave, lane);
+  };
+  auto stB = [&](int half, int kt) {
+    if (kt < nk)
+      stage_tile<128, 8>(p.B, p.ldb, n0 + 128 * half, kt * GBK, buf + pp::B_OFF + (kt % 3) * pp::BB + half * pp::HT,
+                         wave, lane);
+  };
+
+  f4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+  s8v fa[8][2], fb[4][2];
+  auto load = [&](int kt) {   // L segment: every fragment of K-tile kt this wave multiplies
+    const bf16_t* bA = buf + pp::A_OFF + (kt & 1) * pp::AB + wr * pp::HT;
+    const bf16_t* bB = buf + pp::B_OFF + (kt % 3) * pp::BB + (wc >> 1) * pp::HT;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j][kk] = frag_sw(bB, (wc & 1) * 64 + 16 * j + l16, kk * 4 + g4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i][kk] = frag_sw(bA, 16 * i + l16, kk * 4 + g4);
+    }
+  };
+  auto compute = [&]() {      // C segment: 64 MFMAs, no LDS access
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // the MFMA wave first when both can issue
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(fa[i][kk], fb[j][kk], acc[i][j]);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  auto even_end = [&](int t) {   // end of interval 2t
+    if (t + 2 < nk) pp::wait_vm_lgkm0<10>(); else pp::wait_vm_lgkm0<0>();
+    pp::barrier();
+  };
+  auto odd_end = [&](int t) {    // end of interval 2t+1
+    if (t + 2 < nk) pp::wait_vm_lgkm0<8>(); else pp::wait_vm_lgkm0<0>();
+    pp::barrier();
+  };
+  auto stage_even = [&](int t) {
+    stA(1, t + 1);
+    stB(0, t + 2);
+  };
+  auto stage_odd = [&](int t) {
+    stA(0, t + 2);
+    stB(1, t + 2);
+  };
+
+  // prologue: K-tile 0 whole, then what intervals -2 / -1 would have staged: A1(0) B0(1), A0(1) B1(1)
+  stA(0, 0);
+  stB(0, 0);
+  stB(1, 0);
+  stA(1, 0);
+  stB(0, 1);
+  stA(0, 1);
+  stB(1, 1);
+  if (nk > 1) pp::wait_vm_lgkm0<6>(); else pp::wait_vm_lgkm0<0>();
+  pp::barrier();
+  if (wr == 0) {
+    for (int t = 0; t < nk; ++t) {
+      stage_even(t);
+      load(t);                     // interval 2t
+      even_end(t);
+      stage_odd(t);
+      compute();                   // interval 2t+1
+      odd_end(t);
+    }
+  } else {
+    stage_even(0);                 // interval 0: nothing to multiply yet
+    even_end(0);
+    stage_odd(0);
+    load(0);                       // interval 1
+    odd_end(0);
+    for (int t = 1; t < nk; ++t) {
+      stage_even(t);
+      compute();                   // interval 2t
+      even_end(t);
+      stage_odd(t);
+      load(t);                     // interval 2t+1
+      odd_end(t);
+    }
+    compute();                     // interval 2nk
+  }
+  pp::wait_vm_lgkm0<0>();
+  pp::barrier();   // every wave is done with the K-loop buffers
+
+  // ------------------------------------------------------------------ epilogues
+  const int wm0 = wr * 128, wn0 = wc * 64;   // this wave's block of the tile
+  float bj[4];                                // bias of this lane's 4 columns: loaded once
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bj[j] = 0.f;
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bj[j] = p.bias[n0 + wn0 + 16 * j + l16];
+  }
+  if constexpr (EPI == EPI_F32) {
+    float* out = reinterpret_cast<float*>(p.out);
+    auto store = [&](auto accumulate) {   // the accumulate branch hoisted out of the element loops
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn0 + 16 * j + l16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm0 + 16 * i + 4 * g4 + r;
+            float* o = out + (size_t)m * p.ldo + n;
+            const float v = p.alpha * acc[i][j][r] + bj[j];
+            if constexpr (decltype(accumulate)::value) *o += v; else *o = v;
+          }
+        }
+    };
+    if (p.accumulate) store(std::true_type{}); else store(std::false_type{});
+  } else {
+    bf16_t* sC = buf;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nl = wn0 + 16 * j + l16, ml = wm0 + 16 * i + 4 * g4;
+        const float bb = bj[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = p.alpha * acc[i][j][r] + bb;
+          sC[(ml + r) * pp::SC + nl] = f2bf(p.relu ? fmaxf(x, 0.f) : x);
+        }
+      }
+    __syncthreads();
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+    for (int c = tid; c < 256 * 32; c += pp::NT) {
+      const int r = c >> 5, k = (c & 31) * 8;
+      *reinterpret_cast<uint4*>(out + (size_t)(m0 + r) * p.ldo + n0 + k) = *reinterpret_cast<const uint4*>(sC + r * pp::SC + k);
+    }
+  }
+}
+
+template <int EPI, int PRIO = 0>
+static hipError_t launch_gemm_pp(const GemmArgs& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       pp::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, PRIO>), dim3((p.M / 256) * (p.N / 256)), dim3(pp::NT), pp::LDS_BYTES, s, p);
   return hipGetLastError();
 }
 
@@ -288,21 +514,29 @@ static hipError_t launch_gemm(const GemmArgs& p, hipStream_t s) {
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
 //       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU),
 //       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output)
-extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
-  if (tile < 0 || tile > 6) return hipErrorInvalidValue;
+// n same-shape products (same tile / epilogue / split) in one launch; st_gemm_nt = n 1
+extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi, int tile, hipStream_t stream) {
+  if (tile < 0 || tile > 6 || n < 1 || n > st::GEMM_MAXB) return hipErrorInvalidValue;
   const int bm = (tile == 3 || tile == 6) ? 256 : (tile == 1 ? 64 : 128);
   const int bn = (tile == 1 || tile == 2) ? 64 : (tile == 6 ? 256 : 128);
-  if (tile == 6 && p->outT) return hipErrorInvalidValue;
-  if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
-  if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
-  if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
-  if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return hipErrorInvalidValue;
-  if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return hipErrorInvalidValue;
+  st::GemmBatch b;
+  b.n = n;
+  for (int i = 0; i < n; ++i) {
+    const st::GemmArgs* p = ps + i;
+    if (p->M != ps->M || p->N != ps->N || p->K != ps->K || p->splitk != ps->splitk) return hipErrorInvalidValue;
+    if (tile == 6 && p->outT) return hipErrorInvalidValue;
+    if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
+    if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
+    if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
+    if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return hipErrorInvalidValue;
+    if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return hipErrorInvalidValue;
+    b.a[i] = *p;
+  }
 #define ST_G(BM_, BN_, S_)                                                               \
   switch (epi) {                                                                         \
-    case 0: return st::launch_gemm<BM_, BN_, 0, S_>(*p, stream);                         \
-    case 1: return st::launch_gemm<BM_, BN_, 1, S_>(*p, stream);                         \
-    case 2: return st::launch_gemm<BM_, BN_, 2, S_>(*p, stream);                         \
+    case 0: return st::launch_gemm<BM_, BN_, 0, S_>(b, stream);                          \
+    case 1: return st::launch_gemm<BM_, BN_, 1, S_>(b, stream);                          \
+    case 2: return st::launch_gemm<BM_, BN_, 2, S_>(b, stream);                          \
     default: return hipErrorInvalidValue;                                                \
   }
   if (tile == 0) { ST_G(128, 128, 2) }
@@ -314,4 +548,22 @@ extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipSt
   if (tile == 6) { ST_G(256, 256, 2) }
 #undef ST_G
   return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
+  if (tile == 7 || tile == 8) {   // 256x256 ping-pong (8: with s_setprio); one product per launch,
+                                 // bf16 / fp32 epilogues, no C^T, no split-K
+    if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
+    if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)
+      return hipErrorInvalidValue;
+    if (tile == 8) {
+      if (epi == st::EPI_BF16) return st::launch_gemm_pp<st::EPI_BF16, 1>(*p, stream);
+      if (epi == st::EPI_F32) return st::launch_gemm_pp<st::EPI_F32, 1>(*p, stream);
+      return hipErrorInvalidValue;
+    }
+    if (epi == st::EPI_BF16) return st::launch_gemm_pp<st::EPI_BF16>(*p, stream);
+    if (epi == st::EPI_F32) return st::launch_gemm_pp<st::EPI_F32>(*p, stream);
+    return hipErrorInvalidValue;
+  }
+  return st_gemm_nt_batched(p, 1, epi, tile, stream);
 }

@@ -13,7 +13,8 @@ from . import native
 EPI_BF16, EPI_RELU_GRAD, EPI_F32 = 0, 1, 2
 # (BM, BN) or (BM, BN, LDS stages) -> st_gemm_nt tile id (csrc/gemm_bf16.hip)
 TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2, (256, 128): 3, (128, 128, 3): 4, (128, 128, 4): 5,
-         (256, 256): 6}
+         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8}
+# 7: 8-wave ping-pong, 8: the same with s_setprio on the MFMA segments; gemm_nt only (no batch / C^T / split-K)
 
 
 class GemmArgs(C.Structure):
@@ -30,6 +31,8 @@ def _bind():
     if not getattr(L, "_gemm_bound", False):
         L.st_gemm_nt.argtypes = [C.POINTER(GemmArgs), C.c_int, C.c_int, C.c_void_p]
         L.st_gemm_nt.restype = C.c_int
+        L.st_gemm_nt_batched.argtypes = [C.POINTER(GemmArgs), C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.st_gemm_nt_batched.restype = C.c_int
         L._gemm_bound = True
     return L
 
@@ -94,10 +97,25 @@ def pick_splitk(M: int, N: int, K: int, tile) -> int:
     return s
 
 
+PINGPONG = True   # auto_tile may pick the ping-pong kernel (benchmarks/bench_deep.py --no-pingpong turns it off)
+
+
+def auto_tile(M: int, N: int, epi: int, kw: dict) -> tuple:
+    """The 256x256 ping-pong kernel where it applies (bf16 / fp32 epilogue without C^T or split-K) and
+    its tiles fill every CU (measured faster from 256 tiles up: profiles/r2_gemm_pingpong.md), else
+    pick_tile."""
+    if (PINGPONG and epi != EPI_RELU_GRAD and kw.get("outT") is None and kw.get("splitk", 1) in (1, "auto") and
+            M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= 256):
+        return (256, 256, "pp")
+    return pick_tile(M, N)
+
+
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_BF16, tile=None, **kw) -> torch.Tensor:
     """``out = A . B^T`` (+ epilogue).  ``splitk="auto"`` (fp32 epilogue only) splits long-K,
     few-tile products (weight gradients) over extra workgroups with atomic accumulation."""
-    t = tile or pick_tile(A.shape[0], B.shape[0])
+    t = tile or auto_tile(A.shape[0], B.shape[0], epi, kw)
+    if len(t) == 3 and t[2] in ("pp", "ppp") and kw.get("splitk", 1) == "auto":
+        kw = dict(kw, splitk=1)
     sk = kw.pop("splitk", 1)
     prezeroed = kw.pop("prezeroed", False)   # split-K output already zeroed by an earlier kernel
     if sk == "auto":
@@ -109,3 +127,32 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_
         raise ValueError(f"gemm_nt: shape {g.M}x{g.N}x{g.K} not a multiple of tile {t} / BK 64")
     native.check(_bind().st_gemm_nt(g, epi, TILES[t], native.stream_handle()), "st_gemm_nt")
     return out
+
+
+GEMM_MAXB = 4
+
+
+def gemm_nt_batched(problems, epi: int = EPI_BF16, tile=None) -> None:
+    """Up to 4 same-shape products ``out_i = A_i . B_i^T`` (same epilogue / tile / split) in ONE
+    launch: ``problems`` is a list of ``(A, B, out, kwargs)``.  Replaces a fork / join of
+    concurrent streams (e.g. the online and target forward of one layer) by one grid that holds
+    the tiles of all of them."""
+    if not 1 <= len(problems) <= GEMM_MAXB:
+        raise ValueError(f"gemm_nt_batched: 1..{GEMM_MAXB} problems")
+    A0, B0 = problems[0][0], problems[0][1]
+    t = tile or pick_tile(A0.shape[0], B0.shape[0])
+    arr = (GemmArgs * len(problems))()
+    for i, (A, B, out, kw) in enumerate(problems):
+        kw = dict(kw)
+        sk = kw.pop("splitk", 1)
+        prezeroed = kw.pop("prezeroed", False)
+        if sk > 1 and not kw.get("accumulate", False) and not prezeroed:
+            out.zero_()
+        g = make_args(A, B, out, epi, splitk=sk, **kw)
+        if g.M % t[0] or g.N % t[1] or g.K % 64:
+            raise ValueError(f"gemm_nt_batched: shape {g.M}x{g.N}x{g.K} not a multiple of tile {t} / BK 64")
+        if i and (g.M, g.N, g.K, g.splitk) != (arr[0].M, arr[0].N, arr[0].K, arr[0].splitk):
+            raise ValueError("gemm_nt_batched: every problem needs the shape / split of the first")
+        arr[i] = g
+    native.check(_bind().st_gemm_nt_batched(arr, len(problems), epi, TILES[t], native.stream_handle()),
+                 "st_gemm_nt_batched")

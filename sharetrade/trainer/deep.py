@@ -109,7 +109,8 @@ class DeepDQN:
     def __init__(self, cfg: Config, device: torch.device, envs: int = 16384, batch: int = 4096,
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
-                 concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False):
+                 concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
+                 batched_fwd: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -132,6 +133,9 @@ class DeepDQN:
         # weights, as in the serial order).  Only difference from the serial order: the update samples
         # the ring as it was BEFORE this iteration's 16k inserts (one act step older).
         self.overlap_act = bool(overlap_act)
+        # batched_fwd: the online and target forward of each layer as ONE launch of the batched GEMM
+        # (both problems' tiles in one grid) instead of two GEMM chains on two streams
+        self.batched_fwd = bool(batched_fwd)
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -325,7 +329,7 @@ class DeepDQN:
                                           self.Wv[l].data_ptr(), self.Wmask[l].data_ptr())
             w.wb, w.wbT, w.gT = self.Wb[l].data_ptr(), self.WbT[l].data_ptr(), None
             w.O, w.I, w.ldg, w.nb, w.bias = O, I, 0, 0, 0
-            w.blocks = ((I + 31) // 32) * ((O + 31) // 32)
+            w.blocks = ((I + 63) // 64) * ((O + 63) // 64)
             b = _AdamSeg()
             b.w, b.g, b.m, b.v, b.mask = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
                                           self.bv[l].data_ptr(), self.bmask[l].data_ptr())
@@ -361,6 +365,18 @@ class DeepDQN:
                 a = acts[l + 1]
             else:
                 gm.gemm_nt(a, Wb[l], Q, gm.EPI_F32, bias=bias[l])
+
+    def _forward_pair(self, acts, actsT, actsN) -> None:
+        """Online forward on x (+ transposed activations for the backward) and target forward on x',
+        one batched launch per layer."""
+        for l in range(self.L):
+            if l < self.L - 1:
+                gm.gemm_nt_batched([(acts[l], self.Wb[l], acts[l + 1], dict(outT=actsT[l + 1], bias=self.b[l], relu=True)),
+                                    (actsN[l], self.Wt[l], actsN[l + 1], dict(bias=self.bt[l], relu=True))],
+                                   gm.EPI_BF16)
+            else:
+                gm.gemm_nt_batched([(acts[l], self.Wb[l], self.Q, dict(bias=self.b[l])),
+                                    (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l]))], gm.EPI_F32)
 
     def act_step(self) -> None:
         """One env step of all E envs: gather -> Q forward -> select/transition/replay insert."""
@@ -401,7 +417,9 @@ class DeepDQN:
                                          self.in_p, sh), "transpose X")
         acts = [self.X] + self.Act[1:]
         actsT = [self.XT] + self.ActT[1:]
-        if side is not None:
+        if self.batched_fwd:
+            self._forward_pair(acts, actsT, [self.Xn] + self.ActN[1:])
+        elif side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)

@@ -43,10 +43,12 @@ def test_replay_ring_and_env_step(native_built):
     assert int(d.rp_ctrl[1]) == d.cap and int(d.rp["pos"][0]) == 16
 
 
-@pytest.mark.parametrize("dw_gemm,concurrent,fused", [("hip", True, True), ("hipblaslt", True, True),
-                                                       ("hip", False, False), ("hipblaslt", False, True)])
-def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused):
-    kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused)
+@pytest.mark.parametrize("dw_gemm,concurrent,fused,batched", [("hip", True, True, True), ("hipblaslt", True, True, True),
+                                                               ("hip", False, False, False),
+                                                               ("hipblaslt", False, True, True),
+                                                               ("hipblaslt", True, True, False)])
+def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused, batched):
+    kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused, batched_fwd=batched)
     d = _dqn(**kw)
     for _ in range(8):
         d.act_step()
@@ -101,6 +103,24 @@ def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused):
             v = (1 - a.adam_betas[1]) * g * g / (1 - a.adam_betas[1])
             want = (p0 - a.lr * m / (v.sqrt() + a.adam_eps)) * msk + p0 * (1 - msk)
             assert torch.allclose(p1.view_as(want), want, rtol=1e-5, atol=1e-6 * a.lr), l
+
+
+def test_batched_forward_equals_two_chains(native_built):
+    """batched_fwd (online + target forward of a layer in one launch) == the two-stream GEMM chains:
+    identical activations, transposed activations and Q values of both networks."""
+    res = []
+    for batched in (True, False):
+        d = _dqn(batched_fwd=batched)
+        for _ in range(8):
+            d.act_step()
+        d.update_step()
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    assert torch.equal(a.Q, b.Q) and torch.equal(a.Qt, b.Qt)
+    for l in range(1, a.L):
+        assert torch.equal(a.Act[l], b.Act[l]) and torch.equal(a.ActN[l], b.ActN[l]), l
+        assert torch.equal(a.ActT[l], b.ActT[l]), l
 
 
 @pytest.mark.parametrize("dw_gemm,concurrent", [("hip", True), ("hipblaslt", True), ("hipblaslt", False)])

@@ -115,3 +115,77 @@ def test_gemm_256x256_tile(native_built, M, N, K):
     assert torch.allclose(out.float(), r, rtol=1e-2, atol=1e-2 * float(r.abs().max()))
     with pytest.raises(RuntimeError):
         gemm_nt(A, B, out, EPI_BF16, tile=(256, 256), outT=torch.empty(N, M, dtype=torch.bfloat16, device="cuda"))
+
+
+@pytest.mark.parametrize("epi,tile,sk", [(0, (128, 128), 1), (2, (64, 64), 1), (2, (128, 128), 4), (1, (128, 64), 1)])
+def test_gemm_batched_equals_single_launches(native_built, epi, tile, sk):
+    """gemm_nt_batched: 3 same-shape problems in one grid == 3 single launches, bit for bit."""
+    from sharetrade.ops.gemm import EPI_BF16, EPI_F32, EPI_RELU_GRAD, gemm_nt, gemm_nt_batched
+
+    M, N, K = 512, 256, 1024
+    probs, outs1, outs2 = [], [], []
+    for i in range(3):
+        A, B = _bf((M, K), 20 + i), _bf((N, K), 30 + i)
+        kw = {}
+        if epi == EPI_BF16:
+            kw = dict(bias=torch.randn(N, device="cuda"), relu=True,
+                      outT=torch.empty(N, M, dtype=torch.bfloat16, device="cuda"))
+        elif epi == EPI_RELU_GRAD:
+            kw = dict(auxT=torch.relu(torch.randn(N, M, device="cuda")).to(torch.bfloat16),
+                      outT=torch.empty(N, M, dtype=torch.bfloat16, device="cuda"))
+        else:
+            kw = dict(splitk=sk, bias=torch.randn(N, device="cuda"))
+        dt = torch.float32 if epi == EPI_F32 else torch.bfloat16
+        o1, o2 = torch.empty(M, N, dtype=dt, device="cuda"), torch.empty(M, N, dtype=dt, device="cuda")
+        kw2 = dict(kw)
+        if "outT" in kw:
+            kw2["outT"] = torch.empty_like(kw["outT"])
+        gemm_nt(A, B, o1, epi, tile=tile, **kw)
+        probs.append((A, B, o2, kw2))
+        outs1.append((o1, kw.get("outT")))
+        outs2.append((o2, kw2.get("outT")))
+    gemm_nt_batched(probs, epi, tile=tile)
+    torch.cuda.synchronize()
+    for (o1, t1), (o2, t2) in zip(outs1, outs2):
+        if sk > 1:
+            assert torch.allclose(o1, o2, rtol=1e-5, atol=1e-4)   # split-K: atomic summation order
+        else:
+            assert torch.equal(o1, o2)
+        if t1 is not None:
+            assert torch.equal(t1, t2)
+    with pytest.raises(ValueError):
+        gemm_nt_batched([probs[0], (_bf((M, K), 1), _bf((2 * N, K), 2), torch.empty(M, 2 * N, dtype=o1.dtype,
+                                                                                   device="cuda"), {})], epi, tile)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 1024),
+                                   (2048, 1024, 512)])
+def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
+    """256x256 ping-pong kernel (8 waves, two groups one barrier interval apart, LDS-DMA staging with
+    counted waits): bit-identical to the 128x128 kernel (same k order per output), both epilogues;
+    nk = 1, 2, 3 cover the pipeline fill / drain paths.  Repeated launches: a staging race would show
+    as a mismatch on some run."""
+    from sharetrade.ops.gemm import EPI_BF16, EPI_F32, gemm_nt
+
+    A, B = _bf((M, K), 11), _bf((N, K), 12)
+    bias = torch.randn(N, device="cuda")
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    gemm_nt(A, B, ref, EPI_BF16, tile=(128, 128), bias=bias, relu=True)
+    out = torch.empty_like(ref)
+    for _ in range(3):
+        out.fill_(7)
+        gemm_nt(A, B, out, EPI_BF16, tile=(256, 256, "pp"), bias=bias, relu=True)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    r32 = torch.empty(M, N, device="cuda")
+    gemm_nt(A, B, r32, EPI_F32, tile=(128, 128), bias=bias, alpha=0.5)
+    o32 = torch.full((M, N), float("nan"), device="cuda")
+    gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), bias=bias, alpha=0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(o32, r32)
+    gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), alpha=0.5, accumulate=True)
+    full = 0.5 * (A.float() @ B.float().t())
+    torch.cuda.synchronize()
+    assert torch.allclose(o32, r32 + full, rtol=1e-4, atol=1e-3 * float(full.abs().max()))
+    with pytest.raises(RuntimeError):   # no transposed output
+        gemm_nt(A, B, out, EPI_BF16, tile=(256, 256, "pp"), outT=torch.empty(N, M, dtype=torch.bfloat16, device="cuda"))
