@@ -390,22 +390,29 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
   };
   if (S.bias) {
     // 32 entries: wave w reduces rows 8w..8w+7 of gT (nb bf16 each, 16-byte loads)
+    // (the 8 rows advance together: 8 independent 16-byte loads in flight per lane and step)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i0 = b * 32;
-#pragma unroll 1
-    for (int r = 0; r < 8; ++r) {
-      const int i = i0 + 8 * wave + r;
-      float acc = 0.f;
-      if (i < S.I) {
-        const bf16_t* row = S.gT + (size_t)i * S.ldg;
-        for (int c = 8 * lane; c < S.nb; c += 512) {
-          const uint4 q = *reinterpret_cast<const uint4*>(row + c);
-          const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+    float acc[8];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) acc += bf2f((bf16_t)(u[k] & 0xFFFF)) + bf2f((bf16_t)(u[k] >> 16));
-        }
+    for (int r = 0; r < 8; ++r) acc[r] = 0.f;
+    for (int c = 8 * lane; c < S.nb; c += 512) {
+      uint4 q[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = i0 + 8 * wave + r;
+        q[r] = i < S.I ? *reinterpret_cast<const uint4*>(S.gT + (size_t)i * S.ldg + c) : make_uint4(0u, 0u, 0u, 0u);
       }
-      acc = wave_sum(acc);
-      if (lane == 0) red[8 * wave + r] = acc;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t u[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[r] += bf2f((bf16_t)(u[k] & 0xFFFF)) + bf2f((bf16_t)(u[k] >> 16));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float t = wave_sum(acc[r]);
+      if (lane == 0) red[8 * wave + r] = t;
     }
     __syncthreads();
     if (threadIdx.x < 32) {
@@ -424,17 +431,32 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
     const int tiles_i = (S.I + 63) / 64;
     const int o0 = (b / tiles_i) * 64, i0 = (b % tiles_i) * 64;
     const int ic = 4 * (threadIdx.x & 15), orow = threadIdx.x >> 4, i = i0 + ic;
+    // all 4 rows' loads are issued before any store (20 float4 in flight per lane): the stores could
+    // alias the later loads as far as the compiler knows, which would otherwise serialize the rows
+    float4 W[4], G[4], M[4], V[4], K[4];
+    bool ok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = o0 + orow + 16 * r;
+      ok[r] = o < S.O && i < S.I;
+      const size_t idx = ok[r] ? (size_t)o * S.I + i : 0;
+      W[r] = *reinterpret_cast<const float4*>(S.w + idx);
+      G[r] = *reinterpret_cast<const float4*>(S.g + idx);
+      M[r] = *reinterpret_cast<const float4*>(S.m + idx);
+      V[r] = *reinterpret_cast<const float4*>(S.v + idx);
+      K[r] = S.mask ? *reinterpret_cast<const float4*>(S.mask + idx) : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int ol = orow + 16 * r, o = o0 + ol;
       uint32_t lo = 0, hi = 0;
-      if (o < S.O && i < S.I) {
+      if (ok[r]) {
         const size_t idx = (size_t)o * S.I + i;
-        float4 w = *reinterpret_cast<const float4*>(S.w + idx);
-        const float4 g4 = *reinterpret_cast<const float4*>(S.g + idx);
-        float4 m = *reinterpret_cast<const float4*>(S.m + idx);
-        float4 v = *reinterpret_cast<const float4*>(S.v + idx);
-        const float4 mk = S.mask ? *reinterpret_cast<const float4*>(S.mask + idx) : make_float4(1.f, 1.f, 1.f, 1.f);
+        float4 w = W[r];
+        const float4 g4 = G[r];
+        float4 m = M[r];
+        float4 v = V[r];
+        const float4 mk = K[r];
         auto one = [&](float& wv, float& mv, float& vv, float g, float k) {
           if (k != 0.f) {
             g *= k;

@@ -111,26 +111,25 @@ ST_DEV void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <int BM, int BN, int EPI, int S = 2>
-__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_nt_kernel(GemmBatch batch) {
+// workgroups of one problem: tiles x K-splits
+template <int BM, int BN>
+ST_DEV int gemm_blocks(const GemmArgs& p) {
+  return (p.N / BN) * (p.M / BM) * (p.splitk > 1 ? p.splitk : 1);
+}
+ST_DEV int xcd_remap(int bid, int all) {   // neighbouring ids on one XCD's L2 (bijective)
+  const int xcd = bid % 8, q = all / 8, r = all % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// one workgroup's tile (and K split) of product p; bid = its index within p's blocks
+template <int BM, int BN, int EPI, int S>
+ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
   using G = GemmGeo<BM, BN, S>;
   constexpr int NW = G::NT / 64;
-  static_assert(G::NT == gemm_threads<BM, BN>() && G::MINB == gemm_min_blocks<BM, BN, S>(), "launch bounds");
-  extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
-  // XCD-aware tile order: neighbouring tiles (sharing A rows) on one XCD's L2; every problem of a
-  // batch has the shape of the first (checked on the host)
-  const int ntn = batch.a[0].N / BN, ntm = batch.a[0].M / BM, nwg = ntn * ntm;
-  const int nsplit = batch.a[0].splitk > 1 ? batch.a[0].splitk : 1, ntot = nwg * nsplit;
-  int bid = blockIdx.x;
-  {
-    const int all = ntot * batch.n, xcd = bid % 8, q = all / 8, r = all % 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-  }
-  const int pi = __builtin_amdgcn_readfirstlane(bid / ntot);
-  bid -= pi * ntot;
-  const GemmArgs& p = batch.a[pi];
+  const int ntn = p.N / BN, ntm = p.M / BM, nwg = ntn * ntm;
+  const int nsplit = p.splitk > 1 ? p.splitk : 1;
   const int ks = bid / nwg;   // K split (split-major: one split's tiles stay on one XCD's L2)
   bid -= ks * nwg;
   const int tm = bid / ntn, tn = bid % ntn;
@@ -280,6 +279,30 @@ __global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM,
       }
     }
   }
+}
+
+// a batch of same-shape products (one problem per range of workgroups)
+template <int BM, int BN, int EPI, int S = 2>
+__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_nt_kernel(GemmBatch batch) {
+  using G = GemmGeo<BM, BN, S>;
+  static_assert(G::NT == gemm_threads<BM, BN>() && G::MINB == gemm_min_blocks<BM, BN, S>(), "launch bounds");
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int ntot = gemm_blocks<BM, BN>(batch.a[0]);   // every problem has the first one's shape
+  int bid = xcd_remap(blockIdx.x, ntot * batch.n);
+  const int pi = __builtin_amdgcn_readfirstlane(bid / ntot);
+  gemm_body<BM, BN, EPI, S>(batch.a[pi], bid - pi * ntot, gsm);
+}
+
+// two products of any shapes and epilogues in one grid (e.g. a layer's data gradient beside the
+// next layer's split-K weight gradient): no fork / join of streams between them
+template <int BM, int BN, int EPI0, int EPI1, int S = 2>
+__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_dual_kernel(GemmArgs a0,
+                                                                                                          GemmArgs a1) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int n0 = gemm_blocks<BM, BN>(a0), n1 = gemm_blocks<BM, BN>(a1);
+  const int bid = xcd_remap(blockIdx.x, n0 + n1);
+  if (bid < n0) gemm_body<BM, BN, EPI0, S>(a0, bid, gsm);
+  else gemm_body<BM, BN, EPI1, S>(a1, bid - n0, gsm);
 }
 
 template <int BM, int BN, int EPI, int S = 2>
@@ -514,6 +537,17 @@ static hipError_t launch_gemm_pp(const GemmArgs& p, hipStream_t s) {
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
 //       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU),
 //       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output)
+// shape / stride / epilogue checks of one product for a BM x BN tile (the kernel assumes whole tiles)
+static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool has_t) {
+  if (!has_t && p->outT) return false;
+  if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return false;
+  if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return false;
+  if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return false;
+  if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return false;
+  if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return false;
+  return true;
+}
+
 // n same-shape products (same tile / epilogue / split) in one launch; st_gemm_nt = n 1
 extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi, int tile, hipStream_t stream) {
   if (tile < 0 || tile > 6 || n < 1 || n > st::GEMM_MAXB) return hipErrorInvalidValue;
@@ -524,12 +558,7 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
   for (int i = 0; i < n; ++i) {
     const st::GemmArgs* p = ps + i;
     if (p->M != ps->M || p->N != ps->N || p->K != ps->K || p->splitk != ps->splitk) return hipErrorInvalidValue;
-    if (tile == 6 && p->outT) return hipErrorInvalidValue;
-    if (p->M % bm || p->N % bn || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
-    if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8)) return hipErrorInvalidValue;
-    if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return hipErrorInvalidValue;
-    if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return hipErrorInvalidValue;
-    if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return hipErrorInvalidValue;
+    if (!gemm_args_ok(p, epi, bm, bn, tile != 6)) return hipErrorInvalidValue;
     b.a[i] = *p;
   }
 #define ST_G(BM_, BN_, S_)                                                               \
@@ -547,6 +576,25 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
   if (tile == 5) { ST_G(128, 128, 4) }
   if (tile == 6) { ST_G(256, 256, 2) }
 #undef ST_G
+  return hipErrorInvalidValue;
+}
+
+// two products of any shapes / epilogues on 128x128 tiles in one launch (epi pairs: relu-grad + f32,
+// f32 + f32, bf16 + f32)
+extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::GemmArgs* a1, int epi1, hipStream_t stream) {
+  if (!gemm_args_ok(a0, epi0, 128, 128, true) || !gemm_args_ok(a1, epi1, 128, 128, true)) return hipErrorInvalidValue;
+  using G = st::GemmGeo<128, 128, 2>;
+  const int nwg = (a0->M / 128) * (a0->N / 128) * (a0->splitk > 1 ? a0->splitk : 1) +
+                  (a1->M / 128) * (a1->N / 128) * (a1->splitk > 1 ? a1->splitk : 1);
+  auto go = [&](auto kern) -> hipError_t {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(G::NT), G::LDS_BYTES, stream, *a0, *a1);
+    return hipGetLastError();
+  };
+  if (epi0 == st::EPI_RELU_GRAD && epi1 == st::EPI_F32) return go(st::gemm_dual_kernel<128, 128, 1, 2, 2>);
+  if (epi0 == st::EPI_F32 && epi1 == st::EPI_F32) return go(st::gemm_dual_kernel<128, 128, 2, 2, 2>);
+  if (epi0 == st::EPI_BF16 && epi1 == st::EPI_F32) return go(st::gemm_dual_kernel<128, 128, 0, 2, 2>);
   return hipErrorInvalidValue;
 }
 

@@ -33,6 +33,8 @@ def _bind():
         L.st_gemm_nt.restype = C.c_int
         L.st_gemm_nt_batched.argtypes = [C.POINTER(GemmArgs), C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.st_gemm_nt_batched.restype = C.c_int
+        L.st_gemm_dual.argtypes = [C.POINTER(GemmArgs), C.c_int, C.POINTER(GemmArgs), C.c_int, C.c_void_p]
+        L.st_gemm_dual.restype = C.c_int
         L._gemm_bound = True
     return L
 
@@ -156,3 +158,23 @@ def gemm_nt_batched(problems, epi: int = EPI_BF16, tile=None) -> None:
         arr[i] = g
     native.check(_bind().st_gemm_nt_batched(arr, len(problems), epi, TILES[t], native.stream_handle()),
                  "st_gemm_nt_batched")
+
+
+def gemm_dual(first, epi0: int, second, epi1: int) -> None:
+    """Two products of any shapes / epilogues on 128x128 tiles in ONE launch (``first`` / ``second``
+    = ``(A, B, out, kwargs)``; epilogue pairs relu-grad + f32, f32 + f32, bf16 + f32): e.g. a layer's
+    data gradient beside the next layer's split-K weight gradient, with no stream fork / join."""
+    args = []
+    for (A, B, out, kw), epi in ((first, epi0), (second, epi1)):
+        kw = dict(kw)
+        sk = kw.pop("splitk", 1)
+        prezeroed = kw.pop("prezeroed", False)
+        if sk == "auto":
+            sk = pick_splitk(A.shape[0], B.shape[0], A.shape[1], (128, 128)) if epi == EPI_F32 else 1
+        if sk > 1 and not kw.get("accumulate", False) and not prezeroed:
+            out.zero_()
+        g = make_args(A, B, out, epi, splitk=sk, **kw)
+        if g.M % 128 or g.N % 128 or g.K % 64:
+            raise ValueError(f"gemm_dual: shape {g.M}x{g.N}x{g.K} not a multiple of 128x128 / BK 64")
+        args.append(g)
+    native.check(_bind().st_gemm_dual(args[0], epi0, args[1], epi1, native.stream_handle()), "st_gemm_dual")

@@ -110,7 +110,7 @@ class DeepDQN:
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
-                 batched_fwd: bool = True):
+                 batched_fwd: bool = True, dual_bwd: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -136,6 +136,10 @@ class DeepDQN:
         # batched_fwd: the online and target forward of each layer as ONE launch of the batched GEMM
         # (both problems' tiles in one grid) instead of two GEMM chains on two streams
         self.batched_fwd = bool(batched_fwd)
+        # dual_bwd: for the hidden layers, each layer's data gradient and the weight gradient of the
+        # layer above run as ONE launch of the two-product GEMM (split-K weight gradient), instead of a
+        # fork / join of two streams per layer (each join left a ~10-17 us gap in the graph)
+        self.dual_bwd = bool(dual_bwd)
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -193,8 +197,29 @@ class DeepDQN:
             if self.dw_gemm == "hipblaslt" or (self.dw_gemm == "auto" and o >= 1024 and i >= 1024):
                 self._dw_plan.append(("blaslt", None))
             else:
-                wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else gm.pick_tile(o, i)
+                # few output tiles, long K: 64x64 tiles split over K (1024x256: 10.6 us vs 16.3 with
+                # 128x128 split 8; tools/bench_dw.py, profiles/r2_config4_dual_bwd.md)
+                if o % 64 == 0 and i % 64 == 0 and (o // 64) * (i // 64) <= 256:
+                    wt = (64, 64)
+                else:
+                    wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else gm.pick_tile(o, i)
                 self._dw_plan.append(("hip", (wt, gm.pick_splitk(o, self.pdims[l], self.B, wt))))
+        # output layer of the batched forward: split K until both problems' tiles reach ~256 workgroups
+        self._q_splitk = 1
+        if self.batched_fwd:
+            qt = gm.pick_tile(self.B, ACT_PAD)
+            tiles = 2 * (self.B // qt[0]) * (ACT_PAD // qt[1])      # online + target problems
+            ktiles = self.pdims[-2] // 64
+            while tiles * self._q_splitk < 256 and ktiles % (2 * self._q_splitk) == 0 and \
+                    ktiles // (2 * self._q_splitk) >= 4:
+                self._q_splitk *= 2
+        self._dual = [False] * self.L   # layer l's weight gradient in a dual launch with G_{l-1}
+        if self.dual_bwd:
+            for l in range(1, self.L - 1):
+                o, i = self.pdims[l + 1], self.pdims[l]
+                if o % 128 == 0 and i % 128 == 0 and self.B % 128 == 0:
+                    self._dw_plan[l] = ("hip", ((128, 128), gm.pick_splitk(o, i, self.B, (128, 128))))
+                    self._dual[l] = True
         sk_layers = [l for l, (k, a) in enumerate(self._dw_plan) if k == "hip" and a[1] > 1]
         self._zero_span = (0, 0)
         if sk_layers:
@@ -240,8 +265,8 @@ class DeepDQN:
         self.ActN = [None] + [torch.zeros(M, h, dtype=b16, device=dev) for h in hid]
         self.G = [torch.zeros(M, self.pdims[l + 1], dtype=b16, device=dev) for l in range(self.L)]
         self.GT = [torch.zeros(self.pdims[l + 1], M, dtype=b16, device=dev) for l in range(self.L)]
-        self.Q = torch.zeros(M, ACT_PAD, device=dev)
-        self.Qt = torch.zeros(M, ACT_PAD, device=dev)
+        self._Qpair = torch.zeros(2, M, ACT_PAD, device=dev)   # online / target Q: one zero range
+        self.Q, self.Qt = self._Qpair[0], self._Qpair[1]
         self.r_b = torch.zeros(M, device=dev)
         self.a_b = torch.zeros(M, dtype=i32, device=dev)
         self.d_b = torch.zeros(M, device=dev)
@@ -285,7 +310,9 @@ class DeepDQN:
         gr.r_out, gr.a_out, gr.done_out = self.r_b.data_ptr(), self.a_b.data_ptr(), self.d_b.data_ptr()
         z0, zn = self._zero_span
         gr.zero0 = self._dW_flat.data_ptr() + 4 * z0 if zn else None
-        gr.zero0_n, gr.zero1, gr.zero1_n = zn, None, 0
+        gr.zero0_n = zn
+        # the batched output layer accumulates Q / Q_t over K splits: zeroed here as well
+        gr.zero1, gr.zero1_n = (self._Qpair.data_ptr(), self._Qpair.numel()) if self._q_splitk > 1 else (None, 0)
         self._gather_rp = gr
         ev = _Env()
         ev.prices, ev.T, ev.H, ev.E = self.prices.data_ptr(), self.T, self.H, self.E
@@ -325,18 +352,24 @@ class DeepDQN:
         for l in range(self.L):
             O, I = self.pdims[l + 1], self.pdims[l]
             w = _AdamSeg()
-            w.w, w.g, w.m, w.v, w.mask = (self.W[l].data_ptr(), self.dW[l].data_ptr(), self.Wm[l].data_ptr(),
-                                          self.Wv[l].data_ptr(), self.Wmask[l].data_ptr())
+            # all-ones masks (hidden layers) are not read: 4 of the ~36 bytes per parameter
+            w.w, w.g, w.m, w.v = (self.W[l].data_ptr(), self.dW[l].data_ptr(), self.Wm[l].data_ptr(),
+                                  self.Wv[l].data_ptr())
+            w.mask = None if bool(self.Wmask[l].bool().all()) else self.Wmask[l].data_ptr()
             w.wb, w.wbT, w.gT = self.Wb[l].data_ptr(), self.WbT[l].data_ptr(), None
             w.O, w.I, w.ldg, w.nb, w.bias = O, I, 0, 0, 0
             w.blocks = ((I + 63) // 64) * ((O + 63) // 64)
             b = _AdamSeg()
-            b.w, b.g, b.m, b.v, b.mask = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
-                                          self.bv[l].data_ptr(), self.bmask[l].data_ptr())
+            b.w, b.g, b.m, b.v = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
+                                  self.bv[l].data_ptr())
+            b.mask = None if bool(self.bmask[l].bool().all()) else self.bmask[l].data_ptr()
             b.wb, b.wbT, b.gT = None, None, self.GT[l].data_ptr()
             b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
             b.blocks = (O + 31) // 32
             segs += [w, b]
+        # bias segments first: their blocks (32 rows x batch of gradient sums each) are the longest,
+        # started first they do not form the tail
+        segs = [sg for sg in segs if sg.bias] + [sg for sg in segs if not sg.bias]
         if len(segs) > ADAM_MAX_SEG:
             self.fused_adam = False
         else:
@@ -375,8 +408,10 @@ class DeepDQN:
                                     (actsN[l], self.Wt[l], actsN[l + 1], dict(bias=self.bt[l], relu=True))],
                                    gm.EPI_BF16)
             else:
-                gm.gemm_nt_batched([(acts[l], self.Wb[l], self.Q, dict(bias=self.b[l])),
-                                    (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l]))], gm.EPI_F32)
+                sk = self._q_splitk   # few output tiles, long K: split (outputs zeroed by the replay gather)
+                gm.gemm_nt_batched([(acts[l], self.Wb[l], self.Q, dict(bias=self.b[l], splitk=sk, prezeroed=True)),
+                                    (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l], splitk=sk, prezeroed=True))],
+                                   gm.EPI_F32)
 
     def act_step(self) -> None:
         """One env step of all E envs: gather -> Q forward -> select/transition/replay insert."""
@@ -430,20 +465,27 @@ class DeepDQN:
             self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)
         native.check(k.st_deep_td(self._td, sh), "deep_td")
         for l in reversed(range(self.L)):
-            if side is not None:
-                side.wait_stream(main)        # G_l is ready
-                with torch.cuda.stream(side):
-                    self._dw(l, actsT)
+            if self._dual[l]:
+                # one launch: G_{l-1} = (G_l . W_l) * (A_l > 0)  and  dW_l = G_l^T . A_l (split-K)
+                _, (_, sk) = self._dw_plan[l]
+                gm.gemm_dual((self.G[l], self.WbT[l], self.G[l - 1], dict(outT=self.GT[l - 1], auxT=actsT[l])),
+                             gm.EPI_RELU_GRAD,
+                             (self.GT[l], actsT[l], self.dW[l], dict(splitk=sk, prezeroed=sk > 1)), gm.EPI_F32)
             else:
-                self._dw(l, actsT)
+                if side is not None and not self.dual_bwd:
+                    side.wait_stream(main)        # G_l is ready
+                    with torch.cuda.stream(side):
+                        self._dw(l, actsT)
+                else:   # dual_bwd: the two small leftover weight gradients stay on the main stream
+                    self._dw(l, actsT)
             if not self.fused_adam:
                 native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
                                                self.db[l].data_ptr(), sh), "bias grad")
-            if l > 0:
+            if l > 0 and not self._dual[l]:
                 # G_{l-1} = (G_l . W_l) * (A_l > 0)
                 gm.gemm_nt(self.G[l], self.WbT[l], self.G[l - 1], gm.EPI_RELU_GRAD, outT=self.GT[l - 1],
                            auxT=actsT[l])
-        if side is not None:
+        if side is not None and not self.dual_bwd:
             main.wait_stream(side)
         if act is not None:
             main.wait_stream(act)              # the act step's GEMMs read the pre-update weights

@@ -43,12 +43,13 @@ def test_replay_ring_and_env_step(native_built):
     assert int(d.rp_ctrl[1]) == d.cap and int(d.rp["pos"][0]) == 16
 
 
-@pytest.mark.parametrize("dw_gemm,concurrent,fused,batched", [("hip", True, True, True), ("hipblaslt", True, True, True),
-                                                               ("hip", False, False, False),
-                                                               ("hipblaslt", False, True, True),
-                                                               ("hipblaslt", True, True, False)])
-def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused, batched):
-    kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused, batched_fwd=batched)
+@pytest.mark.parametrize("dw_gemm,concurrent,fused,batched,dual", [("hip", True, True, True, True),
+                                                                    ("hipblaslt", True, True, True, False),
+                                                                    ("hip", False, False, False, False),
+                                                                    ("hipblaslt", False, True, True, True),
+                                                                    ("hipblaslt", True, True, False, False)])
+def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused, batched, dual):
+    kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused, batched_fwd=batched, dual_bwd=dual)
     d = _dqn(**kw)
     for _ in range(8):
         d.act_step()
@@ -117,7 +118,8 @@ def test_batched_forward_equals_two_chains(native_built):
         torch.cuda.synchronize()
         res.append(d)
     a, b = res
-    assert torch.equal(a.Q, b.Q) and torch.equal(a.Qt, b.Qt)
+    # Q / Q_t: the batched output layer is split over K (fp32 atomics): equal up to summation order
+    assert torch.allclose(a.Q, b.Q, rtol=1e-5, atol=1e-5) and torch.allclose(a.Qt, b.Qt, rtol=1e-5, atol=1e-5)
     for l in range(1, a.L):
         assert torch.equal(a.Act[l], b.Act[l]) and torch.equal(a.ActN[l], b.ActN[l]), l
         assert torch.equal(a.ActT[l], b.ActT[l]), l

@@ -189,3 +189,29 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     assert torch.allclose(o32, r32 + full, rtol=1e-4, atol=1e-3 * float(full.abs().max()))
     with pytest.raises(RuntimeError):   # no transposed output
         gemm_nt(A, B, out, EPI_BF16, tile=(256, 256, "pp"), outT=torch.empty(N, M, dtype=torch.bfloat16, device="cuda"))
+
+
+@pytest.mark.parametrize("sk", [1, 4])
+def test_gemm_dual_equals_two_launches(native_built, sk):
+    """gemm_dual: a relu-grad product (with C^T) and a differently shaped f32 product (split-K) in one
+    grid == the two single launches."""
+    from sharetrade.ops.gemm import EPI_F32, EPI_RELU_GRAD, gemm_dual, gemm_nt
+
+    M0, N0, K0 = 512, 256, 256
+    M1, N1, K1 = 256, 384, 1024
+    A0, B0 = _bf((M0, K0), 41), _bf((N0, K0), 42)
+    A1, B1 = _bf((M1, K1), 43), _bf((N1, K1), 44)
+    aux = torch.relu(torch.randn(N0, M0, device="cuda")).to(torch.bfloat16)
+    r0 = torch.empty(M0, N0, dtype=torch.bfloat16, device="cuda")
+    r0T = torch.empty(N0, M0, dtype=torch.bfloat16, device="cuda")
+    r1 = torch.empty(M1, N1, device="cuda")
+    gemm_nt(A0, B0, r0, EPI_RELU_GRAD, tile=(128, 128), outT=r0T, auxT=aux)
+    gemm_nt(A1, B1, r1, EPI_F32, tile=(128, 128), splitk=sk)
+    o0, o0T, o1 = torch.empty_like(r0), torch.empty_like(r0T), torch.full_like(r1, float("nan"))
+    gemm_dual((A0, B0, o0, dict(outT=o0T, auxT=aux)), EPI_RELU_GRAD, (A1, B1, o1, dict(splitk=sk)), EPI_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(o0, r0) and torch.equal(o0T, r0T)
+    if sk == 1:
+        assert torch.equal(o1, r1)
+    else:
+        assert torch.allclose(o1, r1, rtol=1e-5, atol=1e-4)

@@ -55,6 +55,23 @@ def main():
         print(f"| {o} | {i} | {B} | {t1:.1f} | {fl / t1 / 1e6:.0f} | {t2:.1f} | {fl / t2 / 1e6:.0f} | "
               f"{r(d1):.1e} / {r(d2):.1e} |")
 
+    # tile / split sweep (output prezeroed elsewhere in the update: zeroing not timed)
+    print()
+    print("| out | in | tile | split | us |")
+    print("|---|---|---|---|---|")
+    for o, i in [(1024, 256), (64, 1024)]:
+        GT = torch.randn(o, B, device=dev).to(torch.bfloat16)
+        AT = torch.randn(i, B, device=dev).to(torch.bfloat16)
+        d1 = torch.zeros(o, i, device=dev)
+        for t in ((128, 128), (128, 64), (64, 64)):
+            if o % t[0] or i % t[1]:
+                continue
+            for sk in (1, 2, 4, 8, 16, 32):
+                if (B // 64) % sk or B // 64 // sk < 2:
+                    continue
+                us = timeit(lambda: gemm_nt(GT, AT, d1, EPI_F32, tile=t, splitk=sk, prezeroed=True))
+                print(f"| {o} | {i} | {t} | {sk} | {us:.1f} |")
+
 
 if __name__ == "__main__":
     main()
