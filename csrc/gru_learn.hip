@@ -54,20 +54,40 @@ __global__ void __launch_bounds__(256) gru_gather_kernel(GruGather g) {
   const size_t idx = (size_t)(((((unsigned long long)c0) << 32) | c1) % (sz ? sz : 1ull));
   const int S = g.S;
   const uint4 z = {0u, 0u, 0u, 0u};
-  for (int j = lane; j < (S + 1) * 8; j += 64) {
-    const int t = j >> 3, c = j & 7;
-    uint4 v = z;
-    if (c < RF / 8) v = reinterpret_cast<const uint4*>(g.rx + (idx * (size_t)(S + 1) + t) * RF)[c];
-    if (c == RF / 8) v.x = 0x3F80u;   // column RF = 1.0: the dW_ih GEMM's column RF is then db_ih
-    reinterpret_cast<uint4*>(g.X + ((size_t)t * g.B + b) * RFL)[c] = v;
-  }
-  const s4v hv = *reinterpret_cast<const s4v*>(g.rh0 + idx * RH + 4 * lane);
-  *reinterpret_cast<float4*>(g.H0 + (size_t)b * RH + 4 * lane) =
-      make_float4(bf2f((bf16_t)hv[0]), bf2f((bf16_t)hv[1]), bf2f((bf16_t)hv[2]), bf2f((bf16_t)hv[3]));
-  if (lane < S) {
-    g.A[(size_t)lane * g.B + b] = g.ra[idx * S + lane];
-    g.R[(size_t)lane * g.B + b] = g.rr[idx * S + lane];
-    g.D[(size_t)lane * g.B + b] = (float)g.rd[idx * S + lane];
+  // every load of the segment is issued before the first store (the stores could alias the later
+  // loads as far as the compiler knows, which would otherwise make each a dependent round trip)
+  constexpr int XP = 3;   // x pieces per lane held at once: (S + 1) * 8 <= 192 covers S <= 23 in one pass
+  for (int j0 = 0; j0 < (S + 1) * 8; j0 += 64 * XP) {
+    uint4 v[XP];
+#pragma unroll
+    for (int k = 0; k < XP; ++k) {
+      const int j = j0 + 64 * k + lane, t = j >> 3, c = j & 7;
+      v[k] = z;
+      if (j < (S + 1) * 8 && c < RF / 8) v[k] = reinterpret_cast<const uint4*>(g.rx + (idx * (size_t)(S + 1) + t) * RF)[c];
+      if (c == RF / 8) v[k].x = 0x3F80u;   // column RF = 1.0: the dW_ih GEMM's column RF is then db_ih
+    }
+    const s4v hv = *reinterpret_cast<const s4v*>(g.rh0 + idx * RH + 4 * lane);
+    unsigned char a = 0, d = 0;
+    float r = 0.f;
+    if (j0 == 0 && lane < S) {
+      a = g.ra[idx * S + lane];
+      r = g.rr[idx * S + lane];
+      d = g.rd[idx * S + lane];
+    }
+#pragma unroll
+    for (int k = 0; k < XP; ++k) {
+      const int j = j0 + 64 * k + lane, t = j >> 3, c = j & 7;
+      if (j < (S + 1) * 8) reinterpret_cast<uint4*>(g.X + ((size_t)t * g.B + b) * RFL)[c] = v[k];
+    }
+    if (j0 == 0) {
+      *reinterpret_cast<float4*>(g.H0 + (size_t)b * RH + 4 * lane) =
+          make_float4(bf2f((bf16_t)hv[0]), bf2f((bf16_t)hv[1]), bf2f((bf16_t)hv[2]), bf2f((bf16_t)hv[3]));
+      if (lane < S) {
+        g.A[(size_t)lane * g.B + b] = a;
+        g.R[(size_t)lane * g.B + b] = r;
+        g.D[(size_t)lane * g.B + b] = (float)d;
+      }
+    }
   }
 }
 
