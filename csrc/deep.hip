@@ -60,9 +60,13 @@ __global__ void __launch_bounds__(256) deep_gather_kernel(DeepGather g) {
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (g.mode == 1) {
+    // 16-byte stores where the span allows (the spans start 16-byte aligned: checked on the host)
     const int gid = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
-    for (int i = gid; i < g.zero0_n; i += gs) g.zero0[i] = 0.f;
-    for (int i = gid; i < g.zero1_n; i += gs) g.zero1[i] = 0.f;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = gid; i < g.zero0_n / 4; i += gs) reinterpret_cast<float4*>(g.zero0)[i] = z4;
+    for (int i = (g.zero0_n & ~3) + gid; i < g.zero0_n; i += gs) g.zero0[i] = 0.f;
+    for (int i = gid; i < g.zero1_n / 4; i += gs) reinterpret_cast<float4*>(g.zero1)[i] = z4;
+    for (int i = (g.zero1_n & ~3) + gid; i < g.zero1_n; i += gs) g.zero1[i] = 0.f;
   }
   if (row >= g.B) return;
   int e, ps, s, s2 = 0;
@@ -513,6 +517,7 @@ extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
 }
 
 extern "C" hipError_t st_deep_gather(const st::DeepGather* g, hipStream_t s) {
+  if ((reinterpret_cast<uintptr_t>(g->zero0) & 15) || (reinterpret_cast<uintptr_t>(g->zero1) & 15)) return hipErrorInvalidValue;
   if (g->in_p > 256 || g->in_p % 4 || g->H + 2 > g->in_p) return hipErrorInvalidValue;
   const int waves = g->B, per = 4;
   hipLaunchKernelGGL(st::deep_gather_kernel, dim3((waves + per - 1) / per), dim3(256), 0, s, *g);
