@@ -110,7 +110,7 @@ class DeepDQN:
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
-                 batched_fwd: bool = True, dual_bwd: bool = True):
+                 batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -140,6 +140,9 @@ class DeepDQN:
         # layer above run as ONE launch of the two-product GEMM (split-K weight gradient), instead of a
         # fork / join of two streams per layer (each join left a ~10-17 us gap in the graph)
         self.dual_bwd = bool(dual_bwd)
+        # act_inline (with overlap_act): the act step in the same graph and order, but on the update's
+        # stream (no fork / join; the two GEMM chains then run back to back instead of side by side)
+        self.act_inline = bool(act_inline)
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -445,9 +448,13 @@ class DeepDQN:
         if with_act:
             if act is None:
                 raise RuntimeError("update_step(with_act=True) needs overlap_act=True")
-            act.wait_stream(main)              # the batch is sampled: the act step may insert now
-            with torch.cuda.stream(act):
-                self.act_step()
+            if self.act_inline:
+                self.act_step()                # same order, same stream
+                act = None
+            else:
+                act.wait_stream(main)          # the batch is sampled: the act step may insert now
+                with torch.cuda.stream(act):
+                    self.act_step()
         native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
                                          self.in_p, sh), "transpose X")
         acts = [self.X] + self.Act[1:]

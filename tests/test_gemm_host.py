@@ -1,0 +1,45 @@
+"""Host-side GEMM dispatch (CPU): tile selection and the shape checks that run before any launch."""
+import pytest
+import torch
+
+from sharetrade.ops import gemm as gm
+
+
+def _t(*shape, dtype=torch.bfloat16):
+    return torch.zeros(*shape, dtype=dtype)
+
+
+def test_auto_tile_prefers_pingpong_for_big_plain_products():
+    assert gm.auto_tile(16384, 1024, gm.EPI_BF16, {}) == (256, 256, "pp")
+    assert gm.auto_tile(16384, 1024, gm.EPI_F32, {"splitk": "auto"}) == (256, 256, "pp")
+    # C^T, relu-grad masks and explicit split-K stay on the 128-family kernels
+    assert gm.auto_tile(16384, 1024, gm.EPI_BF16, {"outT": _t(1024, 16384)}) == gm.pick_tile(16384, 1024)
+    assert gm.auto_tile(16384, 1024, gm.EPI_RELU_GRAD, {}) == gm.pick_tile(16384, 1024)
+    assert gm.auto_tile(16384, 1024, gm.EPI_F32, {"splitk": 4}) == gm.pick_tile(16384, 1024)
+    # too few 256x256 tiles to fill 256 CUs
+    assert gm.auto_tile(4096, 1024, gm.EPI_BF16, {}) == gm.pick_tile(4096, 1024)
+    old = gm.PINGPONG
+    try:
+        gm.PINGPONG = False
+        assert gm.auto_tile(16384, 1024, gm.EPI_BF16, {}) == gm.pick_tile(16384, 1024)
+    finally:
+        gm.PINGPONG = old
+
+
+def test_pick_splitk_fills_the_chip():
+    assert gm.pick_splitk(1024, 1024, 4096, (128, 128)) == 4        # 64 tiles -> 256 workgroups
+    assert gm.pick_splitk(1024, 256, 4096, (64, 64)) == 4           # 64 tiles -> 256
+    assert gm.pick_splitk(4096, 1024, 1024, (128, 128)) == 1        # already 256 tiles
+
+
+def test_batched_and_dual_reject_bad_shapes_before_launch():
+    A, B = _t(256, 128), _t(256, 128)
+    ok = (A, B, _t(256, 256), {})
+    with pytest.raises(ValueError):   # second problem has another shape
+        gm.gemm_nt_batched([ok, (_t(256, 128), _t(512, 128), _t(256, 512), {})], gm.EPI_BF16, (128, 128))
+    with pytest.raises(ValueError):   # more than GEMM_MAXB problems
+        gm.gemm_nt_batched([ok] * (gm.GEMM_MAXB + 1), gm.EPI_BF16, (128, 128))
+    with pytest.raises(ValueError):   # 64-row product on 128x128 tiles
+        gm.gemm_dual(ok, gm.EPI_BF16, (_t(64, 128), _t(256, 128), _t(64, 256, dtype=torch.float32), {}), gm.EPI_F32)
+    with pytest.raises(ValueError):   # split-K needs the fp32 epilogue
+        gm.make_args(A, B, _t(256, 256), gm.EPI_BF16, splitk=2)
