@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--serial", action="store_true", help="one stream (no concurrent GEMM chains in the update)")
     ap.add_argument("--unfused-adam", action="store_true", help="per-layer Adam + row-sum + counter launches")
     ap.add_argument("--no-pingpong", action="store_true", help="no 256x256 ping-pong GEMM for the act-step layers")
+    ap.add_argument("--fuse-act", action="store_true",
+                    help="the act step's forward layers grouped into the update's forward launches (one stream)")
     ap.add_argument("--act-inline", action="store_true",
                     help="the act step inside the iteration graph on the update's stream (no fork / join)")
     ap.add_argument("--no-dual-bwd", action="store_true",
@@ -57,7 +59,8 @@ def main():
     dev = torch.device("cuda", 0)
     d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay, dw_gemm=a.dw_gemm,
                 concurrent=not a.serial, fused_adam=not a.unfused_adam, overlap_act=not a.no_overlap_act,
-                batched_fwd=not a.unbatched_fwd, dual_bwd=not a.no_dual_bwd, act_inline=a.act_inline)
+                batched_fwd=not a.unbatched_fwd, dual_bwd=not a.no_dual_bwd, act_inline=a.act_inline,
+                fuse_act=a.fuse_act)
     for _ in range(a.warmup):
         d.act_step()
     d.capture()
@@ -96,7 +99,7 @@ def main():
         "update_tflops": round(upd_flop / t_upd / 1e12, 1), "replay_size": s["replay_size"],
         "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
         "concurrent_update": d.concurrent, "fused_adam": d.fused_adam, "overlap_act": d.overlap_act,
-        "batched_fwd": d.batched_fwd, "pingpong_gemm": not a.no_pingpong, "dual_bwd": d.dual_bwd, "act_inline": d.act_inline,
+        "batched_fwd": d.batched_fwd, "pingpong_gemm": not a.no_pingpong, "dual_bwd": d.dual_bwd, "act_inline": d.act_inline, "fuse_act": d.fuse_act,
     }
     print(json.dumps(out))
 

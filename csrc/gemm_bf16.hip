@@ -47,8 +47,8 @@ struct GemmArgs {
                          // added into out (which then holds the prior value / zeros)
 };
 
-// a batch of same-shape products in one launch (e.g. the online and target networks' forward
-// of one layer): workgroups [i*T, (i+1)*T) compute problem i, T = tiles x K-splits per problem
+// a group of up to 4 products with one epilogue / tile in one launch (e.g. the online and target
+// networks' forward of one layer): consecutive workgroup ranges compute problems 0, 1, ...
 constexpr int GEMM_MAXB = 4;
 struct GemmBatch {
   GemmArgs a[GEMM_MAXB];
@@ -287,10 +287,17 @@ __global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM,
   using G = GemmGeo<BM, BN, S>;
   static_assert(G::NT == gemm_threads<BM, BN>() && G::MINB == gemm_min_blocks<BM, BN, S>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  const int ntot = gemm_blocks<BM, BN>(batch.a[0]);   // every problem has the first one's shape
-  int bid = xcd_remap(blockIdx.x, ntot * batch.n);
-  const int pi = __builtin_amdgcn_readfirstlane(bid / ntot);
-  gemm_body<BM, BN, EPI, S>(batch.a[pi], bid - pi * ntot, gsm);
+  // problems may differ in shape (grouped GEMM): workgroup ranges in problem order
+  int all = 0;
+  for (int i = 0; i < batch.n; ++i) all += gemm_blocks<BM, BN>(batch.a[i]);
+  int bid = xcd_remap(blockIdx.x, all), pi = 0;
+  for (; pi + 1 < batch.n; ++pi) {
+    const int nb = gemm_blocks<BM, BN>(batch.a[pi]);
+    if (bid < nb) break;
+    bid -= nb;
+  }
+  pi = __builtin_amdgcn_readfirstlane(pi);
+  gemm_body<BM, BN, EPI, S>(batch.a[pi], bid, gsm);
 }
 
 // two products of any shapes and epilogues in one grid (e.g. a layer's data gradient beside the
@@ -315,8 +322,8 @@ static hipError_t launch_gemm(const GemmBatch& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const GemmArgs& a = p.a[0];
-  const int nwg = (a.M / BM) * (a.N / BN) * (a.splitk > 1 ? a.splitk : 1) * p.n;
+  int nwg = 0;
+  for (int i = 0; i < p.n; ++i) nwg += (p.a[i].M / BM) * (p.a[i].N / BN) * (p.a[i].splitk > 1 ? p.a[i].splitk : 1);
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI, S>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
   return hipGetLastError();
 }
@@ -548,7 +555,7 @@ static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool ha
   return true;
 }
 
-// n same-shape products (same tile / epilogue / split) in one launch; st_gemm_nt = n 1
+// n products (any shapes; same tile and epilogue) in one launch; st_gemm_nt = n 1
 extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi, int tile, hipStream_t stream) {
   if (tile < 0 || tile > 6 || n < 1 || n > st::GEMM_MAXB) return hipErrorInvalidValue;
   const int bm = (tile == 3 || tile == 6) ? 256 : (tile == 1 ? 64 : 128);
@@ -557,7 +564,6 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
   b.n = n;
   for (int i = 0; i < n; ++i) {
     const st::GemmArgs* p = ps + i;
-    if (p->M != ps->M || p->N != ps->N || p->K != ps->K || p->splitk != ps->splitk) return hipErrorInvalidValue;
     if (!gemm_args_ok(p, epi, bm, bn, tile != 6)) return hipErrorInvalidValue;
     b.a[i] = *p;
   }

@@ -135,10 +135,10 @@ GEMM_MAXB = 4
 
 
 def gemm_nt_batched(problems, epi: int = EPI_BF16, tile=None) -> None:
-    """Up to 4 same-shape products ``out_i = A_i . B_i^T`` (same epilogue / tile / split) in ONE
-    launch: ``problems`` is a list of ``(A, B, out, kwargs)``.  Replaces a fork / join of
-    concurrent streams (e.g. the online and target forward of one layer) by one grid that holds
-    the tiles of all of them."""
+    """Up to 4 products ``out_i = A_i . B_i^T`` (one epilogue and tile; shapes and K splits may
+    differ: a grouped GEMM) in ONE launch: ``problems`` is a list of ``(A, B, out, kwargs)``.
+    Replaces a fork / join of concurrent streams (e.g. the online and target forward of one layer)
+    by one grid that holds the tiles of all of them."""
     if not 1 <= len(problems) <= GEMM_MAXB:
         raise ValueError(f"gemm_nt_batched: 1..{GEMM_MAXB} problems")
     A0, B0 = problems[0][0], problems[0][1]
@@ -153,8 +153,6 @@ def gemm_nt_batched(problems, epi: int = EPI_BF16, tile=None) -> None:
         g = make_args(A, B, out, epi, splitk=sk, **kw)
         if g.M % t[0] or g.N % t[1] or g.K % 64:
             raise ValueError(f"gemm_nt_batched: shape {g.M}x{g.N}x{g.K} not a multiple of tile {t} / BK 64")
-        if i and (g.M, g.N, g.K, g.splitk) != (arr[0].M, arr[0].N, arr[0].K, arr[0].splitk):
-            raise ValueError("gemm_nt_batched: every problem needs the shape / split of the first")
         arr[i] = g
     native.check(_bind().st_gemm_nt_batched(arr, len(problems), epi, TILES[t], native.stream_handle()),
                  "st_gemm_nt_batched")

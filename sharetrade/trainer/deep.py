@@ -110,7 +110,8 @@ class DeepDQN:
                  replay_capacity: int = 1 << 20, hidden: Optional[List[int]] = None, target_every: int = 1000,
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
-                 batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False):
+                 batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
+                 fuse_act: bool = False):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -143,6 +144,10 @@ class DeepDQN:
         # act_inline (with overlap_act): the act step in the same graph and order, but on the update's
         # stream (no fork / join; the two GEMM chains then run back to back instead of side by side)
         self.act_inline = bool(act_inline)
+        # fuse_act (with overlap_act and batched_fwd): the act step's forward layers join the update's
+        # grouped forward launches (online x, target x', act states: three products per launch), its
+        # env step follows on the same stream -- one stream, no fork / join, every launch fuller
+        self.fuse_act = bool(fuse_act)
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -402,19 +407,24 @@ class DeepDQN:
             else:
                 gm.gemm_nt(a, Wb[l], Q, gm.EPI_F32, bias=bias[l])
 
-    def _forward_pair(self, acts, actsT, actsN) -> None:
+    def _forward_pair(self, acts, actsT, actsN, actsE=None) -> None:
         """Online forward on x (+ transposed activations for the backward) and target forward on x',
-        one batched launch per layer."""
+        one grouped launch per layer; with ``actsE`` the act step's forward on the env states (online
+        weights, no transposed copy) is a third product of the same launches."""
         for l in range(self.L):
             if l < self.L - 1:
-                gm.gemm_nt_batched([(acts[l], self.Wb[l], acts[l + 1], dict(outT=actsT[l + 1], bias=self.b[l], relu=True)),
-                                    (actsN[l], self.Wt[l], actsN[l + 1], dict(bias=self.bt[l], relu=True))],
-                                   gm.EPI_BF16)
+                probs = [(acts[l], self.Wb[l], acts[l + 1], dict(outT=actsT[l + 1], bias=self.b[l], relu=True)),
+                         (actsN[l], self.Wt[l], actsN[l + 1], dict(bias=self.bt[l], relu=True))]
+                if actsE is not None:
+                    probs.append((actsE[l], self.Wb[l], actsE[l + 1], dict(bias=self.b[l], relu=True)))
+                gm.gemm_nt_batched(probs, gm.EPI_BF16, tile=gm.pick_tile(self.B, self.pdims[l + 1]))
             else:
                 sk = self._q_splitk   # few output tiles, long K: split (outputs zeroed by the replay gather)
-                gm.gemm_nt_batched([(acts[l], self.Wb[l], self.Q, dict(bias=self.b[l], splitk=sk, prezeroed=True)),
-                                    (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l], splitk=sk, prezeroed=True))],
-                                   gm.EPI_F32)
+                probs = [(acts[l], self.Wb[l], self.Q, dict(bias=self.b[l], splitk=sk, prezeroed=True)),
+                         (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l], splitk=sk, prezeroed=True))]
+                if actsE is not None:
+                    probs.append((actsE[l], self.Wb[l], self.Qe, dict(bias=self.b[l])))
+                gm.gemm_nt_batched(probs, gm.EPI_F32, tile=gm.pick_tile(self.B, ACT_PAD))
 
     def act_step(self) -> None:
         """One env step of all E envs: gather -> Q forward -> select/transition/replay insert."""
@@ -448,7 +458,10 @@ class DeepDQN:
         if with_act:
             if act is None:
                 raise RuntimeError("update_step(with_act=True) needs overlap_act=True")
-            if self.act_inline:
+            if self.fuse_act and self.batched_fwd:
+                native.check(k.st_deep_gather(self._gather_env, sh), "deep_gather(env)")
+                act = None                     # forward grouped with the update's below
+            elif self.act_inline:
                 self.act_step()                # same order, same stream
                 act = None
             else:
@@ -459,7 +472,10 @@ class DeepDQN:
                                          self.in_p, sh), "transpose X")
         acts = [self.X] + self.Act[1:]
         actsT = [self.XT] + self.ActT[1:]
-        if self.batched_fwd:
+        if self.batched_fwd and with_act and self.fuse_act:
+            self._forward_pair(acts, actsT, [self.Xn] + self.ActN[1:], [self.Xe] + self.Acte[1:])
+            native.check(k.st_deep_env_step(self._env, sh), "deep_env_step")
+        elif self.batched_fwd:
             self._forward_pair(acts, actsT, [self.Xn] + self.ActN[1:])
         elif side is not None:
             side.wait_stream(main)

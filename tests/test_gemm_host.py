@@ -35,8 +35,8 @@ def test_pick_splitk_fills_the_chip():
 def test_batched_and_dual_reject_bad_shapes_before_launch():
     A, B = _t(256, 128), _t(256, 128)
     ok = (A, B, _t(256, 256), {})
-    with pytest.raises(ValueError):   # second problem has another shape
-        gm.gemm_nt_batched([ok, (_t(256, 128), _t(512, 128), _t(256, 512), {})], gm.EPI_BF16, (128, 128))
+    with pytest.raises(ValueError):   # second problem not a multiple of the tile
+        gm.gemm_nt_batched([ok, (_t(192, 128), _t(256, 128), _t(192, 256), {})], gm.EPI_BF16, (128, 128))
     with pytest.raises(ValueError):   # more than GEMM_MAXB problems
         gm.gemm_nt_batched([ok] * (gm.GEMM_MAXB + 1), gm.EPI_BF16, (128, 128))
     with pytest.raises(ValueError):   # 64-row product on 128x128 tiles

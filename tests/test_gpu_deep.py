@@ -140,13 +140,15 @@ def test_graph_iteration_runs(native_built, dw_gemm, concurrent):
     assert all(torch.isfinite(w).all() for w in d.W)
 
 
-def test_overlapped_act_matches_same_order_serial(native_built):
-    """overlap_act: the act step on its own stream beside the update's GEMM chains (captured graph)
-    equals the same sequence run on one stream -- update gather, act step, rest of the update -- up to
-    fp32 atomic summation order: identical env state and replay contents, same weights within 1e-5."""
+@pytest.mark.parametrize("fuse", [False, True])
+def test_overlapped_act_matches_same_order_serial(native_built, fuse):
+    """overlap_act: the act step on its own stream beside the update's GEMM chains (captured graph) --
+    or, with fuse_act, its forward layers grouped into the update's forward launches -- equals the same
+    sequence run on one stream -- update gather, act step, rest of the update -- up to fp32 atomic
+    summation order: identical env state and replay contents, same weights within 1e-5."""
     res = []
     for serial in (False, True):
-        d = _dqn(dw_gemm="hipblaslt", overlap_act=True)
+        d = _dqn(dw_gemm="hipblaslt", overlap_act=True, fuse_act=fuse and not serial)
         for _ in range(6):
             d.act_step()
         if serial:

@@ -153,9 +153,26 @@ def test_gemm_batched_equals_single_launches(native_built, epi, tile, sk):
             assert torch.equal(o1, o2)
         if t1 is not None:
             assert torch.equal(t1, t2)
-    with pytest.raises(ValueError):
-        gemm_nt_batched([probs[0], (_bf((M, K), 1), _bf((2 * N, K), 2), torch.empty(M, 2 * N, dtype=o1.dtype,
-                                                                                   device="cuda"), {})], epi, tile)
+
+
+def test_gemm_grouped_mixed_shapes(native_built):
+    """gemm_nt_batched with different shapes per problem (grouped GEMM) == single launches."""
+    from sharetrade.ops.gemm import EPI_BF16, gemm_nt, gemm_nt_batched
+
+    shapes = [(1024, 256, 512), (256, 512, 128), (512, 128, 1024)]
+    probs, refs = [], []
+    for i, (M, N, K) in enumerate(shapes):
+        A, B = _bf((M, K), 50 + i), _bf((N, K), 60 + i)
+        bias = torch.randn(N, device="cuda")
+        r = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        gemm_nt(A, B, r, EPI_BF16, tile=(128, 128), bias=bias, relu=True)
+        o = torch.empty_like(r)
+        probs.append((A, B, o, dict(bias=bias, relu=True)))
+        refs.append(r)
+    gemm_nt_batched(probs, EPI_BF16, tile=(128, 128))
+    torch.cuda.synchronize()
+    for (_, _, o, _), r in zip(probs, refs):
+        assert torch.equal(o, r)
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 1024),
