@@ -539,6 +539,154 @@ static hipError_t launch_gemm_pp(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- 256x256, 4 waves of 128x128
+// One wave per SIMD, each with a 128x128 accumulator block (256 AGPRs) -- 4 MFMAs per fragment read
+// (the ping-pong kernel's 8 waves of 128x64 get 2.7) -- and two fragment register sets, so every
+// LDS read is issued a whole 64-MFMA k-step ahead of its use.  Per K-tile t (BK = 64, LDS buffer
+// t & 1, 2 x 64 KB):
+//   phase X(t): 64 MFMAs on F0 = k-step 0 of tile t;  read F1 = k-step 1 of tile t
+//   -- vmcnt(0) (tile t+1 landed) + lgkmcnt(0) + raw s_barrier --
+//   phase Y(t): stage tile t+2 into buffer t & 1 (its last reads, F1(t), retired before the barrier);
+//               64 MFMAs on F1;  read F0 = k-step 0 of tile t+1 (landed and visible since the barrier)
+// One barrier per K-tile; a tile is staged 2 phases (one K-tile) before the wait that retires it,
+// and no wave ever waits on an LDS read: the barrier is passed with X(t)'s MFMAs still in the pipe.
+namespace w4 {
+constexpr int NT = 256;
+constexpr int TILE = 256 * GBK;                         // one operand of one K-tile (elements)
+constexpr int BUF = 2 * TILE;                           // A + B
+constexpr int KLOOP_BYTES = 2 * BUF * 2;                // 128 KB
+constexpr int SC = 256 + 8;
+constexpr int EPI_BYTES = 256 * SC * 2;
+constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
+static_assert(LDS_BYTES <= 163840, "LDS");
+}  // namespace w4
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = p.N / 256, ntm = p.M / 256;
+  const int bid = xcd_remap(blockIdx.x, ntn * ntm);
+  const int m0 = (bid / ntn) * 256, n0 = (bid % ntn) * 256;
+  const int nk = p.K / GBK;
+
+  auto stage = [&](int kt) {   // both operands of K-tile kt (8 + 8 global_load_lds per thread)
+    if (kt < nk) {
+      bf16_t* b = buf + (kt & 1) * w4::BUF;
+      stage_tile<256, 4>(p.A, p.lda, m0, kt * GBK, b, wave, lane);
+      stage_tile<256, 4>(p.B, p.ldb, n0, kt * GBK, b + w4::TILE, wave, lane);
+    }
+  };
+  s8v F0a[8], F0b[8], F1a[8], F1b[8];
+  auto read = [&](s8v (&fa)[8], s8v (&fb)[8], int kt, int kk) {
+    const bf16_t* bA = buf + (kt & 1) * w4::BUF;
+    const bf16_t* bB = bA + w4::TILE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = frag_sw(bA, wr * 128 + 16 * i + l16, kk * 4 + g4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[j] = frag_sw(bB, wc * 128 + 16 * j + l16, kk * 4 + g4);
+  };
+  f4v acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = zero4();
+  auto mma = [&](const s8v (&fa)[8], const s8v (&fb)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+  };
+
+  // prologue: tiles 0 and 1 staged, tile 0 landed; F0 = k-step 0 of tile 0
+  stage(0);
+  stage(1);
+  if (nk > 1) pp::wait_vm_lgkm0<16>(); else pp::wait_vm_lgkm0<0>();
+  pp::barrier();
+  read(F0a, F0b, 0, 0);
+  for (int t = 0; t + 1 < nk; ++t) {   // (the last K-tile is peeled: no conditional fragment read in
+                                      // the loop, which made the allocator shuffle accumulators)
+    // ---- X(t)
+    read(F1a, F1b, t, 1);
+    mma(F0a, F0b);
+    pp::wait_vm_lgkm0<0>();          // tile t+1 landed (this wave's part); F1 read retired
+    pp::barrier();
+    // ---- Y(t)
+    stage(t + 2);
+    read(F0a, F0b, t + 1, 0);
+    mma(F1a, F1b);
+  }
+  read(F1a, F1b, nk - 1, 1);          // X(nk-1), Y(nk-1)
+  mma(F0a, F0b);
+  mma(F1a, F1b);
+  pp::wait_vm_lgkm0<0>();
+  pp::barrier();   // every wave is done with the K-loop buffers
+
+  // ------------------------------------------------------------------ epilogues
+  const int wm0 = wr * 128, wn0 = wc * 128;
+  float bj[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bj[j] = 0.f;
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bj[j] = p.bias[n0 + wn0 + 16 * j + l16];
+  }
+  if constexpr (EPI == EPI_F32) {
+    float* out = reinterpret_cast<float*>(p.out);
+    auto store = [&](auto accumulate) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = n0 + wn0 + 16 * j + l16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm0 + 16 * i + 4 * g4 + r;
+            float* o = out + (size_t)m * p.ldo + n;
+            const float v = p.alpha * acc[i][j][r] + bj[j];
+            if constexpr (decltype(accumulate)::value) *o += v; else *o = v;
+          }
+        }
+    };
+    if (p.accumulate) store(std::true_type{}); else store(std::false_type{});
+  } else {
+    bf16_t* sC = buf;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int nl = wn0 + 16 * j + l16, ml = wm0 + 16 * i + 4 * g4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = p.alpha * acc[i][j][r] + bj[j];
+          sC[(ml + r) * w4::SC + nl] = f2bf(p.relu ? fmaxf(x, 0.f) : x);
+        }
+      }
+    __syncthreads();
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+    for (int c = tid; c < 256 * 32; c += w4::NT) {
+      const int r = c >> 5, k = (c & 31) * 8;
+      *reinterpret_cast<uint4*>(out + (size_t)(m0 + r) * p.ldo + n0 + k) = *reinterpret_cast<const uint4*>(sC + r * w4::SC + k);
+    }
+  }
+}
+
+template <int EPI>
+static hipError_t launch_gemm_w4(const GemmArgs& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       w4::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3((p.M / 256) * (p.N / 256)), dim3(w4::NT), w4::LDS_BYTES, s, p);
+  return hipGetLastError();
+}
+
 }  // namespace st
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
@@ -605,6 +753,14 @@ extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::G
 }
 
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
+  if (tile == 9) {   // 256x256, 4 waves of 128x128 (bf16 / fp32 epilogues, no C^T, no split-K)
+    if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
+    if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)
+      return hipErrorInvalidValue;
+    if (epi == st::EPI_BF16) return st::launch_gemm_w4<st::EPI_BF16>(*p, stream);
+    if (epi == st::EPI_F32) return st::launch_gemm_w4<st::EPI_F32>(*p, stream);
+    return hipErrorInvalidValue;
+  }
   if (tile == 7 || tile == 8) {   // 256x256 ping-pong (8: with s_setprio); one product per launch,
                                  // bf16 / fp32 epilogues, no C^T, no split-K
     if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;

@@ -189,17 +189,20 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     ref = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     gemm_nt(A, B, ref, EPI_BF16, tile=(128, 128), bias=bias, relu=True)
     out = torch.empty_like(ref)
-    for _ in range(3):
-        out.fill_(7)
-        gemm_nt(A, B, out, EPI_BF16, tile=(256, 256, "pp"), bias=bias, relu=True)
-        torch.cuda.synchronize()
-        assert torch.equal(out, ref)
+    for t in ((256, 256, "pp"), (256, 256, "w4")):
+        for _ in range(3):
+            out.fill_(7)
+            gemm_nt(A, B, out, EPI_BF16, tile=t, bias=bias, relu=True)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), t
+    o32w = torch.full((M, N), float("nan"), device="cuda")
     r32 = torch.empty(M, N, device="cuda")
     gemm_nt(A, B, r32, EPI_F32, tile=(128, 128), bias=bias, alpha=0.5)
     o32 = torch.full((M, N), float("nan"), device="cuda")
     gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), bias=bias, alpha=0.5)
+    gemm_nt(A, B, o32w, EPI_F32, tile=(256, 256, "w4"), bias=bias, alpha=0.5)
     torch.cuda.synchronize()
-    assert torch.equal(o32, r32)
+    assert torch.equal(o32, r32) and torch.equal(o32w, r32)
     gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), alpha=0.5, accumulate=True)
     full = 0.5 * (A.float() @ B.float().t())
     torch.cuda.synchronize()
