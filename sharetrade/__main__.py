@@ -5,6 +5,8 @@ Commands
 ``train``   run the ShareTradeHelper application (`ShareTradeHelper.scala`):
             price service -> router -> workers -> learner; prints avg/std.
 ``engine``  run the vectorised engine directly for N steps and print metrics.
+``deep``    train the 4x1024-MLP replay DQN (BASELINE config 4) for N iterations.
+``recurrent`` train the GRU(256) minute-bar DQN (BASELINE config 5) for N iterations.
 ``config``  print the resolved configuration (JSON).
 
 Common flags: ``--preset {reference_compat,intended,flagship,test}``,
@@ -30,9 +32,9 @@ def _cfg(a) -> Config:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="sharetrade")
     sub = ap.add_subparsers(dest="cmd", required=True)
-    for name in ("train", "engine", "config"):
+    for name in ("train", "engine", "deep", "recurrent", "config"):
         p = sub.add_parser(name)
-        p.add_argument("--preset", default="reference_compat")
+        p.add_argument("--preset", default={"deep": "flagship", "recurrent": "recurrent"}.get(name, "reference_compat"))
         p.add_argument("--config", default=None)
         p.add_argument("--set", action="append", default=[])
         if name == "train":
@@ -50,6 +52,18 @@ def main(argv=None) -> int:
             p.add_argument("--resume", action="store_true")
             p.add_argument("--trace", default=None, help="Chrome trace output path (torch.profiler)")
             p.add_argument("--no-graph", action="store_true")
+        if name in ("deep", "recurrent"):
+            p.add_argument("--iterations", type=int, default=200)
+            p.add_argument("--envs", type=int, default=None)
+            p.add_argument("--batch", type=int, default=None)
+            if name == "deep":
+                p.add_argument("--hidden", default="1024,1024,1024,1024", help="hidden widths (config 4: 4x1024)")
+            p.add_argument("--metrics", default=None, help="JSONL metrics output path")
+            p.add_argument("--log-every", type=int, default=50)
+            p.add_argument("--ckpt-dir", default=None)
+            p.add_argument("--ckpt-every", type=int, default=0)
+            p.add_argument("--resume", action="store_true")
+            p.add_argument("--no-graph", action="store_true")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -63,6 +77,23 @@ def main(argv=None) -> int:
         res = run(cfg, engine=a.engine, device=a.device, max_prices=a.max_prices)
         print(json.dumps(res))
         return 0 if res.get("completed") else 1
+    if a.cmd in ("deep", "recurrent"):
+        import torch
+
+        from .trainer.runs import run as run_learner
+
+        kw = {}
+        if a.cmd == "deep":
+            kw["hidden"] = [int(x) for x in a.hidden.split(",")]
+        if a.envs:
+            kw["envs"] = a.envs
+        if a.batch:
+            kw["batch"] = a.batch
+        res = run_learner(a.cmd, cfg, a.iterations, device=torch.device("cuda", 0), metrics_path=a.metrics,
+                          log_every=a.log_every, ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume,
+                          graph=not a.no_graph, **kw)
+        print(json.dumps(res, default=float))
+        return 0
     if a.cmd == "engine":
         from .parallel import dist as D
         from .trainer.engine import resolve_device

@@ -537,6 +537,8 @@ class DeepDQN:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         self.env_steps += 1
         self.updates += 1
+        if self.target_every and self.updates % self.target_every == 0:   # as iteration()
+            self.sync_target()
         self._g_act = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_act):
             self.act_step()
@@ -574,6 +576,40 @@ class DeepDQN:
             self.updates += 1
             if self.target_every and self.updates % self.target_every == 0:
                 self.sync_target()
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    _ENV_KEYS = ("budget", "shares", "value", "pos", "episodes", "last_final", "env_ctrl", "rp_ctrl", "t_ctr",
+                 "stats", "loss")
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """Everything a resumed run needs to continue exactly (host copies): fp32 masters, Adam moments,
+        target net, update / env-step / sampling counters, env state and the whole replay ring.  The
+        price bank is not saved: it is regenerated from the config seed (or passed in again)."""
+        d: Dict[str, torch.Tensor] = {}
+        for l in range(self.L):
+            for name, lst in (("W", self.W), ("b", self.b), ("Wm", self.Wm), ("Wv", self.Wv), ("bm", self.bm),
+                              ("bv", self.bv), ("Wt", self.Wt), ("bt", self.bt)):
+                d[f"{name}{l}"] = lst[l].detach().cpu().clone()
+        for k in self._ENV_KEYS:
+            d[k] = getattr(self, k).detach().cpu().clone()
+        for k, t in self.rp.items():
+            d[f"rp_{k}"] = t.detach().cpu().clone()
+        d["counters"] = torch.tensor([self.updates, self.env_steps], dtype=torch.int64)
+        return d
+
+    def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
+        for l in range(self.L):
+            for name, lst in (("W", self.W), ("b", self.b), ("Wm", self.Wm), ("Wv", self.Wv), ("bm", self.bm),
+                              ("bv", self.bv), ("Wt", self.Wt), ("bt", self.bt)):
+                lst[l].copy_(d[f"{name}{l}"].to(lst[l].device))
+            # the bf16 operand copies are a rounding of the masters (what the Adam kernel writes)
+            self.Wb[l].copy_(self.W[l].to(torch.bfloat16))
+            self.WbT[l].copy_(self.W[l].t().contiguous().to(torch.bfloat16))
+        for k in self._ENV_KEYS:
+            getattr(self, k).copy_(d[k].to(self.dev))
+        for k, t in self.rp.items():
+            t.copy_(d[f"rp_{k}"].to(self.dev))
+        self.updates, self.env_steps = (int(x) for x in d["counters"].tolist())
 
     def stats_dict(self) -> Dict[str, float]:
         s = self.stats.cpu().tolist()

@@ -335,6 +335,8 @@ class RecurrentDQN:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         self.launches += 1
         self.updates += 1
+        if self.updates % self.target_every == 0:   # the warm-up is a full iteration (as iteration())
+            self.sync_target()
         self._g_act = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_act):
             self.act()
@@ -378,6 +380,25 @@ class RecurrentDQN:
             self.act_step()
         for _ in range(updates):
             self.update_step()
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    _STATE_KEYS = ("flat", "mflat", "vflat", "tflat", "opt_ctrl", "h", "pos", "ep_start", "position", "entry",
+                   "ep_ret", "episodes", "last_ret", "rx", "ra", "rr", "rd", "rh0", "rctrl", "ctrl", "stats", "loss")
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """Host copies of the parameters, Adam moments, target net, counters, env / recurrent state and
+        the replay ring; the minute bars are regenerated from the seed.  Packed (MX-fp8) weights are
+        derived and re-packed on load."""
+        d = {k: getattr(self, k).detach().cpu().clone() for k in self._STATE_KEYS}
+        d["counters"] = torch.tensor([self.updates, self.launches], dtype=torch.int64)
+        return d
+
+    def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
+        for k in self._STATE_KEYS:
+            getattr(self, k).copy_(d[k].to(self.dev))
+        self.updates, self.launches = (int(x) for x in d["counters"].tolist())
+        self.pack("on")
+        self.pack("tg")
 
     @property
     def env_steps(self) -> int:

@@ -1,0 +1,83 @@
+"""Training runs of the north-star learners (BASELINE configs 4 and 5) with the same run-level services
+as the vectorised engine (`trainer/loop.py`): JSONL metrics, periodic checkpoints with retention,
+bit-reproducible resume.
+
+* ``deep``      -- :class:`~sharetrade.trainer.deep.DeepDQN` (4x1024 MLP, 1M-transition HBM replay);
+* ``recurrent`` -- :class:`~sharetrade.trainer.recurrent.RecurrentDQN` (GRU(256), MX-fp8 actor).
+
+One *iteration* is what the benchmarks time: one act step (deep) or one actor launch of S bars
+(recurrent) plus one learner update, captured into HIP graphs after the first (eager) iteration.
+A checkpoint written after iteration k holds the learner's whole state (`state_dict`); resuming
+loads it and continues with iteration k+1.  The reference's `saveSnapshot` stub
+(`QDecisionPolicyActor.scala:91-93`) is the model for the interval semantics (every N, not at 0).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..config import Config
+from ..persist.checkpoint import CheckpointManager, load as load_ckpt
+from ..utils.metrics import MetricsLogger
+
+
+def build(kind: str, cfg: Config, device: torch.device, **kw):
+    if kind == "deep":
+        from .deep import DeepDQN
+
+        kw.setdefault("overlap_act", True)
+        return DeepDQN(cfg, device, **kw)
+    if kind == "recurrent":
+        from .recurrent import RecurrentDQN
+
+        kw.setdefault("overlap_act", True)
+        return RecurrentDQN(cfg, device, **kw)
+    raise ValueError(f"unknown learner {kind!r}")
+
+
+def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] = None,
+        metrics_path: Optional[str] = None, log_every: int = 50, ckpt_dir: Optional[str] = None,
+        ckpt_every: int = 0, resume: bool = False, graph: bool = True, learner=None,
+        **learner_kw) -> Dict[str, Any]:
+    """Run ``iterations`` act + update iterations (counting any restored ones); returns final stats."""
+    dev = device or torch.device("cuda", 0)
+    d = learner if learner is not None else build(kind, cfg, dev, **learner_kw)
+    mgr = CheckpointManager(ckpt_dir, interval=ckpt_every) if ckpt_dir else None
+    done = 0
+    if mgr is not None and resume and mgr.latest():
+        st, meta = load_ckpt(mgr.latest())
+        if meta.get("kind") != kind:
+            raise ValueError(f"checkpoint is a {meta.get('kind')!r} run, not {kind!r}")
+        d.load_state_dict(st)
+        done = int(meta["step"])
+    ml = MetricsLogger(metrics_path)
+    t0 = time.perf_counter()
+    last_t, last_i = t0, done
+
+    def one() -> None:
+        nonlocal done
+        if graph and getattr(d, "_g_iter", None) is None and getattr(d, "_g_upd", None) is None:
+            d.capture()                  # one eager warm-up iteration (counted), then the graphs
+        else:
+            d.iteration(1)
+        done += 1
+
+    while done < iterations:
+        one()
+        if mgr is not None and mgr.should_save(done):
+            torch.cuda.synchronize(dev)
+            mgr.save(done, d.state_dict(), {"kind": kind, "config": cfg.to_dict()})
+        if log_every and done % log_every == 0:
+            torch.cuda.synchronize(dev)
+            now = time.perf_counter()
+            s = d.stats_dict()
+            rec = dict(kind=kind, iteration=done, it_per_s=(done - last_i) / max(now - last_t, 1e-9), **s)
+            ml.log(rec)
+            last_t, last_i = now, done
+    torch.cuda.synchronize(dev)
+    out = dict(kind=kind, iterations=done, wall_s=time.perf_counter() - t0, **d.stats_dict())
+    ml.close()
+    return out
