@@ -312,6 +312,22 @@ __global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM,
   else gemm_body<BM, BN, EPI1, S>(a1, bid - n0, gsm);
 }
 
+template <int EPI0, int EPI1>
+static hipError_t launch_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  using G = GemmGeo<128, 128, 2>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_dual_kernel<128, 128, EPI0, EPI1, 2>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nwg = (a0.M / 128) * (a0.N / 128) * (a0.splitk > 1 ? a0.splitk : 1) +
+                  (a1.M / 128) * (a1.N / 128) * (a1.splitk > 1 ? a1.splitk : 1);
+  hipLaunchKernelGGL((gemm_dual_kernel<128, 128, EPI0, EPI1, 2>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, a0, a1);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int EPI, int S = 2>
 static hipError_t launch_gemm(const GemmBatch& p, hipStream_t s) {
   using G = GemmGeo<BM, BN, S>;
@@ -737,18 +753,9 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
 // f32 + f32, bf16 + f32)
 extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::GemmArgs* a1, int epi1, hipStream_t stream) {
   if (!gemm_args_ok(a0, epi0, 128, 128, true) || !gemm_args_ok(a1, epi1, 128, 128, true)) return hipErrorInvalidValue;
-  using G = st::GemmGeo<128, 128, 2>;
-  const int nwg = (a0->M / 128) * (a0->N / 128) * (a0->splitk > 1 ? a0->splitk : 1) +
-                  (a1->M / 128) * (a1->N / 128) * (a1->splitk > 1 ? a1->splitk : 1);
-  auto go = [&](auto kern) -> hipError_t {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(G::NT), G::LDS_BYTES, stream, *a0, *a1);
-    return hipGetLastError();
-  };
-  if (epi0 == st::EPI_RELU_GRAD && epi1 == st::EPI_F32) return go(st::gemm_dual_kernel<128, 128, 1, 2, 2>);
-  if (epi0 == st::EPI_F32 && epi1 == st::EPI_F32) return go(st::gemm_dual_kernel<128, 128, 2, 2, 2>);
-  if (epi0 == st::EPI_BF16 && epi1 == st::EPI_F32) return go(st::gemm_dual_kernel<128, 128, 0, 2, 2>);
+  if (epi0 == st::EPI_RELU_GRAD && epi1 == st::EPI_F32) return st::launch_dual<1, 2>(*a0, *a1, stream);
+  if (epi0 == st::EPI_F32 && epi1 == st::EPI_F32) return st::launch_dual<2, 2>(*a0, *a1, stream);
+  if (epi0 == st::EPI_BF16 && epi1 == st::EPI_F32) return st::launch_dual<0, 2>(*a0, *a1, stream);
   return hipErrorInvalidValue;
 }
 
