@@ -64,6 +64,7 @@ def main(argv=None) -> int:
             p.add_argument("--ckpt-every", type=int, default=0)
             p.add_argument("--resume", action="store_true")
             p.add_argument("--no-graph", action="store_true")
+            p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -89,10 +90,16 @@ def main(argv=None) -> int:
             kw["envs"] = a.envs
         if a.batch:
             kw["batch"] = a.batch
-        res = run_learner(a.cmd, cfg, a.iterations, device=torch.device("cuda", 0), metrics_path=a.metrics,
+        from .parallel import dist as D
+
+        # under torch.distributed.run: one rank per GPU, synchronous data parallel over RCCL
+        ctx = D.init(backend=a.dist_backend, device="cuda")
+        res = run_learner(a.cmd, cfg, a.iterations, device=ctx.device, metrics_path=a.metrics,
                           log_every=a.log_every, ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume,
-                          graph=not a.no_graph, **kw)
-        print(json.dumps(res, default=float))
+                          graph=not a.no_graph, ctx=ctx, **kw)
+        if ctx.is_main:
+            print(json.dumps(res, default=float))
+        D.shutdown(ctx)
         return 0
     if a.cmd == "engine":
         from .parallel import dist as D

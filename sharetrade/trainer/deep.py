@@ -111,7 +111,7 @@ class DeepDQN:
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
-                 fuse_act: bool = False):
+                 fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -148,6 +148,13 @@ class DeepDQN:
         # grouped forward launches (online x, target x', act states: three products per launch), its
         # env step follows on the same stream -- one stream, no fork / join, every launch fuller
         self.fuse_act = bool(fuse_act)
+        # data parallel (one process per GPU, trainer/runs.py): grad_sync(grad_flat) sums the weight and
+        # bias gradients (one flat buffer) over the ranks before Adam; the TD coefficient carries
+        # 1/world_size.  The fused Adam reduces the bias gradients itself, so DP uses the per-layer path.
+        self.world_size = int(world_size)
+        self.grad_sync = grad_sync
+        if self.world_size > 1 or grad_sync is not None:
+            self.fused_adam = False
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -191,14 +198,18 @@ class DeepDQN:
             self.WbT.append(self.W[l].t().contiguous().to(b16))
             self.Wt.append(self.Wb[l].clone())
             self.bt.append(self.b[l].clone())
-            self.db.append(torch.zeros(1, o, device=dev))
-        # weight gradients: views of one flat fp32 buffer (the replay gather zeroes the split-K span)
+        # weight + bias gradients: views of one flat fp32 buffer (dW first: the replay gather zeroes
+        # the split-K span; the whole buffer is the data-parallel all-reduce bucket)
         sizes = [self.pdims[l + 1] * self.pdims[l] for l in range(self.L)]
-        self._dW_flat = torch.zeros(sum(sizes), device=dev)
+        self.grad_flat = torch.zeros(sum(sizes) + sum(self.pdims[1:]), device=dev)
+        self._dW_flat = self.grad_flat[:sum(sizes)]
         off = 0
         for l in range(self.L):
             self.dW.append(self._dW_flat[off:off + sizes[l]].view(self.pdims[l + 1], self.pdims[l]))
             off += sizes[l]
+        for l in range(self.L):
+            self.db.append(self.grad_flat[off:off + self.pdims[l + 1]].view(1, self.pdims[l + 1]))
+            off += self.pdims[l + 1]
         self._dw_plan = []   # per layer: ("blaslt", None) or ("hip", (tile, splitk))
         for l in range(self.L):
             o, i = self.pdims[l + 1], self.pdims[l]
@@ -246,7 +257,7 @@ class DeepDQN:
             bank.copy_(prices)
             self.prices = bank
         else:
-            self.prices = make_price_bank(cfg, self.E, dev, seed=0)
+            self.prices = make_price_bank(cfg, self.E, dev, seed=int(bank_seed))
         if self.prices.shape[0] != self.E:
             raise ValueError("price bank rows != envs")
         self.T = int(self.prices.shape[1])
@@ -337,7 +348,7 @@ class DeepDQN:
                                             self.a_b.data_ptr(), self.d_b.data_ptr())
         td.dq, td.dqT, td.loss = self.G[-1].data_ptr(), self.GT[-1].data_ptr(), self.loss.data_ptr()
         td.B, td.ldq, td.n_actions = self.B, ACT_PAD, self.n_act
-        td.gamma, td.coef = float(cfg.agent.gamma), 2.0 / self.B
+        td.gamma, td.coef = float(cfg.agent.gamma), 2.0 / (self.B * self.world_size)
         td.t = self.t_ctr.data_ptr()   # the update counter advances in the TD kernel
         self._td = td
         a = cfg.agent
@@ -443,12 +454,13 @@ class DeepDQN:
             gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=tile, splitk=sk,
                        prezeroed=sk > 1)   # zeroed by this update's replay gather
 
-    def update_step(self, with_act: bool = False) -> None:
+    def update_step(self, with_act: bool = False, split: bool = False) -> None:
         """One DQN update: sample B transitions, Q(x) online / Q(x') target, TD, backward, Adam.
 
         With ``concurrent``: the target-network forward runs beside the online forward, and each
         layer's weight gradient beside the next data-backward GEMM, on a second stream (fork / join
-        with stream waits, so the whole update still captures into one HIP graph)."""
+        with stream waits, so the whole update still captures into one HIP graph).  ``split``: stop
+        before the gradient all-reduce and Adam (data-parallel capture, see capture())."""
         sh = native.stream_handle()
         k = self.k
         main = torch.cuda.current_stream(self.dev)
@@ -512,11 +524,30 @@ class DeepDQN:
             main.wait_stream(side)
         if act is not None:
             main.wait_stream(act)              # the act step's GEMMs read the pre-update weights
+        if split:
+            return
+        if self.grad_sync is not None:
+            self.grad_sync(self.grad_flat)
+        self._adam_step()
+
+    def _adam_step(self) -> None:
+        sh = native.stream_handle()
+        k = self.k
         if self.fused_adam:
             native.check(k.st_adam_multi(self._adam_multi, sh), "adam_multi")
         else:
             for ad in self._adam:
                 native.check(k.st_adam_tile(ad, sh), "adam")
+
+    def sync_params(self, ctx) -> None:
+        """Data-parallel start: every rank takes rank 0's parameters (online and target net)."""
+        from ..parallel.dist import broadcast_tensors
+
+        broadcast_tensors(ctx, list(self.W) + list(self.b))
+        for l in range(self.L):
+            self.Wb[l].copy_(self.W[l].to(torch.bfloat16))
+            self.WbT[l].copy_(self.W[l].t().contiguous().to(torch.bfloat16))
+        self.sync_target()
 
     def sync_target(self) -> None:
         for l in range(self.L):
@@ -542,18 +573,40 @@ class DeepDQN:
         self._g_act = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_act):
             self.act_step()
-        self._g_upd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_upd):
-            self.update_step()
-        self._g_iter = None
-        if self.overlap_act:
-            self._g_iter = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_iter):
-                self.update_step(with_act=True)
+        self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
+        if self.grad_sync is None:
+            self._g_upd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_upd):
+                self.update_step()
+            if self.overlap_act:
+                self._g_iter = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_iter):
+                    self.update_step(with_act=True)
+        else:
+            # data parallel: the gradient all-reduce runs between two graphs (act + gradients | Adam);
+            # the collective itself stays outside the capture
+            self._g_pre = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_pre):
+                self.update_step(split=True)
+            if self.overlap_act:
+                self._g_pre_act = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_pre_act):
+                    self.update_step(with_act=True, split=True)
+            self._g_post = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_post):
+                self._adam_step()
+        self._captured = True
+
+    def _replay_dp(self, with_act: bool) -> None:
+        (self._g_pre_act if with_act else self._g_pre).replay()
+        self.grad_sync(self.grad_flat)
+        self._g_post.replay()
 
     def iteration(self, updates_per_step: int = 1) -> None:
         if self.overlap_act and updates_per_step >= 1:
-            if getattr(self, "_g_iter", None) is not None:
+            if getattr(self, "_g_pre_act", None) is not None:
+                self._replay_dp(True)
+            elif getattr(self, "_g_iter", None) is not None:
                 self._g_iter.replay()
             else:
                 self.update_step(with_act=True)
@@ -569,7 +622,9 @@ class DeepDQN:
                 self.act_step()
             self.env_steps += 1
         for _ in range(updates_per_step):
-            if self._g_upd is not None:
+            if getattr(self, "_g_pre", None) is not None:
+                self._replay_dp(False)
+            elif self._g_upd is not None:
                 self._g_upd.replay()
             else:
                 self.update_step()

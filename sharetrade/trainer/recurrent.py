@@ -48,7 +48,7 @@ class RecurrentDQN:
                  replay_segments: int = 1 << 17, bars: int = 4096, ep_len: int = 390, burn_in: int = 4,
                  target_every: int = 100, cost: float = 0.01, lr: float = 3e-4, seed: Optional[int] = None,
                  bar_params: Optional[mb.BarParams] = None, actor_grid: int = 0, grad_sync=None,
-                 overlap_act: bool = False, actor_kernel: str = "auto"):
+                 overlap_act: bool = False, actor_kernel: str = "auto", world_size: int = 1):
         if device.type != "cuda":
             raise ValueError("RecurrentDQN runs on the GPU (MX-fp8 / bf16 MFMA kernels)")
         if envs % G.RN:
@@ -74,7 +74,11 @@ class RecurrentDQN:
         if actor_kernel == "pair" and self.S > smax:
             raise ValueError(f"the two-chunk actor needs seq <= {smax}")
         self.actor_kernel = ("pair" if self.S <= smax else "single") if actor_kernel == "auto" else actor_kernel
+        # data parallel (one process per GPU, trainer/runs.py): grad_sync(gflat) sums the gradient over
+        # the ranks between the weight-gradient GEMMs and Adam; the TD coefficient carries 1/world_size
+        # so the sum is the mean over the global batch (B x world_size segments)
         self.grad_sync = grad_sync
+        self.world_size = int(world_size)
         # overlap_act: one captured graph per iteration in which the update samples its segments first,
         # then the actor launch runs on a side stream beside the rest of the update (unroll, BPTT,
         # weight-gradient GEMMs, Adam); the MX-fp8 re-pack of the actor weights waits for it (the actor
@@ -234,7 +238,7 @@ class RecurrentDQN:
         td.Q, td.Qt, td.A, td.R, td.D = (self.Q.data_ptr(), self.Q_t.data_ptr(), self.A.data_ptr(), self.R.data_ptr(),
                                          self.D.data_ptr())
         td.dQ, td.loss, td.B, td.S, td.burn = self.dQ.data_ptr(), self.loss.data_ptr(), self.B, self.S, self.burn
-        td.gamma, td.coef = self.gamma, 2.0 / (self.B * (self.S - self.burn))
+        td.gamma, td.coef = self.gamma, 2.0 / (self.B * (self.S - self.burn) * self.world_size)
         self._td = td
         bw = G.SeqBwdArgs()
         bw.sv, bw.dQ, bw.D, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
@@ -283,6 +287,14 @@ class RecurrentDQN:
         """One learner update on B sampled segments: gather -> fused unroll of both nets (MX-fp8) ->
         TD -> fused BPTT (bf16) -> split-K weight-gradient GEMMs -> Adam -> repack the actor weights.
         ``with_act``: the actor launch runs on a side stream right after the gather (see overlap_act)."""
+        act = self._grads(with_act)
+        if self.grad_sync is not None:
+            self.grad_sync(self.gflat)
+        self._apply(act)
+
+    def _grads(self, with_act: bool = False, join: bool = False):
+        """Gather -> unroll -> TD -> BPTT -> weight gradients into ``gflat``.  Returns the actor's side
+        stream when it is still running (``join`` makes the main stream wait for it here instead)."""
         sh = native.stream_handle()
         k, kd = self.k, self.kd
         S, B = self.S, self.B
@@ -308,14 +320,29 @@ class RecurrentDQN:
         native.check(k.st_gru_grad_fixup(self.dWhh_ext.data_ptr(), HID + 64, self.dP["w_hh"].data_ptr(),
                                          self.dP["b_hh"].data_ptr(), self.dP["w_ih"].data_ptr(),
                                          self.dP["b_ih"].data_ptr(), sh), "grad fixup")
-        if self.grad_sync is not None:
-            self.grad_sync(self.gflat)
+        if act is not None and join:
+            main.wait_stream(act)
+            act = None
+        return act
+
+    def _apply(self, act=None) -> None:
+        """Adam on the (synchronised) gradient, then re-pack the actor's MX-fp8 weights."""
+        sh = native.stream_handle()
         nl = native.lib()
         native.check(nl.st_advance(self.opt_ctrl.data_ptr(), sh), "advance")
         native.check(nl.st_reduce_optim(self._opt, sh), "adam")
         if act is not None:
-            main.wait_stream(act)          # the actor reads the packed weights the re-pack overwrites
+            torch.cuda.current_stream(self.dev).wait_stream(act)   # the actor reads the packed weights
         self.pack("on")
+
+    def sync_params(self, ctx) -> None:
+        """Data-parallel start: every rank takes rank 0's parameters (online and target net)."""
+        from ..parallel.dist import broadcast_tensors
+
+        broadcast_tensors(ctx, [self.flat])
+        self.tflat.copy_(self.flat)
+        self.pack("on")
+        self.pack("tg")
 
     def sync_target(self) -> None:
         self.tflat.copy_(self.flat)
@@ -340,14 +367,34 @@ class RecurrentDQN:
         self._g_act = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_act):
             self.act()
-        self._g_upd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_upd):
-            self.update()
-        self._g_iter = None
-        if self.overlap_act:
-            self._g_iter = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_iter):
-                self.update(with_act=True)
+        self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
+        if self.grad_sync is None:
+            self._g_upd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_upd):
+                self.update()
+            if self.overlap_act:
+                self._g_iter = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_iter):
+                    self.update(with_act=True)
+        else:
+            # data parallel: the gradient all-reduce runs between two graphs (gradients | Adam + re-pack),
+            # the collective itself stays outside the capture; the actor joins at the end of the first
+            self._g_pre = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_pre):
+                self._grads()
+            if self.overlap_act:
+                self._g_pre_act = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_pre_act):
+                    self._grads(with_act=True, join=True)
+            self._g_post = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_post):
+                self._apply()
+        self._captured = True
+
+    def _replay_dp(self, with_act: bool) -> None:
+        (self._g_pre_act if with_act else self._g_pre).replay()
+        self.grad_sync(self.gflat)
+        self._g_post.replay()
 
     def act_step(self) -> None:
         if self._g_act is not None:
@@ -357,7 +404,9 @@ class RecurrentDQN:
         self.launches += 1
 
     def update_step(self) -> None:
-        if self._g_upd is not None:
+        if getattr(self, "_g_pre", None) is not None:
+            self._replay_dp(False)
+        elif self._g_upd is not None:
             self._g_upd.replay()
         else:
             self.update()
@@ -367,7 +416,9 @@ class RecurrentDQN:
 
     def iteration(self, updates: int = 1) -> None:
         if self.overlap_act and updates >= 1:
-            if getattr(self, "_g_iter", None) is not None:
+            if getattr(self, "_g_pre_act", None) is not None:
+                self._replay_dp(True)
+            elif getattr(self, "_g_iter", None) is not None:
                 self._g_iter.replay()
             else:
                 self.update(with_act=True)

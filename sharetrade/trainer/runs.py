@@ -10,6 +10,13 @@ One *iteration* is what the benchmarks time: one act step (deep) or one actor la
 A checkpoint written after iteration k holds the learner's whole state (`state_dict`); resuming
 loads it and continues with iteration k+1.  The reference's `saveSnapshot` stub
 (`QDecisionPolicyActor.scala:91-93`) is the model for the interval semantics (every N, not at 0).
+
+Data parallel (``ctx`` from :func:`sharetrade.parallel.dist.init`, one process per GPU under
+``torch.distributed.run``): every rank runs its own envs and replay (seed + rank), starts from rank 0's
+parameters, and sums its gradients with the others' (one flat bucket, RCCL all-reduce) before each Adam
+step, so the parameters stay identical on all ranks -- the reference's many workers feeding ONE shared
+policy (`TrainerRouterActor.scala`), with synchronous gradient averaging in place of the shared actor.
+Metrics come from rank 0 (its own envs); each rank checkpoints its own state under ``rank<r>/``.
 """
 from __future__ import annotations
 
@@ -40,11 +47,31 @@ def build(kind: str, cfg: Config, device: torch.device, **kw):
 
 def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] = None,
         metrics_path: Optional[str] = None, log_every: int = 50, ckpt_dir: Optional[str] = None,
-        ckpt_every: int = 0, resume: bool = False, graph: bool = True, learner=None,
-        **learner_kw) -> Dict[str, Any]:
+        ckpt_every: int = 0, resume: bool = False, graph: bool = True, learner=None, ctx=None,
+        bucket_mb: float = 64.0, **learner_kw) -> Dict[str, Any]:
     """Run ``iterations`` act + update iterations (counting any restored ones); returns final stats."""
-    dev = device or torch.device("cuda", 0)
+    dp = ctx is not None and ctx.is_distributed
+    dev = device or (ctx.device if ctx is not None else torch.device("cuda", 0))
+    if dp:
+        if learner is None:           # own envs / replay per rank; parameters come from rank 0
+            seed = learner_kw.pop("seed", None)
+            learner_kw["seed"] = (cfg.agent.seed if seed is None else int(seed)) + ctx.rank
+            learner_kw["world_size"] = ctx.world_size
+            if kind == "deep":
+                learner_kw.setdefault("bank_seed", ctx.rank)     # each rank its own price series
+        if ckpt_dir:
+            ckpt_dir = os.path.join(ckpt_dir, f"rank{ctx.rank}")
     d = learner if learner is not None else build(kind, cfg, dev, **learner_kw)
+    if dp:
+        if d.world_size != ctx.world_size:
+            raise ValueError(f"learner built for world_size={d.world_size}, the group has {ctx.world_size}")
+        from ..parallel.dist import GradSync
+
+        gflat = d.grad_flat if kind == "deep" else d.gflat
+        d.grad_sync = GradSync(ctx, gflat.numel(), bucket_mb=bucket_mb).all_reduce
+        d.sync_params(ctx)
+    if dp and not ctx.is_main:
+        metrics_path = None
     mgr = CheckpointManager(ckpt_dir, interval=ckpt_every) if ckpt_dir else None
     done = 0
     if mgr is not None and resume and mgr.latest():
@@ -59,7 +86,7 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
 
     def one() -> None:
         nonlocal done
-        if graph and getattr(d, "_g_iter", None) is None and getattr(d, "_g_upd", None) is None:
+        if graph and not getattr(d, "_captured", False):
             d.capture()                  # one eager warm-up iteration (counted), then the graphs
         else:
             d.iteration(1)
@@ -74,10 +101,12 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
             torch.cuda.synchronize(dev)
             now = time.perf_counter()
             s = d.stats_dict()
-            rec = dict(kind=kind, iteration=done, it_per_s=(done - last_i) / max(now - last_t, 1e-9), **s)
+            rec = dict(kind=kind, iteration=done, it_per_s=(done - last_i) / max(now - last_t, 1e-9),
+                       world_size=ctx.world_size if dp else 1, **s)
             ml.log(rec)
             last_t, last_i = now, done
     torch.cuda.synchronize(dev)
-    out = dict(kind=kind, iterations=done, wall_s=time.perf_counter() - t0, **d.stats_dict())
+    out = dict(kind=kind, iterations=done, wall_s=time.perf_counter() - t0, world_size=ctx.world_size if dp else 1,
+               **d.stats_dict())
     ml.close()
     return out

@@ -1,0 +1,130 @@
+"""Data parallelism of the config-4 / config-5 learners (sharetrade/trainer/runs.py ``ctx=``):
+
+* two ranks sharing cuda:0 over gloo (the box has one GPU; the 8-GPU run uses RCCL) run their own envs
+  and replay, start from rank 0's parameters and sum gradients before every Adam step -- after a few
+  captured iterations both ranks hold bit-identical parameters while their env state differs;
+* the DP capture (gradients graph | all-reduce | Adam graph) over a one-rank RCCL group with
+  world_size forced to 2 matches the eager DP iteration (counters and env state exact, weights up to
+  fp32 reduction order)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+_DEEP = dict(envs=256, batch=256, replay_capacity=4096, hidden=[256, 256], overlap_act=True, target_every=3)
+_REC = dict(envs=256, seq=8, batch=128, bars=600, ep_len=5, replay_segments=2048, burn_in=1, overlap_act=True,
+            target_every=3)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(kind):
+    from sharetrade.config import preset_config
+
+    return preset_config("flagship" if kind == "deep" else "recurrent")
+
+
+def _params(kind, st):
+    if kind == "recurrent":
+        return st["flat"]
+    return torch.cat([st[f"{n}{l}"].flatten() for l in range(3) for n in ("W", "b", "Wt", "bt")])
+
+
+def _gloo_worker(rank, world, port, kind, iters, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from sharetrade.parallel.dist import DistContext
+    from sharetrade.trainer.runs import run
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = DistContext(rank, world, 0, "gloo", dev, dist.group.WORLD)
+    kw = dict(_DEEP if kind == "deep" else _REC)
+    res = run(kind, _cfg(kind), iters, device=dev, ctx=ctx, ckpt_dir=out, ckpt_every=iters, log_every=0, **kw)
+    assert res["world_size"] == world and res["iterations"] == iters
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["deep", "recurrent"])
+def test_two_rank_dp_keeps_parameters_identical(native_built, kind):
+    from sharetrade.persist.checkpoint import CheckpointManager, load
+    from sharetrade.trainer.runs import build
+
+    iters, world = 7, 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_gloo_worker, args=(world, _port(), kind, iters, d), nprocs=world, join=True,
+                           start_method="spawn")
+        st = [load(CheckpointManager(os.path.join(d, f"rank{r}")).latest())[0] for r in range(world)]
+    p0, p1 = _params(kind, st[0]), _params(kind, st[1])
+    assert torch.isfinite(p0).all()
+    assert torch.equal(p0, p1)                       # one shared model
+    env_key = "pos" if kind == "recurrent" else "budget"
+    assert not torch.equal(st[0][env_key], st[1][env_key])      # each rank its own envs
+    # and the model trained away from rank 0's initial parameters
+    fresh = build(kind, _cfg(kind), torch.device("cuda", 0), **dict(_DEEP if kind == "deep" else _REC))
+    assert not torch.equal(_params(kind, {k: v.cpu() for k, v in fresh.state_dict().items()}), p0)
+
+
+def _rccl_worker(_rank, port, kind, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from sharetrade.parallel.dist import DistContext
+    from sharetrade.trainer.runs import run
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    ctx = DistContext(0, 2, 0, "nccl", dev, dist.group.WORLD)     # the DP code path over one rank
+    cfg = _cfg(kind)
+    cfg.agent.epsilon = 0.0
+    kw = dict(_DEEP if kind == "deep" else _REC)
+    if kind == "deep":
+        # bit-reproducible weight gradients (no split-K atomics), as in tests/test_gpu_runs.py
+        kw.update(dw_gemm="hipblaslt", concurrent=False, batched_fwd=False, dual_bwd=False)
+    res = {}
+    for graph in (False, True):
+        from sharetrade.trainer.runs import build
+
+        kw2 = dict(kw, world_size=2)
+        d = build(kind, cfg, dev, **kw2)
+        run(kind, cfg, 6, device=dev, ctx=ctx, learner=d, graph=graph, log_every=0)
+        assert (getattr(d, "_g_pre_act", None) is not None) == graph
+        torch.cuda.synchronize()
+        res[str(graph)] = {k: v for k, v in d.state_dict().items()}
+    torch.save(res, os.path.join(out, "cap.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["deep", "recurrent"])
+def test_dp_capture_matches_eager_over_rccl(native_built, kind):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rccl_worker, args=(_port(), kind, d), nprocs=1, join=True, start_method="spawn")
+        res = torch.load(os.path.join(d, "cap.pt"), weights_only=True)
+    e, g = res["False"], res["True"]
+    assert e.keys() == g.keys() and torch.equal(e["counters"], g["counters"])
+    # as tests/test_gpu_runs.py: weight-dependent values equal up to fp32 reduction order (float
+    # atomics), env / replay / counters exact (epsilon = 0: actions do not depend on Q)
+    approx = ("flat", "mflat", "vflat", "tflat", "h", "rh0", "loss", "stats") if kind == "recurrent" \
+        else ("loss", "stats")
+    for k in e:
+        x, y = e[k], g[k]
+        if k in approx or (kind == "deep" and k.rstrip("0123456789") in ("W", "b", "Wm", "Wv", "bm", "bv", "Wt", "bt")):
+            assert torch.allclose(x.float(), y.float(), rtol=1e-4, atol=1e-5), k
+        elif x.is_floating_point():
+            assert torch.equal(x.float().nan_to_num(-7.0), y.float().nan_to_num(-7.0)), k
+        else:
+            assert torch.equal(x, y), k
