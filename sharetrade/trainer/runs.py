@@ -31,6 +31,11 @@ from ..persist.checkpoint import CheckpointManager, load as load_ckpt
 from ..utils.metrics import MetricsLogger
 
 
+def _sync(dev: torch.device) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def build(kind: str, cfg: Config, device: torch.device, **kw):
     if kind == "deep":
         from .deep import DeepDQN
@@ -95,17 +100,17 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
     while done < iterations:
         one()
         if mgr is not None and mgr.should_save(done):
-            torch.cuda.synchronize(dev)
+            _sync(dev)
             mgr.save(done, d.state_dict(), {"kind": kind, "config": cfg.to_dict()})
         if log_every and done % log_every == 0:
-            torch.cuda.synchronize(dev)
+            _sync(dev)
             now = time.perf_counter()
             s = d.stats_dict()
             rec = dict(kind=kind, iteration=done, it_per_s=(done - last_i) / max(now - last_t, 1e-9),
                        world_size=ctx.world_size if dp else 1, **s)
             ml.log(rec)
             last_t, last_i = now, done
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     out = dict(kind=kind, iterations=done, wall_s=time.perf_counter() - t0, world_size=ctx.world_size if dp else 1,
                **d.stats_dict())
     ml.close()
