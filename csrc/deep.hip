@@ -356,7 +356,8 @@ struct AdamSeg {
   const float* mask;     // trainable mask (null = all trainable)
   bf16_t* wb;            // weights: bf16 copy [O][I]
   bf16_t* wbT;           // weights: bf16 transposed copy [I][O]
-  const bf16_t* gT;      // biases: layer gradient transposed [I][ldg] (bf16); row sums over nb columns
+  const bf16_t* gT;      // biases: layer gradient transposed [I][ldg] (bf16); row sums over nb columns --
+                         // or null: the bias gradient is already in g (data parallel: summed over ranks)
   int O, I;              // weights: [O][I]; biases: O = 1, I = n
   int ldg, nb;
   int bias;
@@ -368,6 +369,8 @@ struct AdamMulti {
   const unsigned long long* t;   // update counter, already advanced by deep_td (1-based t = *t)
   int total;
   float lr, beta1, beta2, eps;
+  int grads_only;        // bias segments only: write the reduced gradients to g, no update (data parallel:
+                         // the gradients are all-reduced, then a second launch with gT = null updates)
 };
 
 __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
@@ -392,7 +395,12 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
     }
     return w;
   };
-  if (S.bias) {
+  if (S.bias && !S.gT) {
+    if (threadIdx.x < 32) {
+      const int i = b * 32 + threadIdx.x;
+      if (i < S.I) upd((size_t)i, S.g[i]);
+    }
+  } else if (S.bias) {
     // 32 entries: wave w reduces rows 8w..8w+7 of gT (nb bf16 each, 16-byte loads)
     // (the 8 rows advance together: 8 independent 16-byte loads in flight per lane and step)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i0 = b * 32;
@@ -424,7 +432,7 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
       if (i < S.I) {
         const float g = red[threadIdx.x];
         S.g[i] = g;
-        upd((size_t)i, g);
+        if (!p.grads_only) upd((size_t)i, g);
       }
     }
   } else {
@@ -507,8 +515,9 @@ extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
   for (int i = 0; i < p->nseg; ++i) {
     const st::AdamSeg& g = p->seg[i];
     const int want = g.bias ? (g.I + 31) / 32 : ((g.I + 63) / 64) * ((g.O + 63) / 64);
-    if (g.blocks != want || (g.bias && (g.nb % 8 || g.ldg % 8 || !g.gT))) return hipErrorInvalidValue;
+    if (g.blocks != want || (g.bias && g.gT && (g.nb % 8 || g.ldg % 8))) return hipErrorInvalidValue;
     if (!g.bias && (g.I % 4 || g.O % 8)) return hipErrorInvalidValue;   // vector paths of the weight tiles
+    if (p->grads_only && !(g.bias && g.gT)) return hipErrorInvalidValue;
     total += g.blocks;
   }
   if (total != p->total) return hipErrorInvalidValue;

@@ -77,7 +77,7 @@ class _AdamSeg(C.Structure):
 
 class _AdamMulti(C.Structure):
     _fields_ = [("seg", _AdamSeg * ADAM_MAX_SEG), ("nseg", C.c_int), ("t", C.c_void_p), ("total", C.c_int), ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float),
-                ("eps", C.c_float)]
+                ("eps", C.c_float), ("grads_only", C.c_int)]
 
 
 def _bind():
@@ -150,11 +150,18 @@ class DeepDQN:
         self.fuse_act = bool(fuse_act)
         # data parallel (one process per GPU, trainer/runs.py): grad_sync(grad_flat) sums the weight and
         # bias gradients (one flat buffer) over the ranks before Adam; the TD coefficient carries
-        # 1/world_size.  The fused Adam reduces the bias gradients itself, so DP uses the per-layer path.
+        # 1/world_size.  The bias gradients then come from row-sum launches (all-reduced with the rest)
+        # and the fused Adam reads them instead of reducing the layer gradients itself.
         self.world_size = int(world_size)
         self.grad_sync = grad_sync
-        if self.world_size > 1 or grad_sync is not None:
-            self.fused_adam = False
+        # capture_sync: the backend's collectives can be captured (RCCL): the all-reduce stays inside the
+        # update graph; with layer_sync (callable issuing an all-reduce of one tensor on the current
+        # stream) each layer's dW / db is reduced on a comm stream as soon as the backward has produced
+        # it, overlapped with the rest of the backward; Adam waits for the comm stream
+        self.capture_sync = False
+        self.layer_sync = None
+        self._comm = torch.cuda.Stream(device=device)
+        self._bias_from_db = self.world_size > 1 or grad_sync is not None
         self.H = cfg.model.history
         self.in_real = self.H + 2
         self.in_p = 256
@@ -207,6 +214,7 @@ class DeepDQN:
         for l in range(self.L):
             self.dW.append(self._dW_flat[off:off + sizes[l]].view(self.pdims[l + 1], self.pdims[l]))
             off += sizes[l]
+        self._db_flat = self.grad_flat[off:]
         for l in range(self.L):
             self.db.append(self.grad_flat[off:off + self.pdims[l + 1]].view(1, self.pdims[l + 1]))
             off += self.pdims[l + 1]
@@ -378,13 +386,7 @@ class DeepDQN:
             w.wb, w.wbT, w.gT = self.Wb[l].data_ptr(), self.WbT[l].data_ptr(), None
             w.O, w.I, w.ldg, w.nb, w.bias = O, I, 0, 0, 0
             w.blocks = ((I + 63) // 64) * ((O + 63) // 64)
-            b = _AdamSeg()
-            b.w, b.g, b.m, b.v = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
-                                  self.bv[l].data_ptr())
-            b.mask = None if bool(self.bmask[l].bool().all()) else self.bmask[l].data_ptr()
-            b.wb, b.wbT, b.gT = None, None, self.GT[l].data_ptr()
-            b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
-            b.blocks = (O + 31) // 32
+            b = self._bias_seg(l, reduce=not self._bias_from_db)
             segs += [w, b]
         # bias segments first: their blocks (32 rows x batch of gradient sums each) are the longest,
         # started first they do not form the tail
@@ -399,6 +401,30 @@ class DeepDQN:
             am.lr, am.beta1, am.beta2, am.eps = (float(a.lr), float(a.adam_betas[0]), float(a.adam_betas[1]),
                                                  float(a.adam_eps))
         self._adam_multi = am
+        # data parallel + fused Adam: every layer's bias gradient in ONE launch after the backward (the
+        # multi-tensor kernel's reduction, no update), all-reduced, then read by the fused Adam
+        self._bias_multi = None
+        if self._bias_from_db and self.fused_adam:
+            bm = _AdamMulti()
+            for l in range(self.L):
+                bm.seg[l] = self._bias_seg(l, reduce=True)
+            bm.nseg, bm.t, bm.grads_only = self.L, self.t_ctr.data_ptr(), 1
+            bm.total = sum(bm.seg[l].blocks for l in range(self.L))
+            bm.lr, bm.beta1, bm.beta2, bm.eps = am.lr, am.beta1, am.beta2, am.eps
+            self._bias_multi = bm
+
+    def _bias_seg(self, l: int, reduce: bool) -> _AdamSeg:
+        """Multi-tensor Adam segment of bias l: ``reduce`` = its gradient is the row sums of GT[l] (reduced
+        in the kernel), else it is read from db[l]."""
+        O = self.pdims[l + 1]
+        b = _AdamSeg()
+        b.w, b.g, b.m, b.v = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
+                              self.bv[l].data_ptr())
+        b.mask = None if bool(self.bmask[l].bool().all()) else self.bmask[l].data_ptr()
+        b.wb, b.wbT, b.gT = None, None, self.GT[l].data_ptr() if reduce else None
+        b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
+        b.blocks = (O + 31) // 32
+        return b
 
     def _bscratch(self, l: int) -> torch.Tensor:
         if not hasattr(self, "_bias_bf"):
@@ -516,18 +542,36 @@ class DeepDQN:
             if not self.fused_adam:
                 native.check(k.st_row_sum_bf16(self.GT[l].data_ptr(), self.B, self.pdims[l + 1], self.B,
                                                self.db[l].data_ptr(), sh), "bias grad")
+            if self.layer_sync is not None and not split:
+                comm = self._comm
+                comm.wait_stream(main)
+                if side is not None and not self.dual_bwd:
+                    comm.wait_stream(side)        # dW_l came from the side stream
+                with torch.cuda.stream(comm):
+                    self.layer_sync(self.dW[l])
+                    if self._bias_multi is None:
+                        self.layer_sync(self.db[l])
             if l > 0 and not self._dual[l]:
                 # G_{l-1} = (G_l . W_l) * (A_l > 0)
                 gm.gemm_nt(self.G[l], self.WbT[l], self.G[l - 1], gm.EPI_RELU_GRAD, outT=self.GT[l - 1],
                            auxT=actsT[l])
+        if self._bias_multi is not None:
+            # every bias gradient in one launch, ahead of the joins (the act step may still be running)
+            native.check(k.st_adam_multi(self._bias_multi, sh), "bias grads")
+            if self.layer_sync is not None and not split:
+                self._comm.wait_stream(main)
+                with torch.cuda.stream(self._comm):
+                    self.layer_sync(self._db_flat)
         if side is not None and not self.dual_bwd:
             main.wait_stream(side)
+        if not split and self.layer_sync is None and self.grad_sync is not None:
+            self.grad_sync(self.grad_flat)     # one flat all-reduce, beside a still-running act step
         if act is not None:
             main.wait_stream(act)              # the act step's GEMMs read the pre-update weights
         if split:
             return
-        if self.grad_sync is not None:
-            self.grad_sync(self.grad_flat)
+        if self.layer_sync is not None:
+            main.wait_stream(self._comm)
         self._adam_step()
 
     def _adam_step(self) -> None:
@@ -574,7 +618,7 @@ class DeepDQN:
         with torch.cuda.graph(self._g_act):
             self.act_step()
         self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
-        if self.grad_sync is None:
+        if self.grad_sync is None or self.capture_sync:
             self._g_upd = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_upd):
                 self.update_step()

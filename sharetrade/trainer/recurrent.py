@@ -79,6 +79,9 @@ class RecurrentDQN:
         # so the sum is the mean over the global batch (B x world_size segments)
         self.grad_sync = grad_sync
         self.world_size = int(world_size)
+        # capture_sync: the backend's collectives can be captured (RCCL): the all-reduce stays inside the
+        # update graph, on the main stream while the overlapped actor still runs on its side stream
+        self.capture_sync = False
         # overlap_act: one captured graph per iteration in which the update samples its segments first,
         # then the actor launch runs on a side stream beside the rest of the update (unroll, BPTT,
         # weight-gradient GEMMs, Adam); the MX-fp8 re-pack of the actor weights waits for it (the actor
@@ -368,7 +371,7 @@ class RecurrentDQN:
         with torch.cuda.graph(self._g_act):
             self.act()
         self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
-        if self.grad_sync is None:
+        if self.grad_sync is None or self.capture_sync:
             self._g_upd = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_upd):
                 self.update()

@@ -53,7 +53,8 @@ def build(kind: str, cfg: Config, device: torch.device, **kw):
 def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] = None,
         metrics_path: Optional[str] = None, log_every: int = 50, ckpt_dir: Optional[str] = None,
         ckpt_every: int = 0, resume: bool = False, graph: bool = True, learner=None, ctx=None,
-        bucket_mb: float = 64.0, **learner_kw) -> Dict[str, Any]:
+        bucket_mb: float = 64.0, capture_sync: bool = True, layer_overlap: bool = True,
+        **learner_kw) -> Dict[str, Any]:
     """Run ``iterations`` act + update iterations (counting any restored ones); returns final stats."""
     dp = ctx is not None and ctx.is_distributed
     dev = device or (ctx.device if ctx is not None else torch.device("cuda", 0))
@@ -74,6 +75,14 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
 
         gflat = d.grad_flat if kind == "deep" else d.gflat
         d.grad_sync = GradSync(ctx, gflat.numel(), bucket_mb=bucket_mb).all_reduce
+        if ctx.backend == "nccl" and capture_sync:
+            # RCCL collectives capture into HIP graphs: keep the all-reduce inside the update graph
+            # (config 4: per layer on a comm stream, overlapped with the rest of the backward)
+            import torch.distributed as dist
+
+            d.capture_sync = True
+            if kind == "deep" and layer_overlap:
+                d.layer_sync = lambda t: dist.all_reduce(t, group=ctx.group)
         d.sync_params(ctx)
     if dp and not ctx.is_main:
         metrics_path = None

@@ -43,13 +43,18 @@ def test_replay_ring_and_env_step(native_built):
     assert int(d.rp_ctrl[1]) == d.cap and int(d.rp["pos"][0]) == 16
 
 
-@pytest.mark.parametrize("dw_gemm,concurrent,fused,batched,dual", [("hip", True, True, True, True),
-                                                                    ("hipblaslt", True, True, True, False),
-                                                                    ("hip", False, False, False, False),
-                                                                    ("hipblaslt", False, True, True, True),
-                                                                    ("hipblaslt", True, True, False, False)])
-def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused, batched, dual):
+@pytest.mark.parametrize("dw_gemm,concurrent,fused,batched,dual,dp", [("hip", True, True, True, True, False),
+                                                                       ("hipblaslt", True, True, True, False, False),
+                                                                       ("hip", False, False, False, False, False),
+                                                                       ("hipblaslt", False, True, True, True, False),
+                                                                       ("hipblaslt", True, True, False, False, False),
+                                                                       ("hip", True, True, True, True, True)])
+def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused, batched, dual, dp):
     kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused, batched_fwd=batched, dual_bwd=dual)
+    if dp:
+        # the data-parallel gradient path on one rank: bias gradients from row-sum launches into the flat
+        # all-reduce bucket, the fused Adam reading them (the sync hook is the identity here)
+        kw["grad_sync"] = lambda g: None
     d = _dqn(**kw)
     for _ in range(8):
         d.act_step()

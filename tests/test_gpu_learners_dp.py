@@ -3,9 +3,10 @@
 * two ranks sharing cuda:0 over gloo (the box has one GPU; the 8-GPU run uses RCCL) run their own envs
   and replay, start from rank 0's parameters and sum gradients before every Adam step -- after a few
   captured iterations both ranks hold bit-identical parameters while their env state differs;
-* the DP capture (gradients graph | all-reduce | Adam graph) over a one-rank RCCL group with
-  world_size forced to 2 matches the eager DP iteration (counters and env state exact, weights up to
-  fp32 reduction order)."""
+* over a one-rank RCCL group with world_size forced to 2, both captured DP forms -- the all-reduce
+  between two graphs (gradients | Adam), and the all-reduce inside the update graph (config 4: per
+  layer on a comm stream beside the backward) -- match the eager DP iteration (counters and env state
+  exact, weights up to fp32 reduction order)."""
 import os
 import socket
 import tempfile
@@ -78,12 +79,12 @@ def test_two_rank_dp_keeps_parameters_identical(native_built, kind):
     assert not torch.equal(_params(kind, {k: v.cpu() for k, v in fresh.state_dict().items()}), p0)
 
 
-def _rccl_worker(_rank, port, kind, out):
+def _rccl_worker(_rank, port, kind, fast, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
     from sharetrade.parallel.dist import DistContext
-    from sharetrade.trainer.runs import run
+    from sharetrade.trainer.runs import build, run
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -91,40 +92,44 @@ def _rccl_worker(_rank, port, kind, out):
     ctx = DistContext(0, 2, 0, "nccl", dev, dist.group.WORLD)     # the DP code path over one rank
     cfg = _cfg(kind)
     cfg.agent.epsilon = 0.0
-    kw = dict(_DEEP if kind == "deep" else _REC)
-    if kind == "deep":
+    kw = dict(_DEEP if kind == "deep" else _REC, world_size=2)
+    if kind == "deep" and not fast:
         # bit-reproducible weight gradients (no split-K atomics), as in tests/test_gpu_runs.py
         kw.update(dw_gemm="hipblaslt", concurrent=False, batched_fwd=False, dual_bwd=False)
     res = {}
-    for graph in (False, True):
-        from sharetrade.trainer.runs import build
-
-        kw2 = dict(kw, world_size=2)
-        d = build(kind, cfg, dev, **kw2)
-        run(kind, cfg, 6, device=dev, ctx=ctx, learner=d, graph=graph, log_every=0)
-        assert (getattr(d, "_g_pre_act", None) is not None) == graph
+    # eager; captured with the all-reduce between two graphs; captured with the all-reduce inside the
+    # update graph (config 4: per layer on a comm stream)
+    for mode, graph, cap in (("eager", False, True), ("split", True, False), ("ingraph", True, True)):
+        d = build(kind, cfg, dev, **kw)
+        run(kind, cfg, 6, device=dev, ctx=ctx, learner=d, graph=graph, capture_sync=cap, log_every=0)
+        if graph:
+            assert (d._g_pre_act is not None) == (not cap) and (d._g_iter is not None) == cap
+            assert (getattr(d, "layer_sync", None) is not None) == (cap and kind == "deep")
         torch.cuda.synchronize()
-        res[str(graph)] = {k: v for k, v in d.state_dict().items()}
+        res[mode] = d.state_dict()
     torch.save(res, os.path.join(out, "cap.pt"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["deep", "recurrent"])
-def test_dp_capture_matches_eager_over_rccl(native_built, kind):
+@pytest.mark.parametrize("kind,fast", [("deep", False), ("deep", True), ("recurrent", True)])
+def test_dp_capture_matches_eager_over_rccl(native_built, kind, fast):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rccl_worker, args=(_port(), kind, d), nprocs=1, join=True, start_method="spawn")
+        mp.start_processes(_rccl_worker, args=(_port(), kind, fast, d), nprocs=1, join=True, start_method="spawn")
         res = torch.load(os.path.join(d, "cap.pt"), weights_only=True)
-    e, g = res["False"], res["True"]
-    assert e.keys() == g.keys() and torch.equal(e["counters"], g["counters"])
     # as tests/test_gpu_runs.py: weight-dependent values equal up to fp32 reduction order (float
     # atomics), env / replay / counters exact (epsilon = 0: actions do not depend on Q)
     approx = ("flat", "mflat", "vflat", "tflat", "h", "rh0", "loss", "stats") if kind == "recurrent" \
         else ("loss", "stats")
-    for k in e:
-        x, y = e[k], g[k]
-        if k in approx or (kind == "deep" and k.rstrip("0123456789") in ("W", "b", "Wm", "Wv", "bm", "bv", "Wt", "bt")):
-            assert torch.allclose(x.float(), y.float(), rtol=1e-4, atol=1e-5), k
-        elif x.is_floating_point():
-            assert torch.equal(x.float().nan_to_num(-7.0), y.float().nan_to_num(-7.0)), k
-        else:
-            assert torch.equal(x, y), k
+    e = res["eager"]
+    for mode in ("split", "ingraph"):
+        g = res[mode]
+        assert e.keys() == g.keys() and torch.equal(e["counters"], g["counters"])
+        for k in e:
+            x, y = e[k], g[k]
+            if k in approx or (kind == "deep" and k.rstrip("0123456789") in ("W", "b", "Wm", "Wv", "bm", "bv", "Wt",
+                                                                              "bt")):
+                assert torch.allclose(x.float(), y.float(), rtol=1e-4, atol=1e-5), (mode, k)
+            elif x.is_floating_point():
+                assert torch.equal(x.float().nan_to_num(-7.0), y.float().nan_to_num(-7.0)), (mode, k)
+            else:
+                assert torch.equal(x, y), (mode, k)
