@@ -566,6 +566,9 @@ static hipError_t launch_gemm_pp(const GemmArgs& p, hipStream_t s) {
 //               64 MFMAs on F1;  read F0 = k-step 0 of tile t+1 (landed and visible since the barrier)
 // One barrier per K-tile; a tile is staged 2 phases (one K-tile) before the wait that retires it,
 // and no wave ever waits on an LDS read: the barrier is passed with X(t)'s MFMAs still in the pipe.
+#ifndef ST_W4_ASM
+#define ST_W4_ASM 1
+#endif
 namespace w4 {
 constexpr int NT = 256;
 constexpr int TILE = 256 * GBK;                         // one operand of one K-tile (elements)
@@ -614,7 +617,15 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+      for (int j = 0; j < 8; ++j) {
+#if ST_W4_ASM
+        // accumulators pinned to AGPRs ("+a"): the builtin left the allocator free to move them
+        // between the VGPR and AGPR files (~940 v_accvgpr_* per kernel)
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[j]));
+#else
+        acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+#endif
+      }
   };
 
   // prologue: tiles 0 and 1 staged, tile 0 landed; F0 = k-step 0 of tile 0
@@ -638,6 +649,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p) {
   read(F1a, F1b, nk - 1, 1);          // X(nk-1), Y(nk-1)
   mma(F0a, F0b);
   mma(F1a, F1b);
+#if ST_W4_ASM
+  // the hazard recognizer does not see through the asm MFMAs: cover the last MFMA's result latency
+  // before the epilogue's accumulator reads
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+#endif
   pp::wait_vm_lgkm0<0>();
   pp::barrier();   // every wave is done with the K-loop buffers
 
