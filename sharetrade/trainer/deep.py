@@ -30,6 +30,12 @@ from ..utils import rng
 ACT_PAD = 64  # output layer rows padded to a GEMM tile
 
 
+# HIP-graph capture mode: "thread_local" -- with an RCCL process group alive, its watchdog thread
+# polls collective events during our captures; in the default global mode that poll invalidates the
+# capture (hipErrorStreamCaptureInvalidated) and kills the watchdog.  Our own thread stays checked.
+_CAPTURE_MODE = "thread_local"
+
+
 class _Replay(C.Structure):
     _fields_ = [("env", C.c_void_p), ("pos", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p),
                 ("action", C.c_void_p), ("reward", C.c_void_p), ("budget2", C.c_void_p), ("shares2", C.c_void_p),
@@ -615,29 +621,29 @@ class DeepDQN:
         if self.target_every and self.updates % self.target_every == 0:   # as iteration()
             self.sync_target()
         self._g_act = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_act):
+        with torch.cuda.graph(self._g_act, capture_error_mode=_CAPTURE_MODE):
             self.act_step()
         self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
         if self.grad_sync is None or self.capture_sync:
             self._g_upd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_upd):
+            with torch.cuda.graph(self._g_upd, capture_error_mode=_CAPTURE_MODE):
                 self.update_step()
             if self.overlap_act:
                 self._g_iter = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_iter):
+                with torch.cuda.graph(self._g_iter, capture_error_mode=_CAPTURE_MODE):
                     self.update_step(with_act=True)
         else:
             # data parallel: the gradient all-reduce runs between two graphs (act + gradients | Adam);
             # the collective itself stays outside the capture
             self._g_pre = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_pre):
+            with torch.cuda.graph(self._g_pre, capture_error_mode=_CAPTURE_MODE):
                 self.update_step(split=True)
             if self.overlap_act:
                 self._g_pre_act = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_pre_act):
+                with torch.cuda.graph(self._g_pre_act, capture_error_mode=_CAPTURE_MODE):
                     self.update_step(with_act=True, split=True)
             self._g_post = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_post):
+            with torch.cuda.graph(self._g_post, capture_error_mode=_CAPTURE_MODE):
                 self._adam_step()
         self._captured = True
 

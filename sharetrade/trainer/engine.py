@@ -40,6 +40,12 @@ STAT_NAMES = ("reward_sum", "loss_sum", "explore", "episodes_done", "final_sum",
 OPT_KIND = {"sgd": 0, "adagrad": 1, "adam": 2}
 
 
+# HIP-graph capture mode: "thread_local" -- with an RCCL process group alive, its watchdog thread
+# polls collective events during our captures; in the default global mode that poll invalidates the
+# capture (hipErrorStreamCaptureInvalidated) and kills the watchdog.  Our own thread stays checked.
+_CAPTURE_MODE = "thread_local"
+
+
 def resolve_device(spec: str) -> torch.device:
     if spec == "auto":
         return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
@@ -480,14 +486,14 @@ class VectorEngine:
                 self.step_count += 1
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
             self._native_step()
         self._graph = g
         k = int(self.cfg.engine.graph_steps if graph_steps is None else graph_steps)
         self._graph_k = None
         if k > 1:
             gk = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gk):
+            with torch.cuda.graph(gk, capture_error_mode=_CAPTURE_MODE):
                 for _ in range(k):
                     self._native_step()
             self._graph_k = (gk, k)

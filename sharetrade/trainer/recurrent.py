@@ -41,6 +41,12 @@ from .deep import _bind as _bind_deep
 HID, GATES, XA, XL = G.HID, G.GATES, G.XA, G.XL
 
 
+# HIP-graph capture mode: "thread_local" -- with an RCCL process group alive, its watchdog thread
+# polls collective events during our captures; in the default global mode that poll invalidates the
+# capture (hipErrorStreamCaptureInvalidated) and kills the watchdog.  Our own thread stays checked.
+_CAPTURE_MODE = "thread_local"
+
+
 class RecurrentDQN:
     """E minute-bar envs + segment replay + GRU(256) learner on one GPU."""
 
@@ -368,29 +374,29 @@ class RecurrentDQN:
         if self.updates % self.target_every == 0:   # the warm-up is a full iteration (as iteration())
             self.sync_target()
         self._g_act = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_act):
+        with torch.cuda.graph(self._g_act, capture_error_mode=_CAPTURE_MODE):
             self.act()
         self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
         if self.grad_sync is None or self.capture_sync:
             self._g_upd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_upd):
+            with torch.cuda.graph(self._g_upd, capture_error_mode=_CAPTURE_MODE):
                 self.update()
             if self.overlap_act:
                 self._g_iter = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_iter):
+                with torch.cuda.graph(self._g_iter, capture_error_mode=_CAPTURE_MODE):
                     self.update(with_act=True)
         else:
             # data parallel: the gradient all-reduce runs between two graphs (gradients | Adam + re-pack),
             # the collective itself stays outside the capture; the actor joins at the end of the first
             self._g_pre = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_pre):
+            with torch.cuda.graph(self._g_pre, capture_error_mode=_CAPTURE_MODE):
                 self._grads()
             if self.overlap_act:
                 self._g_pre_act = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_pre_act):
+                with torch.cuda.graph(self._g_pre_act, capture_error_mode=_CAPTURE_MODE):
                     self._grads(with_act=True, join=True)
             self._g_post = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_post):
+            with torch.cuda.graph(self._g_post, capture_error_mode=_CAPTURE_MODE):
                 self._apply()
         self._captured = True
 

@@ -42,7 +42,7 @@ def _params(kind, st):
     return torch.cat([st[f"{n}{l}"].flatten() for l in range(3) for n in ("W", "b", "Wt", "bt")])
 
 
-def _gloo_worker(rank, world, port, kind, iters, out):
+def _gloo_worker(rank, world, port, kind, iters, out, ckpt_every=None, resume=False, eps0=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -54,7 +54,11 @@ def _gloo_worker(rank, world, port, kind, iters, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = DistContext(rank, world, 0, "gloo", dev, dist.group.WORLD)
     kw = dict(_DEEP if kind == "deep" else _REC)
-    res = run(kind, _cfg(kind), iters, device=dev, ctx=ctx, ckpt_dir=out, ckpt_every=iters, log_every=0, **kw)
+    cfg = _cfg(kind)
+    if eps0:
+        cfg.agent.epsilon = 0.0      # actions from the Philox draws only: trajectories do not depend on Q
+    res = run(kind, cfg, iters, device=dev, ctx=ctx, ckpt_dir=out, ckpt_every=ckpt_every or iters,
+              resume=resume, log_every=0, **kw)
     assert res["world_size"] == world and res["iterations"] == iters
     dist.destroy_process_group()
 
@@ -77,6 +81,39 @@ def test_two_rank_dp_keeps_parameters_identical(native_built, kind):
     # and the model trained away from rank 0's initial parameters
     fresh = build(kind, _cfg(kind), torch.device("cuda", 0), **dict(_DEEP if kind == "deep" else _REC))
     assert not torch.equal(_params(kind, {k: v.cpu() for k, v in fresh.state_dict().items()}), p0)
+
+
+@pytest.mark.parametrize("kind", ["deep", "recurrent"])
+def test_two_rank_dp_resume_continues_the_run(native_built, kind):
+    """Per-rank checkpoints: a 2-rank run stopped after iteration 4 and resumed to 7 ends where the
+    uninterrupted 7-iteration run ends (env state / counters exact, weights up to fp32 reduction order)."""
+    import shutil
+
+    from sharetrade.persist.checkpoint import CheckpointManager, load
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        a, b = os.path.join(d, "a"), os.path.join(d, "b")
+        mp.start_processes(_gloo_worker, args=(world, _port(), kind, 7, a, 7, False, True), nprocs=world, join=True,
+                           start_method="spawn")
+        mp.start_processes(_gloo_worker, args=(world, _port(), kind, 4, b, 4, False, True), nprocs=world, join=True,
+                           start_method="spawn")
+        for r in range(world):     # keep only the iteration-4 checkpoints, then resume to 7
+            mgr = CheckpointManager(os.path.join(b, f"rank{r}"))
+            assert [os.path.basename(p) for p in mgr.list()] == ["ckpt-000000000004.stck"]
+        mp.start_processes(_gloo_worker, args=(world, _port(), kind, 7, b, 7, True, True), nprocs=world, join=True,
+                           start_method="spawn")
+        for r in range(world):
+            sa = load(CheckpointManager(os.path.join(a, f"rank{r}")).latest())[0]
+            sb = load(CheckpointManager(os.path.join(b, f"rank{r}")).latest())[0]
+            assert torch.equal(sa["counters"], sb["counters"])
+            env_keys = ("pos", "ep_start", "rctrl", "position") if kind == "recurrent" else \
+                ("rp_ctrl", "env_ctrl", "t_ctr", "budget", "shares")
+            for k in env_keys:
+                assert torch.equal(sa[k], sb[k]), (r, k)
+            pa, pb = _params(kind, sa).float(), _params(kind, sb).float()
+            assert torch.allclose(pa, pb, rtol=1e-3, atol=1e-5), (r, float((pa - pb).abs().max()))
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def _rccl_worker(_rank, port, kind, fast, out):
