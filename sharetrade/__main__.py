@@ -65,6 +65,7 @@ def main(argv=None) -> int:
             p.add_argument("--resume", action="store_true")
             p.add_argument("--no-graph", action="store_true")
             p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
+            p.add_argument("--trace", default=None, help="Chrome trace output path (torch.profiler)")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -96,7 +97,7 @@ def main(argv=None) -> int:
         ctx = D.init(backend=a.dist_backend, device="cuda")
         res = run_learner(a.cmd, cfg, a.iterations, device=ctx.device, metrics_path=a.metrics,
                           log_every=a.log_every, ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume,
-                          graph=not a.no_graph, ctx=ctx, **kw)
+                          graph=not a.no_graph, ctx=ctx, trace_path=a.trace, **kw)
         if ctx.is_main:
             print(json.dumps(res, default=float))
         D.shutdown(ctx)

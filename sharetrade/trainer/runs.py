@@ -54,7 +54,7 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
         metrics_path: Optional[str] = None, log_every: int = 50, ckpt_dir: Optional[str] = None,
         ckpt_every: int = 0, resume: bool = False, graph: bool = True, learner=None, ctx=None,
         bucket_mb: float = 64.0, capture_sync: bool = True, layer_overlap: bool = True,
-        **learner_kw) -> Dict[str, Any]:
+        trace_path: Optional[str] = None, **learner_kw) -> Dict[str, Any]:
     """Run ``iterations`` act + update iterations (counting any restored ones); returns final stats."""
     dp = ctx is not None and ctx.is_distributed
     dev = device or (ctx.device if ctx is not None else torch.device("cuda", 0))
@@ -95,6 +95,13 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
         d.load_state_dict(st)
         done = int(meta["step"])
     ml = MetricsLogger(metrics_path)
+    prof = None
+    if trace_path and (not dp or ctx.is_main):      # Chrome trace of the run (host spans + GPU kernels)
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if dev.type == "cuda":
+            acts.append(torch.profiler.ProfilerActivity.CUDA)
+        prof = torch.profiler.profile(activities=acts)
+        prof.__enter__()
     t0 = time.perf_counter()
     last_t, last_i = t0, done
 
@@ -120,6 +127,10 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
             ml.log(rec)
             last_t, last_i = now, done
     _sync(dev)
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(os.path.dirname(os.path.abspath(trace_path)) or ".", exist_ok=True)
+        prof.export_chrome_trace(trace_path)
     out = dict(kind=kind, iterations=done, wall_s=time.perf_counter() - t0, world_size=ctx.world_size if dp else 1,
                **d.stats_dict())
     ml.close()

@@ -102,3 +102,14 @@ def test_run_dp_rejects_a_learner_built_for_another_world():
     ctx = DistContext(0, 2, 0, "gloo", torch.device("cpu"), None)
     with pytest.raises(ValueError, match="world_size"):
         run("recurrent", preset_config("recurrent"), 1, device=torch.device("cpu"), ctx=ctx, learner=_Learner(0, 1))
+
+
+def test_run_writes_a_chrome_trace(tmp_path):
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.runs import run
+
+    t = tmp_path / "trace.json"
+    res = run("recurrent", preset_config("recurrent"), 3, device=torch.device("cpu"), learner=_Learner(0, 1),
+              log_every=0, trace_path=str(t))
+    assert res["iterations"] == 3
+    assert "traceEvents" in json.loads(t.read_text())
