@@ -6,8 +6,9 @@ Q-learning (select -> env step -> TD update -> Adam) over ``--envs`` vectorised
 Buy/Sell/Hold trading envs per GPU on synthetic random-walk price series
 (6,047 days each, like the reference's MSFT file) with random-init weights;
 one process per GPU, gradients all-reduced every step with RCCL.  Default
-1,048,576 envs per GPU (weak scaling: per-GPU work fixed as N grows); the env
-state, the per-env price banks and their aligned replicas stay resident in HBM.
+1,835,008 envs per GPU (weak scaling: per-GPU work fixed as N grows); the env
+state, the per-env price banks and their aligned replicas stay resident in HBM
+(~225 of the 309 GB per GPU).
 
 Single GPU:   python bench.py --steps 200 --warmup 20
 N GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -39,9 +40,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 1 << 20)),
-                    help="vectorised envs per GPU (default 1,048,576: ~127 GB of HBM-resident price banks "
-                         "per GPU; fixed per-step costs amortised, profiles/r1_env_sweep.md)")
+    ap.add_argument("--envs", type=int, default=int(os.environ.get("SHARETRADE_BENCH_ENVS", 7 << 18)),
+                    help="vectorised envs per GPU (default 1,835,008 = 112 64-env chunks per CU: ~225 GB of the "
+                         "309 GB HBM per GPU, mostly the per-env price banks; fixed per-step costs amortised, "
+                         "profiles/r2_env_sweep.md)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) | gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
@@ -217,6 +219,10 @@ def main() -> int:
             "mean_td_loss": st[1] / max(n_trans, 1),
             "vs_reference_floor": round(value / REFERENCE_FLOOR, 1),
         }
+        if torch.cuda.is_available():
+            free, total = torch.cuda.mem_get_info(eng.device)
+            out["hbm_used_gb"] = round((total - free) / 1e9, 1)
+            out["hbm_total_gb"] = round(total / 1e9, 1)
         if allreduce_ms is not None:
             out["allreduce_ms_per_step"] = allreduce_ms
         print(json.dumps(out))
