@@ -51,24 +51,18 @@ struct DeepGather {
   int zero0_n;
   float* zero1;
   int zero1_n;
+  // replay mode, optional: X transposed [in_p][ldxt] as well (the layer-0 weight gradient's operand),
+  // written from LDS 16 rows at a time -- replaces a transpose launch in the update
+  bf16_t* XT;
+  int ldxt;
 };
 
 ST_DEV float dfeat_price(float w, float inv, int mode) { return mode ? (w * inv - 1.0f) : w; }
 
 // One wave per row: lane L owns columns 4L..4L+3 (in_p <= 256).
-__global__ void __launch_bounds__(256) deep_gather_kernel(DeepGather g) {
-  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (g.mode == 1) {
-    // 16-byte stores where the span allows (the spans start 16-byte aligned: checked on the host)
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = gid; i < g.zero0_n / 4; i += gs) reinterpret_cast<float4*>(g.zero0)[i] = z4;
-    for (int i = (g.zero0_n & ~3) + gid; i < g.zero0_n; i += gs) g.zero0[i] = 0.f;
-    for (int i = gid; i < g.zero1_n / 4; i += gs) reinterpret_cast<float4*>(g.zero1)[i] = z4;
-    for (int i = (g.zero1_n & ~3) + gid; i < g.zero1_n; i += gs) g.zero1[i] = 0.f;
-  }
-  if (row >= g.B) return;
+// One gathered row (one wave, lane L owns columns 4L..4L+3): x (and x' in replay mode) as bf16 to X / Xn,
+// the sampled reward / action / done; returns the row's x values in xv.
+ST_DEV void gather_row(const DeepGather& g, int row, int lane, float (&xv)[4]) {
   int e, ps, s, s2 = 0;
   float b, b2 = 0.f;
   if (g.mode == 0) {
@@ -99,7 +93,7 @@ __global__ void __launch_bounds__(256) deep_gather_kernel(DeepGather g) {
   const int H = g.H;
   const float last = pr[H - 1], vnew = pr[H];
   const float inv = 1.0f / last, invn = 1.0f / vnew;
-  float xv[4], xnv[4];
+  float xnv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = 4 * lane + j;
@@ -115,6 +109,49 @@ __global__ void __launch_bounds__(256) deep_gather_kernel(DeepGather g) {
   if (4 * lane < g.in_p) {
     lds_st4(g.X + (size_t)row * g.in_p + 4 * lane, xv[0], xv[1], xv[2], xv[3]);  // 8-byte global store
     if (g.mode == 1) lds_st4(g.Xn + (size_t)row * g.in_p + 4 * lane, xnv[0], xnv[1], xnv[2], xnv[3]);
+  }
+}
+
+constexpr int GT_ROWS = 16;   // rows per block of the transposed-copy path
+
+__global__ void __launch_bounds__(1024) deep_gather_kernel(DeepGather g) {
+  const int lane = threadIdx.x & 63;
+  if (g.mode == 1) {
+    // 16-byte stores where the span allows (the spans start 16-byte aligned: checked on the host)
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = gid; i < g.zero0_n / 4; i += gs) reinterpret_cast<float4*>(g.zero0)[i] = z4;
+    for (int i = (g.zero0_n & ~3) + gid; i < g.zero0_n; i += gs) g.zero0[i] = 0.f;
+    for (int i = gid; i < g.zero1_n / 4; i += gs) reinterpret_cast<float4*>(g.zero1)[i] = z4;
+    for (int i = (g.zero1_n & ~3) + gid; i < g.zero1_n; i += gs) g.zero1[i] = 0.f;
+  }
+  if (!g.XT) {
+    const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (row >= g.B) return;
+    float xv[4];
+    gather_row(g, row, lane, xv);
+    return;
+  }
+  // transposed copy as well: 16 waves per block, wave w gathers row r0 + w (one row per wave, as
+  // above) into an LDS tile, then thread c < in_p writes column c of the 16 rows to XT as two 16-byte
+  // stores (B % 16 == 0, checked on the host)
+  __shared__ __attribute__((aligned(16))) bf16_t t[GT_ROWS][256 + 8];
+  const int r0 = blockIdx.x * GT_ROWS, wave = threadIdx.x >> 6;
+  {
+    float xv[4];
+    gather_row(g, r0 + wave, lane, xv);
+    if (4 * lane < g.in_p) lds_st4(&t[wave][4 * lane], xv[0], xv[1], xv[2], xv[3]);
+  }
+  __syncthreads();
+  const int c = threadIdx.x;
+  if (c < g.in_p) {
+    uint32_t u[GT_ROWS / 2];
+#pragma unroll
+    for (int r = 0; r < GT_ROWS / 2; ++r)
+      u[r] = (uint32_t)t[2 * r][c] | ((uint32_t)t[2 * r + 1][c] << 16);
+    uint4* o = reinterpret_cast<uint4*>(g.XT + (size_t)c * g.ldxt + r0);
+    o[0] = make_uint4(u[0], u[1], u[2], u[3]);
+    o[1] = make_uint4(u[4], u[5], u[6], u[7]);
   }
 }
 
@@ -528,6 +565,13 @@ extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
 extern "C" hipError_t st_deep_gather(const st::DeepGather* g, hipStream_t s) {
   if ((reinterpret_cast<uintptr_t>(g->zero0) & 15) || (reinterpret_cast<uintptr_t>(g->zero1) & 15)) return hipErrorInvalidValue;
   if (g->in_p > 256 || g->in_p % 4 || g->H + 2 > g->in_p) return hipErrorInvalidValue;
+  if (g->XT) {
+    if (g->mode != 1 || g->B % st::GT_ROWS || g->ldxt < g->B || g->ldxt % 8 ||
+        (reinterpret_cast<uintptr_t>(g->XT) & 15))
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(st::deep_gather_kernel, dim3(g->B / st::GT_ROWS), dim3(64 * st::GT_ROWS), 0, s, *g);
+    return hipGetLastError();
+  }
   const int waves = g->B, per = 4;
   hipLaunchKernelGGL(st::deep_gather_kernel, dim3((waves + per - 1) / per), dim3(256), 0, s, *g);
   return hipGetLastError();

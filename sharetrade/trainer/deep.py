@@ -48,7 +48,8 @@ class _Gather(C.Structure):
                 ("budget", C.c_void_p), ("shares", C.c_void_p), ("rp", _Replay), ("key0", C.c_uint32),
                 ("key1", C.c_uint32), ("step", C.c_void_p), ("X", C.c_void_p), ("Xn", C.c_void_p),
                 ("r_out", C.c_void_p), ("a_out", C.c_void_p), ("done_out", C.c_void_p),
-                ("zero0", C.c_void_p), ("zero0_n", C.c_int), ("zero1", C.c_void_p), ("zero1_n", C.c_int)]
+                ("zero0", C.c_void_p), ("zero0_n", C.c_int), ("zero1", C.c_void_p), ("zero1_n", C.c_int),
+                ("XT", C.c_void_p), ("ldxt", C.c_int)]
 
 
 class _Env(C.Structure):
@@ -117,7 +118,8 @@ class DeepDQN:
                  prices: Optional[torch.Tensor] = None, seed: Optional[int] = None, dw_gemm: str = "auto",
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
-                 fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0):
+                 fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
+                 fuse_xt: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -154,6 +156,9 @@ class DeepDQN:
         # grouped forward launches (online x, target x', act states: three products per launch), its
         # env step follows on the same stream -- one stream, no fork / join, every launch fuller
         self.fuse_act = bool(fuse_act)
+        # fuse_xt: the replay gather also writes X transposed (the layer-0 weight gradient's operand)
+        # instead of a separate transpose launch in the update
+        self.fuse_xt = bool(fuse_xt)
         # data parallel (one process per GPU, trainer/runs.py): grad_sync(grad_flat) sums the weight and
         # bias gradients (one flat buffer) over the ranks before Adam; the TD coefficient carries
         # 1/world_size.  The bias gradients then come from row-sum launches (all-reduced with the rest)
@@ -346,6 +351,7 @@ class DeepDQN:
         gr.zero0_n = zn
         # the batched output layer accumulates Q / Q_t over K splits: zeroed here as well
         gr.zero1, gr.zero1_n = (self._Qpair.data_ptr(), self._Qpair.numel()) if self._q_splitk > 1 else (None, 0)
+        gr.XT, gr.ldxt = (self.XT.data_ptr(), self.B) if self.fuse_xt else (None, 0)
         self._gather_rp = gr
         ev = _Env()
         ev.prices, ev.T, ev.H, ev.E = self.prices.data_ptr(), self.T, self.H, self.E
@@ -512,8 +518,9 @@ class DeepDQN:
                 act.wait_stream(main)          # the batch is sampled: the act step may insert now
                 with torch.cuda.stream(act):
                     self.act_step()
-        native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
-                                         self.in_p, sh), "transpose X")
+        if not self.fuse_xt:
+            native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
+                                             self.in_p, sh), "transpose X")
         acts = [self.X] + self.Act[1:]
         actsT = [self.XT] + self.ActT[1:]
         if self.batched_fwd and with_act and self.fuse_act:

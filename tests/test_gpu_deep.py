@@ -176,3 +176,16 @@ def test_overlapped_act_matches_same_order_serial(native_built, fuse):
         assert torch.equal(a.rp[k], b.rp[k]), k
     for wa, wb in zip(a.W, b.W):
         assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
+
+
+@pytest.mark.parametrize("fuse_xt", [True, False])
+def test_replay_gather_writes_x_transposed(native_built, fuse_xt):
+    """fuse_xt: the replay gather writes X^T itself (16 rows per block through LDS) -- the same bits
+    as X transposed; without it the update's transpose launch does."""
+    d = _dqn(fuse_xt=fuse_xt)
+    for _ in range(8):
+        d.act_step()
+    d.update_step()
+    torch.cuda.synchronize()
+    assert torch.equal(d.XT, d.X.t().contiguous())
+    assert d.X.float().abs().sum() > 0
