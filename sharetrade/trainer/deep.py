@@ -119,7 +119,7 @@ class DeepDQN:
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
-                 fuse_xt: bool = True):
+                 fuse_xt: bool = True, act_after_fwd: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -159,6 +159,9 @@ class DeepDQN:
         # fuse_xt: the replay gather also writes X transposed (the layer-0 weight gradient's operand)
         # instead of a separate transpose launch in the update
         self.fuse_xt = bool(fuse_xt)
+        # act_after_fwd (with overlap_act): fork the act step after the update's forward instead of
+        # right after the replay sample
+        self.act_after_fwd = bool(act_after_fwd)
         # data parallel (one process per GPU, trainer/runs.py): grad_sync(grad_flat) sums the weight and
         # bias gradients (one flat buffer) over the ranks before Adam; the TD coefficient carries
         # 1/world_size.  The bias gradients then come from row-sum launches (all-reduced with the rest)
@@ -514,7 +517,7 @@ class DeepDQN:
             elif self.act_inline:
                 self.act_step()                # same order, same stream
                 act = None
-            else:
+            elif not self.act_after_fwd:
                 act.wait_stream(main)          # the batch is sampled: the act step may insert now
                 with torch.cuda.stream(act):
                     self.act_step()
@@ -537,6 +540,12 @@ class DeepDQN:
         else:
             self._forward(self.X, acts, actsT, self.Wb, self.b, self.Q)
             self._forward(self.Xn, [self.Xn] + self.ActN[1:], None, self.Wt, self.bt, self.Qt)
+        if act is not None and self.act_after_fwd:
+            # the act step beside the backward chain (TD, small GEMMs, dual launches) rather than beside
+            # the forward's GEMMs, which already fill the chip
+            act.wait_stream(main)
+            with torch.cuda.stream(act):
+                self.act_step()
         native.check(k.st_deep_td(self._td, sh), "deep_td")
         for l in reversed(range(self.L)):
             if self._dual[l]:
