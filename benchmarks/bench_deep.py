@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--serial", action="store_true", help="one stream (no concurrent GEMM chains in the update)")
     ap.add_argument("--unfused-adam", action="store_true", help="per-layer Adam + row-sum + counter launches")
     ap.add_argument("--no-pingpong", action="store_true", help="no 256x256 ping-pong GEMM for the act-step layers")
+    ap.add_argument("--early-adam", action="store_true",
+                    help="Adam waits for the act step's forward only (its env step may run beside Adam)")
     ap.add_argument("--act-before-fwd", action="store_true",
                     help="fork the act step right after the replay sample (beside the update's forward GEMMs) "
                          "instead of after the forward (beside the backward chain, the default)")
@@ -65,7 +67,8 @@ def main():
     d = DeepDQN(cfg, dev, envs=a.envs, batch=a.batch, replay_capacity=a.replay, dw_gemm=a.dw_gemm,
                 concurrent=not a.serial, fused_adam=not a.unfused_adam, overlap_act=not a.no_overlap_act,
                 batched_fwd=not a.unbatched_fwd, dual_bwd=not a.no_dual_bwd, act_inline=a.act_inline,
-                fuse_act=a.fuse_act, fuse_xt=not a.no_fuse_xt, act_after_fwd=not a.act_before_fwd)
+                fuse_act=a.fuse_act, fuse_xt=not a.no_fuse_xt, act_after_fwd=not a.act_before_fwd,
+                early_adam=a.early_adam)
     for _ in range(a.warmup):
         d.act_step()
     d.capture()

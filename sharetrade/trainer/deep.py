@@ -119,7 +119,7 @@ class DeepDQN:
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
-                 fuse_xt: bool = True, act_after_fwd: bool = True):
+                 fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -162,6 +162,8 @@ class DeepDQN:
         # act_after_fwd (with overlap_act): fork the act step after the update's forward instead of
         # right after the replay sample
         self.act_after_fwd = bool(act_after_fwd)
+        # early_adam (with overlap_act): Adam waits for the act step's forward only, not its env step
+        self.early_adam = bool(early_adam)
         # data parallel (one process per GPU, trainer/runs.py): grad_sync(grad_flat) sums the weight and
         # bias gradients (one flat buffer) over the ranks before Adam; the TD coefficient carries
         # 1/world_size.  The bias gradients then come from row-sum launches (all-reduced with the rest)
@@ -478,12 +480,24 @@ class DeepDQN:
                     probs.append((actsE[l], self.Wb[l], self.Qe, dict(bias=self.b[l])))
                 gm.gemm_nt_batched(probs, gm.EPI_F32, tile=gm.pick_tile(self.B, ACT_PAD))
 
-    def act_step(self) -> None:
-        """One env step of all E envs: gather -> Q forward -> select/transition/replay insert."""
+    def act_step(self, after_forward=None) -> None:
+        """One env step of all E envs: gather -> Q forward -> select/transition/replay insert.
+        ``after_forward()`` runs between the forward (the last reader of the weights) and the env step."""
         sh = native.stream_handle()
         native.check(self.k.st_deep_gather(self._gather_env, sh), "deep_gather(env)")
         self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe)
+        if after_forward is not None:
+            after_forward()
         native.check(self.k.st_deep_env_step(self._env, sh), "deep_env_step")
+
+    def _fork_act(self, main, act):
+        """The act step on its own stream; returns an event recorded after its forward (Adam, which
+        overwrites the weights, waits for that, not for the env step behind it)."""
+        act.wait_stream(main)
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(act):
+            self.act_step(after_forward=lambda: ev.record(act))
+        return ev
 
     def _dw(self, l: int, actsT) -> None:
         """Weight gradient of layer l: dW = G_l^T . A_l (long-K, few-tile product)."""
@@ -518,9 +532,7 @@ class DeepDQN:
                 self.act_step()                # same order, same stream
                 act = None
             elif not self.act_after_fwd:
-                act.wait_stream(main)          # the batch is sampled: the act step may insert now
-                with torch.cuda.stream(act):
-                    self.act_step()
+                act_fwd_done = self._fork_act(main, act)   # the batch is sampled: the act step may insert now
         if not self.fuse_xt:
             native.check(k.st_transpose_bf16(self.X.data_ptr(), self.in_p, self.XT.data_ptr(), self.B, self.B,
                                              self.in_p, sh), "transpose X")
@@ -543,9 +555,7 @@ class DeepDQN:
         if act is not None and self.act_after_fwd:
             # the act step beside the backward chain (TD, small GEMMs, dual launches) rather than beside
             # the forward's GEMMs, which already fill the chip
-            act.wait_stream(main)
-            with torch.cuda.stream(act):
-                self.act_step()
+            act_fwd_done = self._fork_act(main, act)
         native.check(k.st_deep_td(self._td, sh), "deep_td")
         for l in reversed(range(self.L)):
             if self._dual[l]:
@@ -588,13 +598,22 @@ class DeepDQN:
             main.wait_stream(side)
         if not split and self.layer_sync is None and self.grad_sync is not None:
             self.grad_sync(self.grad_flat)     # one flat all-reduce, beside a still-running act step
-        if act is not None:
-            main.wait_stream(act)              # the act step's GEMMs read the pre-update weights
         if split:
+            if act is not None:
+                main.wait_stream(act)
             return
+        if act is not None:
+            # the act step's GEMMs read the pre-update weights; with early_adam its env step / replay
+            # insert may still run beside Adam
+            if self.early_adam:
+                main.wait_event(act_fwd_done)
+            else:
+                main.wait_stream(act)
         if self.layer_sync is not None:
             main.wait_stream(self._comm)
         self._adam_step()
+        if act is not None and self.early_adam:
+            main.wait_stream(act)
 
     def _adam_step(self) -> None:
         sh = native.stream_handle()
