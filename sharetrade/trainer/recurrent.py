@@ -142,7 +142,11 @@ class RecurrentDQN:
         # the learner's backward dh GEMM reads W_hh^T as resident MX-fp8 fragments too (online net only)
         self.pk["on"]["whhT8"] = torch.zeros(nfr * 8, dtype=i32, device=dev)
         self.pk["on"]["whhTs"] = torch.zeros(nfr, dtype=i32, device=dev)
-        self.whh8, self.whhs = self.pk["on"]["whh8"], self.pk["on"]["whhs"]
+        # a second online set: the overlapped iteration re-packs the updated weights into the other set
+        # while the actor still reads this one, so the re-pack need not wait for the actor (the sets
+        # alternate: ``_par`` is the set holding the current weights)
+        self.pk["on1"] = {k: torch.zeros_like(v) for k, v in self.pk["on"].items()}
+        self._par = 0
         # ---------------------------------------------------------------- data + envs
         self.bp = bar_params or mb.BarParams()
         self.close, self.feat = mb.generate_gpu(self.E, self.T, dev, self.bp, seed=self.seed)
@@ -192,36 +196,55 @@ class RecurrentDQN:
         self.key0, self.key1 = (int(x) for x in rng.key_for(self.seed, 7))
         self.updates = 0
         self.launches = 0
-        self._g_act = None
-        self._g_upd = None
+        self._g_act = self._g_upd = self._g_iter = None
+        self._g_acts, self._g_upds, self._g_iters = {}, {}, {}
         self._build_structs()
-        self.pack("on")
+        self.pack("on", into=0)
+        self.pack("on", into=1)
         self.pack("tg")
 
     # ---------------------------------------------------------------- structs
+    @property
+    def _act(self):
+        """The actor's launch arguments for the current online set."""
+        return self._acts[self._par]
+
+    @property
+    def whh8(self) -> torch.Tensor:
+        return self._on(self._par)["whh8"]
+
+    @property
+    def whhs(self) -> torch.Tensor:
+        return self._on(self._par)["whhs"]
+
+    def _on(self, p: int) -> Dict[str, torch.Tensor]:
+        return self.pk["on" if p == 0 else "on1"]
+
     def _build_structs(self) -> None:
-        a = G.ActArgs()
-        po = self.pk["on"]
-        a.whh8, a.whhs, a.wih, a.bias4, a.wq = (po[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
-        a.feat, a.close, a.ret = self.feat.data_ptr(), self.close.data_ptr(), self.ret.data_ptr()
-        a.E, a.T, a.S, a.ep_len = self.E, self.T, self.S, self.ep_len
-        ag = self.cfg.agent
-        a.eps, a.inv_ramp, a.cost = float(ag.epsilon), float(np.float32(1.0 / ag.ramp)), self.cost
-        a.inv_ep_len = float(np.float32(1.0 / self.ep_len))
-        for n in ("h", "pos", "ep_start", "position", "entry", "ep_ret", "episodes", "last_ret"):
-            setattr(a, n, getattr(self, n).data_ptr())
-        a.rx, a.ra, a.rr, a.rd, a.rh0 = (self.rx.data_ptr(), self.ra.data_ptr(), self.rr.data_ptr(),
-                                         self.rd.data_ptr(), self.rh0.data_ptr())
-        a.rctrl, a.cap = self.rctrl.data_ptr(), self.cap
-        a.key0, a.key1 = (int(x) for x in rng.key_for(self.seed, 5))
-        a.ctrl, a.stats, a.q_out = self.ctrl.data_ptr(), self.stats.data_ptr(), None
-        self._act = a
+        self._acts, self._pack_on = [], []
+        for par in (0, 1):
+            a = G.ActArgs()
+            po = self._on(par)
+            a.whh8, a.whhs, a.wih, a.bias4, a.wq = (po[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
+            a.feat, a.close, a.ret = self.feat.data_ptr(), self.close.data_ptr(), self.ret.data_ptr()
+            a.E, a.T, a.S, a.ep_len = self.E, self.T, self.S, self.ep_len
+            ag = self.cfg.agent
+            a.eps, a.inv_ramp, a.cost = float(ag.epsilon), float(np.float32(1.0 / ag.ramp)), self.cost
+            a.inv_ep_len = float(np.float32(1.0 / self.ep_len))
+            for n in ("h", "pos", "ep_start", "position", "entry", "ep_ret", "episodes", "last_ret"):
+                setattr(a, n, getattr(self, n).data_ptr())
+            a.rx, a.ra, a.rr, a.rd, a.rh0 = (self.rx.data_ptr(), self.ra.data_ptr(), self.rr.data_ptr(),
+                                             self.rd.data_ptr(), self.rh0.data_ptr())
+            a.rctrl, a.cap = self.rctrl.data_ptr(), self.cap
+            a.key0, a.key1 = (int(x) for x in rng.key_for(self.seed, 5))
+            a.ctrl, a.stats, a.q_out = self.ctrl.data_ptr(), self.stats.data_ptr(), None
+            self._acts.append(a)
         self._packs = {}
-        for net, src in (("on", self.P), ("tg", self.T_P)):
+        for net, src in (("on0", self.P), ("on1", self.P), ("tg", self.T_P)):
             p = G.PackArgs()
             p.w_hh, p.w_ih, p.b_ih, p.b_hh, p.w_q, p.b_q = (src[n].data_ptr() for n in
                                                              ("w_hh", "w_ih", "b_ih", "b_hh", "w_q", "b_q"))
-            pk = self.pk[net]
+            pk = self.pk[net] if net == "tg" else self._on(int(net[-1]))
             p.whh8, p.whhs, p.wih, p.bias4, p.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
             if "whhT8" in pk:
                 p.whhT8, p.whhTs = pk["whhT8"].data_ptr(), pk["whhTs"].data_ptr()
@@ -234,29 +257,33 @@ class RecurrentDQN:
         ga.X, ga.H0 = self.X.data_ptr(), self.H0.data_ptr()
         ga.A, ga.R, ga.D = self.A.data_ptr(), self.R.data_ptr(), self.D.data_ptr()
         self._gather = ga
-        f = G.SeqFwdArgs()
-        for net, w in (("on", f.on), ("tg", f.tg)):
-            pk = self.pk[net]
-            w.whh8, w.whhs, w.wih, w.bias4, w.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4", "wq"))
-        f.X, f.H0, f.D = self.X.data_ptr(), self.H0.data_ptr(), self.D.data_ptr()
-        f.Q, f.Qt, f.sv = self.Q.data_ptr(), self.Q_t.data_ptr(), self.sv.data_ptr()
-        f.HT, f.ldht = self.HT.data_ptr(), int(self.HT.stride(0))
-        f.B, f.S = self.B, self.S
-        self._fwd = f
+        self._fwds = []
+        for par in (0, 1):
+            f = G.SeqFwdArgs()
+            for pk, w in ((self._on(par), f.on), (self.pk["tg"], f.tg)):
+                w.whh8, w.whhs, w.wih, w.bias4, w.wq = (pk[k].data_ptr() for k in ("whh8", "whhs", "wih", "bias4",
+                                                                                  "wq"))
+            f.X, f.H0, f.D = self.X.data_ptr(), self.H0.data_ptr(), self.D.data_ptr()
+            f.Q, f.Qt, f.sv = self.Q.data_ptr(), self.Q_t.data_ptr(), self.sv.data_ptr()
+            f.HT, f.ldht = self.HT.data_ptr(), int(self.HT.stride(0))
+            f.B, f.S = self.B, self.S
+            self._fwds.append(f)
         td = G.TDArgs()
         td.Q, td.Qt, td.A, td.R, td.D = (self.Q.data_ptr(), self.Q_t.data_ptr(), self.A.data_ptr(), self.R.data_ptr(),
                                          self.D.data_ptr())
         td.dQ, td.loss, td.B, td.S, td.burn = self.dQ.data_ptr(), self.loss.data_ptr(), self.B, self.S, self.burn
         td.gamma, td.coef = self.gamma, 2.0 / (self.B * (self.S - self.burn) * self.world_size)
         self._td = td
-        bw = G.SeqBwdArgs()
-        bw.sv, bw.dQ, bw.D, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
-                                     self.P["w_q"].data_ptr())
-        bw.whhT8, bw.whhTs = self.pk["on"]["whhT8"].data_ptr(), self.pk["on"]["whhTs"].data_ptr()
-        bw.dGxT, bw.dGhT = self.dGxT.data_ptr(), self.dGhT.data_ptr()
-        bw.gwq, bw.gbq = self.dP["w_q"].data_ptr(), self.dP["b_q"].data_ptr()
-        bw.B, bw.S = self.B, self.S
-        self._bwd = bw
+        self._bwds = []
+        for par in (0, 1):
+            bw = G.SeqBwdArgs()
+            bw.sv, bw.dQ, bw.D, bw.wq = (self.sv.data_ptr(), self.dQ.data_ptr(), self.D.data_ptr(),
+                                         self.P["w_q"].data_ptr())
+            bw.whhT8, bw.whhTs = self._on(par)["whhT8"].data_ptr(), self._on(par)["whhTs"].data_ptr()
+            bw.dGxT, bw.dGhT = self.dGxT.data_ptr(), self.dGhT.data_ptr()
+            bw.gwq, bw.gbq = self.dP["w_q"].data_ptr(), self.dP["b_q"].data_ptr()
+            bw.B, bw.S = self.B, self.S
+            self._bwds.append(bw)
         ag = self.cfg.agent
         op = native.OptimParams()
         op.params, op.mask, op.s1, op.s2 = (self.flat.data_ptr(), self.ones.data_ptr(), self.mflat.data_ptr(),
@@ -280,26 +307,31 @@ class RecurrentDQN:
         rounds = -(-work // avail)
         return -(-work // rounds)
 
-    def pack(self, net: str = "on") -> None:
-        """fp32 masters -> MX-fp8 W_hh fragments, bf16 W_ih fragments, biases, W_q (actor/learner layout)."""
-        native.check(self.k.st_gru_pack(self._packs[net], native.stream_handle()), "st_gru_pack")
+    def pack(self, net: str = "on", into: Optional[int] = None) -> None:
+        """fp32 masters -> MX-fp8 W_hh fragments, bf16 W_ih fragments, biases, W_q (actor/learner layout).
+        ``net="on"`` packs into online set ``into`` (default: the current one)."""
+        key = "tg" if net == "tg" else f"on{self._par if into is None else int(into)}"
+        native.check(self.k.st_gru_pack(self._packs[key], native.stream_handle()), "st_gru_pack")
 
     def act(self) -> None:
         """All E envs advance S minute bars (one actor launch) and write one replay segment each."""
         if self.actor_kernel == "pair":
-            native.check(self.k.st_gru_act_pair(self._act, self.grid, native.stream_handle()), "st_gru_act_pair")
+            native.check(self.k.st_gru_act_pair(self._acts[self._par], self.grid, native.stream_handle()),
+                         "st_gru_act_pair")
         else:
-            native.check(self.k.st_gru_act(self._act, self.grid, native.stream_handle()), "st_gru_act")
+            native.check(self.k.st_gru_act(self._acts[self._par], self.grid, native.stream_handle()), "st_gru_act")
 
     # ---------------------------------------------------------------- learner
-    def update(self, with_act: bool = False) -> None:
+    def update(self, with_act: bool = False, flip: bool = False) -> None:
         """One learner update on B sampled segments: gather -> fused unroll of both nets (MX-fp8) ->
         TD -> fused BPTT (bf16) -> split-K weight-gradient GEMMs -> Adam -> repack the actor weights.
-        ``with_act``: the actor launch runs on a side stream right after the gather (see overlap_act)."""
+        ``with_act``: the actor launch runs on a side stream right after the gather (see overlap_act).
+        ``flip``: re-pack into the other online set without waiting for the actor; the caller then
+        switches ``_par`` (the overlapped iteration)."""
         act = self._grads(with_act)
         if self.grad_sync is not None:
             self.grad_sync(self.gflat)
-        self._apply(act)
+        self._apply(act, flip)
 
     def _grads(self, with_act: bool = False, join: bool = False):
         """Gather -> unroll -> TD -> BPTT -> weight gradients into ``gflat``.  Returns the actor's side
@@ -317,11 +349,11 @@ class RecurrentDQN:
             act.wait_stream(main)          # segments sampled: the actor may insert now
             with torch.cuda.stream(act):
                 self.act()
-        native.check(k.st_gru_seq_fwd(self._fwd, sh), "st_gru_seq_fwd")
+        native.check(k.st_gru_seq_fwd(self._fwds[self._par], sh), "st_gru_seq_fwd")
         self.loss.zero_()
         native.check(k.st_gru_td(self._td, sh), "st_gru_td")
         self.gflat.zero_()
-        native.check(k.st_gru_seq_bwd(self._bwd, sh), "st_gru_seq_bwd")
+        native.check(k.st_gru_seq_bwd(self._bwds[self._par], sh), "st_gru_seq_bwd")
         native.check(kd.st_transpose_bf16(self.X.data_ptr(), XL, self.XT.data_ptr(), R1, RS, XL, sh), "T X")
         # weight gradients; the ones row of HT / ones column RF of X give the bias gradients for free
         gm.gemm_nt(self.dGhT, self.HT[:, :RS], self.dWhh_ext, gm.EPI_F32, splitk="auto")
@@ -334,15 +366,21 @@ class RecurrentDQN:
             act = None
         return act
 
-    def _apply(self, act=None) -> None:
+    def _apply(self, act=None, flip: bool = False) -> None:
         """Adam on the (synchronised) gradient, then re-pack the actor's MX-fp8 weights."""
         sh = native.stream_handle()
         nl = native.lib()
         native.check(nl.st_advance(self.opt_ctrl.data_ptr(), sh), "advance")
         native.check(nl.st_reduce_optim(self._opt, sh), "adam")
-        if act is not None:
-            torch.cuda.current_stream(self.dev).wait_stream(act)   # the actor reads the packed weights
-        self.pack("on")
+        main = torch.cuda.current_stream(self.dev)
+        if flip:
+            self.pack("on", into=1 - self._par)   # the running actor reads the current set
+            if act is not None:
+                main.wait_stream(act)
+        else:
+            if act is not None:
+                main.wait_stream(act)             # the actor reads the packed weights
+            self.pack("on")
 
     def sync_params(self, ctx) -> None:
         """Data-parallel start: every rank takes rank 0's parameters (online and target net)."""
@@ -350,7 +388,8 @@ class RecurrentDQN:
 
         broadcast_tensors(ctx, [self.flat])
         self.tflat.copy_(self.flat)
-        self.pack("on")
+        self.pack("on", into=0)
+        self.pack("on", into=1)
         self.pack("tg")
 
     def sync_target(self) -> None:
@@ -358,36 +397,50 @@ class RecurrentDQN:
         self.pack("tg")
 
     # ---------------------------------------------------------------- driver
+    def _flips(self) -> bool:
+        """Whether the overlapped iteration alternates the online sets (not in the split DP capture)."""
+        return self.grad_sync is None or self.capture_sync
+
     def capture(self) -> None:
-        """Warm up, then capture one actor launch and one learner update into HIP graphs."""
+        """Warm up, then capture the actor launch, the learner update and (overlap_act) the whole
+        iteration into HIP graphs -- one of each per online weight set."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
+        flip = self.overlap_act and self._flips()
         with torch.cuda.stream(s):
             if self.overlap_act:
-                self.update(with_act=True)   # same op order as the captured iteration
+                self.update(with_act=True, flip=flip)   # same op order as the captured iteration
             else:
                 self.act()
                 self.update()
         torch.cuda.current_stream(self.dev).wait_stream(s)
+        if flip:
+            self._par ^= 1
         self.launches += 1
         self.updates += 1
         if self.updates % self.target_every == 0:   # the warm-up is a full iteration (as iteration())
             self.sync_target()
-        self._g_act = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_act, capture_error_mode=_CAPTURE_MODE):
-            self.act()
-        self._g_upd = self._g_iter = self._g_pre = self._g_pre_act = self._g_post = None
-        if self.grad_sync is None or self.capture_sync:
-            self._g_upd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_upd, capture_error_mode=_CAPTURE_MODE):
-                self.update()
-            if self.overlap_act:
-                self._g_iter = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_iter, capture_error_mode=_CAPTURE_MODE):
-                    self.update(with_act=True)
-        else:
+        cur = self._par
+        self._g_acts, self._g_upds, self._g_iters = {}, {}, {}
+        self._g_pre = self._g_pre_act = self._g_post = None
+        for par in (0, 1):
+            self._par = par
+            self._g_acts[par] = g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                self.act()
+            if self._flips():
+                self._g_upds[par] = g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                    self.update()
+                if self.overlap_act:
+                    self._g_iters[par] = g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                        self.update(with_act=True, flip=True)
+        self._par = cur
+        if not self._flips():
             # data parallel: the gradient all-reduce runs between two graphs (gradients | Adam + re-pack),
             # the collective itself stays outside the capture; the actor joins at the end of the first
+            # (the online set never alternates here)
             self._g_pre = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_pre, capture_error_mode=_CAPTURE_MODE):
                 self._grads()
@@ -398,6 +451,7 @@ class RecurrentDQN:
             self._g_post = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_post, capture_error_mode=_CAPTURE_MODE):
                 self._apply()
+        self._g_act, self._g_upd, self._g_iter = (self._g_acts.get(0), self._g_upds.get(0), self._g_iters.get(0))
         self._captured = True
 
     def _replay_dp(self, with_act: bool) -> None:
@@ -406,8 +460,9 @@ class RecurrentDQN:
         self._g_post.replay()
 
     def act_step(self) -> None:
-        if self._g_act is not None:
-            self._g_act.replay()
+        g = self._g_acts.get(self._par)
+        if g is not None:
+            g.replay()
         else:
             self.act()
         self.launches += 1
@@ -415,8 +470,8 @@ class RecurrentDQN:
     def update_step(self) -> None:
         if getattr(self, "_g_pre", None) is not None:
             self._replay_dp(False)
-        elif self._g_upd is not None:
-            self._g_upd.replay()
+        elif self._g_upds.get(self._par) is not None:
+            self._g_upds[self._par].replay()
         else:
             self.update()
         self.updates += 1
@@ -427,10 +482,13 @@ class RecurrentDQN:
         if self.overlap_act and updates >= 1:
             if getattr(self, "_g_pre_act", None) is not None:
                 self._replay_dp(True)
-            elif getattr(self, "_g_iter", None) is not None:
-                self._g_iter.replay()
+            elif self._g_iters.get(self._par) is not None:
+                self._g_iters[self._par].replay()
+                self._par ^= 1
             else:
-                self.update(with_act=True)
+                self.update(with_act=True, flip=self._flips())
+                if self._flips():
+                    self._par ^= 1
             self.launches += 1
             self.updates += 1
             if self.updates % self.target_every == 0:
@@ -457,7 +515,8 @@ class RecurrentDQN:
         for k in self._STATE_KEYS:
             getattr(self, k).copy_(d[k].to(self.dev))
         self.updates, self.launches = (int(x) for x in d["counters"].tolist())
-        self.pack("on")
+        self.pack("on", into=0)
+        self.pack("on", into=1)
         self.pack("tg")
 
     @property

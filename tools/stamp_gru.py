@@ -29,10 +29,12 @@ def main():
     st = torch.zeros(a.seq * 2 * 8 + a.seq * 8, dtype=torch.int64, device="cuda")
     for _ in range(3):
         d.act()
-    d._act.stamps = st.data_ptr()
+    for args in d._acts:
+        args.stamps = st.data_ptr()
     d.act()
     torch.cuda.synchronize()
-    d._act.stamps = None
+    for args in d._acts:
+        args.stamps = None
     allst = st.cpu().numpy().astype(np.int64)
     s = allst[:a.seq * 16].reshape(a.seq, 2, 8)
     arr = allst[a.seq * 16:].reshape(a.seq, 8)   # single kernel: every wave's arrival at barrier 1
