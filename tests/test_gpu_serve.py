@@ -1,0 +1,117 @@
+"""Numerics of the batched serving kernel (``csrc/qserve.hip``) vs the fp32 PyTorch oracle.
+
+The oracle (``sharetrade.serve.reference_select``) rounds the features and hidden activations to
+bf16 where the kernel does; only the fp32 accumulation order differs, so Q values are compared with
+a tight relative tolerance and actions must agree wherever the top-two Q margin is not a near-tie.
+The epsilon-greedy draws use the same Philox counters on both sides.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows(B, H=201, seed=0):
+    g = np.random.default_rng(seed)
+    p = 50.0 * np.exp(np.cumsum(g.normal(0, 0.02, size=(B, H)), axis=1))
+    budget = g.uniform(0, 5000, size=(B, 1))
+    shares = g.integers(0, 40, size=(B, 1)).astype(np.float64)
+    return torch.from_numpy(np.concatenate([p, budget, shares], 1).astype(np.float32))
+
+
+def _cfg(features="relative", output_relu=False):
+    from sharetrade.config import preset_config
+
+    cfg = preset_config("flagship")
+    cfg.env.features = features
+    cfg.model.output_relu = output_relu
+    if features == "raw":
+        cfg.model.init_std = 0.01
+        cfg.model.init = "normal"
+    return cfg
+
+
+def _check(srv, x, steps, seq):
+    from sharetrade.serve import reference_select
+
+    c = srv.cfg
+    a, q = srv.infer(x, steps, return_q=True)
+    a_ref, q_ref = reference_select(srv.params, srv.layout, x.cuda(), history=srv.H, feat_mode=c.env.features,
+                                    output_relu=c.model.output_relu, budget0=c.env.budget,
+                                    epsilon=c.agent.epsilon, ramp=c.agent.ramp, key_seed=srv.seed, seq=seq,
+                                    steps=steps)
+    rel = float((q - q_ref).norm() / (q_ref.norm() + 1e-12))
+    assert rel < 2e-3, rel
+    top2 = q_ref.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-3 * (q_ref.abs().max(1).values + 1e-3)
+    assert clear.float().mean() > 0.5
+    assert torch.equal(a[clear], a_ref[clear])
+
+
+@pytest.mark.parametrize("B", [1, 63, 64, 1000, 70001])
+def test_serve_kernel_matches_oracle(native_built, B):
+    from sharetrade.serve import PolicyServer
+
+    srv = PolicyServer(_cfg(), device=torch.device("cuda", 0), backend="native")
+    assert srv.backend == "native"
+    x = _rows(B, seed=B)
+    _check(srv, x, None, 0)                      # greedy (seq 0)
+    steps = torch.from_numpy(np.random.default_rng(B).uniform(0, 2000, size=B).astype(np.float32))
+    _check(srv, x, steps, 1)                     # epsilon-greedy draws of batch 1
+
+
+@pytest.mark.parametrize("features,output_relu", [("raw", True), ("raw", False), ("relative", True)])
+def test_serve_kernel_feature_modes(native_built, features, output_relu):
+    from sharetrade.serve import PolicyServer
+
+    srv = PolicyServer(_cfg(features, output_relu), device=torch.device("cuda", 0), backend="native")
+    _check(srv, _rows(300, seed=7), None, 0)
+
+
+def test_serve_kernel_strided_rows_and_engine_weights(native_built):
+    """Rows read with their own stride (a wider buffer), weights taken from a training engine."""
+    from sharetrade.serve import PolicyServer, reference_select
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg()
+    cfg.engine.envs_per_rank = 256
+    eng = VectorEngine(cfg, device=torch.device("cuda", 0))
+    eng.run(3)
+    srv = PolicyServer.from_engine(eng)
+    wide = torch.zeros(500, 256)
+    wide[:, :203] = _rows(500, seed=11)
+    a, q = srv.infer(wide[:, :203], return_q=True)   # non-contiguous view -> copied rows
+    a_ref, q_ref = reference_select(eng.params, srv.layout, wide[:, :203].cuda(), history=201,
+                                    feat_mode="relative", output_relu=False, budget0=cfg.env.budget,
+                                    epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, key_seed=srv.seed)
+    assert float((q - q_ref).norm() / q_ref.norm()) < 2e-3
+    # strided launch straight from the wide buffer
+    dev_wide = wide.cuda()
+    acts = torch.empty(500, dtype=torch.int32, device="cuda")
+    q2 = torch.empty(500, 3, device="cuda")
+    srv._kern.launch(dev_wide[:, :203], acts, q2)
+    assert torch.equal(q2, q) and torch.equal(acts, a)
+
+
+def test_batcher_native_path(native_built):
+    import threading
+
+    from sharetrade.serve import DynamicBatcher, PolicyServer
+
+    srv = PolicyServer(_cfg(), device=torch.device("cuda", 0), backend="native")
+    x = _rows(300, seed=5)
+    want = srv.infer(x).cpu().tolist()
+    out = [None] * 300
+    with DynamicBatcher(srv, max_batch=128, max_delay_us=5000, greedy=True) as bat:
+        def client(lo, hi):
+            fs = [(i, bat.submit(x[i])) for i in range(lo, hi)]
+            for i, f in fs:
+                out[i] = f.result(timeout=60)
+
+        ts = [threading.Thread(target=client, args=(k * 100, (k + 1) * 100)) for k in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert out == want

@@ -1,0 +1,149 @@
+"""Policy serving on the CPU backend: server, dynamic batcher and the SelectionAction actor.
+
+The GPU kernel itself is checked against the same oracle in ``tests/test_gpu_serve.py``.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from sharetrade import protocol as P
+from sharetrade.actors.runtime import ActorSystem
+from sharetrade.actors.testkit import EventFilter, TestKit
+from sharetrade.config import preset_config
+from sharetrade.errors import IllegalArgumentException
+from sharetrade.models import qnet as qn
+from sharetrade.serve import (DynamicBatcher, LoadPolicy, PolicyLoaded, PolicyServer, PolicyServingActor,
+                              reference_select)
+
+
+def _rows(B, H=201, seed=0):
+    g = np.random.default_rng(seed)
+    p = 50.0 * np.exp(np.cumsum(g.normal(0, 0.02, size=(B, H)), axis=1))
+    budget = g.uniform(0, 5000, size=(B, 1))
+    shares = g.integers(0, 40, size=(B, 1)).astype(np.float64)
+    return np.concatenate([p, budget, shares], 1).astype(np.float32)
+
+
+def _server(eps=None, **kw):
+    cfg = preset_config("flagship")
+    if eps is not None:
+        cfg.agent.epsilon = eps
+    return PolicyServer(cfg, device=torch.device("cpu"), backend="torch", **kw)
+
+
+def test_greedy_infer_matches_oracle_and_q():
+    srv = _server()
+    x = _rows(37)
+    a, q = srv.infer(x, return_q=True)
+    cfg = srv.cfg
+    a_ref, q_ref = reference_select(srv.params, srv.layout, torch.from_numpy(x), history=201,
+                                    feat_mode="relative", output_relu=False, budget0=cfg.env.budget,
+                                    epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, key_seed=srv.seed)
+    assert torch.equal(a, a_ref) and torch.allclose(q, q_ref)
+    assert a.dtype == torch.int32 and a.shape == (37,) and q.shape == (37, 3)
+    assert torch.equal(a, q.argmax(1).to(torch.int32))
+
+
+def test_epsilon_greedy_ramp_and_reproducible_draws():
+    srv = _server()
+    x = _rows(256, seed=1)
+    greedy = srv.infer(x)
+    # step 0: exploit probability min(eps, 0) = 0 -> every action is the random draw
+    a0 = srv.infer(x, np.zeros(256))
+    # step >> ramp: exploit with probability eps
+    a_hi = srv.infer(x, np.full(256, 1e9))
+    eps = srv.cfg.agent.epsilon
+    agree = float((a_hi == greedy).float().mean())
+    assert agree >= eps - 0.1
+    # same seed, same batch sequence number -> the same draws
+    srv2 = _server()
+    srv2.seq = 1   # a0 was the server's second batch
+    assert torch.equal(srv2.infer(x, np.zeros(256)), a0)
+    assert not torch.equal(srv2.infer(x, np.zeros(256)), a0)   # the next batch draws anew
+    assert set(a0.tolist()) <= {0, 1, 2} and len(set(a0.tolist())) == 3
+
+
+def test_bad_rows_rejected():
+    srv = _server()
+    with pytest.raises(ValueError):
+        srv.infer(np.zeros((2, 50), np.float32))
+    with pytest.raises(ValueError):
+        srv.infer(_rows(3), [1.0, 2.0])
+
+
+def test_load_params_changes_the_policy():
+    srv = _server()
+    x = _rows(64, seed=2)
+    a1, q1 = srv.infer(x, return_q=True)
+    m = srv.cfg.model
+    new = qn.init_params(srv.layout, m, seed=4321)
+    srv.load_params(new)
+    a2, q2 = srv.infer(x, return_q=True)
+    assert not torch.allclose(q1, q2)
+    with pytest.raises(ValueError):
+        srv.load_params(torch.zeros(10))
+
+
+def test_dynamic_batcher_groups_concurrent_requests():
+    srv = _server()
+    x = _rows(200, seed=3)
+    want = srv.infer(x).tolist()
+    out = [None] * 200
+    with DynamicBatcher(srv, max_batch=64, max_delay_us=20000, greedy=True) as bat:
+        def client(lo, hi):
+            futs = [(i, bat.submit(x[i])) for i in range(lo, hi)]
+            for i, f in futs:
+                out[i] = f.result(timeout=30)
+
+        ts = [threading.Thread(target=client, args=(k * 50, (k + 1) * 50)) for k in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        st = bat.stats()
+    assert out == want
+    assert st["requests"] == 200 and st["max_batch"] <= 64
+    assert st["batches"] < 200   # requests were grouped
+    with pytest.raises(RuntimeError):
+        bat.submit(x[0])
+
+
+def test_batcher_propagates_errors():
+    srv = _server()
+    with DynamicBatcher(srv, max_batch=8, max_delay_us=100) as bat:
+        with pytest.raises(ValueError):
+            bat.submit(np.zeros(7, np.float32))
+
+
+@pytest.fixture
+def system():
+    s = ActorSystem("serve", loglevel="DEBUG")
+    yield s
+    s.terminate()
+
+
+def test_serving_actor_answers_selection_action(system):
+    kit = TestKit(system)
+    srv = _server(eps=1.0)   # exploit probability min(1, step / ramp) = 1 at step 1e9: greedy
+    x = _rows(5, seed=4)
+    ref = srv.infer(x)
+    act = system.actor_of(PolicyServingActor.props(srv))
+    for i in range(5):
+        kit.tell(act, P.SelectionAction(x[i:i + 1], 1e9))
+    got = [kit.expect_msg_type(P.Action) for _ in range(5)]
+    assert [g.index for g in got] == ref.tolist()
+    assert srv.requests == 10 and srv.batches <= 6   # queued selections share launches
+
+
+def test_serving_actor_wrong_shape_and_load_policy(system):
+    kit = TestKit(system)
+    srv = _server()
+    act = system.actor_of(PolicyServingActor.props(srv))
+    with EventFilter(system, IllegalArgumentException, occurrences=1).intercept():
+        kit.tell(act, P.SelectionAction(list(range(10)), 0))
+    new = qn.init_params(srv.layout, srv.cfg.model, seed=99)
+    kit.tell(act, LoadPolicy(new))
+    kit.expect_msg(PolicyLoaded)
+    assert torch.equal(srv.params, new)
