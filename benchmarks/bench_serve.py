@@ -76,11 +76,15 @@ def main() -> int:
     w1, b1 = L.w(srv.params_bf, 1), L.b(srv.params, 1).to(torch.bfloat16)
     w2, b2 = L.w(srv.params_bf, 2), L.b(srv.params, 2).to(torch.bfloat16)
     for B in [int(b) for b in args.batches.split(",")]:
-        x = rows(B, seed=B).to(dev)
+        x203 = rows(B, seed=B).to(dev)
+        x = torch.zeros(B, srv.ld, device=dev)   # the server's aligned staging stride (dwordx4 gather)
+        x[:, :203] = x203
+        x = x[:, :203]
         steps = torch.full((B,), 500.0, device=dev)
         acts = torch.empty(B, dtype=torch.int32, device=dev)
         iters = max(20, min(2000, 2_000_000 // B))
         us = time_launches(lambda: srv._kern.launch(x, acts, None, steps, seq=1), iters)
+        us_unaligned = time_launches(lambda: srv._kern.launch(x203, acts, None, steps, seq=1), iters)
         # library path: features precomputed (not timed), then three bf16 linear layers + argmax
         feats = tr.features(x[:, :201], x[:, 201], x[:, 202], "relative", cfg.env.budget)
         xp = torch.zeros(B, 224, device=dev, dtype=torch.bfloat16)
@@ -101,7 +105,7 @@ def main() -> int:
         us_graph = time_launches(g.replay, iters)
         print(json.dumps({"bench": "kernel", "batch": B, "us_per_launch": round(us, 2),
                           "requests_per_s": round(B / us * 1e6, 1), "tflops": round(B * flops_row / us * 1e-6, 1),
-                          "us_graph_replay": round(us_graph, 2),
+                          "us_graph_replay": round(us_graph, 2), "us_rows_stride_203": round(us_unaligned, 2),
                           "us_torch_library_path": round(us_lib, 2),
                           "speedup_vs_library": round(us_lib / us, 2)}), flush=True)
 

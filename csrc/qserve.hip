@@ -48,6 +48,8 @@ struct ServeParams {
   unsigned long long seq;   // draw counter: (row, seq_lo, seq_hi, stream 2)
 };
 
+// VEC: rows 16-byte aligned (ld % 4 == 0, aligned base): one dwordx4 load per column quad
+template <bool VEC>
 __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* sX = reinterpret_cast<bf16_t*>(smem);   // [C][SX]; also H2 [C][SH] after layer 1
@@ -101,8 +103,14 @@ __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
         const int it = tid + NT * (qb + j), r = it / QPR, c = 4 * (it - r * QPR);
         // 32-bit element offsets off one uniform base (the host checks B * ld < 2^30)
         const unsigned ro = (unsigned)min(r0 + r, p.B - 1) * (unsigned)p.ld;
+        if constexpr (VEC) {
+          // quads past the one holding column H+1 re-read it: their columns take no row value
+          const float4 t = *reinterpret_cast<const float4*>(p.states + ro + (unsigned)min(c, (H + 1) & ~3));
+          v[j][0] = t.x; v[j][1] = t.y; v[j][2] = t.z; v[j][3] = t.w;
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[j][q] = p.states[ro + (unsigned)min(c + q, H + 1)];
+          for (int q = 0; q < 4; ++q) v[j][q] = p.states[ro + (unsigned)min(c + q, H + 1)];
+        }
         lastv[j] = p.states[ro + (unsigned)(H - 1)];
       }
 #pragma unroll
@@ -235,13 +243,7 @@ extern "C" hipError_t st_qserve_launch(const st::serve::ServeParams* p, int grid
   if (p->H < 2 || p->H + 3 > INP || p->ld < p->H + 2 || p->states == nullptr || p->actions == nullptr ||
       p->wq == nullptr || p->wf == nullptr || (long long)p->B * p->ld >= (1LL << 30))
     return hipErrorInvalidValue;
-  static int attr_set = 0;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)qserve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = 1;
-  }
+  const bool vec = (p->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(p->states) & 15) == 0);
   const int ntiles = (p->B + C - 1) / C;
   if (grid <= 0) {
     int dev = 0, cus = 256;
@@ -250,6 +252,9 @@ extern "C" hipError_t st_qserve_launch(const st::serve::ServeParams* p, int grid
     grid = 2 * cus;
   }
   if (grid > ntiles) grid = ntiles;
-  hipLaunchKernelGGL(qserve_kernel, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+  if (vec)
+    hipLaunchKernelGGL(qserve_kernel<true>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+  else
+    hipLaunchKernelGGL(qserve_kernel<false>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
   return hipGetLastError();
 }

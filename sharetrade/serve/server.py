@@ -44,6 +44,8 @@ class PolicyServer:
         m, a = self.cfg.model, self.cfg.agent
         self.layout = qn.QNetLayout.from_config(m)
         self.H = m.history
+        # request rows are staged at a 16-byte-aligned stride: the kernel's dwordx4 gather path
+        self.ld = (self.H + 2 + 3) // 4 * 4
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else \
                 torch.device("cpu")
@@ -100,7 +102,13 @@ class PolicyServer:
               return_q: bool = False) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
         """Actions (int32 [B], on the server's device) for request rows [B, H+2]; ``steps`` (the
         ``SelectionAction`` step of each row) turns on the epsilon-greedy draw, None = greedy."""
-        x = self._rows(states).to(self.device, non_blocking=True)
+        x = self._rows(states)
+        if self.backend == "native":
+            xd = torch.empty(x.shape[0], self.ld, dtype=torch.float32, device=self.device)
+            xd[:, : self.H + 2].copy_(x, non_blocking=True)
+            x = xd
+        else:
+            x = x.to(self.device)
         st = None if steps is None else torch.as_tensor(steps, dtype=torch.float32).reshape(-1).to(self.device)
         if st is not None and st.numel() != x.shape[0]:
             raise ValueError("one step per request row")
@@ -112,7 +120,7 @@ class PolicyServer:
             if self.backend == "native":
                 acts = torch.empty(x.shape[0], dtype=torch.int32, device=self.device)
                 q = torch.empty(x.shape[0], 3, dtype=torch.float32, device=self.device) if return_q else None
-                self._kern.launch(x.contiguous(), acts, q, st, seq=seq)
+                self._kern.launch(x, acts, q, st, seq=seq)
             else:
                 acts, q = self._torch_select(x, st, seq)
         return (acts, q) if return_q else acts
@@ -150,11 +158,11 @@ class DynamicBatcher:
         self._q: List[Tuple[np.ndarray, float, Future]] = []
         self._stop = False
         self.batch_sizes: List[int] = []
-        W = server.H + 2
+        W = server.ld   # aligned row stride (the first H + 2 values of a row are the request)
         self._native = server.backend == "native"
         if self._native:
             dev = server.device
-            self._h_x = torch.empty(self.max_batch, W, dtype=torch.float32, pin_memory=True)
+            self._h_x = torch.zeros(self.max_batch, W, dtype=torch.float32, pin_memory=True)
             self._h_s = torch.empty(self.max_batch, dtype=torch.float32, pin_memory=True)
             self._h_a = torch.empty(self.max_batch, dtype=torch.int32, pin_memory=True)
             self._d_x = torch.empty(self.max_batch, W, dtype=torch.float32, device=dev)
@@ -228,7 +236,7 @@ class DynamicBatcher:
         with srv._lock:
             seq = srv.seq
             srv.seq += 1
-        self._h_x[:n].numpy()[:] = X
+        self._h_x[:n, : X.shape[1]].numpy()[:] = X
         self._h_s[:n].numpy()[:] = S
         with torch.cuda.stream(self._stream):
             self._d_x[:n].copy_(self._h_x[:n], non_blocking=True)

@@ -115,3 +115,18 @@ def test_batcher_native_path(native_built):
         for t in ts:
             t.join()
     assert out == want
+
+
+def test_aligned_and_unaligned_gathers_agree(native_built):
+    """Rows at stride 203 (dword gather) and at the server's aligned stride 204 (dwordx4 gather)."""
+    from sharetrade.serve import PolicyServer
+
+    srv = PolicyServer(_cfg(), device=torch.device("cuda", 0), backend="native")
+    x = _rows(777, seed=13)
+    a, q = srv.infer(x, torch.full((777,), 700.0), return_q=True)   # aligned staging, batch seq 0
+    xd = x.cuda().contiguous()
+    assert xd.stride(0) == 203
+    a2 = torch.empty(777, dtype=torch.int32, device="cuda")
+    q2 = torch.empty(777, 3, device="cuda")
+    srv._kern.launch(xd, a2, q2, torch.full((777,), 700.0, device="cuda"), seq=0)
+    assert torch.equal(q2, q) and torch.equal(a2, a)
