@@ -7,6 +7,8 @@ Commands
 ``engine``  run the vectorised engine directly for N steps and print metrics.
 ``deep``    train the 4x1024-MLP replay DQN (BASELINE config 4) for N iterations.
 ``recurrent`` train the GRU(256) minute-bar DQN (BASELINE config 5) for N iterations.
+``serve``   serve SelectionAction over HTTP from the batched GPU kernel (weights from an
+            engine checkpoint or random init).
 ``config``  print the resolved configuration (JSON).
 
 Common flags: ``--preset {reference_compat,intended,flagship,test}``,
@@ -32,9 +34,10 @@ def _cfg(a) -> Config:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="sharetrade")
     sub = ap.add_subparsers(dest="cmd", required=True)
-    for name in ("train", "engine", "deep", "recurrent", "config"):
+    for name in ("train", "engine", "deep", "recurrent", "serve", "config"):
         p = sub.add_parser(name)
-        p.add_argument("--preset", default={"deep": "flagship", "recurrent": "recurrent"}.get(name, "reference_compat"))
+        p.add_argument("--preset", default={"deep": "flagship", "recurrent": "recurrent",
+                                            "serve": "flagship"}.get(name, "reference_compat"))
         p.add_argument("--config", default=None)
         p.add_argument("--set", action="append", default=[])
         if name == "train":
@@ -66,6 +69,13 @@ def main(argv=None) -> int:
             p.add_argument("--no-graph", action="store_true")
             p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
             p.add_argument("--trace", default=None, help="Chrome trace output path (torch.profiler)")
+        if name == "serve":
+            p.add_argument("--ckpt", default=None, help="engine checkpoint file or directory (default: random init)")
+            p.add_argument("--host", default="127.0.0.1")
+            p.add_argument("--port", type=int, default=8000)
+            p.add_argument("--device", default="auto")
+            p.add_argument("--max-batch", type=int, default=4096)
+            p.add_argument("--max-delay-us", type=float, default=200.0)
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -101,6 +111,21 @@ def main(argv=None) -> int:
         if ctx.is_main:
             print(json.dumps(res, default=float))
         D.shutdown(ctx)
+        return 0
+    if a.cmd == "serve":
+        import uvicorn
+
+        from .serve import DynamicBatcher, PolicyServer
+        from .serve.http import load_checkpoint_params, make_app
+        from .trainer.engine import resolve_device
+
+        params = load_checkpoint_params(a.ckpt) if a.ckpt else None
+        srv = PolicyServer(cfg, params=params, device=resolve_device(a.device))
+        bat = DynamicBatcher(srv, max_batch=a.max_batch, max_delay_us=a.max_delay_us)
+        try:
+            uvicorn.run(make_app(srv, bat), host=a.host, port=a.port, log_level="warning")
+        finally:
+            bat.close()
         return 0
     if a.cmd == "engine":
         from .parallel import dist as D

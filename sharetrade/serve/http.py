@@ -1,0 +1,103 @@
+"""HTTP front end of the policy server (FastAPI): ``python -m sharetrade serve``.
+
+Routes (JSON):
+
+* ``POST /selection_action`` ``{"current_state": [203 floats], "step": s}`` -> ``{"action": "Buy"|"Sell"|"Hold",
+  "index": i}`` -- the reference's ``SelectionAction`` message (``QDecisionPolicyActor.scala:32,56-62``),
+  one request per call, grouped with concurrent calls by the :class:`DynamicBatcher`;
+* ``POST /select`` ``{"states": [[...], ...], "steps": [...] | null, "return_q": bool}`` -> ``{"actions": [...],
+  "q": [[...]]}`` -- a whole batch in one launch (``steps`` null = greedy);
+* ``POST /load`` ``{"checkpoint": path}`` -> swaps in the weights of an engine checkpoint;
+* ``GET /health`` -> backend, device, served batches / requests.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+from typing import List, Optional
+
+import torch
+from pydantic import BaseModel
+
+from ..protocol import action_of
+from .server import DynamicBatcher, PolicyServer
+
+
+def load_checkpoint_params(path: str) -> torch.Tensor:
+    """Flat fp32 params from an engine checkpoint: a ``.stck`` file, a ``CheckpointManager`` directory
+    (latest file) or a sharded multi-rank directory (rank 0 of the newest committed step)."""
+    from ..persist.checkpoint import CheckpointManager, load
+
+    if os.path.isdir(path):
+        from ..parallel.dp_train import committed_steps
+
+        steps = committed_steps(path)
+        if steps:
+            path = os.path.join(path, f"step-{steps[-1]:09d}", "rank-0.stck")
+        else:
+            latest = CheckpointManager(path).latest()
+            if latest is None:
+                raise FileNotFoundError(f"no checkpoint under {path}")
+            path = latest
+    state, _ = load(path)
+    if "params" not in state:
+        raise KeyError(f"{path} holds no 'params' tensor (not an engine checkpoint)")
+    return state["params"]
+
+
+class SelectionActionReq(BaseModel):
+    current_state: List[float]
+    step: float = 0.0
+
+
+class SelectReq(BaseModel):
+    states: List[List[float]]
+    steps: Optional[List[float]] = None
+    return_q: bool = False
+
+
+class LoadReq(BaseModel):
+    checkpoint: str
+
+
+def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
+    from fastapi import FastAPI, HTTPException
+
+    app = FastAPI(title="sharetrade policy server")
+
+    @app.post("/selection_action")
+    async def selection_action(req: SelectionActionReq):
+        if len(req.current_state) != server.H + 2:
+            raise HTTPException(400, f"policy input size({server.H + 2}) and state({len(req.current_state)}) "
+                                     f"size do not match")
+        if batcher is not None:
+            a = await asyncio.wrap_future(batcher.submit(req.current_state, req.step))
+        else:
+            a = int(server.infer([req.current_state], [req.step]).cpu()[0])
+        return {"action": repr(action_of(a)), "index": int(a)}
+
+    @app.post("/select")
+    def select(req: SelectReq):
+        try:
+            out = server.infer(req.states, req.steps, return_q=req.return_q)
+        except ValueError as e:
+            raise HTTPException(400, str(e))
+        if req.return_q:
+            acts, q = out
+            return {"actions": acts.cpu().tolist(), "q": q.cpu().tolist()}
+        return {"actions": out.cpu().tolist()}
+
+    @app.post("/load")
+    def load(req: LoadReq):
+        try:
+            server.load_params(load_checkpoint_params(req.checkpoint))
+        except (OSError, KeyError, ValueError) as e:
+            raise HTTPException(400, str(e))
+        return {"loaded": req.checkpoint}
+
+    @app.get("/health")
+    def health():
+        return {"backend": server.backend, "device": str(server.device), "batches": server.batches,
+                "requests": server.requests, "params": server.layout.numel}
+
+    return app

@@ -130,3 +130,21 @@ def test_aligned_and_unaligned_gathers_agree(native_built):
     q2 = torch.empty(777, 3, device="cuda")
     srv._kern.launch(xd, a2, q2, torch.full((777,), 700.0, device="cuda"), seq=0)
     assert torch.equal(q2, q) and torch.equal(a2, a)
+
+
+def test_http_front_end_native(native_built):
+    from fastapi.testclient import TestClient
+
+    from sharetrade.serve import DynamicBatcher, PolicyServer
+    from sharetrade.serve.http import make_app
+
+    srv = PolicyServer(_cfg(), device=torch.device("cuda", 0), backend="native")
+    x = _rows(9, seed=21)
+    want = srv.infer(x).cpu().tolist()
+    with DynamicBatcher(srv, max_batch=32, max_delay_us=500, greedy=True) as bat:
+        c = TestClient(make_app(srv, bat))
+        r = c.post("/select", json={"states": x.tolist()})
+        assert r.status_code == 200 and r.json()["actions"] == want
+        r = c.post("/selection_action", json={"current_state": x[4].tolist(), "step": 0.0})
+        assert r.status_code == 200 and r.json()["index"] == want[4]   # greedy batcher
+        assert c.get("/health").json()["backend"] == "native"

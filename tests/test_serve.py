@@ -147,3 +147,68 @@ def test_serving_actor_wrong_shape_and_load_policy(system):
     kit.tell(act, LoadPolicy(new))
     kit.expect_msg(PolicyLoaded)
     assert torch.equal(srv.params, new)
+
+
+def test_http_front_end(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from sharetrade.persist.checkpoint import CheckpointManager
+    from sharetrade.serve.http import load_checkpoint_params, make_app
+
+    srv = _server(eps=1.0)
+    x = _rows(6, seed=8)
+    with DynamicBatcher(srv, max_batch=16, max_delay_us=1000) as bat:
+        c = TestClient(make_app(srv, bat))
+        r = c.post("/select", json={"states": x.tolist(), "return_q": True})
+        assert r.status_code == 200
+        want = srv.infer(x).tolist()
+        assert r.json()["actions"] == want and len(r.json()["q"]) == 6
+        # the reference's message shape: greedy at step 1e9 with eps = 1
+        r = c.post("/selection_action", json={"current_state": x[2].tolist(), "step": 1e9})
+        assert r.status_code == 200 and r.json()["index"] == want[2]
+        assert r.json()["action"] == ("Buy", "Sell", "Hold")[want[2]]
+        assert c.post("/selection_action", json={"current_state": [1.0, 2.0], "step": 0}).status_code == 400
+        assert c.post("/select", json={"states": [[1.0, 2.0]]}).status_code == 400
+        # weights from an engine checkpoint (CheckpointManager directory)
+        new = qn.init_params(srv.layout, srv.cfg.model, seed=77)
+        CheckpointManager(str(tmp_path), interval=1).save(5, {"params": new, "step": torch.tensor([5])})
+        assert torch.equal(load_checkpoint_params(str(tmp_path)), new)
+        r = c.post("/load", json={"checkpoint": str(tmp_path)})
+        assert r.status_code == 200 and torch.equal(srv.params, new)
+        assert c.post("/load", json={"checkpoint": str(tmp_path / "missing")}).status_code == 400
+        h = c.get("/health").json()
+        assert h["backend"] == "torch" and h["requests"] >= 8
+
+
+def test_cli_serve_process():
+    """``python -m sharetrade serve`` as a process: health and one SelectionAction over HTTP."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    import httpx
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    proc = subprocess.Popen([sys.executable, "-m", "sharetrade", "serve", "--device", "cpu", "--port", str(port)],
+                            cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        url = f"http://127.0.0.1:{port}"
+        for _ in range(300):
+            try:
+                if httpx.get(url + "/health", timeout=1.0).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                time.sleep(0.1)
+        else:
+            raise AssertionError("server did not come up")
+        r = httpx.post(url + "/selection_action", json={"current_state": _rows(1)[0].tolist(), "step": 5.0},
+                       timeout=10.0)
+        assert r.status_code == 200 and r.json()["action"] in ("Buy", "Sell", "Hold")
+    finally:
+        proc.terminate()
+        proc.wait(timeout=30)
