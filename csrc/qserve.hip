@@ -15,10 +15,14 @@
 //  * every weight lives in VGPRs for the whole launch: a wave owns 32 hidden units of both hidden
 //    layers (A operands: 2 m-tiles x (7 + 4) k-steps of v_mfma_f32_16x16x32_bf16 fragments) and the
 //    output-layer fragments (4 k-steps), 104 registers per lane, loaded once per workgroup;
-//  * LDS holds only the 64-row activation tiles (X, H1; H2 reuses X): 49 KB, so two workgroups share
-//    a CU and one's feature gather overlaps the other's MFMA phases;
-//  * persistent grid (<= 2 workgroups per CU) walking 64-row tiles, so the per-workgroup weight load
-//    (~90 KB of L2 reads) is paid once per launch, not once per tile.
+//  * persistent grid walking 64-row tiles, so the per-workgroup weight load (~106 KB of L2 reads) is
+//    paid once per launch, not once per tile;
+//  * STREAM (rows at a 16-byte-aligned stride <= 208 floats): the next tile's raw rows stream into a
+//    second LDS buffer by LDS-DMA (global_load_lds_dwordx4, one contiguous 64 x ld block) for the
+//    whole of the current tile; the phases are separated by raw s_barriers that wait for LDS traffic
+//    only, so the DMA stays in flight across them.  One workgroup per CU (156 KB of LDS);
+//  * otherwise (any stride): register gather with every load unconditional (clamped indices) and 7
+//    quads x 5 loads in flight per thread; activation tiles only in LDS (49 KB), two workgroups per CU.
 #include "common.h"
 
 namespace st {
@@ -31,7 +35,24 @@ constexpr int NET = C / 16;                     // 16-row tiles per tile
 constexpr int MT = HP / (16 * NW);              // 16-unit m-tiles per wave (2)
 constexpr int KS0 = INP / 32, KS1 = HP / 32;
 constexpr int SX = INP + 16, SH = HP + 16;      // activation row strides (bf16)
-constexpr int LDS_BYTES = (C * SX + C * SH) * 2;
+constexpr int MAXLD = 208;                      // STREAM: widest row stride staged (floats)
+constexpr int ACT_BYTES = (C * SX + C * SH) * 2;
+constexpr int RAW_BYTES = 2 * C * MAXLD * 4;    // two row buffers: tile t+1 lands while tile t runs
+constexpr int LDS_BYTES = ACT_BYTES;                                   // register-gather build
+constexpr int LDS_BYTES_STREAM = RAW_BYTES + ACT_BYTES + 2 * C * 4;    // + staged rows, steps, 1/last
+
+// s_waitcnt immediates (gfx9 split vmcnt field): lgkmcnt(0) only / vmcnt(0) only
+ST_DEV void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4)); }
+ST_DEV void wait_vm0() { __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8)); }
+// global_load_lds_dwordx4 issued from inline asm: with the builtin, hipcc orders every later LDS store
+// behind the DMA (s_waitcnt vmcnt(0) at the first ds_write after it: the MFMA phases' epilogues), which
+// drains it one phase after the issue.  The kernel retires it itself (wait_vm0 before reading the rows).
+// lds_off: wave-uniform LDS byte offset of this wave-instruction's 1 KiB destination.
+ST_DEV void glds16(const float* gsrc, unsigned lds_off) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_off) : "memory");
+}
 
 struct ServeParams {
   const float* states;   // [B][ld] fp32 request rows: H prices, budget, shares
@@ -48,12 +69,14 @@ struct ServeParams {
   unsigned long long seq;   // draw counter: (row, seq_lo, seq_hi, stream 2)
 };
 
-// VEC: rows 16-byte aligned (ld % 4 == 0, aligned base): one dwordx4 load per column quad
-template <bool VEC>
-__global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
+template <bool STREAM>
+__global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* sX = reinterpret_cast<bf16_t*>(smem);   // [C][SX]; also H2 [C][SH] after layer 1
+  float* sRaw = reinterpret_cast<float*>(smem);   // STREAM: the tile's raw rows [C][ld]
+  bf16_t* sX = reinterpret_cast<bf16_t*>(smem + (STREAM ? RAW_BYTES : 0));   // [C][SX]; H2 [C][SH] later
   bf16_t* sH1 = sX + C * SX;                        // [C][SH]
+  float* sSteps = reinterpret_cast<float*>(reinterpret_cast<char*>(sX) + ACT_BYTES);   // STREAM: [C]
+  float* sInv = sSteps + C;                                                            // STREAM: [C]
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = 16 * MT * wave;
@@ -84,57 +107,105 @@ __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
 #pragma unroll
   for (int j = 0; j < 3; ++j) b2[j] = p.wf[p.off_b2 + j];
 
+  // barrier between phases: STREAM waits for LDS traffic only (a __syncthreads() would also drain the
+  // row DMA in flight: vmcnt(0))
+  auto bar = [&]() {
+    if constexpr (STREAM) {
+      wait_lgkm0();
+      asm volatile("s_barrier" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
+  // STREAM: tile t's rows = one contiguous block of C * ld floats = ld / 4 wave-instructions of 64 x 16 B
+  // (pieces past the end of the array re-read its last 16 B: those rows are not live)
+  const unsigned npieces = (unsigned)p.B * (unsigned)p.ld / 4u;
+  auto stage = [&](int t, int buf) {
+    const unsigned base = (unsigned)t * (unsigned)C * (unsigned)p.ld / 4u;
+    const unsigned raw0 = (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)sRaw) +
+                          (unsigned)buf * (unsigned)(C * MAXLD * 4);
+    for (int j = wave; j < p.ld / 4; j += NW) {
+      const unsigned pc = min(base + (unsigned)(j * 64 + lane), npieces - 1u);
+      glds16(p.states + 4u * pc, __builtin_amdgcn_readfirstlane(raw0 + (unsigned)j * 1024u));
+    }
+  };
+
   const int ntiles = (p.B + C - 1) / C;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  if constexpr (STREAM) {
+    if ((int)blockIdx.x < ntiles) stage(blockIdx.x, 0);
+  }
+  int it_ = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it_) {
     const int r0 = tile * C;
+    const float* rows = sRaw + (it_ & 1) * (C * MAXLD);   // STREAM: this tile's staged rows
+    if constexpr (STREAM) {
+      wait_vm0();   // this wave's row DMA (and the previous tile's output stores) landed
+      if (tid < C) sSteps[tid] = p.steps != nullptr ? p.steps[min(r0 + tid, p.B - 1)] : 0.f;
+      bar();        // every wave's DMA landed; every wave is done with the other buffer
+      // the next tile's rows stream into the other buffer through this whole tile
+      if (tile + (int)gridDim.x < ntiles) stage(tile + gridDim.x, (it_ + 1) & 1);
+      // one correctly rounded 1 / last price per row (torch: 1.0 / last), not one per column quad
+      if (tid < C) sInv[tid] = p.feat_mode ? __fdiv_rn(1.0f, rows[tid * p.ld + H - 1]) : 1.0f;
+      bar();
+    }
     // -------------------------------------------------------------- P0: request rows -> features
-    // 64 rows x 56 column quads, 14 quads per thread in two batches of 7: every load unconditional
-    // (row and column indices clamped), all of a batch in flight before the first use -- loads under
-    // per-element branches were issued one wait at a time (~8 us per tile).  The row's last price
-    // (the relative-feature normaliser) is one more load per quad; budget / shares are columns H,
-    // H+1 of the quad that covers them.
-    constexpr int QPR = INP / 4, QPT = C * QPR / NT, QB = 7;
-    static_assert(QPT % QB == 0, "quad batches");
+    // Thread = (row tid / 4, column quads tid % 4 + 4m, m < 14): the row offset, the row's 1 / last
+    // price and its liveness are per thread, and quad slot m is a price quad on every lane while
+    // 16m + 15 < H (a scalar branch: packed fp32 mul / sub, then bf16); only the slots reaching
+    // columns H .. H+2 (budget, shares, the constant-1 bias input) take the select chain.  Two batches of 7
+    // quads, all loads of a batch in flight before its first use (register gather: unconditional,
+    // clamped loads -- loads under per-element branches were issued one wait at a time).
+    {
+      constexpr int QB = 7, NQ = INP / 16;   // 14 quads per thread
+      const int r = tid >> 2, t4 = tid & 3;
+      const bool live = r0 + r < p.B;
+      const unsigned ro = (unsigned)min(r0 + r, p.B - 1) * (unsigned)p.ld;   // host: B * ld < 2^30
+      const float* rowp = STREAM ? rows + r * p.ld : nullptr;
+      const float last = STREAM ? rowp[H - 1] : p.states[ro + (unsigned)(H - 1)];
+      const float inv = !p.feat_mode ? 1.0f : STREAM ? sInv[r] : __fdiv_rn(1.0f, last);
+      const int cmax = (H + 1) & ~3;   // the last quad holding row data (column H + 1)
+      // price quads: x * iv - off with (iv, off) = (1 / last, 1) relative, (1, 0) raw (exact), (0, 0) for a
+      // row past B (its clamped, finite values give 0): no per-quad selects
+      const float ivq = live ? inv : 0.f, offq = (live && p.feat_mode) ? 1.0f : 0.f;
 #pragma unroll 1
-    for (int qb = 0; qb < QPT; qb += QB) {
-      float v[QB][4], lastv[QB];
+      for (int mb = 0; mb < NQ; mb += QB) {
+        float v[QB][4];
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        const int it = tid + NT * (qb + j), r = it / QPR, c = 4 * (it - r * QPR);
-        // 32-bit element offsets off one uniform base (the host checks B * ld < 2^30)
-        const unsigned ro = (unsigned)min(r0 + r, p.B - 1) * (unsigned)p.ld;
-        if constexpr (VEC) {
-          // quads past the one holding column H+1 re-read it: their columns take no row value
-          const float4 t = *reinterpret_cast<const float4*>(p.states + ro + (unsigned)min(c, (H + 1) & ~3));
-          v[j][0] = t.x; v[j][1] = t.y; v[j][2] = t.z; v[j][3] = t.w;
-        } else {
+        for (int m = 0; m < QB; ++m) {
+          const int c = min(4 * (t4 + 4 * (mb + m)), cmax);
+          if constexpr (STREAM) {
+            const float4 t = *reinterpret_cast<const float4*>(rowp + c);
+            v[m][0] = t.x; v[m][1] = t.y; v[m][2] = t.z; v[m][3] = t.w;
+          } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[j][q] = p.states[ro + (unsigned)min(c + q, H + 1)];
+            for (int q = 0; q < 4; ++q) v[m][q] = p.states[ro + (unsigned)min(c + q, H + 1)];
+          }
         }
-        lastv[j] = p.states[ro + (unsigned)(H - 1)];
-      }
 #pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        const int it = tid + NT * (qb + j), r = it / QPR, c = 4 * (it - r * QPR);
-        const bool live = r0 + r < p.B;
-        const float last = lastv[j];
-        const float inv = p.feat_mode ? __fdiv_rn(1.0f, last) : 1.0f;
-        float x[4];
+        for (int m = 0; m < QB; ++m) {
+          const int c = 4 * (t4 + 4 * (mb + m));
+          float x[4];
+          if (16 * (mb + m) + 15 < H) {   // prices only, on every lane of the wave (a scalar branch)
+            // packed fp32 mul then sub: the same IEEE roundings as feat_price
+            const f32x2_t iv = {ivq, ivq}, off = {offq, offq};
+            const f32x2_t x01 = f32x2_t{v[m][0], v[m][1]} * iv - off, x23 = f32x2_t{v[m][2], v[m][3]} * iv - off;
+            lds_st4(sX + r * SX + c, x01.x, x01.y, x23.x, x23.y);
+          } else {   // quads at / past column H: budget, shares, the constant 1, padding
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = c + q;
-          const float w = v[j][q];
-          float f = 0.f;
-          if (k < H) f = p.feat_mode ? __fsub_rn(__fmul_rn(w, inv), 1.0f) : w;
-          else if (k == H) f = p.feat_mode ? __fmul_rn(w, p.inv_b0) : w;
-          else if (k == H + 1) f = p.feat_mode ? __fmul_rn(__fmul_rn(w, last), p.inv_b0) : w;
-          else if (k == H + 2) f = 1.0f;   // constant-1 column: layer 1's bias
-          x[q] = live ? f : 0.f;
+            for (int q = 0; q < 4; ++q) {
+              const int k = c + q;
+              const float w = v[m][q];
+              const float fp = p.feat_mode ? __fsub_rn(__fmul_rn(w, inv), 1.0f) : w;
+              const float fb = p.feat_mode ? __fmul_rn(w, p.inv_b0) : w;
+              const float fs = p.feat_mode ? __fmul_rn(__fmul_rn(w, last), p.inv_b0) : w;
+              x[q] = live ? (k < H ? fp : k == H ? fb : k == H + 1 ? fs : k == H + 2 ? 1.0f : 0.0f) : 0.0f;
+            }
+            lds_st4(sX + r * SX + c, x[0], x[1], x[2], x[3]);
+          }
         }
-        lds_st4(sX + r * SX + c, x[0], x[1], x[2], x[3]);
       }
     }
-    __syncthreads();
+    bar();
     // -------------------------------------------------------------- P1: layer 1
     {
       f4v acc[MT][NET];
@@ -161,7 +232,7 @@ __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
                   fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
         }
     }
-    __syncthreads();
+    bar();
     // -------------------------------------------------------------- P2: layer 2 (+ b1) -> H2 (over X)
     bf16_t* sH2 = sX;
     {
@@ -189,7 +260,7 @@ __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
                   fmaxf(v[1] + bb[i][1], 0.f), fmaxf(v[2] + bb[i][2], 0.f), fmaxf(v[3] + bb[i][3], 0.f));
         }
     }
-    __syncthreads();
+    bar();
     // -------------------------------------------------------------- P3: output, argmax, epsilon-greedy
     {
       f4v acc = zero4();   // wave w: 16-row tile w; lanes g4 == 0 end up with q[0..3] of row 16w + l16
@@ -213,7 +284,8 @@ __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
                    c3 = 2u;
           philox4x32(c0, c1, c2, c3, p.key0, p.key1);
           const float u1 = u24(c0), u2 = u24(c1);
-          const bool exploit = u1 < fminf(p.eps, __fmul_rn(p.steps[row], p.inv_ramp));
+          const float st = STREAM ? sSteps[16 * wave + l16] : p.steps[row];
+          const bool exploit = u1 < fminf(p.eps, __fmul_rn(st, p.inv_ramp));
           int rnd = (int)(u2 * 3.0f);
           rnd = rnd > 2 ? 2 : rnd;
           a = exploit ? a : rnd;
@@ -226,16 +298,17 @@ __global__ void __launch_bounds__(NT, 2) qserve_kernel(ServeParams p) {
         }
       }
     }
-    __syncthreads();   // the next tile's features overwrite X / H2
+    bar();   // the next tile's features overwrite X / H2 (and its steps sSteps)
   }
+  if constexpr (STREAM) wait_vm0();
 }
 
 }  // namespace serve
 }  // namespace st
 
-extern "C" int st_qserve_lds_bytes() { return st::serve::LDS_BYTES; }
+extern "C" int st_qserve_lds_bytes(int stream) { return stream ? st::serve::LDS_BYTES_STREAM : st::serve::LDS_BYTES; }
 
-// grid <= 0: min(tiles, 2 x CUs).  Pre-launch checks: the padded dims are fixed (224 / 128 / 16) and the
+// grid <= 0: min(tiles, CUs) (STREAM) or min(tiles, 2 x CUs).  Pre-launch checks: the padded dims are fixed (224 / 128 / 16) and the
 // request rows must hold H + 2 values with H + 3 <= 224 (prices, budget, shares, constant 1).
 extern "C" hipError_t st_qserve_launch(const st::serve::ServeParams* p, int grid, hipStream_t stream) {
   using namespace st::serve;
@@ -243,17 +316,26 @@ extern "C" hipError_t st_qserve_launch(const st::serve::ServeParams* p, int grid
   if (p->H < 2 || p->H + 3 > INP || p->ld < p->H + 2 || p->states == nullptr || p->actions == nullptr ||
       p->wq == nullptr || p->wf == nullptr || (long long)p->B * p->ld >= (1LL << 30))
     return hipErrorInvalidValue;
-  const bool vec = (p->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(p->states) & 15) == 0);
+  const bool strm = (p->ld % 4 == 0) && p->ld <= MAXLD && ((reinterpret_cast<uintptr_t>(p->states) & 15) == 0);
+  if (strm) {
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute((const void*)qserve_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         LDS_BYTES_STREAM);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+  }
   const int ntiles = (p->B + C - 1) / C;
   if (grid <= 0) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = 2 * cus;
+    grid = (strm ? 1 : 2) * cus;
   }
   if (grid > ntiles) grid = ntiles;
-  if (vec)
-    hipLaunchKernelGGL(qserve_kernel<true>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+  if (strm)
+    hipLaunchKernelGGL(qserve_kernel<true>, dim3(grid), dim3(NT), LDS_BYTES_STREAM, stream, *p);
   else
     hipLaunchKernelGGL(qserve_kernel<false>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
   return hipGetLastError();
