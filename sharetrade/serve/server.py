@@ -79,6 +79,9 @@ class PolicyServer:
         if flat.numel() != self.layout.numel:
             raise ValueError(f"expected {self.layout.numel} flat params, got {flat.numel()}")
         with self._lock:
+            if self.device.type == "cuda":
+                # launches already queued (any stream: the batcher has its own) still read the old set
+                torch.cuda.synchronize(self.device)
             self.params.copy_(flat.to(self.device))
             self.params_bf.copy_(self.params.to(torch.bfloat16))
             if self.device.type == "cuda":
