@@ -83,6 +83,14 @@ constexpr bool ASWZ = ST_WIDE_ASWZ;
 // multiplies) are computed in P1 by the last wave for all 64 envs (lane = env row) and left in
 // sEnvI[.][2]; P3 only resolves exploit ? argmax : random action.  Same draws, same actions.
 constexpr bool DRAW_EARLY = ST_WIDE_DRAW_EARLY;
+#ifndef ST_WIDE_OFOLD
+#define ST_WIDE_OFOLD 0
+#endif
+// OFOLD: the output layer of Q(x) folded into layer 2's epilogue -- each wave multiplies its own 16
+// bf16-rounded h2 units (its accumulator tile IS the B operand of a 16x16x16 MFMA) by its W2 slice and
+// leaves a partial q in LDS (R1, dead from P1 to P4); P3 sums the eight partials in wave order instead
+// of running the 4-deep dependent fwd_out chain (same operands, fp32 summation order differs).
+constexpr bool OFOLD = ST_WIDE_OFOLD;
 // asw(r, lo): the swizzled offset of column base + lo for a base that is a multiple of 16 and lo < 16
 // (then (base + lo) ^ 8 bit2(r) = base + (lo ^ 8 bit2(r)): the base stays an immediate offset)
 ST_DEV int asw(int r, int lo) { return ASWZ ? (lo ^ ((r & 4) << 1)) : lo; }
@@ -139,8 +147,9 @@ struct Geo {
 // out^T[m][env] for this wave's MT m-tiles and the chunk's NET env tiles; A fragments given per
 // (m-tile, k-step) by the functor, B = activation rows.  Epilogue: + bias, ReLU, bf16 store into
 // out image [env][m].
-template <int MT, int K, int SB, int SO, bool ALDS, typename AFrag>
-ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* bias, int m0, int l16, int g4) {
+template <int MT, int K, int SB, int SO, bool ALDS, typename AFrag, bool OF = false, int SW2_ = 0>
+ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* bias, int m0, int l16, int g4,
+                       const bf16_t* sW2 = nullptr, float* sPart = nullptr, int wave = 0) {
   float bb[MT][4];   // bias read up front (its LDS latency under the MFMAs)
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -193,6 +202,28 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
 #pragma unroll
       for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(a, b[n], acc[i][n]);
     }
+  }
+  if constexpr (OF) {
+    // partial q^T[a][env] = W2[a][this wave's units] . h2[units][env]: lane (env l16, g4) holds units
+    // 4 g4 .. 4 g4 + 3 of its accumulator -- the B-operand layout of v_mfma_f32_16x16x16_bf16
+    s4v aw[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) aw[i] = lds_ld4(sW2 + l16 * SW2_ + m0 + 16 * i + 4 * g4);
+#pragma unroll
+    for (int n = 0; n < NET; ++n) {
+      f4v pq = zero4();
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const f4v v = acc[i][n];
+        uint2 hv;
+        hv.x = pack_bf2(fmaxf(v[0] + bb[i][0], 0.f), fmaxf(v[1] + bb[i][1], 0.f));
+        hv.y = pack_bf2(fmaxf(v[2] + bb[i][2], 0.f), fmaxf(v[3] + bb[i][3], 0.f));
+        *reinterpret_cast<uint2*>(sO + (16 * n + l16) * SO + m0 + 16 * i + asw(l16, 4 * g4)) = hv;
+        pq = mfma16(aw[i], __builtin_bit_cast(s4v, hv), pq);
+      }
+      if (g4 == 0) *reinterpret_cast<f4v*>(sPart + (wave * C + 16 * n + l16) * 4) = pq;   // actions 0..3
+    }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -561,13 +592,27 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     fwd_hidden<MT, INP, G::SX, G::SH1, false>(a_w0, sX, sH1, nullptr, m0, l16, g4);
     if (dyn && tid == 0) sCl[0] = dyn_chunk((unsigned)gx + claim_v);   // read in P9
     __syncthreads();
-    fwd_hidden<MT, H1P, G::SH1, G::SH2, true>(a_w1, sH1, sH2, sB1, m0, l16, g4);
+    float* sPart = reinterpret_cast<float*>(sR1);   // OFOLD: [NW][C][4] partial q (R1 is dead until P4)
+    if constexpr (OFOLD)
+      fwd_hidden<MT, H1P, G::SH1, G::SH2, true, decltype(a_w1), true, G::SW2>(a_w1, sH1, sH2, sB1, m0, l16, g4, sW2,
+                                                                            sPart, wave);
+    else
+      fwd_hidden<MT, H1P, G::SH1, G::SH2, true>(a_w1, sH1, sH2, sB1, m0, l16, g4);
     __syncthreads();
     STW_STAMP(2);
     // ------------------------------------------------------------ P3: Q(x), epsilon-greedy, env step
     // wave w < NET: output tile of env tile w; lanes g4 == 0 own env 16*w + l16
     if (wave < NET) {
-      const f4v qa = fwd_out<H2P, G::SW2, G::SH2>(sW2, sH2, wave, l16, g4);
+      f4v qa;
+      if constexpr (OFOLD) {
+        qa = zero4();
+        if (g4 == 0) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) qa += *reinterpret_cast<const f4v*>(sPart + (w * C + 16 * wave + l16) * 4);
+        }
+      } else {
+        qa = fwd_out<H2P, G::SW2, G::SH2>(sW2, sH2, wave, l16, g4);
+      }
       if (g4 == 0) {
         const int r = 16 * wave + l16, e = ebase + r;
         float q[3];

@@ -465,3 +465,29 @@ def test_graph_priming_is_rank_uniform(native_built):
     s1 = eng.step_count
     assert eng.prime_graph(5) == 5 and eng.step_count == s1 + 20
     eng.world_size = 1
+
+
+def test_ofold_variant_matches_default(native_built):
+    """engine.step_variant = "ofold" (Q(x)'s output layer folded into layer 2's epilogue) vs the default
+    8-wave kernel: same operands, fp32 summation order of q differs -> actions equal except near-ties,
+    gradients equal to fp32 rounding."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 256
+    prices = _prices(E, seed=9)
+    dev = torch.device("cuda", 0)
+    out = []
+    for variant in ("", "ofold"):
+        cfg = _cfg()
+        cfg.agent.epsilon = 0.9
+        cfg.engine.step_variant = variant
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
+        eng.ctrl.fill_(2000)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        out.append((eng.actions_out.cpu().clone(), g))
+    (a0, g0), (a1, g1) = out
+    assert (a0 != a1).float().mean().item() <= 0.02
+    if torch.equal(a0, a1):
+        assert _rel(g1, g0) < 1e-3
