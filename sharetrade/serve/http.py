@@ -8,12 +8,15 @@ Routes (JSON):
 * ``POST /select`` ``{"states": [[...], ...], "steps": [...] | null, "return_q": bool}`` -> ``{"actions": [...],
   "q": [[...]]}`` -- a whole batch in one launch (``steps`` null = greedy);
 * ``POST /load`` ``{"checkpoint": path}`` -> swaps in the weights of an engine checkpoint;
-* ``GET /health`` -> backend, device, served batches / requests.
+* ``GET /health`` -> backend, device, served batches / requests;
+* ``GET /metrics`` -> Prometheus text format: requests / batches / errors per route, request latency
+  histogram, batch-size histogram of the dynamic batcher (one registry per app).
 """
 from __future__ import annotations
 
 import asyncio
 import os
+import time
 from typing import List, Optional
 
 import torch
@@ -62,26 +65,51 @@ class LoadReq(BaseModel):
 
 def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
     from fastapi import FastAPI, HTTPException
+    from fastapi.responses import Response
+    from prometheus_client import CONTENT_TYPE_LATEST, CollectorRegistry, Counter, Histogram, generate_latest
 
     app = FastAPI(title="sharetrade policy server")
+    reg = CollectorRegistry()
+    m_req = Counter("sharetrade_serve_requests", "request rows served", ["route"], registry=reg)
+    m_err = Counter("sharetrade_serve_errors", "rejected calls", ["route"], registry=reg)
+    m_lat = Histogram("sharetrade_serve_latency_seconds", "call latency", ["route"], registry=reg,
+                      buckets=(1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 1e-1, 1.0))
+    m_bs = Histogram("sharetrade_serve_batch_rows", "rows per kernel launch (batcher)", registry=reg,
+                     buckets=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 4096, 16384))
+    seen = {"batches": 0}
+
+    def _batch_sizes() -> None:   # fold the batcher's new batch sizes into the histogram
+        if batcher is not None:
+            bs = batcher.batch_sizes
+            for n in bs[seen["batches"]:len(bs)]:
+                m_bs.observe(n)
+            seen["batches"] = len(bs)
 
     @app.post("/selection_action")
     async def selection_action(req: SelectionActionReq):
+        t0 = time.perf_counter()
         if len(req.current_state) != server.H + 2:
+            m_err.labels("selection_action").inc()
             raise HTTPException(400, f"policy input size({server.H + 2}) and state({len(req.current_state)}) "
                                      f"size do not match")
         if batcher is not None:
             a = await asyncio.wrap_future(batcher.submit(req.current_state, req.step))
         else:
             a = int(server.infer([req.current_state], [req.step]).cpu()[0])
+        m_req.labels("selection_action").inc()
+        m_lat.labels("selection_action").observe(time.perf_counter() - t0)
         return {"action": repr(action_of(a)), "index": int(a)}
 
     @app.post("/select")
     def select(req: SelectReq):
+        t0 = time.perf_counter()
         try:
             out = server.infer(req.states, req.steps, return_q=req.return_q)
         except ValueError as e:
+            m_err.labels("select").inc()
             raise HTTPException(400, str(e))
+        m_req.labels("select").inc(len(req.states))
+        m_lat.labels("select").observe(time.perf_counter() - t0)
         if req.return_q:
             acts, q = out
             return {"actions": acts.cpu().tolist(), "q": q.cpu().tolist()}
@@ -99,5 +127,10 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
     def health():
         return {"backend": server.backend, "device": str(server.device), "batches": server.batches,
                 "requests": server.requests, "params": server.layout.numel}
+
+    @app.get("/metrics")
+    def metrics():
+        _batch_sizes()
+        return Response(generate_latest(reg), media_type=CONTENT_TYPE_LATEST)
 
     return app

@@ -178,6 +178,11 @@ def test_http_front_end(tmp_path):
         assert c.post("/load", json={"checkpoint": str(tmp_path / "missing")}).status_code == 400
         h = c.get("/health").json()
         assert h["backend"] == "torch" and h["requests"] >= 8
+        m = c.get("/metrics").text
+        assert 'sharetrade_serve_requests_total{route="select"} 6.0' in m
+        assert 'sharetrade_serve_requests_total{route="selection_action"} 1.0' in m
+        assert 'sharetrade_serve_errors_total{route="selection_action"} 1.0' in m
+        assert "sharetrade_serve_batch_rows_count 1.0" in m
 
 
 def test_cli_serve_process():
