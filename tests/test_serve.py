@@ -217,3 +217,28 @@ def test_cli_serve_process():
     finally:
         proc.terminate()
         proc.wait(timeout=30)
+
+
+def test_serve_weights_from_engine_checkpoints(tmp_path):
+    """Engine checkpoints in both layouts: a CheckpointManager directory and a sharded multi-rank one
+    (newest committed step, rank 0; an uncommitted newer step is ignored)."""
+    from sharetrade.parallel.dp_train import commit, save_shard
+    from sharetrade.serve.http import load_checkpoint_params
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    cfg.engine.envs_per_rank = 32
+    eng = VectorEngine(cfg, device=torch.device("cpu"), envs=32, backend="torch")
+    eng.run(2)
+    save_shard(str(tmp_path), 2, 0, eng)
+    commit(str(tmp_path), 2, 1)
+    want = eng.params.clone()
+    eng.run(1)
+    save_shard(str(tmp_path), 3, 0, eng)   # not committed
+    got = load_checkpoint_params(str(tmp_path))
+    assert torch.equal(got, want)
+    srv = _server()
+    srv.load_params(got)
+    x = _rows(4, seed=3)
+    a_eng = PolicyServer(eng.cfg, params=want, device=torch.device("cpu"), backend="torch").infer(x)
+    assert torch.equal(srv.infer(x), a_eng)
