@@ -30,9 +30,9 @@ namespace serve {
 
 constexpr int INP = 224, HP = 128, OUTP = 16;   // padded dims of the flagship layout (models/qnet.py)
 constexpr int C = 64;                           // request rows per tile
-constexpr int NW = 4, NT = 64 * NW;
+constexpr int NW = 4, NT = 64 * NW;             // register-gather build (STREAM: 8 waves, see the kernel)
 constexpr int NET = C / 16;                     // 16-row tiles per tile
-constexpr int MT = HP / (16 * NW);              // 16-unit m-tiles per wave (2)
+constexpr int MT = HP / (16 * NW);              // 16-unit m-tiles per wave (2; STREAM: 1)
 constexpr int KS0 = INP / 32, KS1 = HP / 32;
 constexpr int SX = INP + 16, SH = HP + 16;      // activation row strides (bf16)
 constexpr int MAXLD = 208;                      // STREAM: widest row stride staged (floats)
@@ -70,7 +70,11 @@ struct ServeParams {
 };
 
 template <bool STREAM>
-__global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams p) {
+__global__ void __launch_bounds__(STREAM ? 512 : 256, STREAM ? 1 : 2) qserve_kernel(ServeParams p) {
+  // STREAM: one workgroup per CU (156 KB of LDS) of 8 waves -- two per SIMD, each owning 16 hidden
+  // units -- so one wave's MFMAs overlap the other's VALU / LDS work; register gather: 4 waves x 32 units,
+  // two workgroups per CU
+  constexpr int NWk = STREAM ? 8 : 4, NTk = 64 * NWk, MTk = HP / (16 * NWk), TPR = NTk / C;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sRaw = reinterpret_cast<float*>(smem);   // STREAM: the tile's raw rows [C][ld]
   bf16_t* sX = reinterpret_cast<bf16_t*>(smem + (STREAM ? RAW_BYTES : 0));   // [C][SX]; H2 [C][SH] later
@@ -79,13 +83,13 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
   float* sInv = sSteps + C;                                                            // STREAM: [C]
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m0 = 16 * MT * wave;
+  const int m0 = 16 * MTk * wave;
   const int H = p.H;
 
   // ---------------------------------------------------------------- weights -> VGPRs (once)
-  s8v aW0[MT][KS0], aW1[MT][KS1], aW2[KS1];
+  s8v aW0[MTk][KS0], aW1[MTk][KS1], aW2[KS1];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
+  for (int i = 0; i < MTk; ++i) {
     const bf16_t* w0 = p.wq + p.off_w0 + (size_t)(m0 + 16 * i + l16) * INP + 8 * g4;
 #pragma unroll
     for (int ks = 0; ks < KS0; ++ks) aW0[i][ks] = *reinterpret_cast<const s8v*>(w0 + ks * 32);
@@ -98,9 +102,9 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
 #pragma unroll
     for (int ks = 0; ks < KS1; ++ks) aW2[ks] = *reinterpret_cast<const s8v*>(w2 + ks * 32);
   }
-  float bb[MT][4];
+  float bb[MTk][4];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < MTk; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) bb[i][j] = p.wf[p.off_b1 + m0 + 16 * i + 4 * g4 + j];
   float b2[3];
@@ -124,7 +128,7 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
     const unsigned base = (unsigned)t * (unsigned)C * (unsigned)p.ld / 4u;
     const unsigned raw0 = (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)sRaw) +
                           (unsigned)buf * (unsigned)(C * MAXLD * 4);
-    for (int j = wave; j < p.ld / 4; j += NW) {
+    for (int j = wave; j < p.ld / 4; j += NWk) {
       const unsigned pc = min(base + (unsigned)(j * 64 + lane), npieces - 1u);
       glds16(p.states + 4u * pc, __builtin_amdgcn_readfirstlane(raw0 + (unsigned)j * 1024u));
     }
@@ -149,15 +153,17 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
       bar();
     }
     // -------------------------------------------------------------- P0: request rows -> features
-    // Thread = (row tid / 4, column quads tid % 4 + 4m, m < 14): the row offset, the row's 1 / last
-    // price and its liveness are per thread, and quad slot m is a price quad on every lane while
-    // 16m + 15 < H (a scalar branch: packed fp32 mul / sub, then bf16); only the slots reaching
-    // columns H .. H+2 (budget, shares, the constant-1 bias input) take the select chain.  Two batches of 7
-    // quads, all loads of a batch in flight before its first use (register gather: unconditional,
-    // clamped loads -- loads under per-element branches were issued one wait at a time).
+    // Thread = (row tid / TPR, column quads tid % TPR + TPR m): TPR = 4 (register gather, 14 quad slots)
+    // or 8 (STREAM, 7 slots).  The row offset, the row's 1 / last price and its liveness are per thread,
+    // and quad slot m is a price quad on every lane while 4 (TPR - 1 + TPR m) + 3 < H (a scalar branch:
+    // packed fp32 mul / sub, then bf16); only the slots reaching columns H .. H+2 (budget, shares, the
+    // constant-1 bias input) take the select chain.  Batches of 7 quads, all loads of a batch in flight
+    // before its first use (register gather: unconditional, clamped loads -- loads under per-element
+    // branches were issued one wait at a time).
     {
-      constexpr int QB = 7, NQ = INP / 16;   // 14 quads per thread
-      const int r = tid >> 2, t4 = tid & 3;
+      constexpr int QB = 7, NQ = INP / 4 / TPR;   // quad slots per thread
+      static_assert(NQ % QB == 0, "quad batches");
+      const int r = tid / TPR, t4 = tid % TPR;
       const bool live = r0 + r < p.B;
       const unsigned ro = (unsigned)min(r0 + r, p.B - 1) * (unsigned)p.ld;   // host: B * ld < 2^30
       const float* rowp = STREAM ? rows + r * p.ld : nullptr;
@@ -172,7 +178,7 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
         float v[QB][4];
 #pragma unroll
         for (int m = 0; m < QB; ++m) {
-          const int c = min(4 * (t4 + 4 * (mb + m)), cmax);
+          const int c = min(4 * (t4 + TPR * (mb + m)), cmax);
           if constexpr (STREAM) {
             const float4 t = *reinterpret_cast<const float4*>(rowp + c);
             v[m][0] = t.x; v[m][1] = t.y; v[m][2] = t.z; v[m][3] = t.w;
@@ -183,9 +189,9 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
         }
 #pragma unroll
         for (int m = 0; m < QB; ++m) {
-          const int c = 4 * (t4 + 4 * (mb + m));
+          const int c = 4 * (t4 + TPR * (mb + m));
           float x[4];
-          if (16 * (mb + m) + 15 < H) {   // prices only, on every lane of the wave (a scalar branch)
+          if (4 * (TPR - 1 + TPR * (mb + m)) + 3 < H) {   // prices only, on every lane (a scalar branch)
             // packed fp32 mul then sub: the same IEEE roundings as feat_price
             const f32x2_t iv = {ivq, ivq}, off = {offq, offq};
             const f32x2_t x01 = f32x2_t{v[m][0], v[m][1]} * iv - off, x23 = f32x2_t{v[m][2], v[m][3]} * iv - off;
@@ -208,9 +214,9 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
     bar();
     // -------------------------------------------------------------- P1: layer 1
     {
-      f4v acc[MT][NET];
+      f4v acc[MTk][NET];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MTk; ++i)
 #pragma unroll
         for (int n = 0; n < NET; ++n) acc[i][n] = zero4();
 #pragma unroll
@@ -219,12 +225,12 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
 #pragma unroll
         for (int n = 0; n < NET; ++n) b[n] = lds_ld8(sX + (16 * n + l16) * SX + ks * 32 + 8 * g4);
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MTk; ++i)
 #pragma unroll
           for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(aW0[i][ks], b[n], acc[i][n]);
       }
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MTk; ++i)
 #pragma unroll
         for (int n = 0; n < NET; ++n) {
           const f4v v = acc[i][n];
@@ -236,9 +242,9 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
     // -------------------------------------------------------------- P2: layer 2 (+ b1) -> H2 (over X)
     bf16_t* sH2 = sX;
     {
-      f4v acc[MT][NET];
+      f4v acc[MTk][NET];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MTk; ++i)
 #pragma unroll
         for (int n = 0; n < NET; ++n) acc[i][n] = zero4();
 #pragma unroll
@@ -247,12 +253,12 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
 #pragma unroll
         for (int n = 0; n < NET; ++n) b[n] = lds_ld8(sH1 + (16 * n + l16) * SH + ks * 32 + 8 * g4);
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MTk; ++i)
 #pragma unroll
           for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(aW1[i][ks], b[n], acc[i][n]);
       }
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MTk; ++i)
 #pragma unroll
         for (int n = 0; n < NET; ++n) {
           const f4v v = acc[i][n];
@@ -262,7 +268,7 @@ __global__ void __launch_bounds__(NT, STREAM ? 1 : 2) qserve_kernel(ServeParams 
     }
     bar();
     // -------------------------------------------------------------- P3: output, argmax, epsilon-greedy
-    {
+    if (wave < NET) {
       f4v acc = zero4();   // wave w: 16-row tile w; lanes g4 == 0 end up with q[0..3] of row 16w + l16
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
@@ -335,7 +341,7 @@ extern "C" hipError_t st_qserve_launch(const st::serve::ServeParams* p, int grid
   }
   if (grid > ntiles) grid = ntiles;
   if (strm)
-    hipLaunchKernelGGL(qserve_kernel<true>, dim3(grid), dim3(NT), LDS_BYTES_STREAM, stream, *p);
+    hipLaunchKernelGGL(qserve_kernel<true>, dim3(grid), dim3(512), LDS_BYTES_STREAM, stream, *p);
   else
     hipLaunchKernelGGL(qserve_kernel<false>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
   return hipGetLastError();
