@@ -33,6 +33,8 @@ struct OptimParams {
   int slab_bf16;           // slabs are bf16, column-blocked [P/32][G][32] (P % 32 == 0), else fp32 [G][P]
   unsigned* chunk_heads;   // the step kernel's 8 per-XCD chunk-claim heads (stride 32 words) or null:
                            // re-zeroed by the slab pass (it runs after the step kernel, before the next)
+  float* ema;              // [P] Polyak average of the parameters (the weights to serve) or null
+  float ema_decay;         // ema <- ema + (1 - decay) (w - ema) after every update
 };
 
 constexpr int CW = 16;    // 16-byte slab columns per workgroup (256 B of every slab row)
@@ -80,13 +82,14 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
   static_assert(NP <= RT, "one updating thread per parameter");
   const int pidx = blockIdx.x * NP + tid;
   const bool own = tid < NP && pidx < p.P;
-  float w = 0.f, mk = 0.f, s1 = 0.f, s2 = 0.f, gsum = 0.f;
+  float w = 0.f, mk = 0.f, s1 = 0.f, s2 = 0.f, gsum = 0.f, ema = 0.f;
   if (own) {
     mk = p.mask[pidx];
     if (p.mode != 1) {
       w = p.params[pidx];
       if (p.kind >= 1) s1 = p.s1[pidx];
       if (p.kind == 2) s2 = p.s2[pidx];
+      if (p.ema) ema = p.ema[pidx];
     }
   }
   if (p.mode != 2) {
@@ -159,6 +162,7 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
   }
   p.params[pidx] = w;
   if (p.params_bf) p.params_bf[pidx] = f2bf(w);
+  if (p.ema) p.ema[pidx] = ema + (1.f - p.ema_decay) * (w - ema);
 }
 
 // ctrl[1] = ctrl[0] + 1 : the 1-based update count of the step about to run.

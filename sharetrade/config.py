@@ -170,6 +170,11 @@ class EngineConfig:
     # (dynamic for overlapped DP with world_size > 1, else static)
     chunk_schedule: str = "auto"
     grid: int = 0                   # step-kernel workgroups: 0 = one per CU (capped at the chunk count)
+    # > 0: keep a Polyak (exponential moving) average of the parameters, updated by the optimizer pass
+    # after every step: ema <- ema + (1 - ema_decay) (w - ema).  The averaged weights are the ones to
+    # serve (VectorEngine.serving_params; a single online-DQN snapshot's greedy policy drifts between
+    # steps, profiles/r2_serve_eval.md)
+    ema_decay: float = 0.0
 
 
 @dataclass

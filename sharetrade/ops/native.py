@@ -55,6 +55,7 @@ class OptimParams(C.Structure):
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("scale", C.c_float),
         ("tdelay", C.c_int), ("slab_bf16", C.c_int),
         ("chunk_heads", C.c_void_p),
+        ("ema", C.c_void_p), ("ema_decay", C.c_float),
     ]
 
 

@@ -27,8 +27,9 @@ from .server import DynamicBatcher, PolicyServer
 
 
 def load_checkpoint_params(path: str) -> torch.Tensor:
-    """Flat fp32 params from an engine checkpoint: a ``.stck`` file, a ``CheckpointManager`` directory
-    (latest file) or a sharded multi-rank directory (rank 0 of the newest committed step)."""
+    """Flat fp32 params to serve from an engine checkpoint (``params_ema`` when present, else ``params``):
+    a ``.stck`` file, a ``CheckpointManager`` directory (latest file) or a sharded multi-rank directory
+    (rank 0 of the newest committed step)."""
     from ..persist.checkpoint import CheckpointManager, load
 
     if os.path.isdir(path):
@@ -45,7 +46,8 @@ def load_checkpoint_params(path: str) -> torch.Tensor:
     state, _ = load(path)
     if "params" not in state:
         raise KeyError(f"{path} holds no 'params' tensor (not an engine checkpoint)")
-    return state["params"]
+    # the Polyak-averaged weights when the run kept them (engine.ema_decay > 0)
+    return state.get("params_ema", state["params"])
 
 
 class SelectionActionReq(BaseModel):

@@ -88,9 +88,11 @@ class PolicyServer:
                 torch.cuda.current_stream(self.device).synchronize()
 
     @classmethod
-    def from_engine(cls, engine, backend: str = "auto") -> "PolicyServer":
-        """Serve the current weights of a ``VectorEngine`` (same config, same device)."""
-        return cls(engine.cfg, params=engine.params, device=engine.device, backend=backend)
+    def from_engine(cls, engine, backend: str = "auto", averaged: bool = True) -> "PolicyServer":
+        """Serve a ``VectorEngine``'s weights (same config, same device): its Polyak average when it keeps
+        one (``engine.ema_decay > 0``) and ``averaged``, else the live parameters."""
+        w = engine.serving_params if averaged else engine.params
+        return cls(engine.cfg, params=w, device=engine.device, backend=backend)
 
     # ---------------------------------------------------------------- inference
     def _rows(self, states: ArrayLike) -> torch.Tensor:

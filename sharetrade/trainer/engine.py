@@ -187,6 +187,11 @@ class VectorEngine:
         self._real = L.trainable_mask(True).to(self.device)
         self.params.mul_(self._real)
         self.mask = L.trainable_mask(m.train_bias).to(self.device)
+        # Polyak average of the parameters (engine.ema_decay > 0): the weights to serve
+        self.ema_decay = float(cfg.engine.ema_decay)
+        if not 0.0 <= self.ema_decay < 1.0:
+            raise ValueError(f"engine.ema_decay must be in [0, 1), got {self.ema_decay}")
+        self.params_ema = self.params.clone() if self.ema_decay > 0 else None
         self.opt = qn.OptimState(a.optimizer, L.numel, a.adagrad_init_acc, device=self.device)
         self.state = tr.EnvState.create(self.E, cfg.env.budget, cfg.env.shares, device=self.device)
         self.env_offset = rank * self.E
@@ -301,6 +306,8 @@ class VectorEngine:
         o.stats, o.stat_acc, o.nstat = native.ptr(self.stat_slab), native.ptr(self.stat_acc), NSTAT
         o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
         o.chunk_heads = q.chunk_heads   # re-zeroed by every slab pass (modes 0 / 1)
+        if self.params_ema is not None:   # the optimizer pass also advances the Polyak average
+            o.ema, o.ema_decay = native.ptr(self.params_ema), self.ema_decay
         self._op = o
 
     # ---------------------------------------------------------------- stepping
@@ -311,6 +318,7 @@ class VectorEngine:
                 ar = self._sync.all_reduce
             self._f32.step(self.grad, ar)
             self._f32_stats()
+            self._ema_update()
             return
         L = native.lib()
         sh = native.stream_handle()
@@ -420,6 +428,7 @@ class VectorEngine:
             self._sync.all_reduce(grad)
         qn.optimizer_step_ref(self.params, grad, self.opt, self.mask, cfg.agent.lr, cfg.agent.adam_betas,
                               cfg.agent.adam_eps)
+        self._ema_update()
         done = ns.episodes > self.state.episodes
         fin = torch.where(done, ns.last_final, torch.zeros_like(ns.last_final)).double()
         self.stats += torch.tensor([
@@ -429,6 +438,17 @@ class VectorEngine:
         self.state = ns
         self._last_actions = info["actions"]
         self.grad_last = grad
+
+    def _ema_update(self) -> None:
+        """ema <- ema + (1 - decay) (w - ema) in fp32, as csrc/optim.hip does it (host-side paths)."""
+        if self.params_ema is not None:
+            c = float(np.float32(1.0) - np.float32(self.ema_decay))
+            self.params_ema.add_((self.params - self.params_ema) * c)
+
+    @property
+    def serving_params(self) -> torch.Tensor:
+        """The weights to serve: the Polyak average when engine.ema_decay > 0, else the live ones."""
+        return self.params_ema if self.params_ema is not None else self.params
 
     def step(self) -> None:
         if self.backend == "native":
@@ -570,6 +590,8 @@ class VectorEngine:
              "step": torch.tensor([self.step_count], dtype=torch.int64)}
         for k, v in self.state.as_dict().items():
             d["env_" + k] = v
+        if self.params_ema is not None:
+            d["params_ema"] = self.params_ema
         return {k: v.detach().cpu().clone() for k, v in d.items()}
 
     def _opt_count(self) -> int:
@@ -583,6 +605,8 @@ class VectorEngine:
     def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
         self.params.copy_(d["params"].to(self.device))
         self.params.mul_(self._real)
+        if self.params_ema is not None:
+            self.params_ema.copy_(d["params_ema"].to(self.device) if "params_ema" in d else self.params)
         if self.opt.s1.numel():
             self.opt.s1.copy_(d["opt_s1"].to(self.device))
         if self.opt.s2.numel():

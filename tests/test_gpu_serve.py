@@ -148,3 +148,28 @@ def test_http_front_end_native(native_built):
         r = c.post("/selection_action", json={"current_state": x[4].tolist(), "step": 0.0})
         assert r.status_code == 200 and r.json()["index"] == want[4]   # greedy batcher
         assert c.get("/health").json()["backend"] == "native"
+
+
+def test_optimizer_kernel_polyak_average(native_built):
+    """csrc/optim.hip advances ema <- ema + (1 - d)(w - ema) in the optimizer pass: bit-equal to the host
+    recurrence over the engine's parameter trajectory, eager and inside captured graphs."""
+    import numpy as np
+
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg()
+    cfg.engine.ema_decay = 0.95
+    eng = VectorEngine(cfg, device=torch.device("cuda", 0), envs=256)
+    c = float(np.float32(1.0) - np.float32(0.95))
+    want = eng.params.clone()
+    for _ in range(3):
+        eng.step()
+        torch.cuda.synchronize()
+        want = want + (eng.params - want) * c
+    assert torch.equal(eng.params_ema, want)
+    assert eng.capture_graph(warmup=0, graph_steps=2)
+    p_before = eng.params.clone()
+    eng.run(1)   # one single-step graph replay
+    torch.cuda.synchronize()
+    want = want + (eng.params - want) * c
+    assert not torch.equal(p_before, eng.params) and torch.equal(eng.params_ema, want)

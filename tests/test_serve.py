@@ -242,3 +242,35 @@ def test_serve_weights_from_engine_checkpoints(tmp_path):
     x = _rows(4, seed=3)
     a_eng = PolicyServer(eng.cfg, params=want, device=torch.device("cpu"), backend="torch").infer(x)
     assert torch.equal(srv.infer(x), a_eng)
+
+
+def test_engine_polyak_average_for_serving(tmp_path):
+    """engine.ema_decay > 0: ema <- ema + (1 - d)(w - ema) after every update (host path here, the
+    optimizer kernel on the GPU: tests/test_gpu_serve.py); checkpoints carry it and serving prefers it."""
+    from sharetrade.persist.checkpoint import CheckpointManager
+    from sharetrade.serve.http import load_checkpoint_params
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    cfg.engine.ema_decay = 0.9
+    eng = VectorEngine(cfg, device=torch.device("cpu"), envs=32, backend="torch")
+    want = eng.params.clone()
+    c = float(np.float32(1.0) - np.float32(0.9))
+    for _ in range(3):
+        eng.step()
+        want = want + (eng.params - want) * c
+    assert torch.equal(eng.params_ema, want) and not torch.equal(eng.params_ema, eng.params)
+    assert eng.serving_params is eng.params_ema
+    sd = eng.state_dict()
+    assert torch.equal(sd["params_ema"], want)
+    eng2 = VectorEngine(cfg, device=torch.device("cpu"), envs=32, backend="torch")
+    eng2.load_state_dict(sd)
+    assert torch.equal(eng2.params_ema, want)
+    srv = PolicyServer.from_engine(eng, backend="torch")
+    assert torch.equal(srv.params, want)
+    assert torch.equal(PolicyServer.from_engine(eng, backend="torch", averaged=False).params, eng.params)
+    CheckpointManager(str(tmp_path), interval=1).save(3, sd)
+    assert torch.equal(load_checkpoint_params(str(tmp_path)), want)
+    with pytest.raises(ValueError):
+        cfg.engine.ema_decay = 1.0
+        VectorEngine(cfg, device=torch.device("cpu"), envs=32, backend="torch")

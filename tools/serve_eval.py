@@ -55,6 +55,7 @@ def main() -> int:
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--eval-envs", type=int, default=8192)
     ap.add_argument("--phi", type=float, default=0.3)
+    ap.add_argument("--ema-decay", type=float, default=0.999, help="engine.ema_decay: also serve the Polyak average")
     ap.add_argument("-o", "--out", default=None)
     args = ap.parse_args()
 
@@ -70,6 +71,7 @@ def main() -> int:
     cfg = preset_config("flagship")
     cfg.data.source = "ar1"
     cfg.data.ar_phi = args.phi
+    cfg.engine.ema_decay = args.ema_decay
     H, b0 = cfg.model.history, cfg.env.budget
 
     t0 = time.perf_counter()
@@ -82,6 +84,7 @@ def main() -> int:
 
     test = make_price_bank(cfg, args.eval_envs, dev, seed=101)   # another seed: unseen series
     trained = PolicyServer(cfg, params=eng.params, device=dev, backend="native")
+    averaged = PolicyServer(cfg, params=eng.serving_params, device=dev, backend="native")
     untrained = PolicyServer(cfg, params=qn.init_params(trained.layout, cfg.model, seed=cfg.agent.seed), device=dev,
                              backend="native")
     g = torch.Generator(device=dev)
@@ -100,10 +103,13 @@ def main() -> int:
         return torch.full((rows.shape[0],), 0 if t == 0 else 2, device=dev, dtype=torch.long)
 
     res = {}
-    for name, pol in (("trained net, greedy (served)", served(trained)),
-                      ("trained net, epsilon-greedy as in training (served)", served_eps(trained)),
-                      ("untrained net, greedy (served)", served(untrained)),
-                      ("uniform random", rand), ("buy one share, hold", hold_after_buy)):
+    pols = [("trained net, greedy (served)", served(trained))]
+    if args.ema_decay > 0:
+        pols.append((f"Polyak average (decay {args.ema_decay}), greedy (served)", served(averaged)))
+    pols += [("trained net, epsilon-greedy as in training (served)", served_eps(trained)),
+             ("untrained net, greedy (served)", served(untrained)),
+             ("uniform random", rand), ("buy one share, hold", hold_after_buy)]
+    for name, pol in pols:
         t1 = time.perf_counter()
         f = trade(test, H, b0, pol)
         torch.cuda.synchronize()
