@@ -7,6 +7,10 @@ Routes (JSON):
   one request per call, grouped with concurrent calls by the :class:`DynamicBatcher`;
 * ``POST /select`` ``{"states": [[...], ...], "steps": [...] | null, "return_q": bool}`` -> ``{"actions": [...],
   "q": [[...]]}`` -- a whole batch in one launch (``steps`` null = greedy);
+* ``POST /select_bin`` -- the binary form for high-rate clients: the body is little-endian float32
+  rows of H + 3 values (the H + 2 state values, then the step; step < 0 = greedy), the reply is one
+  int8 action per row.  A single-row call goes through the batcher like ``/selection_action``; JSON
+  parsing of 203-float lists is what bounds the JSON routes (``profiles/r2_serve_http.md``);
 * ``POST /load`` ``{"checkpoint": path}`` -> swaps in the weights of an engine checkpoint;
 * ``GET /health`` -> backend, device, served batches / requests;
 * ``GET /metrics`` -> Prometheus text format: requests / batches / errors per route, request latency
@@ -20,6 +24,7 @@ import time
 from typing import List, Optional
 
 import torch
+from fastapi import Request
 from pydantic import BaseModel
 
 from ..protocol import action_of
@@ -66,6 +71,7 @@ class LoadReq(BaseModel):
 
 
 def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
+    import numpy as np
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import Response
     from prometheus_client import CONTENT_TYPE_LATEST, CollectorRegistry, Counter, Histogram, generate_latest
@@ -116,6 +122,28 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
             acts, q = out
             return {"actions": acts.cpu().tolist(), "q": q.cpu().tolist()}
         return {"actions": out.cpu().tolist()}
+
+    @app.post("/select_bin")
+    async def select_bin(request: Request):
+        t0 = time.perf_counter()
+        body = await request.body()
+        W = server.H + 3
+        if len(body) == 0 or len(body) % (4 * W) != 0:
+            m_err.labels("select_bin").inc()
+            raise HTTPException(400, f"body must be float32 rows of {W} values (state + step)")
+        x = np.frombuffer(body, dtype="<f4").reshape(-1, W)
+        steps = x[:, W - 1]
+        if x.shape[0] == 1 and batcher is not None:
+            st = float(steps[0])
+            a = await asyncio.wrap_future(batcher.submit(x[0, : W - 1], max(st, 0.0)))
+            out = np.asarray([a], dtype=np.int8)
+        else:
+            greedy = bool((steps < 0).all())
+            acts = server.infer(x[:, : W - 1], None if greedy else np.maximum(steps, 0.0))
+            out = acts.cpu().numpy().astype(np.int8)
+        m_req.labels("select_bin").inc(x.shape[0])
+        m_lat.labels("select_bin").observe(time.perf_counter() - t0)
+        return Response(out.tobytes(), media_type="application/octet-stream")
 
     @app.post("/load")
     def load(req: LoadReq):

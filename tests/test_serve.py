@@ -178,11 +178,21 @@ def test_http_front_end(tmp_path):
         assert c.post("/load", json={"checkpoint": str(tmp_path / "missing")}).status_code == 400
         h = c.get("/health").json()
         assert h["backend"] == "torch" and h["requests"] >= 8
+        # binary route: float32 rows of state + step (step < 0: greedy), int8 actions back
+        want = srv.infer(x).tolist()   # the weights loaded above
+        body = np.concatenate([x, np.full((6, 1), -1.0, np.float32)], 1).astype("<f4").tobytes()
+        r = c.post("/select_bin", content=body)
+        assert r.status_code == 200 and [int(v) for v in np.frombuffer(r.content, np.int8)] == want
+        one = np.concatenate([x[3], [1e9]]).astype("<f4").tobytes()
+        r = c.post("/select_bin", content=one)   # one row: through the batcher (eps 1, step 1e9: greedy)
+        assert r.status_code == 200 and int(np.frombuffer(r.content, np.int8)[0]) == want[3]
+        assert c.post("/select_bin", content=b"\x00" * 12).status_code == 400
         m = c.get("/metrics").text
         assert 'sharetrade_serve_requests_total{route="select"} 6.0' in m
+        assert 'sharetrade_serve_requests_total{route="select_bin"} 7.0' in m
         assert 'sharetrade_serve_requests_total{route="selection_action"} 1.0' in m
         assert 'sharetrade_serve_errors_total{route="selection_action"} 1.0' in m
-        assert "sharetrade_serve_batch_rows_count 1.0" in m
+        assert "sharetrade_serve_batch_rows_count 2.0" in m
 
 
 def test_cli_serve_process():
