@@ -62,7 +62,6 @@ def main() -> int:
     ap.add_argument("--clients", default="1,16,64")
     ap.add_argument("--requests", type=int, default=100, help="per client")
     ap.add_argument("--batches", default="1024,16384")
-    ap.add_argument("--workers", type=int, default=1, help="uvicorn worker processes of the server")
     args = ap.parse_args()
 
     import httpx
@@ -71,8 +70,7 @@ def main() -> int:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     url = f"http://127.0.0.1:{port}"
-    srv = subprocess.Popen([sys.executable, "-m", "sharetrade", "serve", "--port", str(port), "--max-delay-us", "200",
-                            "--workers", str(args.workers)],
+    srv = subprocess.Popen([sys.executable, "-m", "sharetrade", "serve", "--port", str(port), "--max-delay-us", "200"],
                            cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
         for _ in range(600):
@@ -89,7 +87,7 @@ def main() -> int:
             lat, el = asyncio.run(clients(url, n, args.requests, X, binary))
             us = np.asarray(lat) * 1e6
             print(json.dumps({"bench": "http_select_bin" if binary else "http_selection_action", "backend": backend,
-                              "workers": args.workers, "clients": n,
+                              "clients": n,
                               "requests": len(lat), "requests_per_s": round(len(lat) / el, 1),
                               "latency_us_p50": round(float(np.percentile(us, 50)), 1),
                               "latency_us_p99": round(float(np.percentile(us, 99)), 1)}), flush=True)

@@ -76,9 +76,6 @@ def main(argv=None) -> int:
             p.add_argument("--device", default="auto")
             p.add_argument("--max-batch", type=int, default=4096)
             p.add_argument("--max-delay-us", type=float, default=200.0)
-            p.add_argument("--workers", type=int, default=1,
-                           help="uvicorn worker processes, each with its own server on the device (one worker "
-                                "tops out near 1 k HTTP calls/s: profiles/r2_serve_http.md)")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -114,19 +111,6 @@ def main(argv=None) -> int:
         if ctx.is_main:
             print(json.dumps(res, default=float))
         D.shutdown(ctx)
-        return 0
-    if a.cmd == "serve" and a.workers > 1:
-        import os
-
-        import uvicorn
-
-        from .serve.http import SERVE_ENV
-
-        os.environ[SERVE_ENV] = json.dumps({"preset": a.preset, "config": a.config, "set": a.set, "ckpt": a.ckpt,
-                                            "device": a.device, "max_batch": a.max_batch,
-                                            "max_delay_us": a.max_delay_us})
-        uvicorn.run("sharetrade.serve.http:app_from_env", factory=True, workers=a.workers, host=a.host,
-                    port=a.port, log_level="warning")
         return 0
     if a.cmd == "serve":
         import uvicorn

@@ -164,26 +164,3 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
         return Response(generate_latest(reg), media_type=CONTENT_TYPE_LATEST)
 
     return app
-
-
-SERVE_ENV = "SHARETRADE_SERVE_SPEC"
-
-
-def app_from_env():
-    """uvicorn app factory for ``python -m sharetrade serve --workers N``: every worker process builds its
-    own server (and GPU context) from the JSON spec the launcher leaves in ``SHARETRADE_SERVE_SPEC``
-    (the launcher itself never touches the GPU)."""
-    import json
-
-    from ..config import Config, preset_config
-    from ..trainer.engine import resolve_device
-
-    spec = json.loads(os.environ[SERVE_ENV])
-    cfg = Config.load(spec["config"], spec["preset"]) if spec.get("config") else preset_config(spec["preset"])
-    if spec.get("set"):
-        cfg.override(spec["set"])
-    params = load_checkpoint_params(spec["ckpt"]) if spec.get("ckpt") else None
-    srv = PolicyServer(cfg, params=params, device=resolve_device(spec.get("device", "auto")))
-    bat = DynamicBatcher(srv, max_batch=int(spec.get("max_batch", 4096)),
-                         max_delay_us=float(spec.get("max_delay_us", 200.0)))
-    return make_app(srv, bat)

@@ -195,10 +195,8 @@ def test_http_front_end(tmp_path):
         assert "sharetrade_serve_batch_rows_count 2.0" in m
 
 
-@pytest.mark.parametrize("workers", [1, 2])
-def test_cli_serve_process(workers):
-    """``python -m sharetrade serve`` as a process (one or two uvicorn workers): health and one
-    SelectionAction over HTTP."""
+def test_cli_serve_process():
+    """``python -m sharetrade serve`` as a process: health and one SelectionAction over HTTP."""
     import os
     import socket
     import subprocess
@@ -211,9 +209,8 @@ def test_cli_serve_process(workers):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    proc = subprocess.Popen([sys.executable, "-m", "sharetrade", "serve", "--device", "cpu", "--port", str(port),
-                             "--workers", str(workers)],
-                            cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    proc = subprocess.Popen([sys.executable, "-m", "sharetrade", "serve", "--device", "cpu", "--port", str(port)],
+                            cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     try:
         url = f"http://127.0.0.1:{port}"
         for _ in range(300):
