@@ -147,6 +147,11 @@ def test_http_front_end_native(native_built):
         assert r.status_code == 200 and r.json()["actions"] == want
         r = c.post("/selection_action", json={"current_state": x[4].tolist(), "step": 0.0})
         assert r.status_code == 200 and r.json()["index"] == want[4]   # greedy batcher
+        import numpy as np
+
+        body = np.concatenate([x.numpy(), np.full((9, 1), -1.0, np.float32)], 1).astype("<f4").tobytes()
+        r = c.post("/select_bin", content=body)   # binary rows, greedy
+        assert r.status_code == 200 and [int(v) for v in np.frombuffer(r.content, np.int8)] == want
         assert c.get("/health").json()["backend"] == "native"
 
 
