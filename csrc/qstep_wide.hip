@@ -91,6 +91,31 @@ constexpr bool DRAW_EARLY = ST_WIDE_DRAW_EARLY;
 // leaves a partial q in LDS (R1, dead from P1 to P4); P3 sums the eight partials in wave order instead
 // of running the 4-deep dependent fwd_out chain (same operands, fp32 summation order differs).
 constexpr bool OFOLD = ST_WIDE_OFOLD;
+#ifndef ST_WIDE_WSWZ
+#define ST_WIDE_WSWZ 0
+#endif
+// WSWZ: the weight images W1^T / W2^T at an unpadded 128-element row stride with their 16-byte units
+// XOR-swizzled by row: unit u of row R sits at u ^ wf(R & 15), wf(r) = 2 (r & 7) ^ 9 bit3(r).  Both read
+// forms are then conflict-free (tools/lds_bank_sim.py): the row-fragment reads of the forwards (16 rows
+// per ds_read_b128 lane group; stride 136 costs 2x) and the transposed reads of the backward (8 rows x
+// 32 bytes per ds_read_b64_tr_b16 group; stride 136 costs 2x), and the images shrink by 2.3 KB.
+constexpr bool WSWZ = ST_WIDE_WSWZ;
+ST_DEV int wf(int r) { return ((r & 7) << 1) ^ (((r >> 3) & 1) * 9); }
+// element offset of (row R, column c) in a weight image of row stride S
+ST_DEV int wsw(int R, int c, int S) { return WSWZ ? R * S + ((((c >> 3) ^ wf(R & 15))) << 3) + (c & 7) : R * S + c; }
+// frag_row / frag_tr / the K=16 transposed read on a weight image
+ST_DEV s8v wfrag_row(const bf16_t* img, int S, int r0, int k0, int l16, int g4) {
+  return lds_ld8(img + wsw(r0 + l16, k0 + 8 * g4, S));
+}
+ST_DEV s8v wfrag_tr(const bf16_t* img, int S, int k0, int c0, int l16, int g4) {
+  const int R = k0 + 8 * g4 + (l16 >> 2), c = c0 + 4 * (l16 & 3);
+  s4v lo = lds_tr4(img + wsw(R, c, S));
+  s4v hi = lds_tr4(img + wsw(R + 4, c, S));
+  s8v r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
 // asw(r, lo): the swizzled offset of column base + lo for a base that is a multiple of 16 and lo < 16
 // (then (base + lo) ^ 8 bit2(r) = base + (lo ^ 8 bit2(r)): the base stays an immediate offset)
 ST_DEV int asw(int r, int lo) { return ASWZ ? (lo ^ ((r & 4) << 1)) : lo; }
@@ -115,7 +140,7 @@ static_assert(NW >= NET, "the output layer / env step maps env tile w to wave w 
 
 template <int INP, int H1P, int H2P>
 struct Geo {
-  static constexpr int SW1 = H1P + 8, SW2 = H2P + 8;
+  static constexpr int SW1 = WSWZ ? H1P : H1P + 8, SW2 = WSWZ ? H2P : H2P + 8;
   static constexpr int SX = INP + 16, SH1 = H1P + 16, SH2 = H2P + 16;
   static constexpr int oW1 = 0;
   static constexpr int oW2 = oW1 + H2P * SW1;
@@ -208,7 +233,7 @@ ST_DEV void fwd_hidden(AFrag afrag, const bf16_t* sB, bf16_t* sO, const float* b
     // 4 g4 .. 4 g4 + 3 of its accumulator -- the B-operand layout of v_mfma_f32_16x16x16_bf16
     s4v aw[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) aw[i] = lds_ld4(sW2 + l16 * SW2_ + m0 + 16 * i + 4 * g4);
+    for (int i = 0; i < MT; ++i) aw[i] = lds_ld4(sW2 + wsw(l16, m0 + 16 * i + 4 * g4, SW2_));
 #pragma unroll
     for (int n = 0; n < NET; ++n) {
       f4v pq = zero4();
@@ -243,7 +268,7 @@ ST_DEV f4v fwd_out(const bf16_t* sA, const bf16_t* sB, int nt, int l16, int g4) 
   f4v acc = zero4();
 #pragma unroll
   for (int ks = 0; ks < K / 32; ++ks) {
-    const s8v a = frag_row(sA, SA, 0, ks * 32, l16, g4);
+    const s8v a = wfrag_row(sA, SA, 0, ks * 32, l16, g4);
     const s8v b = afrag_row(sB, SB, 16 * nt, ks * 32, l16, g4);
     acc = mfma32(a, b, acc);
   }
@@ -273,7 +298,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
     for (int n = 0; n < NET; ++n) b[n] = lds_ld4(sDZ + (16 * n + l16) * SD + 4 * g4);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const s4v a = lds_tr4(sWT + (4 * g4 + (l16 >> 2)) * SW + m0 + 16 * i + 4 * (l16 & 3));
+      const s4v a = lds_tr4(sWT + wsw(4 * g4 + (l16 >> 2), m0 + 16 * i + 4 * (l16 & 3), SW));
 #pragma unroll
       for (int n = 0; n < NET; ++n) acc[i][n] = mfma16(a, b[n], acc[i][n]);
     }
@@ -283,7 +308,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
 #pragma unroll
     for (int n = 0; n < NET; ++n) b[0][n] = afrag_row(sDZ, SD, 16 * n, 0, l16, g4);
 #pragma unroll
-    for (int i = 0; i < MT; ++i) a[0][i] = frag_tr(sWT, SW, 0, m0 + 16 * i, l16, g4);
+    for (int i = 0; i < MT; ++i) a[0][i] = wfrag_tr(sWT, SW, 0, m0 + 16 * i, l16, g4);
     __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -292,7 +317,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
 #pragma unroll
         for (int n = 0; n < NET; ++n) b[c ^ 1][n] = afrag_row(sDZ, SD, 16 * n, (ks + 1) * 32, l16, g4);
 #pragma unroll
-        for (int i = 0; i < MT; ++i) a[c ^ 1][i] = frag_tr(sWT, SW, (ks + 1) * 32, m0 + 16 * i, l16, g4);
+        for (int i = 0; i < MT; ++i) a[c ^ 1][i] = wfrag_tr(sWT, SW, (ks + 1) * 32, m0 + 16 * i, l16, g4);
         __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
       }
 #pragma unroll
@@ -309,7 +334,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
       for (int n = 0; n < NET; ++n) b[n] = afrag_row(sDZ, SD, 16 * n, ks * 32, l16, g4);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const s8v a = frag_tr(sWT, SW, ks * 32, m0 + 16 * i, l16, g4);
+        const s8v a = wfrag_tr(sWT, SW, ks * 32, m0 + 16 * i, l16, g4);
 #pragma unroll
         for (int n = 0; n < NET; ++n) acc[i][n] = mfma32(a, b[n], acc[i][n]);
       }
@@ -432,12 +457,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     const bf16_t* w1 = p.wq + p.off_w1;
     for (int i = tid; i < H2P * H1P / 8; i += NT) {
       const int r = i / (H1P / 8), c = (i % (H1P / 8)) * 8;
-      *reinterpret_cast<uint4*>(sW1 + r * G::SW1 + c) = *reinterpret_cast<const uint4*>(w1 + r * H1P + c);
+      *reinterpret_cast<uint4*>(sW1 + wsw(r, c, G::SW1)) = *reinterpret_cast<const uint4*>(w1 + r * H1P + c);
     }
     const bf16_t* w2 = p.wq + p.off_w2;
     for (int i = tid; i < OUTP * H2P / 8; i += NT) {
       const int r = i / (H2P / 8), c = (i % (H2P / 8)) * 8;
-      *reinterpret_cast<uint4*>(sW2 + r * G::SW2 + c) = *reinterpret_cast<const uint4*>(w2 + r * H2P + c);
+      *reinterpret_cast<uint4*>(sW2 + wsw(r, c, G::SW2)) = *reinterpret_cast<const uint4*>(w2 + r * H2P + c);
     }
     for (int i = tid; i < H2P; i += NT) sB1[i] = p.wf[p.off_b1 + i];
     if (tid < OUTP) sB2[tid] = p.wf[p.off_b2 + tid];
@@ -577,7 +602,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
     STW_STAMP(1);
     // ------------------------------------------------------------ P1-P2: hidden layers of Q(x)
     auto a_w0 = [&](int i, int ks) { return aW0[i][ks]; };
-    auto a_w1 = [&](int i, int ks) { return frag_row(sW1, G::SW1, m0 + 16 * i, ks * 32, l16, g4); };
+    auto a_w1 = [&](int i, int ks) { return wfrag_row(sW1, G::SW1, m0 + 16 * i, ks * 32, l16, g4); };
     if (DRAW_EARLY && wave == NW - 1) {
       const int pos = sEnvI[lane * 4 + 0];
       uint32_t c0 = (uint32_t)(p.env_offset + ebase + lane), c1 = (uint32_t)(step & 0xFFFFFFFFull),

@@ -491,3 +491,26 @@ def test_ofold_variant_matches_default(native_built):
     assert (a0 != a1).float().mean().item() <= 0.02
     if torch.equal(a0, a1):
         assert _rel(g1, g0) < 1e-3
+
+
+def test_wswz_variant_bit_identical(native_built):
+    """engine.step_variant = "wswz" (XOR-swizzled weight images) reorders LDS addresses only: actions,
+    rewards and gradients bit-identical to the default 8-wave kernel."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 256
+    prices = _prices(E, seed=4)
+    dev = torch.device("cuda", 0)
+    out = []
+    for variant in ("", "wswz"):
+        cfg = _cfg()
+        cfg.agent.epsilon = 0.9
+        cfg.engine.step_variant = variant
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 150)
+        eng.ctrl.fill_(3000)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        out.append((eng.actions_out.cpu().clone(), eng.rewards_out.cpu().clone(), g))
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
