@@ -133,9 +133,10 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
             raise HTTPException(400, f"body must be float32 rows of {W} values (state + step)")
         x = np.frombuffer(body, dtype="<f4").reshape(-1, W)
         steps = x[:, W - 1]
-        if x.shape[0] == 1 and batcher is not None:
-            st = float(steps[0])
-            a = await asyncio.wrap_future(batcher.submit(x[0, : W - 1], max(st, 0.0)))
+        if x.shape[0] == 1 and batcher is not None and float(steps[0]) >= 0.0:
+            # one epsilon-greedy row: grouped with concurrent calls (the batcher draws with steps; a
+            # greedy row, step < 0, is answered directly below)
+            a = await asyncio.wrap_future(batcher.submit(x[0, : W - 1], float(steps[0])))
             out = np.asarray([a], dtype=np.int8)
         else:
             greedy = bool((steps < 0).all())

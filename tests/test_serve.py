@@ -186,10 +186,13 @@ def test_http_front_end(tmp_path):
         one = np.concatenate([x[3], [1e9]]).astype("<f4").tobytes()
         r = c.post("/select_bin", content=one)   # one row: through the batcher (eps 1, step 1e9: greedy)
         assert r.status_code == 200 and int(np.frombuffer(r.content, np.int8)[0]) == want[3]
+        one_greedy = np.concatenate([x[4], [-1.0]]).astype("<f4").tobytes()   # step < 0: greedy, not batched
+        r = c.post("/select_bin", content=one_greedy)
+        assert r.status_code == 200 and int(np.frombuffer(r.content, np.int8)[0]) == want[4]
         assert c.post("/select_bin", content=b"\x00" * 12).status_code == 400
         m = c.get("/metrics").text
         assert 'sharetrade_serve_requests_total{route="select"} 6.0' in m
-        assert 'sharetrade_serve_requests_total{route="select_bin"} 7.0' in m
+        assert 'sharetrade_serve_requests_total{route="select_bin"} 8.0' in m
         assert 'sharetrade_serve_requests_total{route="selection_action"} 1.0' in m
         assert 'sharetrade_serve_errors_total{route="selection_action"} 1.0' in m
         assert "sharetrade_serve_batch_rows_count 2.0" in m
