@@ -76,6 +76,9 @@ def main(argv=None) -> int:
             p.add_argument("--device", default="auto")
             p.add_argument("--max-batch", type=int, default=4096)
             p.add_argument("--max-delay-us", type=float, default=200.0)
+            p.add_argument("--weights", choices=["average", "live"], default="average",
+                           help="with a checkpoint that keeps a Polyak average (engine.ema_decay): serve it or the "
+                                "live weights (profiles/r2_serve_eval.md: evaluate both)")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(level=getattr(logging, cfg.log.loglevel, logging.INFO),
@@ -119,7 +122,7 @@ def main(argv=None) -> int:
         from .serve.http import load_checkpoint_params, make_app
         from .trainer.engine import resolve_device
 
-        params = load_checkpoint_params(a.ckpt) if a.ckpt else None
+        params = load_checkpoint_params(a.ckpt, averaged=a.weights == "average") if a.ckpt else None
         srv = PolicyServer(cfg, params=params, device=resolve_device(a.device))
         bat = DynamicBatcher(srv, max_batch=a.max_batch, max_delay_us=a.max_delay_us)
         try:

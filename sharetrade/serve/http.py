@@ -31,8 +31,9 @@ from ..protocol import action_of
 from .server import DynamicBatcher, PolicyServer
 
 
-def load_checkpoint_params(path: str) -> torch.Tensor:
-    """Flat fp32 params to serve from an engine checkpoint (``params_ema`` when present, else ``params``):
+def load_checkpoint_params(path: str, averaged: bool = True) -> torch.Tensor:
+    """Flat fp32 params to serve from an engine checkpoint (``params_ema`` when present and ``averaged``,
+    else ``params``):
     a ``.stck`` file, a ``CheckpointManager`` directory (latest file) or a sharded multi-rank directory
     (rank 0 of the newest committed step)."""
     from ..persist.checkpoint import CheckpointManager, load
@@ -51,8 +52,8 @@ def load_checkpoint_params(path: str) -> torch.Tensor:
     state, _ = load(path)
     if "params" not in state:
         raise KeyError(f"{path} holds no 'params' tensor (not an engine checkpoint)")
-    # the Polyak-averaged weights when the run kept them (engine.ema_decay > 0)
-    return state.get("params_ema", state["params"])
+    # the Polyak-averaged weights when the run kept them (engine.ema_decay > 0) and ``averaged``
+    return state["params_ema"] if averaged and "params_ema" in state else state["params"]
 
 
 class SelectionActionReq(BaseModel):
@@ -68,6 +69,7 @@ class SelectReq(BaseModel):
 
 class LoadReq(BaseModel):
     checkpoint: str
+    averaged: bool = True   # the Polyak average when the checkpoint holds one
 
 
 def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
@@ -149,7 +151,7 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
     @app.post("/load")
     def load(req: LoadReq):
         try:
-            server.load_params(load_checkpoint_params(req.checkpoint))
+            server.load_params(load_checkpoint_params(req.checkpoint, req.averaged))
         except (OSError, KeyError, ValueError) as e:
             raise HTTPException(400, str(e))
         return {"loaded": req.checkpoint}

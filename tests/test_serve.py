@@ -284,6 +284,7 @@ def test_engine_polyak_average_for_serving(tmp_path):
     assert torch.equal(PolicyServer.from_engine(eng, backend="torch", averaged=False).params, eng.params)
     CheckpointManager(str(tmp_path), interval=1).save(3, sd)
     assert torch.equal(load_checkpoint_params(str(tmp_path)), want)
+    assert torch.equal(load_checkpoint_params(str(tmp_path), averaged=False), sd["params"])
     with pytest.raises(ValueError):
         cfg.engine.ema_decay = 1.0
         VectorEngine(cfg, device=torch.device("cpu"), envs=32, backend="torch")
