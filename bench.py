@@ -16,7 +16,10 @@ N GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
 
 Every timed step is a full learner step (all envs act, every env's TD error
 is back-propagated, the optimizer updates all parameters); nothing is skipped.
-Rank 0 prints ONE JSON line.
+After the timed window (untimed) every env plays one complete 5,846-step episode
+with the policy being learned and one with a uniformly random policy: the
+"episode return" half of the metric (final portfolio - budget, mean / std over
+all envs of all ranks).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -69,6 +72,11 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # native build BEFORE any process group exists (build.build_all serialises concurrent builders
+    # with a file lock): no rank waits in a collective while another compiles
+    import build as _build  # in-tree native build (no-op when up to date)
+
+    _build.build_all()
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
         return 2
@@ -77,24 +85,24 @@ def main() -> int:
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # the DP step is captured in HIP graphs with its RCCL all-reduce: no user-buffer registration
         # of captured collectives (it goes through IPC handles; the pool's driver is dmabuf-only)
         os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
+        # a dead or stuck peer fails the job within the collective timeout instead of hanging it
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = {"device_id": dev} if args.dist_backend == "nccl" else {}
-        dist.init_process_group(args.dist_backend, rank=rank, world_size=world, **kw)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.pg_timeout), **kw)
         group = dist.group.WORLD
-
-    import build as _build  # in-tree native build (no-op when up to date)
-
-    if rank == 0 or world == 1:
-        _build.build_all()
-    if world > 1:
-        torch.distributed.barrier()
+        world = dist.get_world_size(group)   # as the communicator sees it
 
     from sharetrade.config import preset_config
+    from sharetrade.trainer import benchkit
     from sharetrade.trainer.engine import VectorEngine
 
     cfg = preset_config("flagship")
@@ -115,31 +123,17 @@ def main() -> int:
     # and the clock then needs ~40 steps to settle (tools/dvfs_probe.py, profiles/r2_dvfs_probe.md)
     eng.current_portfolios().double().clone()
     torch.cuda.synchronize()
-    use_graph = not args.no_graph and not cfg.engine.dp_overlap
-    if use_graph:
-        try:
-            # 2 eager steps before capture, then one replay of each captured graph (graph upload);
-            # all of them untimed and reported as "graph_prime_steps"
-            # (N > 1: a fixed 6 replays on every rank -- each replay holds the all-reduce)
-            use_graph = eng.capture_graph(warmup=2, prime=True, prime_reps=4 if world == 1 else 6)
-        except Exception as e:  # noqa: BLE001 -- fall back to eager launches, same math
-            print(f"bench: HIP graph capture failed ({str(e).splitlines()[0]}); running eagerly", file=sys.stderr)
-            from sharetrade.ops import native as _native
-
-            _native.clear_last_error()
-            torch.cuda.synchronize()
-            eng._graph, eng._graph_k, use_graph = None, None, False
-    if not use_graph:
-        # eager launches (--no-graph, overlapped DP, or a failed capture): the same clock settling as the
-        # graph priming, a fixed 64 steps on every rank (each step holds the DP all-reduce)
-        eng.run(64)
+    # capture -> vote (all ranks agree on graphs vs eager) -> prime with the same step counts on every
+    # rank (each step holds the DP all-reduce); untimed, reported as "graph_prime_steps"
+    use_graph, _ = benchkit.prepare_steps(eng, not args.no_graph and not cfg.engine.dp_overlap, rank, world,
+                                          group, prime_reps=4 if world == 1 else 6)
     prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    # start-of-window portfolio (episode return is measured over the timed window)
+    # start-of-window portfolio (window_return_mean: the portfolio change over the timed window)
     pf0 = eng.current_portfolios().double().clone()
     prof = None
     if args.trace:
@@ -181,9 +175,17 @@ def main() -> int:
         allreduce_ms = round(float(t[0]), 4)
     total_steps = eng.E * world * args.steps
     value = total_steps / el
+    n_trans = eng.E * world * eng.step_count   # every step taken (prime + warmup + timed)
+    st = stats.cpu().tolist()
+    episodes = None
+    if not args.no_episode:
+        # untimed, after the timed window: every env plays one complete episode over its series
+        # (T - H = 5,846 online-learning steps), first with the policy being learned, then with a
+        # uniformly random policy on the same banks (the baseline)
+        learned = benchkit.full_episode_returns(eng, world, group)
+        rnd = benchkit.full_episode_returns(eng, world, group, random_policy=True)
+        episodes = {"learned": learned, "random": rnd}
     if rank == 0:
-        st = stats.cpu().tolist()
-        n_trans = eng.E * world * eng.step_count   # every step taken (prime + warmup + timed)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -213,8 +215,12 @@ def main() -> int:
                 "chunk_schedule": getattr(eng, "chunk_schedule", "static"),
             },
             "graph_prime_steps": prime_steps,
-            "episode_return_mean": round(float(ret[0] / ret[1]), 4),
-            "episode_return_window_steps": args.steps,
+            "world_size": world,
+            # one optimizer update per step (sync DP: one global update over every rank's envs)
+            "updates_per_s": round(args.steps / el, 1),
+            "samples_per_update": eng.E * world,
+            "window_return_mean": round(float(ret[0] / ret[1]), 4),
+            "window_return_steps": args.steps,
             "mean_reward_per_step": st[0] / max(n_trans, 1),
             "mean_td_loss": st[1] / max(n_trans, 1),
             "vs_reference_floor": round(value / REFERENCE_FLOOR, 1),
@@ -225,6 +231,16 @@ def main() -> int:
             out["hbm_total_gb"] = round(total / 1e9, 1)
         if allreduce_ms is not None:
             out["allreduce_ms_per_step"] = allreduce_ms
+        if episodes is not None:
+            lr_, rd_ = episodes["learned"], episodes["random"]
+            out["episode_return"] = {
+                "what": "final portfolio - initial budget, one complete episode per env (untimed, after the "
+                        "timed window), mean / population std over all envs of all ranks",
+                "episode_steps": lr_["steps"],
+                "learned_mean": round(lr_["mean"], 4), "learned_std": round(lr_["std"], 4),
+                "random_mean": round(rd_["mean"], 4), "random_std": round(rd_["std"], 4),
+                "episodes": lr_["n"], "complete_frac": round(lr_["complete_frac"], 6),
+            }
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

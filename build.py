@@ -79,6 +79,8 @@ def _run(cmd):
 def build_hip(force: bool = False, jobs: int = 8) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "*.h")))
+    if not force and not _newer(HIP_LIB, srcs + hdrs):
+        return HIP_LIB   # library newer than every source: nothing to do (the object dir need not exist)
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(OUT, exist_ok=True)
     objs = []
@@ -108,10 +110,22 @@ def build_rt(force: bool = False) -> str:
 
 
 def build_all(force: bool = False, jobs: int = 8):
-    libs = [build_hip(force, jobs)]
-    rt = build_rt(force)
-    if rt:
-        libs.append(rt)
+    """Build (or confirm up to date) both libraries.  Serialised across processes by an exclusive
+    lock on ``build/.lock``: the ranks of a multi-GPU job all call this before they initialise the
+    process group, the first one builds, the others wait on the lock and find the libraries current
+    (no rank sits in a collective while another compiles)."""
+    import fcntl
+
+    os.makedirs(os.path.dirname(OBJ), exist_ok=True)
+    with open(os.path.join(os.path.dirname(OBJ), ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            libs = [build_hip(force, jobs)]
+            rt = build_rt(force)
+            if rt:
+                libs.append(rt)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return libs
 
 

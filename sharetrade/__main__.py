@@ -71,6 +71,9 @@ def main(argv=None) -> int:
             p.add_argument("--trace", default=None, help="Chrome trace output path (torch.profiler)")
         if name == "serve":
             p.add_argument("--ckpt", default=None, help="engine checkpoint file or directory (default: random init)")
+            p.add_argument("--ckpt-root", default=None,
+                           help="directory POST /load may read checkpoints from (default: the --ckpt directory; "
+                                "without either, /load is disabled)")
             p.add_argument("--host", default="127.0.0.1")
             p.add_argument("--port", type=int, default=8000)
             p.add_argument("--device", default="auto")
@@ -126,7 +129,11 @@ def main(argv=None) -> int:
         srv = PolicyServer(cfg, params=params, device=resolve_device(a.device))
         bat = DynamicBatcher(srv, max_batch=a.max_batch, max_delay_us=a.max_delay_us)
         try:
-            uvicorn.run(make_app(srv, bat), host=a.host, port=a.port, log_level="warning")
+            import os
+
+            root = a.ckpt_root or (None if not a.ckpt else
+                                   a.ckpt if os.path.isdir(a.ckpt) else os.path.dirname(os.path.abspath(a.ckpt)))
+            uvicorn.run(make_app(srv, bat, ckpt_root=root), host=a.host, port=a.port, log_level="warning")
         finally:
             bat.close()
         return 0

@@ -116,6 +116,9 @@ class Watchdog:
         self.timeout, self.poll, self.stall = timeout_s, poll_s, stall_timeout_s
         self.on_dead = on_dead
         self.dead: List[int] = []
+        # ranks whose process has exited cleanly: their heartbeat goes stale by design, never flag them
+        # (a peer still committing its last checkpoint would otherwise fail a finished generation)
+        self.finished: set = set()
         self._last: Dict[int, tuple] = {}       # rank -> (progress value, local time it last changed)
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, name="watchdog", daemon=True)
@@ -132,6 +135,8 @@ class Watchdog:
         now = time.time()
         dead = []
         for r in range(self.world):
+            if r in self.finished:
+                continue
             v = self._get(f"hb/{self.gen}/{r}")
             if v is not None and now - float(v) > self.timeout:
                 dead.append(r)
@@ -254,10 +259,13 @@ class ElasticRunner:
                     break
                 if all(c == 0 for c in codes):
                     break
-                if wd is not None and wd.dead:
-                    self.flagged.extend((gen, r) for r in wd.dead)
-                    failed = True
-                    break
+                if wd is not None:
+                    wd.finished.update(r for r, c in enumerate(codes) if c == 0)
+                    live_dead = [r for r in wd.dead if codes[r] != 0]
+                    if live_dead:
+                        self.flagged.extend((gen, r) for r in live_dead)
+                        failed = True
+                        break
                 if time.monotonic() > deadline:
                     failed = True
                     break

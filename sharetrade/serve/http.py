@@ -11,7 +11,9 @@ Routes (JSON):
   rows of H + 3 values (the H + 2 state values, then the step; step < 0 = greedy), the reply is one
   int8 action per row.  A single-row call goes through the batcher like ``/selection_action``; JSON
   parsing of 203-float lists is what bounds the JSON routes (``profiles/r2_serve_http.md``);
-* ``POST /load`` ``{"checkpoint": path}`` -> swaps in the weights of an engine checkpoint;
+* ``POST /load`` ``{"checkpoint": path}`` -> swaps in the weights of an engine checkpoint; the path is
+  resolved under the server's checkpoint root (``ckpt_root``, ``--ckpt-root``) and anything outside it
+  is refused (403); without a root the route is disabled;
 * ``GET /health`` -> backend, device, served batches / requests;
 * ``GET /metrics`` -> Prometheus text format: requests / batches / errors per route, request latency
   histogram, batch-size histogram of the dynamic batcher (one registry per app).
@@ -72,7 +74,35 @@ class LoadReq(BaseModel):
     averaged: bool = True   # the Polyak average when the checkpoint holds one
 
 
-def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
+MAX_BIN_ROWS = 1 << 20   # /select_bin rows per call (HTTP 413 above): bounds one call's device work
+
+
+def resolve_under(root: str, path: str) -> str:
+    """``path`` (absolute, or relative to ``root``) resolved with symlinks; PermissionError unless it
+    lies inside ``root`` -- a client may only name checkpoints the operator put under the root."""
+    base = os.path.realpath(root)
+    cand = os.path.realpath(path if os.path.isabs(path) else os.path.join(base, path))
+    if cand != base and not cand.startswith(base + os.sep):
+        raise PermissionError(f"{path!r} is outside the checkpoint root")
+    return cand
+
+
+def select_mixed(server: PolicyServer, x, steps):
+    """Actions for rows whose step may be negative (= greedy) or not (= epsilon-greedy at that step):
+    greedy rows and drawing rows go in separate launches and are scattered back in row order."""
+    import numpy as np
+
+    g = steps < 0
+    out = np.empty(x.shape[0], dtype=np.int8)
+    if g.any():
+        out[g] = server.infer(x[g], None).cpu().numpy().astype(np.int8)
+    if (~g).any():
+        out[~g] = server.infer(x[~g], steps[~g]).cpu().numpy().astype(np.int8)
+    return out
+
+
+def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None, ckpt_root: Optional[str] = None,
+             max_bin_rows: int = MAX_BIN_ROWS):
     import numpy as np
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import Response
@@ -133,6 +163,9 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
         if len(body) == 0 or len(body) % (4 * W) != 0:
             m_err.labels("select_bin").inc()
             raise HTTPException(400, f"body must be float32 rows of {W} values (state + step)")
+        if len(body) // (4 * W) > max_bin_rows:
+            m_err.labels("select_bin").inc()
+            raise HTTPException(413, f"at most {max_bin_rows} rows per call")
         x = np.frombuffer(body, dtype="<f4").reshape(-1, W)
         steps = x[:, W - 1]
         if x.shape[0] == 1 and batcher is not None and float(steps[0]) >= 0.0:
@@ -141,17 +174,24 @@ def make_app(server: PolicyServer, batcher: Optional[DynamicBatcher] = None):
             a = await asyncio.wrap_future(batcher.submit(x[0, : W - 1], float(steps[0])))
             out = np.asarray([a], dtype=np.int8)
         else:
-            greedy = bool((steps < 0).all())
-            acts = server.infer(x[:, : W - 1], None if greedy else np.maximum(steps, 0.0))
-            out = acts.cpu().numpy().astype(np.int8)
+            # a launch plus a device sync: off the event loop, so the batcher's futures and /metrics keep
+            # being served meanwhile; greedy (step < 0) and drawing rows in separate launches
+            out = await asyncio.to_thread(select_mixed, server, np.ascontiguousarray(x[:, : W - 1]), steps.copy())
         m_req.labels("select_bin").inc(x.shape[0])
         m_lat.labels("select_bin").observe(time.perf_counter() - t0)
         return Response(out.tobytes(), media_type="application/octet-stream")
 
     @app.post("/load")
     def load(req: LoadReq):
+        if ckpt_root is None:
+            raise HTTPException(403, "checkpoint loading is disabled (start the server with a checkpoint root)")
         try:
-            server.load_params(load_checkpoint_params(req.checkpoint, req.averaged))
+            path = resolve_under(ckpt_root, req.checkpoint)
+        except PermissionError as e:
+            m_err.labels("load").inc()
+            raise HTTPException(403, str(e))
+        try:
+            server.load_params(load_checkpoint_params(path, req.averaged))
         except (OSError, KeyError, ValueError) as e:
             raise HTTPException(400, str(e))
         return {"loaded": req.checkpoint}

@@ -1,0 +1,170 @@
+"""Pieces of the flagship benchmark (``bench.py``) that must behave identically on every rank.
+
+A multi-GPU run is one process per GPU over RCCL; every captured or eager step holds a gradient
+all-reduce, so every rank must issue the SAME sequence of collectives or the job hangs (the
+reference's equivalent invariant: ``router.route(Train(d))`` reaches every routee,
+`TrainerRouterActor.scala:86-88`).  Hence:
+
+* :func:`agree` -- a boolean decided by every rank (MIN all-reduce): one rank's failed HIP-graph
+  capture sends every rank down the eager path with the same step counts;
+* :func:`prepare_steps` -- capture, agree, then prime (graph replays or eager steps: fixed counts on
+  every rank);
+* :func:`full_episode_returns` -- the headline's "episode return" half: every env plays one complete
+  episode over its series (the reference's episode, `TrainerChildActor.scala:64-71`: 6,047 prices ->
+  5,846 online-learning steps), final portfolio minus the initial budget, reduced over all ranks
+  like the router's ``GetAvg`` / ``GetStd`` (`TrainerRouterActor.scala:89-94,148-151`).
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+from typing import Dict, Optional, Tuple
+
+import torch
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist
+
+
+def agree(ok: bool, world: int, group=None, device: Optional[torch.device] = None) -> bool:
+    """True only if ``ok`` on every rank (all-reduce MIN; one collective on every rank)."""
+    if world <= 1:
+        return bool(ok)
+    dist = _dist()
+    dev = device if device is not None else torch.device("cpu")
+    if dist.get_backend(group) == "gloo":
+        dev = torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def _fail_capture_here(rank: int) -> bool:
+    """Fault injection: ``SHARETRADE_FAIL_CAPTURE=<rank>[,<rank>...]`` makes those ranks' graph
+    capture raise (tests of the rank-agreement path)."""
+    spec = os.environ.get("SHARETRADE_FAIL_CAPTURE", "")
+    return bool(spec) and str(rank) in [s.strip() for s in spec.split(",")]
+
+
+def prepare_steps(eng, want_graph: bool, rank: int, world: int, group=None, prime_reps: int = 4,
+                  eager_prime: int = 64, log=None) -> Tuple[bool, int]:
+    """Capture the step graphs (``want_graph``), agree across ranks, then prime.
+
+    Returns ``(use_graph, prime_steps)``.  The 2 eager warm-up steps (each holds an all-reduce) run
+    on every rank BEFORE the capture; the capture itself issues no collective (a captured RCCL call
+    runs at replay), so a rank whose capture fails has issued exactly the collectives its peers
+    have.  The vote follows, then every rank either replays the graphs a fixed number of times or
+    runs ``eager_prime`` eager steps: identical collective counts everywhere."""
+    log = log or (lambda m: print(m, file=sys.stderr))
+    start = eng.step_count
+    ok = False
+    if want_graph:
+        eng.run(2)   # eager (no graph captured yet): lazy init of the kernels and the communicator
+        try:
+            if _fail_capture_here(rank):
+                raise RuntimeError("injected capture failure (SHARETRADE_FAIL_CAPTURE)")
+            ok = bool(eng.capture_graph(warmup=0, prime=False))
+        except Exception as e:  # noqa: BLE001 -- fall back to eager launches, same math
+            log(f"rank {rank}: HIP graph capture failed ({str(e).splitlines()[0]})")
+            ok = False
+        if not ok:
+            _drop_graphs(eng)
+    use_graph = agree(ok, world, group, getattr(eng, "device", None))
+    if not use_graph:
+        _drop_graphs(eng)
+    if use_graph:
+        eng._graph.replay()
+        eng.step_count += 1
+        if world > 1:
+            # a fixed number of multi-step replays on every rank (each replay holds all-reduces)
+            gk = getattr(eng, "_graph_k", None)
+            if gk is not None:
+                for _ in range(max(1, prime_reps)):
+                    gk[0].replay()
+                    eng.step_count += gk[1]
+        else:
+            eng.prime_graph(prime_reps)
+    else:
+        eng.run(eager_prime)
+    return use_graph, eng.step_count - start
+
+
+def _drop_graphs(eng) -> None:
+    eng._graph, eng._graph_k = None, None
+    if getattr(eng, "device", torch.device("cpu")).type == "cuda":
+        try:
+            from ..ops import native as _native
+
+            _native.clear_last_error()
+        except Exception:  # noqa: BLE001
+            pass
+        torch.cuda.synchronize()
+
+
+def reset_episodes(eng) -> torch.Tensor:
+    """Every env back to the start of its series with the initial budget / shares; returns the
+    per-env completed-episode counters before the reset (to detect completions)."""
+    c = eng.cfg.env
+    st = eng.state
+    st.pos.zero_()
+    st.budget.fill_(float(c.budget))
+    st.shares.fill_(int(c.shares))
+    st.value.zero_()
+    st.ret_sum.zero_()
+    st.last_final.fill_(float("nan"))
+    return st.episodes.clone()
+
+
+def full_episode_returns(eng, world: int = 1, group=None, random_policy: bool = False) -> Dict[str, float]:
+    """One complete episode per env (``T - H`` steps, online learning on), then mean / population
+    std of (final portfolio - initial budget) over every env of every rank.
+
+    ``random_policy``: the epsilon-greedy exploit probability is forced to 0 for this episode (every
+    action uniform over Buy / Sell / Hold, same draws, same banks): the baseline a learned policy has
+    to beat.  Native engines run it with eager launches (the captured graphs hold the old
+    parameters struct); the learner still updates, which does not change a random policy's actions."""
+    steps = int(eng.T - eng.H)
+    ep0 = reset_episodes(eng)
+    if random_policy:
+        if eng.backend == "native":
+            qp = eng._qp
+            saved = qp.eps
+            qp.eps = 0.0
+            try:
+                for _ in range(steps):
+                    eng._native_step()
+                    eng.step_count += 1
+            finally:
+                qp.eps = saved
+        else:
+            saved = eng.cfg.agent.epsilon
+            eng.cfg.agent.epsilon = 0.0
+            try:
+                eng.run(steps)
+            finally:
+                eng.cfg.agent.epsilon = saved
+    else:
+        eng.run(steps)
+    eng.synchronize()
+    st = eng.state
+    done = st.episodes > ep0
+    fin = st.last_final.double() - float(eng.cfg.env.budget)
+    fin = torch.where(done, fin, torch.zeros_like(fin))
+    dev = fin.device
+    s = torch.stack([done.double().sum(), fin.sum(), (fin * fin).sum()])
+    if world > 1:
+        dist = _dist()
+        if dist.get_backend(group) == "gloo":
+            s = s.cpu()
+        dist.all_reduce(s, group=group)
+    n, sx, sxx = (float(v) for v in s.cpu())
+    n_total = float(eng.E * world)
+    if n == 0:
+        return {"n": 0, "mean": math.nan, "std": math.nan, "steps": steps, "complete_frac": 0.0}
+    m = sx / n
+    return {"n": int(n), "mean": m, "std": math.sqrt(max(0.0, sxx / n - m * m)), "steps": steps,
+            "complete_frac": n / n_total}

@@ -36,6 +36,25 @@ def _sync(dev: torch.device) -> None:
         torch.cuda.synchronize(dev)
 
 
+def agreed_resume_step(mgr: CheckpointManager, ctx=None) -> Optional[int]:
+    """The step every rank resumes from: this rank's newest valid checkpoint, MIN over ranks.
+
+    A rank killed mid-save (the ElasticRunner tears a failed generation down with SIGKILL) can leave
+    some ranks one checkpoint ahead of others; each loading its own newest file would restart the
+    ranks at different iteration counts -- different numbers of all-reduces (a hang) and different
+    parameters.  Retention keeps ``mgr.keep`` files per rank, so the MIN step is still on disk
+    everywhere.  None: some rank has no checkpoint (every rank starts fresh)."""
+    latest = mgr.latest()
+    mine = int(os.path.basename(latest)[5:-5]) if latest else -1
+    if ctx is not None and ctx.is_distributed:
+        import torch.distributed as dist
+
+        t = torch.tensor([mine], dtype=torch.int64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctx.group)
+        mine = int(t.item())
+    return None if mine < 0 else mine
+
+
 def build(kind: str, cfg: Config, device: torch.device, **kw):
     if kind == "deep":
         from .deep import DeepDQN
@@ -88,12 +107,18 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
         metrics_path = None
     mgr = CheckpointManager(ckpt_dir, interval=ckpt_every) if ckpt_dir else None
     done = 0
-    if mgr is not None and resume and mgr.latest():
-        st, meta = load_ckpt(mgr.latest())
-        if meta.get("kind") != kind:
-            raise ValueError(f"checkpoint is a {meta.get('kind')!r} run, not {kind!r}")
-        d.load_state_dict(st)
-        done = int(meta["step"])
+    if mgr is not None and resume:
+        step = agreed_resume_step(mgr, ctx if dp else None)
+        if step is not None:
+            path = mgr.path_for(step)
+            if not os.path.exists(path):
+                raise RuntimeError(f"rank {ctx.rank if dp else 0}: the agreed resume step {step} is not in {mgr.dir} "
+                                   f"(retention kept {mgr.list()})")
+            st, meta = load_ckpt(path)
+            if meta.get("kind") != kind:
+                raise ValueError(f"checkpoint is a {meta.get('kind')!r} run, not {kind!r}")
+            d.load_state_dict(st)
+            done = int(meta["step"])
     ml = MetricsLogger(metrics_path)
     prof = None
     if trace_path and (not dp or ctx.is_main):      # Chrome trace of the run (host spans + GPU kernels)

@@ -100,3 +100,20 @@ def test_watchdog_flags_stalled_progress():
     wd.stop()
     hb.stop()
     assert wd.dead == [0]
+
+
+def test_watchdog_ignores_cleanly_finished_rank():
+    """A rank that exited 0 stops beating by design; the watchdog must not flag it (a finished
+    generation would otherwise be failed and restarted)."""
+    import time
+
+    store = torch.distributed.HashStore()
+    hb0 = Heartbeat(store, 0, interval_s=0.05).start()
+    Heartbeat(store, 1, interval_s=0.05).beat()          # rank 1 beat, then exited with code 0
+    wd = Watchdog(store, 2, timeout_s=0.3, poll_s=0.05)
+    wd.finished.add(1)
+    wd.start()
+    time.sleep(0.8)
+    wd.stop()
+    hb0.stop()
+    assert wd.dead == []

@@ -158,7 +158,7 @@ def test_http_front_end(tmp_path):
     srv = _server(eps=1.0)
     x = _rows(6, seed=8)
     with DynamicBatcher(srv, max_batch=16, max_delay_us=1000) as bat:
-        c = TestClient(make_app(srv, bat))
+        c = TestClient(make_app(srv, bat, ckpt_root=str(tmp_path)))
         r = c.post("/select", json={"states": x.tolist(), "return_q": True})
         assert r.status_code == 200
         want = srv.infer(x).tolist()
@@ -176,6 +176,11 @@ def test_http_front_end(tmp_path):
         r = c.post("/load", json={"checkpoint": str(tmp_path)})
         assert r.status_code == 200 and torch.equal(srv.params, new)
         assert c.post("/load", json={"checkpoint": str(tmp_path / "missing")}).status_code == 400
+        # only paths under the checkpoint root: absolute paths elsewhere and .. escapes are refused
+        assert c.post("/load", json={"checkpoint": "/etc"}).status_code == 403
+        assert c.post("/load", json={"checkpoint": "../"}).status_code == 403
+        assert c.post("/load", json={"checkpoint": "."}).status_code == 200       # relative to the root
+        assert TestClient(make_app(srv, bat)).post("/load", json={"checkpoint": str(tmp_path)}).status_code == 403
         h = c.get("/health").json()
         assert h["backend"] == "torch" and h["requests"] >= 8
         # binary route: float32 rows of state + step (step < 0: greedy), int8 actions back
@@ -190,9 +195,19 @@ def test_http_front_end(tmp_path):
         r = c.post("/select_bin", content=one_greedy)
         assert r.status_code == 200 and int(np.frombuffer(r.content, np.int8)[0]) == want[4]
         assert c.post("/select_bin", content=b"\x00" * 12).status_code == 400
+        # mixed greedy / drawing rows in one body: the greedy rows stay greedy (eps 1 at step 1e9 = greedy
+        # too; step 0 = always explore, so only the greedy rows are pinned)
+        steps = np.array([-1.0, 0.0, -1.0, 1e9, 0.0, -1.0], np.float32)
+        body = np.concatenate([x, steps[:, None]], 1).astype("<f4").tobytes()
+        for _ in range(4):
+            r = c.post("/select_bin", content=body)
+            got = [int(v) for v in np.frombuffer(r.content, np.int8)]
+            assert r.status_code == 200 and all(got[i] == want[i] for i in (0, 2, 3, 5)), (got, want)
+        small = TestClient(make_app(srv, bat, max_bin_rows=2))
+        assert small.post("/select_bin", content=body).status_code == 413
         m = c.get("/metrics").text
         assert 'sharetrade_serve_requests_total{route="select"} 6.0' in m
-        assert 'sharetrade_serve_requests_total{route="select_bin"} 8.0' in m
+        assert 'sharetrade_serve_requests_total{route="select_bin"} 32.0' in m
         assert 'sharetrade_serve_requests_total{route="selection_action"} 1.0' in m
         assert 'sharetrade_serve_errors_total{route="selection_action"} 1.0' in m
         assert "sharetrade_serve_batch_rows_count 2.0" in m
