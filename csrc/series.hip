@@ -51,7 +51,36 @@ __global__ void __launch_bounds__(256) replicate4_kernel(const float* __restrict
   }
 }
 
+// Weight initialisation on the device (tf.RandomNormalInitializer, QDecisionPolicyActor.scala:41,45,
+// 80-81): W[r][c] = std * N(0,1) for r < rows, c < cols of a row-major [.., ld] block, one Philox4x32-10
+// counter per element -- (c0, c1, c2, c3) = (r * cols + c, 0, stream, 0x1417) -- and one Box-Muller
+// normal from its first two words.  Counter-based, so the values depend only on (key, stream, index):
+// sharetrade/models/qnet.py mirrors it on the host (same formula in fp32; libm vs device ulps).
+__global__ void __launch_bounds__(256) init_normal_kernel(float* __restrict__ out, int rows, int cols, int ld,
+                                                          float std, uint32_t key0, uint32_t key1, uint32_t stream) {
+  const long n = (long)rows * cols;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint32_t c0 = (uint32_t)i, c1 = 0u, c2 = stream, c3 = 0x1417u;
+    philox4x32(c0, c1, c2, c3, key0, key1);
+    const float u1 = ((float)(c0 >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+    const float u2 = u24(c1);
+    const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    out[(size_t)r * ld + c] = std * z;
+  }
+}
+
 }  // namespace st
+
+extern "C" hipError_t st_init_normal(float* out, int rows, int cols, int ld, float std, uint32_t key0, uint32_t key1,
+                                     uint32_t stream, hipStream_t s) {
+  if (rows < 0 || cols < 0 || ld < cols) return hipErrorInvalidValue;
+  const long n = (long)rows * cols;
+  if (n == 0) return hipSuccess;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(st::init_normal_kernel, dim3(grid), dim3(256), 0, s, out, rows, cols, ld, std, key0, key1, stream);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t st_replicate4(const float* src, float* dst, int E, int T, int T4, hipStream_t stream) {
   if (T4 % 4 != 0 || T4 < T) return hipErrorInvalidValue;

@@ -52,6 +52,9 @@ class ModelConfig:
     bias_init: float = 0.1
     init_std: float = 1.0           # tf.RandomNormalInitializer() default N(0,1)
     init: str = "normal"            # "normal" (reference) | "he" (scaled, for deep nets)
+    # weight draws: "philox" (counter-based Philox + Box-Muller: the init_normal HIP kernel on a GPU,
+    # its NumPy mirror on the host) | "torch" (torch's CPU generator)
+    init_rng: str = "philox"
 
     @property
     def input_dim(self) -> int:
@@ -103,7 +106,7 @@ class DataConfig:
     start: str = "1992-01-01"
     end: str = "2015-01-01"
     filter_range: bool = False      # quirk Q10: reference ignores the date range
-    csv_path: Optional[str] = None  # default: bundled MSFT series
+    csv_path: Optional[str] = None  # default: config.default_csv_path() (env var, reference CSV, bundled series)
     length: int = 6047              # synthetic series length
     start_price: float = 50.0
     volatility: float = 0.02
@@ -314,10 +317,28 @@ def preset_config(name: str = "reference_compat") -> Config:
 
 
 REFERENCE_CSV = "/root/reference/src/main/resources/MSFT-stock-prices-revised.txt"
+BUNDLED_SERIES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "msft_prices.npz")
 
 
 def default_csv_path() -> str:
-    """Location of the MSFT price file the reference bundles as a classpath resource
-    (`SharePriceGetter.scala:90`).  The file is read in place (it is data the
-    reference ships, not re-distributed here); ``SHARETRADE_MSFT_CSV`` overrides."""
-    return os.environ.get("SHARETRADE_MSFT_CSV", REFERENCE_CSV)
+    """Where the MSFT daily series comes from (the reference bundles it as a classpath resource,
+    `SharePriceGetter.scala:90`).  Resolution order -- documented, and reported by
+    :func:`price_data_origin`:
+
+    1. ``SHARETRADE_MSFT_CSV`` (any ``price, yyyy-MM-dd`` file, or a ``.npz`` series);
+    2. the reference checkout's CSV, when present (parsed in place);
+    3. ``sharetrade/data/msft_prices.npz``: the same series, parsed once from the reference CSV
+       (``tools/make_msft_fixture.py``; ``tests/test_app.py`` re-checks it against the CSV whenever the
+       CSV exists), so parity runs work on machines without the reference checkout (the GPU boxes).
+    """
+    env = os.environ.get("SHARETRADE_MSFT_CSV")
+    if env:
+        return env
+    if os.path.exists(REFERENCE_CSV):
+        return REFERENCE_CSV
+    return BUNDLED_SERIES
+
+
+def price_data_origin() -> str:
+    p = default_csv_path()
+    return "bundled" if p == BUNDLED_SERIES else ("env" if os.environ.get("SHARETRADE_MSFT_CSV") else "reference")

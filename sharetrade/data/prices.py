@@ -60,6 +60,11 @@ def parse_price_lines(lines: Iterable[str]) -> Dict[Date, float]:
 
 
 def load_csv(path: str) -> Dict[Date, float]:
+    """``price, yyyy-MM-dd`` rows (the reference's file), or a parsed ``.npz`` series
+    (``days``: date ordinals, ``prices``; ``tools/make_msft_fixture.py``)."""
+    if path.endswith(".npz"):
+        z = np.load(path)          # arrays only (allow_pickle stays False)
+        return {Date.fromordinal(int(d)): float(p) for d, p in zip(z["days"], z["prices"])}
     with open(path, "r", encoding="utf-8") as f:
         return parse_price_lines(f)
 

@@ -124,16 +124,55 @@ class QNetLayout:
         return m
 
 
-def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0) -> torch.Tensor:
+def philox_normal(rows: int, cols: int, std: float, seed: int, stream: int) -> torch.Tensor:
+    """Host mirror of ``csrc/series.hip: init_normal_kernel``: element (r, c) = std * Box-Muller normal
+    of Philox4x32-10 counter (r * cols + c, 0, stream, 0x1417), fp32 arithmetic (values agree with the
+    device to a few ulps: libm vs device transcendentals)."""
+    import numpy as np
+
+    from ..utils import rng
+
+    k0, k1 = rng.key_for(seed, 0)
+    n = rows * cols
+    i = np.arange(n, dtype=np.uint64)
+    r0, r1, _, _ = rng.philox4x32((i & np.uint64(0xFFFFFFFF)).astype(np.uint32), np.zeros(n, np.uint32),
+                                  np.full(n, stream, np.uint32), np.full(n, 0x1417, np.uint32),
+                                  np.full(n, k0, np.uint32), np.full(n, k1, np.uint32))
+    u1 = ((r0 >> np.uint32(8)).astype(np.float32) + np.float32(1.0)) * np.float32(1.0 / 16777216.0)
+    u2 = rng.u24(r1)
+    z = np.sqrt(np.float32(-2.0) * np.log(u1)) * np.cos(np.float32(6.283185307179586) * u2)
+    return torch.from_numpy((np.float32(std) * z.astype(np.float32)).reshape(rows, cols))
+
+
+def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0, device=None) -> torch.Tensor:
     """fp32 flat params; ``W ~ N(0, init_std)`` (tf.RandomNormalInitializer,
-    QDecisionPolicyActor.scala:41,45) or He-normal; biases = ``bias_init``."""
-    g = torch.Generator().manual_seed(int(seed))
-    flat = torch.zeros(layout.numel, dtype=torch.float32)
+    QDecisionPolicyActor.scala:41,45) or He-normal; biases = ``bias_init``.
+
+    ``m.init_rng``: ``"philox"`` (default) draws W from the counter-based Philox + Box-Muller
+    generator -- on a GPU ``device`` by the ``init_normal`` HIP kernel (csrc/series.hip), on the host by
+    its NumPy mirror, the same values either way up to libm ulps; ``"torch"`` uses torch's CPU
+    generator (rounds 1-2 behaviour).  The result lives on ``device`` (CPU by default)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    flat = torch.zeros(layout.numel, dtype=torch.float32, device=dev)
+    use_kernel = m.init_rng == "philox" and dev.type == "cuda"
+    if use_kernel:
+        from ..ops import native
+        from ..utils import rng
+
+        k0, k1 = rng.key_for(int(seed), 0)
+    g = torch.Generator().manual_seed(int(seed)) if m.init_rng == "torch" else None
     for l in range(layout.n_layers):
         fan_in, fan_out = layout.dims[l], layout.dims[l + 1]
         std = m.init_std if m.init == "normal" else math.sqrt(2.0 / fan_in)
-        w = torch.randn(fan_out, fan_in, generator=g) * std
-        layout.w(flat, l)[:fan_out, :fan_in] = w
+        wl = layout.w(flat, l)
+        if use_kernel:
+            native.init_normal(wl, fan_out, fan_in, float(std), int(k0), int(k1), l)
+        elif m.init_rng == "philox":
+            wl[:fan_out, :fan_in] = philox_normal(fan_out, fan_in, std, seed, l).to(dev)
+        elif m.init_rng == "torch":
+            wl[:fan_out, :fan_in] = (torch.randn(fan_out, fan_in, generator=g) * std).to(dev)
+        else:
+            raise KeyError(f"model.init_rng: {m.init_rng!r}")
         layout.b(flat, l)[:fan_out] = m.bias_init
     return flat
 

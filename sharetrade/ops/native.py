@@ -110,6 +110,9 @@ def lib() -> C.CDLL:
     L.st_random_walk.restype = C.c_int
     L.st_replicate4.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_replicate4.restype = C.c_int
+    L.st_init_normal.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_uint32, C.c_uint32,
+                                 C.c_uint32, C.c_void_p]
+    L.st_init_normal.restype = C.c_int
     _bind_optional(L)
     _lib = L
     return L
@@ -186,6 +189,17 @@ def replicate4(src: torch.Tensor) -> torch.Tensor:
     out = flat[: 4 * E * T4].view(4, E, T4)
     check(lib().st_replicate4(ptr(src), ptr(out), E, T, T4, stream_handle()), "st_replicate4")
     return out
+
+
+def init_normal(block: torch.Tensor, rows: int, cols: int, std: float, key0: int, key1: int, stream: int) -> None:
+    """``block[:rows, :cols] = std * N(0, 1)`` on the device (csrc/series.hip init_normal_kernel);
+    ``block`` is a row-major [R, ld] fp32 view (e.g. one weight of the flat parameter buffer)."""
+    if not block.is_cuda or block.dtype != torch.float32 or block.dim() != 2 or block.stride(1) != 1:
+        raise ValueError("init_normal: a 2-D row-major fp32 CUDA view is required")
+    if rows > block.shape[0] or cols > block.shape[1]:
+        raise ValueError("init_normal: block too small")
+    check(lib().st_init_normal(ptr(block), rows, cols, block.stride(0), std, key0 & 0xFFFFFFFF, key1 & 0xFFFFFFFF,
+                               stream, stream_handle()), "st_init_normal")
 
 
 def to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:

@@ -57,7 +57,7 @@ class QLearner:
             raise ValueError("native learner backend needs a GPU device")
         self.backend = backend
         self.seed = a.seed if seed is None else seed
-        p = params.clone().float() if params is not None else qn.init_params(self.layout, m, seed=self.seed)
+        p = params.clone().float() if params is not None else qn.init_params(self.layout, m, seed=self.seed, device=dev)
         self.params = p.to(dev)
         self.mask = self.layout.trainable_mask(m.train_bias).to(dev)
         self.opt = qn.OptimState(a.optimizer, self.layout.numel, a.adagrad_init_acc, device=dev)

@@ -180,7 +180,7 @@ class VectorEngine:
             raise ValueError("Stock price count should be more than Tensorflow input nodes")
         # ------------------------------------------------------------ params / optimizer
         m, a = cfg.model, cfg.agent
-        p0 = params.clone().float() if params is not None else qn.init_params(L, m, seed=a.seed)
+        p0 = params.clone().float() if params is not None else qn.init_params(L, m, seed=a.seed, device=self.device)
         self.params = p0.to(self.device)
         # padding entries of the flat layout are exactly zero (csrc/qstep_wide.hip relies on the layer-1
         # padding columns: the gathered rows carry finite non-zero values there)

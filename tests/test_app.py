@@ -1,16 +1,20 @@
-"""End-to-end ShareTradeHelper runs (CPU): price service -> router -> workers -> learner."""
+"""End-to-end ShareTradeHelper runs (CPU): price service -> router -> workers -> learner.
+
+The MSFT series comes from ``config.default_csv_path()``: the reference checkout's CSV when present,
+else the bundled parsed copy (``sharetrade/data/msft_prices.npz``), so these parity runs never skip."""
 import json
 import os
 import subprocess
 import sys
+import time
 
+import numpy as np
 import pytest
 import torch
 
-from sharetrade.config import default_csv_path, preset_config
+from sharetrade.config import BUNDLED_SERIES, REFERENCE_CSV, default_csv_path, preset_config
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HAVE_CSV = os.path.exists(default_csv_path())
 
 
 def _cfg(max_ok=True):
@@ -20,7 +24,24 @@ def _cfg(max_ok=True):
     return cfg
 
 
-@pytest.mark.skipif(not HAVE_CSV, reason="reference MSFT csv not present")
+def test_bundled_series_is_the_reference_csv():
+    """The bundled series is exactly what the CSV parser keeps from the reference's file."""
+    from sharetrade.data.prices import load_csv
+
+    z = np.load(BUNDLED_SERIES)
+    assert len(z["days"]) == 6047 and np.all(np.diff(z["days"]) > 0)
+    if not os.path.exists(REFERENCE_CSV):
+        pytest.skip(f"PARITY SOURCE UNCHECKED: {REFERENCE_CSV} is absent here, so the bundled copy "
+                    f"{BUNDLED_SERIES} (sha256 of its source {str(z['source_sha256'])[:16]}...) is not re-derived")
+    ref = load_csv(REFERENCE_CSV)
+    dates = sorted(ref)
+    assert [d.toordinal() for d in dates] == z["days"].tolist()
+    assert np.array_equal(np.asarray([ref[d] for d in dates]), z["prices"])
+    import hashlib
+
+    assert hashlib.sha256(open(REFERENCE_CSV, "rb").read()).hexdigest() == str(z["source_sha256"])
+
+
 @pytest.mark.parametrize("engine", ["actors", "vector"])
 def test_compat_run_reproduces_reference_avg_std(engine):
     """Reference semantics (quirk Q1): every worker ends at its initial budget -> 2400.0 / 0.0."""
@@ -31,7 +52,22 @@ def test_compat_run_reproduces_reference_avg_std(engine):
     assert res["avg"] == 2400.0 and res["std"] == 0.0
 
 
-@pytest.mark.skipif(not HAVE_CSV, reason="reference MSFT csv not present")
+def test_full_length_compat_run_vector_engine():
+    """The reference's own run at full length (`ShareTradeHelper.scala:20-48`): 10 workers x the whole
+    6,047-price MSFT series = 5,846 steps each (`TrainerChildActor.scala:64-71`), reference_compat
+    semantics, vector engine on the CPU -> exactly avg 2400.0, std 0.0 (reward is identically 0 under
+    quirk Q1, `TrainerChildActor.scala:118-123`)."""
+    from sharetrade.app import run
+
+    cfg = _cfg()
+    cfg.router.poll_interval_s = 0.25
+    t0 = time.perf_counter()
+    res = run(cfg, engine="vector", device="cpu", quiet=True)
+    assert res["completed"] == 1.0, res
+    assert res["avg"] == 2400.0 and res["std"] == 0.0, res
+    assert time.perf_counter() - t0 < 600
+
+
 def test_intended_semantics_trade():
     from sharetrade.app import run
 

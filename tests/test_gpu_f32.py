@@ -148,3 +148,20 @@ def test_fp32_engine_compat_reproduces_reference_portfolio(dev):
     assert float(eng.stat_acc[0]) == 0.0
     fin = eng.final_portfolios().cpu()
     assert torch.all(fin == 2400.0), fin
+
+
+def test_init_normal_kernel_matches_host_mirror(native_built):
+    """The device init kernel (csrc/series.hip, Philox + Box-Muller) vs its NumPy mirror: the same
+    counters, so the same normals up to device-vs-libm transcendental ulps."""
+    import torch
+
+    from sharetrade.config import preset_config
+    from sharetrade.models import qnet as qn
+
+    for preset in ("reference_compat", "flagship"):
+        cfg = preset_config(preset)
+        L = qn.QNetLayout.from_config(cfg.model)
+        host = qn.init_params(L, cfg.model, seed=5)
+        dev = qn.init_params(L, cfg.model, seed=5, device="cuda:0").cpu()
+        assert torch.equal(dev == 0, host == 0)                 # same padding pattern
+        assert torch.allclose(dev, host, rtol=2e-5, atol=2e-6), float((dev - host).abs().max())

@@ -81,7 +81,6 @@ def test_env_transition_rules():
     assert r.tolist() == pytest.approx([0.0, 4.0, 0.0, 1.0])
 
 
-@pytest.mark.skipif(not os.path.exists(default_csv_path()), reason="reference MSFT csv not present")
 def test_compat_msft_run_reproduces_reference_portfolio():
     """Reference quirk Q1: every worker ends at exactly its initial budget."""
     from sharetrade.trainer.engine import VectorEngine
@@ -113,3 +112,21 @@ def test_ar1_price_bank_has_momentum():
     a, b = r[:, 1:] - r[:, 1:].mean(), r[:, :-1] - r[:, :-1].mean()
     rho = float((a * b).sum() / (a.norm() * b.norm()))
     assert abs(rho - 0.3) < 0.03, rho
+
+
+def test_philox_init_is_normal_and_counter_based():
+    """model.init_rng = "philox": W ~ N(0, std) from the counter-based generator (host mirror of
+    csrc/series.hip init_normal_kernel); padding stays zero; the values depend only on (seed, layer,
+    index), not on the padded layout."""
+    from sharetrade.models import qnet as qn
+
+    cfg = preset_config("reference_compat")
+    L = qn.QNetLayout.from_config(cfg.model)
+    p = qn.init_params(L, cfg.model, seed=11)
+    w0 = L.w(p, 0)
+    real = w0[: L.dims[1], : L.dims[0]]
+    assert abs(float(real.mean())) < 0.01 and abs(float(real.std()) - 1.0) < 0.01
+    assert float(w0[L.dims[1]:].abs().sum()) == 0.0 and float(w0[:, L.dims[0] + 1:].abs().sum()) == 0.0
+    assert torch.equal(real, qn.philox_normal(L.dims[1], L.dims[0], 1.0, 11, 0))
+    assert not torch.equal(p, qn.init_params(L, cfg.model, seed=12))
+    assert torch.equal(p, qn.init_params(L, cfg.model, seed=11))
