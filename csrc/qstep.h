@@ -35,6 +35,7 @@ struct QStepParams {
   unsigned* chunk_heads;
   int reward_mode;          // 0: reward = change of portfolio value; 1: its one-step return (change / previous)
   float td_clip;            // > 0: the TD error fed back is clamped to [-td_clip, td_clip] (Huber loss)
+  unsigned* err;            // csrc/qstep_ws.hip: bit 0 = a ring wait gave up (bounded spin), or null
 };
 
 // rows of QStepParams::env

@@ -1,0 +1,627 @@
+// Wave-specialised fused online-DQN engine step on CDNA4 (gfx950): the step of qstep_wide.hip
+// (gather -> Q(x) -> epsilon-greedy + Buy/Sell/Hold env step -> Q(x') -> TD target -> backward ->
+// per-workgroup weight-gradient slabs; QDecisionPolicyActor.scala:54-77, TrainerChildActor.scala:82-146)
+// re-organised so that no phase of the chain waits on a workgroup barrier.
+//
+// Why: qstep_wide.hip splits every layer over the hidden units of all 8 waves, so each of its ten
+// phases per 64-env chunk ends in an s_barrier and MFMA, VALU and LDS time add up instead of
+// overlapping (profiles/r2_pmc_flagship_set*.md: 24 % MFMA-busy, waves waiting 62 % of their cycles).
+//
+// Here a 512-thread workgroup has two kinds of waves, one of each on every SIMD:
+//
+//  * 4 DATA waves (waves 0-3) each run the WHOLE chain for their own 16-env tile with no other wave
+//    involved: the tile's price windows go from HBM straight into MFMA B-operand registers, every
+//    layer's accumulator tiles become the next layer's B operands in registers (a fixed permutation pi
+//    of the hidden units inside each 32-wide k-step, absorbed by the column order of the weight images
+//    in LDS: no activation round trip through LDS), the epsilon-greedy draw / env step / TD target run
+//    in the 16 lanes that hold an env's Q values, and layer 1 of Q(x') (its price-window part) is
+//    issued together with layer 1 of Q(x) -- one read of every W0 fragment feeds both.  At the end of
+//    its tile a data wave publishes the tile's X, H1, H2, dZ2, dZ1, dQ into a slot of an LDS ring.
+//  * 4 GRADIENT waves (waves 4-7) hold the per-workgroup weight-gradient accumulators (188 VGPRs each,
+//    split by hidden unit) and consume ring slots in sequence order: transposed fragment reads of the
+//    slot images (env = the MFMA k dimension), 16x16x16 MFMAs into dW0 / dW1 / dW2 / db1 / db2.
+//
+// The ring (3 slots of 23.5 KB beside the 88.6 KB of bf16 weight images) is the only coupling: an LDS
+// sequence counter, a "full" word per slot (release / acquire at workgroup scope) and a "freed" count
+// per slot.  Data waves never wait for each other; a gradient wave waits only for the next slot.  The
+// co-resident data and gradient waves of a SIMD overlap MFMA, VALU and LDS time.
+//
+// Specialised to the flagship geometry: window H = 201, padded dims 224-128-128-16 (input slots used:
+// 208 = 6 k-steps of 32 + one of 16), 64-env chunks (one 16-env tile per data wave), static chunk
+// schedule.  Numerics: bf16 operands, fp32 accumulation, the same rounding points as qstep_wide.hip;
+// fp32 summation order differs (bias added first, k order pi inside MFMAs, per-16-env gradient sums).
+#include "qstep.h"
+
+namespace st {
+namespace ws {
+
+constexpr int NW = 8, NT = 64 * NW;
+constexpr int ND = 4, NG = 4;    // data waves (0..3), gradient waves (4..7)
+constexpr int C = 64;            // envs per chunk (one 16-env tile per data wave)
+constexpr int INP = 224, HP = 128;
+constexpr int KX = 208;          // input slots used by layer 1
+constexpr int HWIN = 201;        // window length this kernel is built for
+constexpr int NSLOT = 3;
+
+// ---------------------------------------------------------------------------------- LDS layout (bytes)
+constexpr int oW0 = 0;                          // W0p [128][208] bf16: columns in slot order
+constexpr int oW1 = oW0 + HP * KX * 2;          // W1p [128][128] bf16: columns in pi order, 16-B units swizzled
+constexpr int oW2 = oW1 + HP * HP * 2;          // W2p [4][128] bf16 (rows = actions, columns in pi order)
+constexpr int oW2T = oW2 + 4 * HP * 2;          // W2T [128][4] bf16 (row u2: W2[0..3][u2])
+constexpr int oB1 = oW2T + HP * 4 * 2;          // b1 [128] f32
+constexpr int oB2 = oB1 + HP * 4;               // b2 [16] f32
+constexpr int oSLOT = oB2 + 64;
+// one ring slot: X [16][208], H1 / H2 / DZ2 / DZ1 [16][128] (8-byte chunks swizzled), DQ [16][16]
+constexpr int sX = 0, sH1 = sX + 16 * KX * 2, sH2 = sH1 + 16 * HP * 2, sDZ2 = sH2 + 16 * HP * 2,
+              sDZ1 = sDZ2 + 16 * HP * 2, sDQ = sDZ1 + 16 * HP * 2, SLOT_BYTES = sDQ + 16 * 16 * 2;
+constexpr int oCTL = oSLOT + NSLOT * SLOT_BYTES;   // [0] claim, [1..3] full, [4..6] freed
+constexpr int oST = oCTL + 32;                     // [NW][NSTAT] f32
+constexpr int LDS_BYTES = oST + NW * NSTAT * 4;
+static_assert(LDS_BYTES <= 163840, "LDS budget");
+static_assert(SLOT_BYTES % 16 == 0 && oSLOT % 16 == 0, "alignment");
+
+// ---------------------------------------------------------------------------------- index maps
+// input slot -> flat-layout column of W0^T.  Slots 0..191 are window columns; the last 16-wide k-step
+// is permuted so that the lanes holding an env's Q values (g4 == 0) also hold its tail features:
+//   g4 = 0: 201 budget, 202 shares, 203 constant 1 (layer-0 bias column), 204 pad
+//   g4 = 1: 192..195;  g4 = 2: 196..199;  g4 = 3: 200, 205, 206, 207 (pads)
+ST_DEV int slot_col(int s) {
+  if (s < 192) return s;
+  const int t = s - 192, g = t >> 2, j = t & 3;
+  if (g == 0) return 201 + j;
+  if (g == 1) return 192 + j;
+  if (g == 2) return 196 + j;
+  return j == 0 ? 200 : 204 + j;
+}
+// pi: position s (0..127, k-step s/32, lane group (s/8)%4, element s%8) of a B operand built in
+// registers from accumulator tiles 2*ks and 2*ks+1 -> hidden unit index
+ST_DEV int pi_unit(int s) {
+  const int ks = s >> 5, g = (s >> 3) & 3, j = s & 7;
+  return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
+}
+// W1p element offset of (row R, pi-position s): 16-byte units XOR-swizzled by 2 (R & 7) -- conflict-free
+// row-fragment reads (forward), 2-way transposed reads (backward), tools/lds_bank_sim.py
+ST_DEV int w1_off(int R, int s) { return R * HP + ((((s >> 3) ^ (2 * (R & 7)))) << 3) + (s & 7); }
+// 128-wide slot images: 8-byte chunk c8 of row r at c8 ^ 4 (r & 7) (conflict-free transposed reads)
+ST_DEV int a_off(int r, int c) { return r * HP + ((((c >> 2) ^ (4 * (r & 7)))) << 2) + (c & 3); }
+
+ST_DEV s4v zero_s4() { s4v z = {0, 0, 0, 0}; return z; }
+ST_DEV s8v cat8(s4v a, s4v b) {
+  s8v r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+ST_DEV s4v pk4(float a, float b, float c, float d) {
+  uint2 v;
+  v.x = pack_bf2(a, b);
+  v.y = pack_bf2(c, d);
+  return __builtin_bit_cast(s4v, v);
+}
+ST_DEV s4v relu_bf(f4v v) { return pk4(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)); }
+// accumulator tile -> bf16 masked by (act > 0)
+ST_DEV s4v mask_bf(f4v v, s4v act) {
+  return pk4(act[0] > 0 ? v[0] : 0.f, act[1] > 0 ? v[1] : 0.f, act[2] > 0 ? v[2] : 0.f, act[3] > 0 ? v[3] : 0.f);
+}
+ST_DEV s4v lo4(s8v v) { s4v r = {v[0], v[1], v[2], v[3]}; return r; }
+ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
+// bf16 > 0 test on the raw bits (positive finite / +inf: sign clear and not +0)
+ST_DEV bool bpos(short h) { return h > 0; }
+
+// every ring wait is bounded (~1 s at s_sleep 1): a protocol bug ends the launch with an error bit in
+// p.err instead of leaving waves spinning on the GPU
+constexpr int SPIN_LIMIT = 1 << 24;
+ST_DEV void ws_fail(const QStepParams& p) {
+  if (p.err != nullptr && (threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+}
+
+// ---------------------------------------------------------------------------------- the kernel
+template <int FEAT>
+__global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* W0p = reinterpret_cast<bf16_t*>(smem + oW0);
+  bf16_t* W1p = reinterpret_cast<bf16_t*>(smem + oW1);
+  bf16_t* W2p = reinterpret_cast<bf16_t*>(smem + oW2);
+  bf16_t* W2T = reinterpret_cast<bf16_t*>(smem + oW2T);
+  float* sB1 = reinterpret_cast<float*>(smem + oB1);
+  float* sB2 = reinterpret_cast<float*>(smem + oB2);
+  int* ctl = reinterpret_cast<int*>(smem + oCTL);
+  float* sSt = reinterpret_cast<float*>(smem + oST);
+
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned long long step = p.ctrl[0];
+  const int nchunks = p.E / C;
+  const int nmy = (nchunks - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // chunks of this WG
+
+  // ------------------------------------------------------------------ prologue: weight images, ring state
+  {
+    const bf16_t* w0 = p.wq + p.off_w0;
+    for (int i = tid; i < HP * KX; i += NT) {          // W0p[r][s] = W0^T[r][slot_col(s)]
+      const int r = i / KX, s = i % KX;
+      W0p[i] = w0[r * INP + slot_col(s)];
+    }
+    const bf16_t* w1 = p.wq + p.off_w1;
+    for (int i = tid; i < HP * HP; i += NT) {          // W1p[R][s] = W1^T[R][pi(s)] (swizzled)
+      const int R = i >> 7, s = i & 127;
+      W1p[w1_off(R, s)] = w1[R * HP + pi_unit(s)];
+    }
+    const bf16_t* w2 = p.wq + p.off_w2;
+    for (int i = tid; i < 4 * HP; i += NT) {           // W2p[a][s] = W2^T[a][pi(s)];  W2T[u][a] = W2^T[a][u]
+      const int a = i >> 7, s = i & 127;
+      W2p[i] = w2[a * HP + pi_unit(s)];
+      W2T[s * 4 + a] = w2[a * HP + s];
+    }
+    for (int i = tid; i < HP; i += NT) sB1[i] = p.wf[p.off_b1 + i];
+    if (tid < 16) sB2[tid] = tid < 4 ? p.wf[p.off_b2 + tid] : 0.f;
+    for (int i = tid; i < NSLOT * 16 * 16; i += NT) {  // dQ images: columns 4..15 stay zero
+      const int sl = i >> 8;
+      reinterpret_cast<bf16_t*>(smem + oSLOT + sl * SLOT_BYTES + sDQ)[i & 255] = 0;
+    }
+    if (tid < 8) ctl[tid] = 0;
+  }
+  __syncthreads();
+
+  float* slabf = p.slab;
+  if (wave < ND) {
+    // ================================================================ DATA WAVE
+    const int d = wave;
+    float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
+          st_qslot = 0.f;
+    const float b2v[3] = {sB2[0], sB2[1], sB2[2]};
+
+    // env state of tile k (all lanes load their env l16's words)
+    auto env_of = [&](int k) { return (min((int)blockIdx.x + k * (int)gridDim.x, nchunks - 1)) * C + 16 * d + l16; };
+    int e_pos, e_sh, e_ep, n_pos, n_sh, n_ep;
+    float e_b, e_val, e_rs, n_b, n_val, n_rs;
+#define WS_LOAD_ENV(K, POS, B, SH, VAL, RS, EP)                                                   \
+  {                                                                                              \
+    const int e_ = env_of(K);                                                                    \
+    POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                \
+    VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);          \
+  }
+    // raw prices of a tile: per 32-wide k-step 9 floats (x uses 8, x' the 8 shifted by one), the last
+    // 16-wide k-step 5, and the window's last / next price (p[pos + 200], p[pos + 201])
+    float4 pa[6], pb[6];
+    float pc[6];
+    float4 pd;
+    float pe = 0.f;
+    float4 pl;
+#define WS_LOAD_PRICES(K, POS)                                                                    \
+  {                                                                                              \
+    const int e_ = env_of(K);                                                                    \
+    const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
+    const int sh_ = pc_ & 3;                                                                     \
+    const float* b_ = p.prices4 + ((size_t)sh_ * p.E + (size_t)e_) * p.T4 + (size_t)(pc_ - sh_);  \
+    _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
+      const float* q_ = b_ + 32 * ks + 8 * g4;                                                   \
+      pa[ks] = *reinterpret_cast<const float4*>(q_);                                             \
+      pb[ks] = *reinterpret_cast<const float4*>(q_ + 4);                                         \
+      pc[ks] = q_[8];                                                                            \
+    }                                                                                            \
+    const float* r_ = b_ + 192 + 4 * (g4 == 0 ? 2 : g4 - 1);   /* g4 = 0: unused (tail lanes) */   \
+    pd = *reinterpret_cast<const float4*>(r_);                                                   \
+    pe = r_[4];                                                                                  \
+    pl = *reinterpret_cast<const float4*>(b_ + 200);                                             \
+  }
+    WS_LOAD_ENV(0, e_pos, e_b, e_sh, e_val, e_rs, e_ep)
+    WS_LOAD_PRICES(0, e_pos)
+    WS_LOAD_ENV(1, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+
+    unsigned long long* stamps = (p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0) ? p.stamps : nullptr;
+#define WS_STAMP(I) if (stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime();
+
+    for (int k = 0; k < nmy; ++k) {
+      WS_STAMP(0);
+      const int chunk = (int)blockIdx.x + k * (int)gridDim.x;
+      const int e = chunk * C + 16 * d + l16;
+      // ---------------------------------------------------------------- features -> X / X' B operands
+      const float last = pl.x, vnew = pl.y;
+      float inv = 0.f, invn = 0.f;
+      if (FEAT) {
+        inv = __fdiv_rn(1.0f, last);
+        invn = __fdiv_rn(1.0f, vnew);
+      }
+      auto fx = [&](float w) { return FEAT ? __fsub_rn(__fmul_rn(w, inv), 1.0f) : w; };
+      auto fxn = [&](float w) { return FEAT ? __fsub_rn(__fmul_rn(w, invn), 1.0f) : w; };
+      s8v X[6], Xn[6];
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        X[ks] = cat8(pk4(fx(pa[ks].x), fx(pa[ks].y), fx(pa[ks].z), fx(pa[ks].w)),
+                     pk4(fx(pb[ks].x), fx(pb[ks].y), fx(pb[ks].z), fx(pb[ks].w)));
+        Xn[ks] = cat8(pk4(fxn(pa[ks].y), fxn(pa[ks].z), fxn(pa[ks].w), fxn(pb[ks].x)),
+                      pk4(fxn(pb[ks].y), fxn(pb[ks].z), fxn(pb[ks].w), fxn(pc[ks])));
+      }
+      // last k-step (16 wide): g4 = 0 tail (budget, shares, 1, 0); 1, 2 window columns; 3 column 200
+      s4v X6, Xn6;
+      if (g4 == 0) {
+        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, 0.f);
+        Xn6 = zero_s4();   // completed after the env step
+      } else if (g4 < 3) {
+        X6 = pk4(fx(pd.x), fx(pd.y), fx(pd.z), fx(pd.w));
+        Xn6 = pk4(fxn(pd.y), fxn(pd.z), fxn(pd.w), fxn(pe));
+      } else {
+        X6 = pk4(fx(last), 0.f, 0.f, 0.f);
+        Xn6 = pk4(fxn(vnew), 0.f, 0.f, 0.f);
+      }
+      const int pos = e_pos, sh0 = e_sh, ep0 = e_ep;
+      const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
+      // rotate the prefetched env state; load the one after next
+      e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep;
+      WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+      __builtin_amdgcn_sched_barrier(0);
+      WS_STAMP(1);
+      // ---------------------------------------------------------------- layer 1 of Q(x) and of Q(x')'s window
+      f4v a1[8], a1n[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { a1[i] = zero4(); a1n[i] = zero4(); }
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const s8v a = lds_ld8(W0p + (16 * i + l16) * KX + 32 * ks + 8 * g4);
+          a1[i] = mfma32(a, X[ks], a1[i]);
+          a1n[i] = mfma32(a, Xn[ks], a1n[i]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      s4v w06[8];   // the last k-step's A fragments: used again after the env step (x')
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        w06[i] = lds_ld4(W0p + (16 * i + l16) * KX + 192 + 4 * g4);
+        a1[i] = mfma16(w06[i], X6, a1[i]);
+      }
+      s8v H1[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) H1[ks] = cat8(relu_bf(a1[2 * ks]), relu_bf(a1[2 * ks + 1]));
+      __builtin_amdgcn_sched_barrier(0);
+      // ---------------------------------------------------------------- layer 2 of Q(x)
+      f4v a2[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a2[i] = mfma32(lds_ld8(W1p + w1_off(16 * i + l16, 32 * ks + 8 * g4)), H1[ks], a2[i]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      s8v H2[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
+      // ---------------------------------------------------------------- output layer of Q(x)
+      f4v qa = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+        qa = mfma32(a, H2[ks], qa);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      WS_STAMP(2);
+      // ---------------------------------------------------------------- epsilon-greedy + env step (lanes g4 == 0)
+      float b2 = 0.f, rew = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f;
+      int s2 = 0, act = 0;
+      bool exploit = false;
+      if (g4 == 0) {
+        q0 = qa[0] + b2v[0];
+        q1 = qa[1] + b2v[1];
+        q2 = qa[2] + b2v[2];
+        if (p.output_relu) { q0 = fmaxf(q0, 0.f); q1 = fmaxf(q1, 0.f); q2 = fmaxf(q2, 0.f); }
+        int greedy = 0;
+        float best = q0;
+        if (q1 > best) { best = q1; greedy = 1; }
+        if (q2 > best) { best = q2; greedy = 2; }
+        uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
+                 c2 = (uint32_t)(step >> 32), c3 = 0u;
+        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+        const float u1 = u24(c0), u2 = u24(c1);
+        exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
+        int rnd = (int)(u2 * 3.0f);
+        rnd = rnd > 2 ? 2 : rnd;
+        act = exploit ? greedy : rnd;
+        const float bd = p.compat_env ? p.b0 : bud0;
+        const int sd = p.compat_env ? p.s0 : sh0;
+        const bool buy = (act == 0) && (bd >= vnew);
+        const bool sell = (act == 1) && (sd > 0);
+        b2 = buy ? __fsub_rn(bd, vnew) : (sell ? __fadd_rn(bd, vnew) : bd);
+        s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
+        const float cur = __fadd_rn(bud0, __fmul_rn((float)sh0, vprev));
+        const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
+        rew = __fsub_rn(nw, cur);
+        if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
+        Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, 0.f);
+        st_explore += exploit ? 0.f : 1.f;
+        ENV_I(ER_ACTION, e) = act;
+        ENV_F(ER_REWARD, e) = rew;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // ---------------------------------------------------------------- Q(x'): finish layer 1, layer 2, output
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a1n[i] = mfma16(w06[i], Xn6, a1n[i]);
+      s8v H1n[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) H1n[ks] = cat8(relu_bf(a1n[2 * ks]), relu_bf(a1n[2 * ks + 1]));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a2[i] = mfma32(lds_ld8(W1p + w1_off(16 * i + l16, 32 * ks + 8 * g4)), H1n[ks], a2[i]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      s8v H2n[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) H2n[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
+      f4v qn = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+        qn = mfma32(a, H2n[ks], qn);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      WS_STAMP(3);
+      // ---------------------------------------------------------------- TD target, dQ, state write-back
+      s4v dQ = zero_s4();
+      if (g4 == 0) {
+        float n0 = qn[0] + b2v[0], n1 = qn[1] + b2v[1], n2 = qn[2] + b2v[2];
+        if (p.output_relu) { n0 = fmaxf(n0, 0.f); n1 = fmaxf(n1, 0.f); n2 = fmaxf(n2, 0.f); }
+        int am = 0;
+        float mx = n0;
+        if (n1 > mx) { mx = n1; am = 1; }
+        if (n2 > mx) { mx = n2; am = 2; }
+        const int slot = p.target_compat ? am : act;
+        const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
+        const float qs = slot == 0 ? q0 : (slot == 1 ? q1 : q2);
+        const float diff = __fsub_rn(qs, y);
+        float dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
+        if (p.output_relu && !(qs > 0.f)) dq = 0.f;
+        dQ = pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f, slot == 2 ? dq : 0.f, 0.f);
+        const int np = pos + 1;
+        const float rs = rs0 + rew;
+        float fdone = 0.f, ndone = 0.f;
+        if (np >= p.T - HWIN) {
+          const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
+          ENV_F(ER_LAST_FINAL, e) = fin;
+          ENV_I(ER_EPISODES, e) = ep0 + 1;
+          ENV_F(ER_BUDGET, e) = p.b0;
+          ENV_I(ER_SHARES, e) = p.s0;
+          ENV_F(ER_VALUE, e) = 0.f;
+          ENV_I(ER_POS, e) = 0;
+          ENV_F(ER_RET_SUM, e) = 0.f;
+          fdone = fin;
+          ndone = 1.f;
+        } else {
+          ENV_F(ER_BUDGET, e) = b2;
+          ENV_I(ER_SHARES, e) = s2;
+          ENV_F(ER_VALUE, e) = vnew;
+          ENV_I(ER_POS, e) = np;
+          ENV_F(ER_RET_SUM, e) = rs;
+        }
+        st_reward += rew;
+        st_loss += diff * diff;
+        st_qslot += qs;
+        st_done += ndone;
+        st_fsum += fdone;
+        st_fsq += fdone * fdone;
+      }
+      // the next tile's price windows (their registers are live from here to the next tile's features)
+      if (k + 1 < nmy) WS_LOAD_PRICES(k + 1, e_pos)
+      __builtin_amdgcn_sched_barrier(0);
+      WS_STAMP(4);
+      // ---------------------------------------------------------------- backward: dZ2 = (W2^T dQ) * [H2 > 0]
+      s8v DZ2[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s4v t[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * ks + h;
+          const s4v a = g4 == 0 ? lds_ld4(W2T + (16 * i + l16) * 4) : zero_s4();
+          const f4v v = mfma16(a, dQ, zero4());
+          t[h] = mask_bf(v, h ? hi4(H2[ks]) : lo4(H2[ks]));
+        }
+        DZ2[ks] = cat8(t[0], t[1]);
+      }
+      // ---------------------------------------------------------------- dZ1 = (W1^T dZ2) * [H1 > 0]
+      // A = W1^T: transposed reads of W1p (rows = pi positions of u2 match the k order of DZ2)
+      s4v DZ1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        f4v acc = zero4();
+        const int col = 32 * (i >> 1) + 8 * (l16 & 3) + 4 * (i & 1);   // pi^-1 of units 16i + 4(l16&3) + 0..3
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int R = 32 * ks + 4 * g4 + (l16 >> 2);
+          const s4v lo = lds_tr4(W1p + w1_off(R, col));
+          const s4v hi = lds_tr4(W1p + w1_off(R + 16, col));
+          acc = mfma32(cat8(lo, hi), DZ2[ks], acc);
+        }
+        DZ1[i] = mask_bf(acc, (i & 1) ? hi4(H1[i >> 1]) : lo4(H1[i >> 1]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      WS_STAMP(5);
+      // ---------------------------------------------------------------- publish the tile into the ring
+      {
+        int q = 0;
+        if (lane == 0) q = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        q = __builtin_amdgcn_readfirstlane(q);
+        const int sl = q % NSLOT, round = q / NSLOT;
+        for (int spin = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 4 + sl, __ATOMIC_ACQUIRE,
+                                                                             __HIP_MEMORY_SCOPE_WORKGROUP)) < NG * round;
+             ++spin) {
+          __builtin_amdgcn_s_sleep(1);
+          if (spin > SPIN_LIMIT) { ws_fail(p); break; }   // never expected: report, do not hang the GPU
+        }
+        char* sb = smem + oSLOT + sl * SLOT_BYTES;
+        bf16_t* sx = reinterpret_cast<bf16_t*>(sb + sX);
+#pragma unroll
+        for (int ks = 0; ks < 6; ++ks) *reinterpret_cast<s8v*>(sx + l16 * KX + 32 * ks + 8 * g4) = X[ks];
+        *reinterpret_cast<s4v*>(sx + l16 * KX + 192 + 4 * g4) = X6;
+        bf16_t* s1 = reinterpret_cast<bf16_t*>(sb + sH1);
+        bf16_t* s2i = reinterpret_cast<bf16_t*>(sb + sH2);
+        bf16_t* sz2 = reinterpret_cast<bf16_t*>(sb + sDZ2);
+        bf16_t* sz1 = reinterpret_cast<bf16_t*>(sb + sDZ1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int o = a_off(l16, 16 * i + 4 * g4);
+          *reinterpret_cast<s4v*>(s1 + o) = (i & 1) ? hi4(H1[i >> 1]) : lo4(H1[i >> 1]);
+          *reinterpret_cast<s4v*>(s2i + o) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
+          *reinterpret_cast<s4v*>(sz2 + o) = (i & 1) ? hi4(DZ2[i >> 1]) : lo4(DZ2[i >> 1]);
+          *reinterpret_cast<s4v*>(sz1 + o) = DZ1[i];
+        }
+        if (g4 == 0) *reinterpret_cast<s4v*>(reinterpret_cast<bf16_t*>(sb + sDQ) + l16 * 16) = dQ;
+        if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      WS_STAMP(6);
+    }
+#undef WS_LOAD_ENV
+#undef WS_LOAD_PRICES
+#undef WS_STAMP
+    // per-wave statistics -> LDS (folded after the final barrier)
+    const float v[NSTAT - 1] = {st_reward, st_loss, st_explore, st_done, st_fsum, st_fsq, st_qslot};
+#pragma unroll
+    for (int s = 0; s < NSTAT - 1; ++s) {
+      const float t = wave_sum(v[s]);
+      if (lane == 0) sSt[d * NSTAT + s] = t;
+    }
+    if (lane == 0) sSt[d * NSTAT + NSTAT - 1] = 0.f;
+    __syncthreads();
+  } else {
+    // ================================================================ GRADIENT WAVE
+    const int gw = wave - ND;
+    f4v gW0[2][13], gW1[2][8], gB1[2], gW2[2], gB2 = zero4();
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+#pragma unroll
+      for (int n = 0; n < 13; ++n) gW0[m][n] = zero4();
+#pragma unroll
+      for (int n = 0; n < 8; ++n) gW1[m][n] = zero4();
+      gB1[m] = zero4();
+      gW2[m] = zero4();
+    }
+    s4v ones;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ones[j] = (l16 == 0) ? (short)0x3F80 : (short)0;
+    const int r4 = 4 * g4 + (l16 >> 2), q4 = 4 * (l16 & 3);   // transposed-read row / column offset of this lane
+    const int nseq = ND * nmy;
+    for (int q = 0; q < nseq; ++q) {
+      const int sl = q % NSLOT;
+      for (int spin = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 1 + sl, __ATOMIC_ACQUIRE,
+                                                                           __HIP_MEMORY_SCOPE_WORKGROUP)) != q + 1;
+           ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > SPIN_LIMIT) { ws_fail(p); break; }
+      }
+      const char* sb = smem + oSLOT + sl * SLOT_BYTES;
+      const bf16_t* sx = reinterpret_cast<const bf16_t*>(sb + sX);
+      const bf16_t* s1 = reinterpret_cast<const bf16_t*>(sb + sH1);
+      const bf16_t* s2i = reinterpret_cast<const bf16_t*>(sb + sH2);
+      const bf16_t* sz2 = reinterpret_cast<const bf16_t*>(sb + sDZ2);
+      const bf16_t* sz1 = reinterpret_cast<const bf16_t*>(sb + sDZ1);
+      const bf16_t* sdq = reinterpret_cast<const bf16_t*>(sb + sDQ);
+      // dW0^T[u1][slot] += dZ1^T . X   (this wave's u1 rows 32 gw .. 32 gw + 31)
+      s4v a0[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) a0[m] = lds_tr4(sz1 + a_off(r4, 32 * gw + 16 * m + q4));
+#pragma unroll
+      for (int n = 0; n < 13; ++n) {
+        const s4v b = lds_tr4(sx + r4 * KX + 16 * n + q4);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma16(a0[m], b, gW0[m][n]);
+      }
+      // dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
+      s4v a1[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) a1[m] = lds_tr4(sz2 + a_off(r4, 32 * gw + 16 * m + q4));
+      s4v bh[8];
+#pragma unroll
+      for (int n = 0; n < 8; ++n) bh[n] = lds_tr4(s1 + a_off(r4, 16 * n + q4));
+      const s4v aq = lds_tr4(sdq + r4 * 16 + q4);
+      s4v bh2[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) bh2[n] = lds_tr4(s2i + a_off(r4, 16 * (2 * gw + n) + q4));
+      // every fragment of the slot is in registers: hand the slot back before the MFMAs
+      if (lane == 0) __hip_atomic_fetch_add(ctl + 4 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) gW1[m][n] = mfma16(a1[m], bh[n], gW1[m][n]);
+        gB1[m] = mfma16(a1[m], ones, gB1[m]);
+      }
+#pragma unroll
+      for (int n = 0; n < 2; ++n) gW2[n] = mfma16(aq, bh2[n], gW2[n]);
+      gB2 = mfma16(aq, ones, gB2);
+    }
+    __syncthreads();
+    // ------------------------------------------------------------------ gradient slab write-out
+    // this wave's rows: dW0^T / dW1^T rows 32 gw + 16 m + 4 g4 + j; dW2^T u2 columns 16 (2 gw + n) + l16
+    auto put = [&](int idx, float v) {
+      if (p.slab_bf16) {
+        bf16_t* sb = reinterpret_cast<bf16_t*>(p.slab);
+        sb[((size_t)(idx >> 5) * p.slab_rows + blockIdx.x) * 32 + (idx & 31)] = f2bf(v);
+      } else {
+        slabf[(size_t)blockIdx.x * p.P + idx] = v;
+      }
+    };
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = 32 * gw + 16 * m + 4 * g4 + j;
+#pragma unroll
+        for (int n = 0; n < 13; ++n) put(p.off_w0 + u * INP + slot_col(16 * n + l16), gW0[m][n][j]);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) put(p.off_w1 + u * HP + 16 * n + l16, gW1[m][n][j]);
+        if (l16 == 0) put(p.off_b1 + u, gB1[m][j]);
+      }
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) put(p.off_w2 + (4 * g4 + j) * HP + 16 * (2 * gw + n) + l16, gW2[n][j]);
+    if (gw == 0 && l16 == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
+  }
+  // ------------------------------------------------------------------ workgroup statistics (data waves' sums)
+  if (tid < NSTAT) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < ND; ++w) t += sSt[w * NSTAT + tid];
+    p.stats[(size_t)blockIdx.x * NSTAT + tid] = t;
+  }
+  if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;   // 1-based update count for the optimizer
+}
+
+template <int FEAT>
+static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)qstep_ws_kernel<FEAT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((qstep_ws_kernel<FEAT>), dim3(grid), dim3(NT), LDS_BYTES, stream, p);
+  return hipGetLastError();
+}
+
+}  // namespace ws
+}  // namespace st
+
+extern "C" int st_qstep_ws_lds_bytes(int inp, int h1p, int h2p) {
+  if (inp == st::ws::INP && h1p == st::ws::HP && h2p == st::ws::HP) return st::ws::LDS_BYTES;
+  return -1;
+}
+
+// Preconditions (checked here and by sharetrade/trainer/engine.py): E % 64 == 0, 1 <= grid <= E / 64,
+// H == 201, padded dims (224, 128, 128), static chunk schedule, 32-aligned weight offsets for bf16 slabs.
+extern "C" hipError_t st_qstep_ws_launch(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
+                                         hipStream_t stream) {
+  using namespace st::ws;
+  if (inp != INP || h1p != HP || h2p != HP || p->H != HWIN) return hipErrorInvalidValue;
+  if (p->E % C != 0 || grid < 1 || grid > p->E / C || p->chunk_heads != nullptr) return hipErrorInvalidValue;
+  if (p->T < HWIN + 2 || p->T4 < p->T) return hipErrorInvalidValue;
+  if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
+  if (p->slab_bf16 && (p->slab_rows != grid || p->P % 32 != 0)) return hipErrorInvalidValue;
+  return p->feat_mode ? launch_f<1>(*p, grid, stream) : launch_f<0>(*p, grid, stream);
+}

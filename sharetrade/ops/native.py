@@ -43,6 +43,7 @@ class QStepParams(C.Structure):
         ("slab_bf16", C.c_int), ("slab_rows", C.c_int),
         ("chunk_heads", C.c_void_p),
         ("reward_mode", C.c_int), ("td_clip", C.c_float),
+        ("err", C.c_void_p),
     ]
 
 
@@ -97,6 +98,10 @@ def lib() -> C.CDLL:
     L.st_qstep_pair_launch.restype = C.c_int
     L.st_qstep_pair_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
     L.st_qstep_pair_lds_bytes.restype = C.c_int
+    L.st_qstep_ws_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_qstep_ws_launch.restype = C.c_int
+    L.st_qstep_ws_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.st_qstep_ws_lds_bytes.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
     L.st_reduce_optim.restype = C.c_int
     L.st_advance.argtypes = [C.c_void_p, C.c_void_p]
@@ -167,6 +172,14 @@ def qstep_pair_supported(inp: int, h1p: int, h2p: int) -> bool:
     if not available():
         return False
     return lib().st_qstep_pair_lds_bytes(inp, h1p, h2p) > 0
+
+
+def qstep_ws_supported(inp: int, h1p: int, h2p: int) -> bool:
+    """Wave-specialised variant (csrc/qstep_ws.hip: data waves run whole 16-env tiles, gradient waves
+    consume them through an LDS ring)."""
+    if not available():
+        return False
+    return lib().st_qstep_ws_lds_bytes(inp, h1p, h2p) > 0
 
 
 def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float, key0: int, key1: int) -> None:

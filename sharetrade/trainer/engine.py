@@ -139,13 +139,19 @@ class VectorEngine:
         self.chunk = 32
         self.step_kernel = "narrow"
         sk = cfg.engine.step_kernel
-        if sk not in ("auto", "wide", "narrow", "pair"):
+        if sk not in ("auto", "wide", "narrow", "pair", "ws"):
             raise ValueError(f"engine.step_kernel: {sk!r}")
         if self.kernel == "bf16_fused" and sk == "pair":
             if not (self.E % 64 == 0 and native.qstep_pair_supported(L.pdims[0], L.pdims[1], L.pdims[2])):
                 raise NotImplementedError(f"engine.step_kernel='pair' needs E % 64 == 0 and padded dims "
                                           f"(224, 128, 128); got E={self.E}, dims {L.pdims}")
             self.chunk, self.step_kernel = 64, "pair"
+        elif self.kernel == "bf16_fused" and sk == "ws":
+            if not self.ws_ok(cfg, L):
+                raise NotImplementedError(f"engine.step_kernel='ws' needs E % 64 == 0, history 201, padded dims "
+                                          f"(224, 128, 128) and the static chunk schedule; got E={self.E}, "
+                                          f"H={self.H}, dims {L.pdims}")
+            self.chunk, self.step_kernel = 64, "ws"
         elif self.kernel == "bf16_fused":
             want = int(cfg.engine.chunk)
             wide_ok = self.E % 64 == 0 and native.qstep_wide_supported(L.pdims[0], L.pdims[1], L.pdims[2])
@@ -213,6 +219,13 @@ class VectorEngine:
         self._last_actions: Optional[torch.Tensor] = None
         if be == "native":
             self._init_native()
+
+    def ws_ok(self, cfg: Config, L) -> bool:
+        """Geometry of csrc/qstep_ws.hip (wave-specialised step kernel)."""
+        sched = cfg.engine.chunk_schedule
+        dyn = sched == "dynamic" or (sched == "auto" and self.world_size > 1 and cfg.engine.dp_overlap)
+        return (self.E % 64 == 0 and self.H == 201 and tuple(L.pdims[:3]) == (224, 128, 128) and not dyn
+                and native.qstep_ws_supported(L.pdims[0], L.pdims[1], L.pdims[2]))
 
     # ---------------------------------------------------------------- native buffers
     def _init_native(self):
@@ -294,6 +307,8 @@ class VectorEngine:
         q.chunk_heads = native.ptr(self.chunk_heads) if self.chunk_heads is not None else None
         q.reward_mode = {"absolute": 0, "relative": 1}[cfg.agent.reward_mode]
         q.td_clip = float(cfg.agent.td_clip)
+        self.kernel_err = torch.zeros(4, dtype=torch.int32, device=self.device)
+        q.err = native.ptr(self.kernel_err)
         self._qp = q
         a = cfg.agent
         o = native.OptimParams()
@@ -336,7 +351,9 @@ class VectorEngine:
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
 
     def _launch_qstep(self, L, sh) -> None:
-        if self.step_kernel == "pair":
+        if self.step_kernel == "ws":
+            fn = L.st_qstep_ws_launch
+        elif self.step_kernel == "pair":
             fn = L.st_qstep_pair_launch
         elif self.chunk == 64:
             fn = L.st_qstep_wide_launch_w8 if self.cfg.engine.step_waves == 8 else L.st_qstep_wide_launch

@@ -1,0 +1,153 @@
+"""Numerics of the wave-specialised fused step kernel (csrc/qstep_ws.hip) vs the plain-PyTorch fp32 oracle
+and vs the 64-env-chunk kernel (csrc/qstep_wide.hip).
+
+The oracle (`sharetrade.env.trading.engine_step_ref`) rounds to bf16 at the same points as the kernel
+(``emulate_bf16=True``).  Actions agree except on near-ties of Q (the fp32 summation order inside the
+MFMAs differs); with the kernel's actions forced into the oracle, env transitions and rewards must match
+exactly and the gradient within a relative-norm tolerance.  Small ``engine.grid`` values make every
+workgroup run many tiles, so the LDS ring of the kernel wraps around many times.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(compat=False):
+    from sharetrade.config import preset_config
+
+    cfg = preset_config("flagship")
+    cfg.engine.step_kernel = "ws"
+    if compat:
+        cfg.env.compat_decisions = True
+        cfg.agent.target_slot = "compat"
+        cfg.model.output_relu = True
+    return cfg
+
+
+def _prices(E, T=400, seed=3):
+    from sharetrade.data.prices import random_walk
+
+    return torch.from_numpy(random_walk(T, 50.0, 0.02, seed, n_series=E).astype(np.float32))
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def _oracle(cfg, prices, st0, params, layout, step, loss_coef, **kw):
+    from sharetrade.env import trading as tr
+
+    return tr.engine_step_ref(
+        prices, st0.to("cpu"), params, layout, history=cfg.model.history, feature_mode=cfg.env.features,
+        budget0=cfg.env.budget, shares0=cfg.env.shares, compat_env=cfg.env.compat_decisions,
+        target_slot=cfg.agent.target_slot, gamma=cfg.agent.gamma, output_relu=cfg.model.output_relu,
+        epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0, step=step,
+        loss_coef=loss_coef, reward_mode=cfg.agent.reward_mode, td_clip=cfg.agent.td_clip, **kw)
+
+
+@pytest.mark.parametrize("compat", [False, True])
+@pytest.mark.parametrize("E,grid", [(64, 0), (256, 0), (640, 2), (1024, 3), (4096, 0)])
+def test_ws_matches_oracle(native_built, compat, E, grid):
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _cfg(compat)
+    cfg.agent.epsilon = 0.5
+    cfg.engine.grid = grid
+    prices = _prices(E)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    assert eng.step_kernel == "ws"
+    st0 = eng.state.clone()
+    st0.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 3 % 190)
+    st0.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
+    st0.value.copy_(prices[:, 0].to(dev))
+    for k in st0.as_dict():
+        getattr(eng.state, k).copy_(getattr(st0, k))
+    eng.ctrl.fill_(5)
+    params = eng.params.detach().cpu().clone()
+    grad = eng.native_grad().detach().cpu().clone()
+    torch.cuda.synchronize()
+    assert int(eng.kernel_err.sum()) == 0, "ring wait gave up"
+    acts = eng.actions_out.cpu().clone()
+    rew = eng.rewards_out.cpu().clone()
+    _, _, info0 = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=True)
+    mism = (info0["actions"].cpu() != acts).float().mean().item()
+    assert mism <= 0.05, f"action mismatch rate {mism}"
+    ns, g_ref, info = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=True,
+                              forced_actions=acts)
+    assert torch.equal(info["reward"], rew)
+    for k in ("budget", "shares", "value", "pos", "episodes"):
+        assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), k
+    L = eng.layout
+    for l in range(L.n_layers):
+        gw, rw = L.w(grad, l), L.w(g_ref, l)
+        assert _rel(gw, rw) < 3e-2, (l, _rel(gw, rw))
+        if l > 0:
+            assert _rel(L.b(grad, l), L.b(g_ref, l)) < 3e-2, l
+    # statistics slab: reward sum and the number of explore draws
+    st = eng.stat_slab.sum(0).cpu()
+    assert abs(float(st[0]) - float(info["reward"].sum())) < 1e-3 + 1e-4 * float(info["reward"].abs().sum())
+    assert int(round(float(st[2]))) == int((~info0["exploit"]).sum())
+
+
+def test_ws_episode_end_and_reset(native_built):
+    """Envs at the last position of their series finish the episode in this step: last_final, episode
+    counter and the reset of budget / shares / position written by the data waves."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, T = 256, 260
+    cfg = _cfg()
+    prices = _prices(E, T=T, seed=9)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    st0 = eng.state.clone()
+    st0.pos.copy_(torch.full((E,), T - 201 - 1, dtype=torch.int32, device=dev))
+    st0.pos[::2] = 10
+    st0.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 2)
+    st0.value.copy_(prices[:, 5].to(dev))
+    for k in st0.as_dict():
+        getattr(eng.state, k).copy_(getattr(st0, k))
+    eng.ctrl.fill_(3)
+    params = eng.params.detach().cpu().clone()
+    eng.native_grad()
+    torch.cuda.synchronize()
+    acts = eng.actions_out.cpu().clone()
+    ns, _, _ = _oracle(cfg, prices, st0, params, eng.layout, 3, eng.loss_coef, emulate_bf16=True,
+                       forced_actions=acts)
+    for k in ("budget", "shares", "value", "pos", "episodes", "ret_sum"):
+        assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), k
+    done = ns.episodes.cpu() > 0
+    assert int(done.sum()) == E // 2
+    assert torch.equal(ns.last_final[done], eng.state.last_final.cpu()[done])
+
+
+def test_ws_and_wide_agree_over_steps(native_built):
+    """Ten captured steps of each kernel from the same start: the learned parameters stay close (both are
+    bf16 MFMA steps of the same math; fp32 summation orders differ) and the env statistics agree."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 2048
+    prices = _prices(E, seed=4)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for kern in ("wide", "ws"):
+        cfg = _cfg()
+        cfg.engine.step_kernel = kern
+        cfg.agent.epsilon = 0.0          # every action a uniform draw: identical trajectories
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.step_kernel == kern
+        eng.capture_graph(warmup=1)
+        eng.run(10)
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        out[kern] = (eng.params.detach().cpu().clone(), {k: v.cpu().clone() for k, v in eng.state.as_dict().items()},
+                     eng.stat_acc.cpu().clone())
+    pw, sw, stw = out["wide"]
+    pv, sv, stv = out["ws"]
+    for k in ("budget", "shares", "pos", "value"):
+        assert torch.equal(sw[k], sv[k]), k
+    assert _rel(pv, pw) < 1e-2, _rel(pv, pw)
+    assert torch.allclose(stv[0], stw[0], rtol=1e-5, atol=1e-5)     # reward sums
+    assert torch.allclose(stv[1], stw[1], rtol=2e-2)                # TD loss sums
