@@ -10,7 +10,7 @@ timeout -k 10 150 python -u bench.py --steps 20 --warmup 5 --step-kernel ws --no
   || { echo BENCHWS_FAIL; tail -30 gpurun_out/r3b_bench_ws.log; exit 1; }
 tail -1 gpurun_out/r3b_bench_ws.log
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -rs \
-  --deselect tests/test_gpu_qstep_ws.py > gpurun_out/r3b_pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/r3b_pytest.log; exit 1; }
+  --ignore=tests/test_gpu_qstep_ws.py > gpurun_out/r3b_pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/r3b_pytest.log; exit 1; }
 tail -4 gpurun_out/r3b_pytest.log
 timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r3b_bench.log 2>&1 \
   || { echo BENCH_FAIL; tail -30 gpurun_out/r3b_bench.log; exit 1; }
