@@ -67,6 +67,12 @@ def main() -> int:
                     help="step-kernel chunk schedule: auto (dynamic for overlapped DP) | static | dynamic")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per HIP-graph replay in the timed loop (0 = engine.graph_steps)")
+    ap.add_argument("--pg-timeout", type=float, default=300.0,
+                    help="N>1: collective timeout (s); with TORCH_NCCL_ASYNC_ERROR_HANDLING=1 a dead peer fails "
+                         "the job instead of hanging it")
+    ap.add_argument("--no-episode", action="store_true",
+                    help="skip the untimed full-episode returns (learned policy + random-policy baseline) "
+                         "after the timed window")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
