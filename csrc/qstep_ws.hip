@@ -9,27 +9,29 @@
 //
 // Here a 512-thread workgroup has two kinds of waves, one of each on every SIMD:
 //
-//  * 4 DATA waves (waves 0-3) each run the WHOLE chain for their own 16-env tile with no other wave
-//    involved: the tile's price windows go from HBM straight into MFMA B-operand registers, every
+//  * 4 DATA waves (waves 0-3) each run the forward / TD chain for their own 16-env tile with no other
+//    wave involved: the tile's price windows go from HBM straight into MFMA B-operand registers, every
 //    layer's accumulator tiles become the next layer's B operands in registers (a fixed permutation pi
 //    of the hidden units inside each 32-wide k-step, absorbed by the column order of the weight images
 //    in LDS: no activation round trip through LDS), the epsilon-greedy draw / env step / TD target run
-//    in the 16 lanes that hold an env's Q values, and layer 1 of Q(x') (its price-window part) is
-//    issued together with layer 1 of Q(x) -- one read of every W0 fragment feeds both.  At the end of
-//    its tile a data wave publishes the tile's X, H1, H2, dZ2, dZ1, dQ into a slot of an LDS ring.
+//    in the 16 lanes that hold an env's Q values (the tail features of the state live in the same lanes),
+//    and layer 1 of Q(x') (its price-window part) is issued together with layer 1 of Q(x) -- one read of
+//    every W0 fragment feeds both.  A data wave fills a slot of an LDS ring as it goes: X and H1 after
+//    layer 1, H2 after layer 2, dZ2 = (W2^T dQ) * [H2 > 0] and dQ at the end of its tile.
 //  * 4 GRADIENT waves (waves 4-7) hold the per-workgroup weight-gradient accumulators (188 VGPRs each,
-//    split by hidden unit) and consume ring slots in sequence order: transposed fragment reads of the
-//    slot images (env = the MFMA k dimension), 16x16x16 MFMAs into dW0 / dW1 / dW2 / db1 / db2.
+//    split by hidden unit) and consume ring slots in sequence order: the layer-1 data backward for their
+//    own 32 hidden units (dZ1^T computed directly in the A-operand layout of the next MFMA: env = k),
+//    then transposed fragment reads of the slot images and 16x16x16 MFMAs into dW0 / dW1 / dW2 / db.
 //
-// The ring (3 slots of 23.5 KB beside the 88.6 KB of bf16 weight images) is the only coupling: an LDS
+// The ring (4 slots of 18.5 KB beside the 85.6 KB of bf16 weight images) is the only coupling: an LDS
 // sequence counter, a "full" word per slot (release / acquire at workgroup scope) and a "freed" count
 // per slot.  Data waves never wait for each other; a gradient wave waits only for the next slot.  The
 // co-resident data and gradient waves of a SIMD overlap MFMA, VALU and LDS time.
 //
 // Specialised to the flagship geometry: window H = 201, padded dims 224-128-128-16 (input slots used:
 // 208 = 6 k-steps of 32 + one of 16), 64-env chunks (one 16-env tile per data wave), static chunk
-// schedule.  Numerics: bf16 operands, fp32 accumulation, the same rounding points as qstep_wide.hip;
-// fp32 summation order differs (bias added first, k order pi inside MFMAs, per-16-env gradient sums).
+// schedule.  Numerics: bf16 operands, fp32 accumulation, the rounding points of qstep_wide.hip; fp32
+// summation order differs (bias added first, k order pi inside MFMAs, per-16-env gradient sums).
 #include "qstep.h"
 
 namespace st {
@@ -41,37 +43,37 @@ constexpr int C = 64;            // envs per chunk (one 16-env tile per data wav
 constexpr int INP = 224, HP = 128;
 constexpr int KX = 208;          // input slots used by layer 1
 constexpr int HWIN = 201;        // window length this kernel is built for
-constexpr int NSLOT = 3;
+constexpr int NSLOT = 4;
 
 // ---------------------------------------------------------------------------------- LDS layout (bytes)
 constexpr int oW0 = 0;                          // W0p [128][208] bf16: columns in slot order
 constexpr int oW1 = oW0 + HP * KX * 2;          // W1p [128][128] bf16: columns in pi order, 16-B units swizzled
-constexpr int oW2 = oW1 + HP * HP * 2;          // W2p [4][128] bf16 (rows = actions, columns in pi order)
-constexpr int oW2T = oW2 + 4 * HP * 2;          // W2T [128][4] bf16 (row u2: W2[0..3][u2])
-constexpr int oB1 = oW2T + HP * 4 * 2;          // b1 [128] f32
+constexpr int oW2 = oW1 + HP * HP * 2;          // W2p [4][128] bf16 (rows = actions, row 3 zero; pi order)
+constexpr int oB1 = oW2 + 4 * HP * 2;           // b1 [128] f32
 constexpr int oB2 = oB1 + HP * 4;               // b2 [16] f32
 constexpr int oSLOT = oB2 + 64;
-// one ring slot: X [16][208], H1 / H2 / DZ2 / DZ1 [16][128] (8-byte chunks swizzled), DQ [16][16]
+// one ring slot: X [16][208] (slots 204..207 of each row carry dQ[env][0..3]), H1 / H2 [16][128]
+// (8-byte chunks swizzled), DZ2 [16][128] (pi order, 16-byte units swizzled like W1p)
 constexpr int sX = 0, sH1 = sX + 16 * KX * 2, sH2 = sH1 + 16 * HP * 2, sDZ2 = sH2 + 16 * HP * 2,
-              sDZ1 = sDZ2 + 16 * HP * 2, sDQ = sDZ1 + 16 * HP * 2, SLOT_BYTES = sDQ + 16 * 16 * 2;
-constexpr int oCTL = oSLOT + NSLOT * SLOT_BYTES;   // [0] claim, [1..3] full, [4..6] freed
-constexpr int oST = oCTL + 32;                     // [NW][NSTAT] f32
-constexpr int LDS_BYTES = oST + NW * NSTAT * 4;
+              SLOT_BYTES = sDZ2 + 16 * HP * 2;
+constexpr int oCTL = oSLOT + NSLOT * SLOT_BYTES;   // ints: [0] claim, [1..4] full, [5..8] freed, [10..11] zero
+constexpr int oST = oCTL + 64;                     // [ND][NSTAT] f32
+constexpr int LDS_BYTES = oST + ND * NSTAT * 4;
 static_assert(LDS_BYTES <= 163840, "LDS budget");
 static_assert(SLOT_BYTES % 16 == 0 && oSLOT % 16 == 0, "alignment");
 
 // ---------------------------------------------------------------------------------- index maps
 // input slot -> flat-layout column of W0^T.  Slots 0..191 are window columns; the last 16-wide k-step
 // is permuted so that the lanes holding an env's Q values (g4 == 0) also hold its tail features:
-//   g4 = 0: 201 budget, 202 shares, 203 constant 1 (layer-0 bias column), 204 pad
-//   g4 = 1: 192..195;  g4 = 2: 196..199;  g4 = 3: 200, 205, 206, 207 (pads)
+//   g4 = 0: 201 budget, 202 shares, 203 constant 1 (layer-0 bias column), 200 (the window's last price)
+//   g4 = 1: 192..195;  g4 = 2: 196..199;  g4 = 3: pads 204..207
 ST_DEV int slot_col(int s) {
   if (s < 192) return s;
   const int t = s - 192, g = t >> 2, j = t & 3;
-  if (g == 0) return 201 + j;
+  if (g == 0) return j < 3 ? 201 + j : 200;
   if (g == 1) return 192 + j;
   if (g == 2) return 196 + j;
-  return j == 0 ? 200 : 204 + j;
+  return 204 + j;
 }
 // pi: position s (0..127, k-step s/32, lane group (s/8)%4, element s%8) of a B operand built in
 // registers from accumulator tiles 2*ks and 2*ks+1 -> hidden unit index
@@ -79,13 +81,16 @@ ST_DEV int pi_unit(int s) {
   const int ks = s >> 5, g = (s >> 3) & 3, j = s & 7;
   return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
 }
-// W1p element offset of (row R, pi-position s): 16-byte units XOR-swizzled by 2 (R & 7) -- conflict-free
-// row-fragment reads (forward), 2-way transposed reads (backward), tools/lds_bank_sim.py
+// pi position of natural units 16 i + 4 q + (0..3) (4 consecutive positions)
+ST_DEV int pi_pos4(int i, int q) { return 32 * (i >> 1) + 8 * q + 4 * (i & 1); }
+// pi-ordered images (W1p, DZ2): 16-byte units of row R XOR-swizzled by 2 (R & 7) -- conflict-free 16-byte
+// row reads, 2-way transposed reads (the minimum for one half-unit per lane; tools/lds_bank_sim.py)
 ST_DEV int w1_off(int R, int s) { return R * HP + ((((s >> 3) ^ (2 * (R & 7)))) << 3) + (s & 7); }
-// 128-wide slot images: 8-byte chunk c8 of row r at c8 ^ 4 (r & 7) (conflict-free transposed reads)
+// natural-order 128-wide slot images (H1, H2): 8-byte chunk c8 of row r at c8 ^ 4 (r & 7)
 ST_DEV int a_off(int r, int c) { return r * HP + ((((c >> 2) ^ (4 * (r & 7)))) << 2) + (c & 3); }
 
 ST_DEV s4v zero_s4() { s4v z = {0, 0, 0, 0}; return z; }
+ST_DEV s8v zero_s8() { s8v z = {0, 0, 0, 0, 0, 0, 0, 0}; return z; }
 ST_DEV s8v cat8(s4v a, s4v b) {
   s8v r;
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
@@ -99,20 +104,21 @@ ST_DEV s4v pk4(float a, float b, float c, float d) {
   return __builtin_bit_cast(s4v, v);
 }
 ST_DEV s4v relu_bf(f4v v) { return pk4(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)); }
-// accumulator tile -> bf16 masked by (act > 0)
+// accumulator tile -> bf16 masked by (act > 0) (act: bf16 bits, a positive value has a positive short)
 ST_DEV s4v mask_bf(f4v v, s4v act) {
   return pk4(act[0] > 0 ? v[0] : 0.f, act[1] > 0 ? v[1] : 0.f, act[2] > 0 ? v[2] : 0.f, act[3] > 0 ? v[3] : 0.f);
 }
 ST_DEV s4v lo4(s8v v) { s4v r = {v[0], v[1], v[2], v[3]}; return r; }
 ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
-// bf16 > 0 test on the raw bits (positive finite / +inf: sign clear and not +0)
-ST_DEV bool bpos(short h) { return h > 0; }
 
 // every ring wait is bounded (~1 s at s_sleep 1): a protocol bug ends the launch with an error bit in
 // p.err instead of leaving waves spinning on the GPU
 constexpr int SPIN_LIMIT = 1 << 24;
 ST_DEV void ws_fail(const QStepParams& p) {
   if (p.err != nullptr && (threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
+}
+ST_DEV int lds_acq(const int* w) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 
 // ---------------------------------------------------------------------------------- the kernel
@@ -122,7 +128,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   bf16_t* W0p = reinterpret_cast<bf16_t*>(smem + oW0);
   bf16_t* W1p = reinterpret_cast<bf16_t*>(smem + oW1);
   bf16_t* W2p = reinterpret_cast<bf16_t*>(smem + oW2);
-  bf16_t* W2T = reinterpret_cast<bf16_t*>(smem + oW2T);
   float* sB1 = reinterpret_cast<float*>(smem + oB1);
   float* sB2 = reinterpret_cast<float*>(smem + oB2);
   int* ctl = reinterpret_cast<int*>(smem + oCTL);
@@ -147,22 +152,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       W1p[w1_off(R, s)] = w1[R * HP + pi_unit(s)];
     }
     const bf16_t* w2 = p.wq + p.off_w2;
-    for (int i = tid; i < 4 * HP; i += NT) {           // W2p[a][s] = W2^T[a][pi(s)];  W2T[u][a] = W2^T[a][u]
+    for (int i = tid; i < 4 * HP; i += NT) {           // W2p[a][s] = W2^T[a][pi(s)] (row 3 = padding row)
       const int a = i >> 7, s = i & 127;
       W2p[i] = w2[a * HP + pi_unit(s)];
-      W2T[s * 4 + a] = w2[a * HP + s];
     }
     for (int i = tid; i < HP; i += NT) sB1[i] = p.wf[p.off_b1 + i];
     if (tid < 16) sB2[tid] = tid < 4 ? p.wf[p.off_b2 + tid] : 0.f;
-    for (int i = tid; i < NSLOT * 16 * 16; i += NT) {  // dQ images: columns 4..15 stay zero
-      const int sl = i >> 8;
-      reinterpret_cast<bf16_t*>(smem + oSLOT + sl * SLOT_BYTES + sDQ)[i & 255] = 0;
-    }
-    if (tid < 8) ctl[tid] = 0;
+    if (tid < 16) ctl[tid] = 0;
   }
   __syncthreads();
 
-  float* slabf = p.slab;
   if (wave < ND) {
     // ================================================================ DATA WAVE
     const int d = wave;
@@ -180,11 +179,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                \
     VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);          \
   }
-    // raw prices of a tile: per 32-wide k-step 9 floats (x uses 8, x' the 8 shifted by one), the last
-    // 16-wide k-step 5, and the window's last / next price (p[pos + 200], p[pos + 201])
+    // raw prices of a tile: per 32-wide k-step 9 floats (x uses 8, x' the 8 shifted by one); for the last
+    // 16-wide k-step 5 (lanes g4 = 1, 2); the window's last and next price p[pos + 200], p[pos + 201]
     float4 pa[6], pb[6];
     float pc[6];
-    float4 pd;
+    float4 pd = make_float4(0.f, 0.f, 0.f, 0.f);
     float pe = 0.f;
     float4 pl;
 #define WS_LOAD_PRICES(K, POS)                                                                    \
@@ -199,9 +198,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       pb[ks] = *reinterpret_cast<const float4*>(q_ + 4);                                         \
       pc[ks] = q_[8];                                                                            \
     }                                                                                            \
-    const float* r_ = b_ + 192 + 4 * (g4 == 0 ? 2 : g4 - 1);   /* g4 = 0: unused (tail lanes) */   \
-    pd = *reinterpret_cast<const float4*>(r_);                                                   \
-    pe = r_[4];                                                                                  \
+    if (g4 == 1 || g4 == 2) {                                                                    \
+      const float* r_ = b_ + 188 + 4 * g4;                                                       \
+      pd = *reinterpret_cast<const float4*>(r_);                                                 \
+      pe = r_[4];                                                                                \
+    }                                                                                            \
     pl = *reinterpret_cast<const float4*>(b_ + 200);                                             \
   }
     WS_LOAD_ENV(0, e_pos, e_b, e_sh, e_val, e_rs, e_ep)
@@ -210,6 +211,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 
     unsigned long long* stamps = (p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0) ? p.stamps : nullptr;
 #define WS_STAMP(I) if (stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime();
+#define WS_SB() __builtin_amdgcn_sched_barrier(0)
 
     for (int k = 0; k < nmy; ++k) {
       WS_STAMP(0);
@@ -232,24 +234,24 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         Xn[ks] = cat8(pk4(fxn(pa[ks].y), fxn(pa[ks].z), fxn(pa[ks].w), fxn(pb[ks].x)),
                       pk4(fxn(pb[ks].y), fxn(pb[ks].z), fxn(pb[ks].w), fxn(pc[ks])));
       }
-      // last k-step (16 wide): g4 = 0 tail (budget, shares, 1, 0); 1, 2 window columns; 3 column 200
+      // last k-step (16 wide, slot order): g4 = 0 (budget, shares, 1, col 200); 1, 2 window columns; 3 pads
       s4v X6, Xn6;
       if (g4 == 0) {
-        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, 0.f);
+        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, fx(last));
         Xn6 = zero_s4();   // completed after the env step
       } else if (g4 < 3) {
         X6 = pk4(fx(pd.x), fx(pd.y), fx(pd.z), fx(pd.w));
         Xn6 = pk4(fxn(pd.y), fxn(pd.z), fxn(pd.w), fxn(pe));
       } else {
-        X6 = pk4(fx(last), 0.f, 0.f, 0.f);
-        Xn6 = pk4(fxn(vnew), 0.f, 0.f, 0.f);
+        X6 = zero_s4();
+        Xn6 = zero_s4();
       }
       const int pos = e_pos, sh0 = e_sh, ep0 = e_ep;
       const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
       // rotate the prefetched env state; load the one after next
       e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep;
       WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
-      __builtin_amdgcn_sched_barrier(0);
+      WS_SB();
       WS_STAMP(1);
       // ---------------------------------------------------------------- layer 1 of Q(x) and of Q(x')'s window
       f4v a1[8], a1n[8];
@@ -263,7 +265,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
           a1[i] = mfma32(a, X[ks], a1[i]);
           a1n[i] = mfma32(a, Xn[ks], a1n[i]);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        WS_SB();
       }
       s4v w06[8];   // the last k-step's A fragments: used again after the env step (x')
 #pragma unroll
@@ -274,8 +276,30 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s8v H1[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1[ks] = cat8(relu_bf(a1[2 * ks]), relu_bf(a1[2 * ks + 1]));
-      __builtin_amdgcn_sched_barrier(0);
-      // ---------------------------------------------------------------- layer 2 of Q(x)
+      WS_SB();
+      // ---------------------------------------------------------------- claim a ring slot; X and H1 go in now
+      int q = 0;
+      if (lane == 0) q = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      q = __builtin_amdgcn_readfirstlane(q);
+      const int sl = q % NSLOT, round = q / NSLOT;
+      for (int spin = 0; lds_acq(ctl + 5 + sl) < NG * round; ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > SPIN_LIMIT) { ws_fail(p); break; }   // never expected: report, do not hang the GPU
+      }
+      char* sb = smem + oSLOT + sl * SLOT_BYTES;
+      bf16_t* sx = reinterpret_cast<bf16_t*>(sb + sX);
+      bf16_t* sh1 = reinterpret_cast<bf16_t*>(sb + sH1);
+      bf16_t* sh2 = reinterpret_cast<bf16_t*>(sb + sH2);
+      bf16_t* sz2 = reinterpret_cast<bf16_t*>(sb + sDZ2);
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) *reinterpret_cast<s8v*>(sx + l16 * KX + 32 * ks + 8 * g4) = X[ks];
+      if (g4 < 3) *reinterpret_cast<s4v*>(sx + l16 * KX + 192 + 4 * g4) = X6;   // (g4 = 3: dQ, at the end)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        *reinterpret_cast<s4v*>(sh1 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H1[i >> 1]) : lo4(H1[i >> 1]);
+      WS_SB();
+      WS_STAMP(2);
+      // ---------------------------------------------------------------- layer 2 + output of Q(x)
       f4v a2[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
@@ -283,24 +307,25 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) a2[i] = mfma32(lds_ld8(W1p + w1_off(16 * i + l16, 32 * ks + 8 * g4)), H1[ks], a2[i]);
-        __builtin_amdgcn_sched_barrier(0);
+        WS_SB();
       }
       s8v H2[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
-      // ---------------------------------------------------------------- output layer of Q(x)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        *reinterpret_cast<s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
       f4v qa = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : zero_s8();
         qa = mfma32(a, H2[ks], qa);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      WS_STAMP(2);
+      WS_SB();
+      WS_STAMP(3);
       // ---------------------------------------------------------------- epsilon-greedy + env step (lanes g4 == 0)
       float b2 = 0.f, rew = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f;
       int s2 = 0, act = 0;
-      bool exploit = false;
       if (g4 == 0) {
         q0 = qa[0] + b2v[0];
         q1 = qa[1] + b2v[1];
@@ -314,7 +339,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
                  c2 = (uint32_t)(step >> 32), c3 = 0u;
         philox4x32(c0, c1, c2, c3, p.key0, p.key1);
         const float u1 = u24(c0), u2 = u24(c1);
-        exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
+        const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
         int rnd = (int)(u2 * 3.0f);
         rnd = rnd > 2 ? 2 : rnd;
         act = exploit ? greedy : rnd;
@@ -328,12 +353,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
         rew = __fsub_rn(nw, cur);
         if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
-        Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, 0.f);
+        Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fxn(vnew));
         st_explore += exploit ? 0.f : 1.f;
         ENV_I(ER_ACTION, e) = act;
         ENV_F(ER_REWARD, e) = rew;
       }
-      __builtin_amdgcn_sched_barrier(0);
+      WS_SB();
       // ---------------------------------------------------------------- Q(x'): finish layer 1, layer 2, output
 #pragma unroll
       for (int i = 0; i < 8; ++i) a1n[i] = mfma16(w06[i], Xn6, a1n[i]);
@@ -342,11 +367,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int ks = 0; ks < 4; ++ks) H1n[ks] = cat8(relu_bf(a1n[2 * ks]), relu_bf(a1n[2 * ks + 1]));
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
+      WS_SB();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) a2[i] = mfma32(lds_ld8(W1p + w1_off(16 * i + l16, 32 * ks + 8 * g4)), H1n[ks], a2[i]);
-        __builtin_amdgcn_sched_barrier(0);
+        WS_SB();
       }
       s8v H2n[4];
 #pragma unroll
@@ -354,13 +380,14 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v qn = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : s8v{0, 0, 0, 0, 0, 0, 0, 0};
+        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : zero_s8();
         qn = mfma32(a, H2n[ks], qn);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      WS_STAMP(3);
+      WS_SB();
+      WS_STAMP(4);
       // ---------------------------------------------------------------- TD target, dQ, state write-back
-      s4v dQ = zero_s4();
+      float dq = 0.f;
+      int slot = 0;
       if (g4 == 0) {
         float n0 = qn[0] + b2v[0], n1 = qn[1] + b2v[1], n2 = qn[2] + b2v[2];
         if (p.output_relu) { n0 = fmaxf(n0, 0.f); n1 = fmaxf(n1, 0.f); n2 = fmaxf(n2, 0.f); }
@@ -368,13 +395,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         float mx = n0;
         if (n1 > mx) { mx = n1; am = 1; }
         if (n2 > mx) { mx = n2; am = 2; }
-        const int slot = p.target_compat ? am : act;
+        slot = p.target_compat ? am : act;
         const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
         const float qs = slot == 0 ? q0 : (slot == 1 ? q1 : q2);
         const float diff = __fsub_rn(qs, y);
-        float dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
+        dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
         if (p.output_relu && !(qs > 0.f)) dq = 0.f;
-        dQ = pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f, slot == 2 ? dq : 0.f, 0.f);
         const int np = pos + 1;
         const float rs = rs0 + rew;
         float fdone = 0.f, ndone = 0.f;
@@ -405,73 +431,32 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       // the next tile's price windows (their registers are live from here to the next tile's features)
       if (k + 1 < nmy) WS_LOAD_PRICES(k + 1, e_pos)
-      __builtin_amdgcn_sched_barrier(0);
-      WS_STAMP(4);
-      // ---------------------------------------------------------------- backward: dZ2 = (W2^T dQ) * [H2 > 0]
-      s8v DZ2[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s4v t[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int i = 2 * ks + h;
-          const s4v a = g4 == 0 ? lds_ld4(W2T + (16 * i + l16) * 4) : zero_s4();
-          const f4v v = mfma16(a, dQ, zero4());
-          t[h] = mask_bf(v, h ? hi4(H2[ks]) : lo4(H2[ks]));
-        }
-        DZ2[ks] = cat8(t[0], t[1]);
-      }
-      // ---------------------------------------------------------------- dZ1 = (W1^T dZ2) * [H1 > 0]
-      // A = W1^T: transposed reads of W1p (rows = pi positions of u2 match the k order of DZ2)
-      s4v DZ1[8];
+      WS_SB();
+      WS_STAMP(5);
+      // ---------------------------------------------------------------- dZ2 = (W2^T dQ) * [H2 > 0]
+      // dQ has one nonzero entry per env (its slot), so dZ2[env][u2] = bf16(dq) * W2[slot][u2]: an exact
+      // fp32 product, as the MFMA with the bf16 dQ row would give.  (slot, dq) live in lanes g4 == 0.
+      const int slot_b = __shfl(slot, l16, 64);
+      const float dq_b = bf2f(f2bf(__shfl(dq, l16, 64)));
+      s4v dz[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        f4v acc = zero4();
-        const int col = 32 * (i >> 1) + 8 * (l16 & 3) + 4 * (i & 1);   // pi^-1 of units 16i + 4(l16&3) + 0..3
+        const s4v w = lds_ld4(W2p + slot_b * HP + pi_pos4(i, g4));
+        const s4v h = *reinterpret_cast<const s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4));
+        f4v v;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int R = 32 * ks + 4 * g4 + (l16 >> 2);
-          const s4v lo = lds_tr4(W1p + w1_off(R, col));
-          const s4v hi = lds_tr4(W1p + w1_off(R + 16, col));
-          acc = mfma32(cat8(lo, hi), DZ2[ks], acc);
-        }
-        DZ1[i] = mask_bf(acc, (i & 1) ? hi4(H1[i >> 1]) : lo4(H1[i >> 1]));
-        __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < 4; ++j) v[j] = __fmul_rn(dq_b, bf2f((bf16_t)w[j]));
+        dz[i] = mask_bf(v, h);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      WS_STAMP(5);
-      // ---------------------------------------------------------------- publish the tile into the ring
-      {
-        int q = 0;
-        if (lane == 0) q = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        q = __builtin_amdgcn_readfirstlane(q);
-        const int sl = q % NSLOT, round = q / NSLOT;
-        for (int spin = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 4 + sl, __ATOMIC_ACQUIRE,
-                                                                             __HIP_MEMORY_SCOPE_WORKGROUP)) < NG * round;
-             ++spin) {
-          __builtin_amdgcn_s_sleep(1);
-          if (spin > SPIN_LIMIT) { ws_fail(p); break; }   // never expected: report, do not hang the GPU
-        }
-        char* sb = smem + oSLOT + sl * SLOT_BYTES;
-        bf16_t* sx = reinterpret_cast<bf16_t*>(sb + sX);
+      // publish: dZ2 (pi order: tiles 2 ks, 2 ks + 1 form k-step ks), dQ in the X row's pad slots
 #pragma unroll
-        for (int ks = 0; ks < 6; ++ks) *reinterpret_cast<s8v*>(sx + l16 * KX + 32 * ks + 8 * g4) = X[ks];
-        *reinterpret_cast<s4v*>(sx + l16 * KX + 192 + 4 * g4) = X6;
-        bf16_t* s1 = reinterpret_cast<bf16_t*>(sb + sH1);
-        bf16_t* s2i = reinterpret_cast<bf16_t*>(sb + sH2);
-        bf16_t* sz2 = reinterpret_cast<bf16_t*>(sb + sDZ2);
-        bf16_t* sz1 = reinterpret_cast<bf16_t*>(sb + sDZ1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int o = a_off(l16, 16 * i + 4 * g4);
-          *reinterpret_cast<s4v*>(s1 + o) = (i & 1) ? hi4(H1[i >> 1]) : lo4(H1[i >> 1]);
-          *reinterpret_cast<s4v*>(s2i + o) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
-          *reinterpret_cast<s4v*>(sz2 + o) = (i & 1) ? hi4(DZ2[i >> 1]) : lo4(DZ2[i >> 1]);
-          *reinterpret_cast<s4v*>(sz1 + o) = DZ1[i];
-        }
-        if (g4 == 0) *reinterpret_cast<s4v*>(reinterpret_cast<bf16_t*>(sb + sDQ) + l16 * 16) = dQ;
-        if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+      for (int ks = 0; ks < 4; ++ks)
+        *reinterpret_cast<s8v*>(sz2 + w1_off(l16, 32 * ks + 8 * g4)) = cat8(dz[2 * ks], dz[2 * ks + 1]);
+      if (g4 == 0)
+        *reinterpret_cast<s4v*>(sx + l16 * KX + 204) = pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f,
+                                                          slot == 2 ? dq : 0.f, 0.f);
+      if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      WS_SB();
       WS_STAMP(6);
     }
 #undef WS_LOAD_ENV
@@ -488,7 +473,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     __syncthreads();
   } else {
     // ================================================================ GRADIENT WAVE
-    const int gw = wave - ND;
+    const int gw = wave - ND;   // owns hidden units 32 gw .. 32 gw + 31 of both layers, dW2 columns likewise
     f4v gW0[2][13], gW1[2][8], gB1[2], gW2[2], gB2 = zero4();
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -502,46 +487,66 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     s4v ones;
 #pragma unroll
     for (int j = 0; j < 4; ++j) ones[j] = (l16 == 0) ? (short)0x3F80 : (short)0;
-    const int r4 = 4 * g4 + (l16 >> 2), q4 = 4 * (l16 & 3);   // transposed-read row / column offset of this lane
+    const int r4 = 4 * g4 + (l16 >> 2), qq = l16 & 3;   // transposed-read row / chunk of this lane
+    const bf16_t* zchunk = reinterpret_cast<const bf16_t*>(ctl + 10);   // 8 zero bytes
     const int nseq = ND * nmy;
+    // debug stamps of gradient wave 0 of workgroup 0: per slot (wait begins, slot full, slot done) after the
+    // data-wave rows ((nmy + 1) * 16 words in)
+    unsigned long long* gst = (p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
+                                  ? p.stamps + (size_t)(nmy + 1) * 16 : nullptr;
     for (int q = 0; q < nseq; ++q) {
       const int sl = q % NSLOT;
-      for (int spin = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 1 + sl, __ATOMIC_ACQUIRE,
-                                                                           __HIP_MEMORY_SCOPE_WORKGROUP)) != q + 1;
-           ++spin) {
+      if (gst) gst[4 * q] = __builtin_amdgcn_s_memtime();
+      for (int spin = 0; lds_acq(ctl + 1 + sl) != q + 1; ++spin) {
         __builtin_amdgcn_s_sleep(1);
         if (spin > SPIN_LIMIT) { ws_fail(p); break; }
       }
+      if (gst) gst[4 * q + 1] = __builtin_amdgcn_s_memtime();
       const char* sb = smem + oSLOT + sl * SLOT_BYTES;
       const bf16_t* sx = reinterpret_cast<const bf16_t*>(sb + sX);
-      const bf16_t* s1 = reinterpret_cast<const bf16_t*>(sb + sH1);
-      const bf16_t* s2i = reinterpret_cast<const bf16_t*>(sb + sH2);
+      const bf16_t* sh1 = reinterpret_cast<const bf16_t*>(sb + sH1);
+      const bf16_t* sh2 = reinterpret_cast<const bf16_t*>(sb + sH2);
       const bf16_t* sz2 = reinterpret_cast<const bf16_t*>(sb + sDZ2);
-      const bf16_t* sz1 = reinterpret_cast<const bf16_t*>(sb + sDZ1);
-      const bf16_t* sdq = reinterpret_cast<const bf16_t*>(sb + sDQ);
-      // dW0^T[u1][slot] += dZ1^T . X   (this wave's u1 rows 32 gw .. 32 gw + 31)
+      // ---- dZ1 for this wave's u1 tiles i = 2 gw + t:  C[env][u1] = sum_u2 dZ2[env][u2] W1[u2][u1]
+      //      (A = dZ2 rows in pi order, B = W1 read transposed from W1p); the result lane (u1, g4) holds envs
+      //      4 g4 .. 4 g4 + 3 -- the A layout of the dW0 MFMA, no transpose needed
+      f4v c1[2] = {zero4(), zero4()};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const s8v az = lds_ld8(sz2 + w1_off(l16, 32 * ks + 8 * g4));
+        const int R = 32 * ks + 4 * g4 + (l16 >> 2);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int col = pi_pos4(2 * gw + t, qq);
+          c1[t] = mfma32(az, cat8(lds_tr4(W1p + w1_off(R, col)), lds_tr4(W1p + w1_off(R + 16, col))), c1[t]);
+        }
+      }
+      WS_SB();
+      s4v bh[8];   // H1[env 4 g4 .. + 3][u1 = 16 n + l16]
+#pragma unroll
+      for (int n = 0; n < 8; ++n) bh[n] = lds_tr4(sh1 + a_off(r4, 16 * n + 4 * qq));
       s4v a0[2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) a0[m] = lds_tr4(sz1 + a_off(r4, 32 * gw + 16 * m + q4));
+      for (int t = 0; t < 2; ++t) a0[t] = mask_bf(c1[t], bh[2 * gw + t]);
+      WS_SB();
+      // ---- dW0^T[u1][slot] += dZ1^T . X
 #pragma unroll
       for (int n = 0; n < 13; ++n) {
-        const s4v b = lds_tr4(sx + r4 * KX + 16 * n + q4);
+        const s4v b = lds_tr4(sx + r4 * KX + 16 * n + 4 * qq);
 #pragma unroll
         for (int m = 0; m < 2; ++m) gW0[m][n] = mfma16(a0[m], b, gW0[m][n]);
       }
-      // dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
+      WS_SB();
+      // ---- dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
       s4v a1[2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) a1[m] = lds_tr4(sz2 + a_off(r4, 32 * gw + 16 * m + q4));
-      s4v bh[8];
-#pragma unroll
-      for (int n = 0; n < 8; ++n) bh[n] = lds_tr4(s1 + a_off(r4, 16 * n + q4));
-      const s4v aq = lds_tr4(sdq + r4 * 16 + q4);
+      for (int m = 0; m < 2; ++m) a1[m] = lds_tr4(sz2 + w1_off(r4, pi_pos4(2 * gw + m, qq)));
+      const s4v aq = lds_tr4(qq == 0 ? sx + r4 * KX + 204 : zchunk);   // dQ^T[a][env]: a = l16 < 4
       s4v bh2[2];
 #pragma unroll
-      for (int n = 0; n < 2; ++n) bh2[n] = lds_tr4(s2i + a_off(r4, 16 * (2 * gw + n) + q4));
+      for (int n = 0; n < 2; ++n) bh2[n] = lds_tr4(sh2 + a_off(r4, 16 * (2 * gw + n) + 4 * qq));
       // every fragment of the slot is in registers: hand the slot back before the MFMAs
-      if (lane == 0) __hip_atomic_fetch_add(ctl + 4 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
 #pragma unroll
@@ -551,16 +556,18 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int n = 0; n < 2; ++n) gW2[n] = mfma16(aq, bh2[n], gW2[n]);
       gB2 = mfma16(aq, ones, gB2);
+      WS_SB();
+      if (gst) gst[4 * q + 2] = __builtin_amdgcn_s_memtime();
     }
     __syncthreads();
     // ------------------------------------------------------------------ gradient slab write-out
     // this wave's rows: dW0^T / dW1^T rows 32 gw + 16 m + 4 g4 + j; dW2^T u2 columns 16 (2 gw + n) + l16
     auto put = [&](int idx, float v) {
       if (p.slab_bf16) {
-        bf16_t* sb = reinterpret_cast<bf16_t*>(p.slab);
-        sb[((size_t)(idx >> 5) * p.slab_rows + blockIdx.x) * 32 + (idx & 31)] = f2bf(v);
+        bf16_t* sbf = reinterpret_cast<bf16_t*>(p.slab);
+        sbf[((size_t)(idx >> 5) * p.slab_rows + blockIdx.x) * 32 + (idx & 31)] = f2bf(v);
       } else {
-        slabf[(size_t)blockIdx.x * p.P + idx] = v;
+        p.slab[(size_t)blockIdx.x * p.P + idx] = v;
       }
     };
 #pragma unroll
@@ -582,6 +589,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
   }
+#undef WS_SB
   // ------------------------------------------------------------------ workgroup statistics (data waves' sums)
   if (tid < NSTAT) {
     float t = 0.f;
@@ -620,7 +628,7 @@ extern "C" hipError_t st_qstep_ws_launch(const st::QStepParams* p, int inp, int 
   using namespace st::ws;
   if (inp != INP || h1p != HP || h2p != HP || p->H != HWIN) return hipErrorInvalidValue;
   if (p->E % C != 0 || grid < 1 || grid > p->E / C || p->chunk_heads != nullptr) return hipErrorInvalidValue;
-  if (p->T < HWIN + 2 || p->T4 < p->T) return hipErrorInvalidValue;
+  if (p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->slab_bf16 && (p->slab_rows != grid || p->P % 32 != 0)) return hipErrorInvalidValue;
   return p->feat_mode ? launch_f<1>(*p, grid, stream) : launch_f<0>(*p, grid, stream);

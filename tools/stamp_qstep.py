@@ -29,6 +29,8 @@ def main():
     a = ap.parse_args()
     if a.kernel == "pair":
         return pair_stamps(a)
+    if a.kernel == "ws":
+        return ws_stamps(a)
     import build
 
     build.build_all()
@@ -138,3 +140,52 @@ def pair_stamps(a):
 
 if __name__ == "__main__":
     main()
+
+
+def ws_stamps(a):
+    """csrc/qstep_ws.hip: data wave 0 of workgroup 0 per 16-env tile, gradient wave 0 per ring slot."""
+    import build
+
+    build.build_all()
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    cfg.engine.step_kernel = "ws"
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, device=dev, envs=a.envs)
+    eng.run(3)
+    torch.cuda.synchronize()
+    nmy = (a.envs // 64 + eng.grid - 1) // eng.grid
+    st = torch.zeros((nmy + 1) * 16 + 4 * 4 * nmy + 16, dtype=torch.int64, device=dev)
+    eng._qp.stamps = st.data_ptr()
+    eng.step()
+    torch.cuda.synchronize()
+    eng._qp.stamps = None
+    assert int(eng.kernel_err.sum()) == 0
+    raw = st.cpu()
+    s = raw[: nmy * 16].view(nmy, 16).double()
+    names = ["features (+ env prefetch)", "layer 1 of Q(x), Q(x') window + slot claim + X/H1 -> slot",
+             "layer 2 + output of Q(x), H2 -> slot", "epsilon-greedy + env step, rest of Q(x')",
+             "TD + state write-back + next prices issued", "dZ2 + publish"]
+    lines = [f"# ws step kernel: data wave 0 of workgroup 0 ({a.envs} envs, grid {eng.grid}, {nmy} tiles per data "
+             f"wave; s_memtime ticks)\n", "| phase | ticks/tile | % |", "|---|---|---|"]
+    tot = 0.0
+    rows = []
+    for ph in range(6):
+        d = float((s[:, ph + 1] - s[:, ph]).mean())
+        rows.append((names[ph], d))
+        tot += d
+    for n, v in rows:
+        lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
+    loop = float((s[1:, 0] - s[:-1, 0]).mean()) if nmy > 1 else tot
+    lines.append(f"| tile loop (stamp0 -> stamp0) | {loop:.0f} | |")
+    g = raw[(nmy + 1) * 16: (nmy + 1) * 16 + 4 * 4 * nmy].view(4 * nmy, 4).double()
+    wait = float((g[:, 1] - g[:, 0]).mean())
+    work = float((g[:, 2] - g[:, 1]).mean())
+    lines += ["", f"gradient wave 0: per ring slot {work:.0f} ticks of work, {wait:.0f} ticks waiting for the next "
+              f"slot ({4 * nmy} slots; {100 * work / max(work + wait, 1):.0f} % busy)"]
+    txt = "\n".join(lines) + "\n"
+    print(txt)
+    if a.out:
+        open(a.out, "w").write(txt)
