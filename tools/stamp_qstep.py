@@ -138,10 +138,6 @@ def pair_stamps(a):
         open(a.out, "w").write(txt)
 
 
-if __name__ == "__main__":
-    main()
-
-
 def ws_stamps(a):
     """csrc/qstep_ws.hip: data wave 0 of workgroup 0 per 16-env tile, gradient wave 0 per ring slot."""
     import build
@@ -189,3 +185,7 @@ def ws_stamps(a):
     print(txt)
     if a.out:
         open(a.out, "w").write(txt)
+
+
+if __name__ == "__main__":
+    main()
