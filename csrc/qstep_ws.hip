@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 
     unsigned long long* stamps = (p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0) ? p.stamps : nullptr;
 #define WS_STAMP(I) if (stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime();
+#define WS_PIN(V) asm volatile("" ::"v"(V))
 #define WS_SB() __builtin_amdgcn_sched_barrier(0)
 
     for (int k = 0; k < nmy; ++k) {
@@ -251,6 +252,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // rotate the prefetched env state; load the one after next
       e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep;
       WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+      WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
       WS_SB();
       WS_STAMP(1);
       // ---------------------------------------------------------------- layer 1 of Q(x) and of Q(x')'s window
@@ -276,7 +278,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s8v H1[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1[ks] = cat8(relu_bf(a1[2 * ks]), relu_bf(a1[2 * ks + 1]));
+      WS_PIN(H1[3]); WS_PIN(a1n[7]);
       WS_SB();
+      WS_STAMP(2);
       // ---------------------------------------------------------------- claim a ring slot; X and H1 go in now
       int q = 0;
       if (lane == 0) q = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -286,6 +290,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         __builtin_amdgcn_s_sleep(1);
         if (spin > SPIN_LIMIT) { ws_fail(p); break; }   // never expected: report, do not hang the GPU
       }
+      WS_STAMP(3);
       char* sb = smem + oSLOT + sl * SLOT_BYTES;
       bf16_t* sx = reinterpret_cast<bf16_t*>(sb + sX);
       bf16_t* sh1 = reinterpret_cast<bf16_t*>(sb + sH1);
@@ -298,7 +303,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int i = 0; i < 8; ++i)
         *reinterpret_cast<s4v*>(sh1 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H1[i >> 1]) : lo4(H1[i >> 1]);
       WS_SB();
-      WS_STAMP(2);
+      WS_STAMP(4);
       // ---------------------------------------------------------------- layer 2 + output of Q(x)
       f4v a2[8];
 #pragma unroll
@@ -315,14 +320,18 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         *reinterpret_cast<s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
+      WS_PIN(H2[3]);
+      WS_SB();
+      WS_STAMP(5);
       f4v qa = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : zero_s8();
         qa = mfma32(a, H2[ks], qa);
       }
+      WS_PIN(qa);
       WS_SB();
-      WS_STAMP(3);
+      WS_STAMP(6);
       // ---------------------------------------------------------------- epsilon-greedy + env step (lanes g4 == 0)
       float b2 = 0.f, rew = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f;
       int s2 = 0, act = 0;
@@ -358,7 +367,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         ENV_I(ER_ACTION, e) = act;
         ENV_F(ER_REWARD, e) = rew;
       }
+      WS_PIN(Xn6);
       WS_SB();
+      WS_STAMP(7);
       // ---------------------------------------------------------------- Q(x'): finish layer 1, layer 2, output
 #pragma unroll
       for (int i = 0; i < 8; ++i) a1n[i] = mfma16(w06[i], Xn6, a1n[i]);
@@ -383,8 +394,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : zero_s8();
         qn = mfma32(a, H2n[ks], qn);
       }
+      WS_PIN(qn);
       WS_SB();
-      WS_STAMP(4);
+      WS_STAMP(8);
       // ---------------------------------------------------------------- TD target, dQ, state write-back
       float dq = 0.f;
       int slot = 0;
@@ -432,7 +444,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // the next tile's price windows (their registers are live from here to the next tile's features)
       if (k + 1 < nmy) WS_LOAD_PRICES(k + 1, e_pos)
       WS_SB();
-      WS_STAMP(5);
+      WS_STAMP(9);
       // ---------------------------------------------------------------- dZ2 = (W2^T dQ) * [H2 > 0]
       // dQ has one nonzero entry per env (its slot), so dZ2[env][u2] = bf16(dq) * W2[slot][u2]: an exact
       // fp32 product, as the MFMA with the bf16 dQ row would give.  (slot, dq) live in lanes g4 == 0.
@@ -448,6 +460,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         for (int j = 0; j < 4; ++j) v[j] = __fmul_rn(dq_b, bf2f((bf16_t)w[j]));
         dz[i] = mask_bf(v, h);
       }
+      WS_PIN(dz[7]);
+      WS_SB();
+      WS_STAMP(10);
       // publish: dZ2 (pi order: tiles 2 ks, 2 ks + 1 form k-step ks), dQ in the X row's pad slots
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
@@ -457,7 +472,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
                                                           slot == 2 ? dq : 0.f, 0.f);
       if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       WS_SB();
-      WS_STAMP(6);
+      WS_STAMP(11);
     }
 #undef WS_LOAD_ENV
 #undef WS_LOAD_PRICES
@@ -494,14 +509,15 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     // data-wave rows ((nmy + 1) * 16 words in)
     unsigned long long* gst = (p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
                                   ? p.stamps + (size_t)(nmy + 1) * 16 : nullptr;
+#define WS_GST(I) if (gst) gst[8 * q + (I)] = __builtin_amdgcn_s_memtime();
     for (int q = 0; q < nseq; ++q) {
       const int sl = q % NSLOT;
-      if (gst) gst[4 * q] = __builtin_amdgcn_s_memtime();
+      WS_GST(0);
       for (int spin = 0; lds_acq(ctl + 1 + sl) != q + 1; ++spin) {
         __builtin_amdgcn_s_sleep(1);
         if (spin > SPIN_LIMIT) { ws_fail(p); break; }
       }
-      if (gst) gst[4 * q + 1] = __builtin_amdgcn_s_memtime();
+      WS_GST(1);
       const char* sb = smem + oSLOT + sl * SLOT_BYTES;
       const bf16_t* sx = reinterpret_cast<const bf16_t*>(sb + sX);
       const bf16_t* sh1 = reinterpret_cast<const bf16_t*>(sb + sH1);
@@ -521,14 +537,18 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
           c1[t] = mfma32(az, cat8(lds_tr4(W1p + w1_off(R, col)), lds_tr4(W1p + w1_off(R + 16, col))), c1[t]);
         }
       }
+      WS_PIN(c1[0]); WS_PIN(c1[1]);
       WS_SB();
+      WS_GST(2);
       s4v bh[8];   // H1[env 4 g4 .. + 3][u1 = 16 n + l16]
 #pragma unroll
       for (int n = 0; n < 8; ++n) bh[n] = lds_tr4(sh1 + a_off(r4, 16 * n + 4 * qq));
       s4v a0[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) a0[t] = mask_bf(c1[t], bh[2 * gw + t]);
+      WS_PIN(a0[1]);
       WS_SB();
+      WS_GST(3);
       // ---- dW0^T[u1][slot] += dZ1^T . X
 #pragma unroll
       for (int n = 0; n < 13; ++n) {
@@ -536,7 +556,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
         for (int m = 0; m < 2; ++m) gW0[m][n] = mfma16(a0[m], b, gW0[m][n]);
       }
+      WS_PIN(gW0[1][12]);
       WS_SB();
+      WS_GST(4);
       // ---- dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
       s4v a1[2];
 #pragma unroll
@@ -547,6 +569,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int n = 0; n < 2; ++n) bh2[n] = lds_tr4(sh2 + a_off(r4, 16 * (2 * gw + n) + 4 * qq));
       // every fragment of the slot is in registers: hand the slot back before the MFMAs
       if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      WS_GST(5);
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
 #pragma unroll
@@ -556,8 +579,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int n = 0; n < 2; ++n) gW2[n] = mfma16(aq, bh2[n], gW2[n]);
       gB2 = mfma16(aq, ones, gB2);
+      WS_PIN(gW1[1][7]); WS_PIN(gB2);
       WS_SB();
-      if (gst) gst[4 * q + 2] = __builtin_amdgcn_s_memtime();
+      WS_GST(6);
     }
     __syncthreads();
     // ------------------------------------------------------------------ gradient slab write-out
@@ -590,6 +614,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
   }
 #undef WS_SB
+#undef WS_PIN
+#undef WS_GST
   // ------------------------------------------------------------------ workgroup statistics (data waves' sums)
   if (tid < NSTAT) {
     float t = 0.f;

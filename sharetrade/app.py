@@ -40,11 +40,18 @@ logger = logging.getLogger("sharetrade.ShareTradeHelper")
 
 
 def run(cfg: Optional[Config] = None, engine: str = "actors", device: Optional[str] = None,
-        max_prices: Optional[int] = None, quiet: bool = False) -> Dict[str, float]:
-    """Run the application; returns ``{"avg", "std", "completed", "elapsed_s", ...}``."""
+        max_prices: Optional[int] = None, quiet: bool = False, gpus: int = 1,
+        dp: Optional[Dict] = None) -> Dict[str, float]:
+    """Run the application; returns ``{"avg", "std", "completed", "elapsed_s", ...}``.
+
+    ``engine="vector", gpus=N > 1``: the router's N routees are the ranks of a data-parallel group, one
+    process per GPU (``sharetrade/trainer/dp_actors.py``); ``dp`` passes the group's options
+    (``device`` "cuda" / "cpu", ``backend``, ``envs_per_rank``, ``ckpt_dir``, ``ckpt_every``,
+    ``same_device``, ``out_dir``, ``group_kw``).  The parent process never touches the GPU."""
     cfg = cfg or preset_config("reference_compat")
     rc = cfg.router
-    dev = _device(device or cfg.engine.device)
+    dp_mode = engine == "vector" and int(gpus) > 1
+    dev = None if dp_mode else _device(device or cfg.engine.device)
     system = ActorSystem("ShareTradeHelperSystem", loglevel=cfg.log.loglevel)
     t0 = time.perf_counter()
     out: Dict[str, float] = {"completed": 0.0}
@@ -60,7 +67,18 @@ def run(cfg: Optional[Config] = None, engine: str = "actors", device: Optional[s
 
             prices = prices.map(lambda r: StockDataResponse(r.stock_name,
                                                             TreeMap(list(r.share_prices.items())[:max_prices])))
-        if engine == "vector":
+        if dp_mode:
+            from .actors.runtime import Props
+            from .trainer.dp_actors import DPRouterActor, RankGroupActor, rank_routee_props
+
+            o = dict(dp or {})
+            o.setdefault("device", "cuda" if (device or "cuda").startswith("cuda") else "cpu")
+            group = system.actor_of(RankGroupActor.props(cfg, int(gpus), **o), "Rank-group-actor")
+            router = system.actor_of(Props(DPRouterActor, group, policy, budget, shares, cfg,
+                                           child_trainer_props=rank_routee_props(group, cfg), n_children=int(gpus)),
+                                     "Trainer-parent-actor")
+            out["dp_group"] = group
+        elif engine == "vector":
             from .trainer.engine_actor import EngineActor, engine_child_props
 
             eng = system.actor_of(EngineActor.props(cfg, device=dev), "Engine-actor")
@@ -86,10 +104,21 @@ def run(cfg: Optional[Config] = None, engine: str = "actors", device: Optional[s
                     logger.info("avg is %s, std is %s", a.double, s.double)
                 out.update(avg=a.double, std=s.double, completed=1.0)
                 break
+        grp = out.pop("dp_group", None)
+        if grp is not None:
+            # per-rank episode records and the ranks' deaths / generations (tests, CLI report)
+            try:
+                out["dp"] = grp.ask(_DPInfo, 10.0).result(10.0)
+            except Exception:  # noqa: BLE001 - the report is best effort
+                pass
     finally:
+        out.pop("dp_group", None)
         out["elapsed_s"] = time.perf_counter() - t0
         system.terminate()
     return out
+
+
+from .trainer.dp_actors import GetDPInfo as _DPInfo  # noqa: E402
 
 
 def _device(spec: Optional[str]) -> torch.device:

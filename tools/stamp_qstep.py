@@ -153,7 +153,7 @@ def ws_stamps(a):
     eng.run(3)
     torch.cuda.synchronize()
     nmy = (a.envs // 64 + eng.grid - 1) // eng.grid
-    st = torch.zeros((nmy + 1) * 16 + 4 * 4 * nmy + 16, dtype=torch.int64, device=dev)
+    st = torch.zeros((nmy + 1) * 16 + 8 * 4 * nmy + 16, dtype=torch.int64, device=dev)
     eng._qp.stamps = st.data_ptr()
     eng.step()
     torch.cuda.synchronize()
@@ -161,14 +161,15 @@ def ws_stamps(a):
     assert int(eng.kernel_err.sum()) == 0
     raw = st.cpu()
     s = raw[: nmy * 16].view(nmy, 16).double()
-    names = ["features (+ env prefetch)", "layer 1 of Q(x), Q(x') window + slot claim + X/H1 -> slot",
-             "layer 2 + output of Q(x), H2 -> slot", "epsilon-greedy + env step, rest of Q(x')",
-             "TD + state write-back + next prices issued", "dZ2 + publish"]
+    names = ["features", "layer 1 of Q(x) + Q(x') window (56 + 48 MFMA)", "slot claim (wait for a free slot)",
+             "X, H1 -> slot", "layer 2 of Q(x) (32 MFMA) + H2 -> slot", "output of Q(x) (4 MFMA chain)",
+             "epsilon-greedy + env step", "Q(x'): layer-1 tail, layer 2, output (8 + 32 + 4 MFMA)",
+             "TD + state write-back + next prices issued", "dZ2 (VALU rank-1 + mask)", "dZ2, dQ -> slot, publish"]
     lines = [f"# ws step kernel: data wave 0 of workgroup 0 ({a.envs} envs, grid {eng.grid}, {nmy} tiles per data "
              f"wave; s_memtime ticks)\n", "| phase | ticks/tile | % |", "|---|---|---|"]
     tot = 0.0
     rows = []
-    for ph in range(6):
+    for ph in range(11):
         d = float((s[:, ph + 1] - s[:, ph]).mean())
         rows.append((names[ph], d))
         tot += d
@@ -176,11 +177,16 @@ def ws_stamps(a):
         lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
     loop = float((s[1:, 0] - s[:-1, 0]).mean()) if nmy > 1 else tot
     lines.append(f"| tile loop (stamp0 -> stamp0) | {loop:.0f} | |")
-    g = raw[(nmy + 1) * 16: (nmy + 1) * 16 + 4 * 4 * nmy].view(4 * nmy, 4).double()
-    wait = float((g[:, 1] - g[:, 0]).mean())
-    work = float((g[:, 2] - g[:, 1]).mean())
-    lines += ["", f"gradient wave 0: per ring slot {work:.0f} ticks of work, {wait:.0f} ticks waiting for the next "
-              f"slot ({4 * nmy} slots; {100 * work / max(work + wait, 1):.0f} % busy)"]
+    g = raw[(nmy + 1) * 16: (nmy + 1) * 16 + 8 * 4 * nmy].view(4 * nmy, 8).double()
+    gn = ["wait for the next full slot", "dZ1 for own u1 tiles (8 MFMA 16x16x32, 16 transposed W1 reads)",
+          "H1 fragments + dZ1 mask", "dW0 (26 MFMA 16x16x16, 13 X reads)", "dZ2^T / dQ^T / H2 reads + release",
+          "dW1, db1, dW2, db2 (21 MFMA)"]
+    lines += ["", "| gradient wave 0, per ring slot | ticks | % |", "|---|---|---|"]
+    gt = float((g[:, 6] - g[:, 0]).mean())
+    for i, n in enumerate(gn):
+        d = float((g[:, i + 1] - g[:, i]).mean())
+        lines.append(f"| {n} | {d:.0f} | {100 * d / gt:.1f} |")
+    lines.append(f"| slot total | {gt:.0f} | |")
     txt = "\n".join(lines) + "\n"
     print(txt)
     if a.out:
