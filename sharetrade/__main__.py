@@ -44,6 +44,14 @@ def main(argv=None) -> int:
             p.add_argument("--engine", choices=["actors", "vector"], default="actors")
             p.add_argument("--device", default=None)
             p.add_argument("--max-prices", type=int, default=None, help="truncate the series (smoke runs)")
+            p.add_argument("--gpus", type=int, default=1,
+                           help="--engine vector: N > 1 makes the router's N routees the ranks of a data-parallel "
+                                "group, one process per GPU (RCCL), with rank death -> replacement -> resume")
+            p.add_argument("--envs-per-rank", type=int, default=None, help="envs of each rank (--gpus > 1)")
+            p.add_argument("--dist-backend", default=None, help="nccl (= RCCL, GPUs) | gloo")
+            p.add_argument("--ckpt-dir", default=None, help="--gpus > 1: sharded checkpoints of the episode")
+            p.add_argument("--ckpt-every", type=int, default=0)
+            p.add_argument("--same-device", action="store_true", help="--gpus > 1: every rank on cuda:0 (rehearsal)")
         if name == "engine":
             p.add_argument("--steps", type=int, default=100)
             p.add_argument("--envs", type=int, default=None)
@@ -55,6 +63,16 @@ def main(argv=None) -> int:
             p.add_argument("--resume", action="store_true")
             p.add_argument("--trace", default=None, help="Chrome trace output path (torch.profiler)")
             p.add_argument("--no-graph", action="store_true")
+        if name in ("engine", "deep", "recurrent"):
+            p.add_argument("--elastic", type=int, default=0,
+                           help="N > 0: run N rank processes under the elastic launcher (heartbeat + progress "
+                                "watchdog, whole-generation respawn, resume from committed checkpoints)")
+            p.add_argument("--max-restarts", type=int, default=3)
+            p.add_argument("--stall-timeout", type=float, default=120.0, help="--elastic: seconds without progress")
+            p.add_argument("--pg-timeout", type=float, default=120.0, help="--elastic: collective timeout (s)")
+            p.add_argument("--final-dir", default=None, help="each rank writes its final state here")
+            if name == "engine":
+                p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
         if name in ("deep", "recurrent"):
             p.add_argument("--iterations", type=int, default=200)
             p.add_argument("--envs", type=int, default=None)
@@ -92,9 +110,51 @@ def main(argv=None) -> int:
     if a.cmd == "train":
         from .app import run
 
-        res = run(cfg, engine=a.engine, device=a.device, max_prices=a.max_prices)
-        print(json.dumps(res))
+        dp = None
+        if a.gpus > 1:
+            dev = a.device or "cuda"
+            dp = dict(device="cpu" if dev.startswith("cpu") else "cuda", backend=a.dist_backend,
+                      envs_per_rank=a.envs_per_rank or cfg.engine.envs_per_rank, ckpt_dir=a.ckpt_dir,
+                      ckpt_every=a.ckpt_every, same_device=a.same_device)
+        res = run(cfg, engine=a.engine, device=a.device, max_prices=a.max_prices, gpus=a.gpus, dp=dp)
+        print(json.dumps(res, default=str))
         return 0 if res.get("completed") else 1
+    if a.cmd in ("engine", "deep", "recurrent") and a.elastic:
+        # the launcher never touches the GPU: one fresh process per rank (parallel/elastic_cli.py)
+        from .parallel.elastic_cli import run_elastic
+
+        dev = getattr(a, "device", None) or "cuda"
+        dev = "cpu" if dev.startswith("cpu") else "cuda"
+        kw = dict(device=dev, backend=a.dist_backend, metrics=a.metrics, log_every=a.log_every, ckpt_dir=a.ckpt_dir,
+                  ckpt_every=a.ckpt_every, graph=not a.no_graph, final_dir=a.final_dir, pg_timeout_s=a.pg_timeout)
+        if a.cmd == "engine":
+            kw.update(steps=a.steps, envs=a.envs)
+        else:
+            lk = {}
+            if a.cmd == "deep":
+                lk["hidden"] = [int(x) for x in a.hidden.split(",")]
+            if a.envs:
+                lk["envs"] = a.envs
+            if a.batch:
+                lk["batch"] = a.batch
+            kw.update(steps=a.iterations, learner_kw=lk)
+        import os
+        import tempfile
+
+        fd, kw["result_path"] = tempfile.mkstemp(suffix=".json")
+        os.close(fd)
+        r = run_elastic(a.cmd, cfg, a.elastic, kw, max_restarts=a.max_restarts, stall_timeout_s=a.stall_timeout)
+        out = {"ok": r.ok, "restarts": r.restarts, "flagged": r.flagged,
+               "generations": [{"generation": g.generation, "exitcodes": g.exitcodes, "ok": g.ok,
+                                "seconds": round(g.seconds, 2)} for g in r.generations]}
+        try:
+            with open(kw["result_path"]) as f:
+                out["result"] = json.loads(f.read() or "null")
+        except (OSError, ValueError):
+            pass
+        os.unlink(kw["result_path"])
+        print(json.dumps(out, default=str))
+        return 0 if r.ok else 1
     if a.cmd in ("deep", "recurrent"):
         import torch
 
@@ -142,7 +202,7 @@ def main(argv=None) -> int:
         from .trainer.engine import resolve_device
         from .trainer.loop import train
 
-        ctx = D.init(device=None if a.device == "auto" else a.device)
+        ctx = D.init(backend=a.dist_backend, device=None if a.device == "auto" else a.device)
         dev = ctx.device if ctx.is_distributed or a.device == "auto" else resolve_device(a.device)
         res = train(cfg, a.steps, device=dev, envs=a.envs, metrics_path=a.metrics, log_every=a.log_every,
                     ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, trace_path=a.trace,

@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Any, Dict, Optional
+from typing import Any, Callable, Dict, Optional
 
 import torch
 
@@ -19,7 +19,17 @@ from .engine import VectorEngine
 def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: Optional[int] = None,
           metrics_path: Optional[str] = None, log_every: int = 100, ckpt_dir: Optional[str] = None,
           ckpt_every: int = 0, resume: bool = False, trace_path: Optional[str] = None, graph: bool = True,
-          rank: int = 0, world_size: int = 1, group=None) -> Dict[str, Any]:
+          rank: int = 0, world_size: int = 1, group=None, until: Optional[int] = None,
+          on_step: Optional[Callable[[int], None]] = None, final_dir: Optional[str] = None) -> Dict[str, Any]:
+    """``steps`` more steps (or, with ``until``, up to that total step count -- a resumed elastic
+    generation finishes the same job).  ``on_step(step)`` runs before every step (fault injection and
+    the heartbeat's progress mark of ``--elastic`` jobs); without it the steps between two logging /
+    checkpoint points run as whole multi-step graph replays (``VectorEngine.run``).  ``final_dir``: each
+    rank writes its final state there (``final-rank-<r>.stck``).
+
+    Several ranks (one process per GPU, RCCL): the synchronous DP step -- kernel, slab reduce, all-reduce,
+    optimizer -- is captured in HIP graphs on every rank; the ranks vote (MIN all-reduce) so that a
+    capture failure on one rank sends every rank down the eager path with the same collectives."""
     eng = VectorEngine(cfg, device=device, envs=envs, rank=rank, world_size=world_size, group=group)
     # one process: CheckpointManager files; several ranks: one shard per rank per step, committed by
     # rank 0 after a barrier (parallel/dp_train.py) -- every rank owns different envs / price banks
@@ -34,8 +44,15 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
             st, _ = load_ckpt(mgr.latest())
             eng.load_state_dict(st)
     eng.sync_params_from(0)
-    if graph and eng.backend == "native" and world_size == 1:
-        eng.capture_graph(warmup=1)
+    if graph and eng.backend == "native":
+        from .benchkit import agree
+
+        try:
+            ok = bool(eng.capture_graph(warmup=0 if world_size > 1 else 1))
+        except Exception:  # noqa: BLE001 -- eager launches, same math
+            ok = False
+        if not agree(ok, world_size, group, eng.device):
+            eng._graph, eng._graph_k = None, None
     if eng._sync is not None:
         eng._sync.enable_timing()          # metrics: mean all-reduce ms per logging window
     ml = MetricsLogger(metrics_path)
@@ -50,8 +67,18 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
         prof.__enter__()
     t0 = time.perf_counter()
     start = eng.step_count
-    while eng.step_count < start + steps:
-        eng.step()
+    target = int(until) if until is not None else start + steps
+    while eng.step_count < target:
+        if on_step is not None:
+            on_step(eng.step_count)
+            eng.step()
+        else:
+            # whole graph replays up to the next logging / checkpoint point
+            nxt = target
+            for every in (log_every, ckpt_every):
+                if every:
+                    nxt = min(nxt, (eng.step_count // every + 1) * every)
+            eng.run(nxt - eng.step_count)
         s = eng.step_count
         if log_every and s % log_every == 0:
             eng.synchronize()
@@ -68,6 +95,12 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
             _save_sharded(ckpt_dir, s, rank, world_size, eng, group)
     eng.synchronize()
     dt = time.perf_counter() - t0
+    if final_dir:
+        from ..persist import checkpoint as ck
+
+        os.makedirs(final_dir, exist_ok=True)
+        ck.save(os.path.join(final_dir, f"final-rank-{rank}.stck"), eng.state_dict(), {"rank": rank})
+    steps = eng.step_count - start
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(os.path.dirname(os.path.abspath(trace_path)) or ".", exist_ok=True)

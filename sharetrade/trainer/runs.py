@@ -73,8 +73,11 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
         metrics_path: Optional[str] = None, log_every: int = 50, ckpt_dir: Optional[str] = None,
         ckpt_every: int = 0, resume: bool = False, graph: bool = True, learner=None, ctx=None,
         bucket_mb: float = 64.0, capture_sync: bool = True, layer_overlap: bool = True,
-        trace_path: Optional[str] = None, **learner_kw) -> Dict[str, Any]:
-    """Run ``iterations`` act + update iterations (counting any restored ones); returns final stats."""
+        trace_path: Optional[str] = None, on_step=None, final_dir: Optional[str] = None,
+        **learner_kw) -> Dict[str, Any]:
+    """Run ``iterations`` act + update iterations (counting any restored ones); returns final stats.
+    ``on_step(i)`` runs before every iteration (``--elastic``: fault injection + heartbeat progress);
+    ``final_dir``: each rank writes its final learner state there (``final-rank-<r>.stck``)."""
     dp = ctx is not None and ctx.is_distributed
     dev = device or (ctx.device if ctx is not None else torch.device("cuda", 0))
     if dp:
@@ -139,6 +142,8 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
         done += 1
 
     while done < iterations:
+        if on_step is not None:
+            on_step(done)
         one()
         if mgr is not None and mgr.should_save(done):
             _sync(dev)
@@ -152,6 +157,11 @@ def run(kind: str, cfg: Config, iterations: int, device: Optional[torch.device] 
             ml.log(rec)
             last_t, last_i = now, done
     _sync(dev)
+    if final_dir:
+        from ..persist import checkpoint as ck
+
+        os.makedirs(final_dir, exist_ok=True)
+        ck.save(os.path.join(final_dir, f"final-rank-{ctx.rank if dp else 0}.stck"), d.state_dict(), {"kind": kind})
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(os.path.dirname(os.path.abspath(trace_path)) or ".", exist_ok=True)
