@@ -124,10 +124,9 @@ class DeepDQN:
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
         self.E, self.B, self.cap = int(envs), int(batch), int(replay_capacity)
-        # weight-gradient GEMMs (plain bf16 -> fp32 products, no epilogue): "hip" = csrc/gemm_bf16.hip
-        # split-K, "hipblaslt" = torch.mm(out_dtype=fp32), "auto" = hipBLASLt where it measured faster
-        # (both dims >= 1024: 19 vs 30 us at 1024x1024x4096, tools/bench_dw.py / profiles/r1_dw_gemm.md)
-        if dw_gemm not in ("auto", "hip", "hipblaslt"):
+        # weight-gradient GEMMs (plain bf16 -> fp32 products, no epilogue): csrc/gemm_bf16.hip, split-K for
+        # the long-K / few-tile shapes ("auto" and "hip" are the same; there is no library GEMM path)
+        if dw_gemm not in ("auto", "hip"):
             raise ValueError(f"dw_gemm: {dw_gemm!r}")
         self.dw_gemm = dw_gemm
         # concurrent: the independent GEMM chains of an update (online / target forward; weight
@@ -234,19 +233,16 @@ class DeepDQN:
         for l in range(self.L):
             self.db.append(self.grad_flat[off:off + self.pdims[l + 1]].view(1, self.pdims[l + 1]))
             off += self.pdims[l + 1]
-        self._dw_plan = []   # per layer: ("blaslt", None) or ("hip", (tile, splitk))
+        self._dw_plan = []   # per layer: ("hip", (tile, splitk))
         for l in range(self.L):
             o, i = self.pdims[l + 1], self.pdims[l]
-            if self.dw_gemm == "hipblaslt" or (self.dw_gemm == "auto" and o >= 1024 and i >= 1024):
-                self._dw_plan.append(("blaslt", None))
+            # few output tiles, long K: 64x64 tiles split over K (1024x256: 10.6 us vs 16.3 with
+            # 128x128 split 8; tools/bench_dw.py, profiles/r2_config4_dual_bwd.md)
+            if o % 64 == 0 and i % 64 == 0 and (o // 64) * (i // 64) <= 256:
+                wt = (64, 64)
             else:
-                # few output tiles, long K: 64x64 tiles split over K (1024x256: 10.6 us vs 16.3 with
-                # 128x128 split 8; tools/bench_dw.py, profiles/r2_config4_dual_bwd.md)
-                if o % 64 == 0 and i % 64 == 0 and (o // 64) * (i // 64) <= 256:
-                    wt = (64, 64)
-                else:
-                    wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else gm.pick_tile(o, i)
-                self._dw_plan.append(("hip", (wt, gm.pick_splitk(o, self.pdims[l], self.B, wt))))
+                wt = (128, 128) if o % 128 == 0 and i % 128 == 0 else gm.pick_tile(o, i)
+            self._dw_plan.append(("hip", (wt, gm.pick_splitk(o, self.pdims[l], self.B, wt))))
         # output layer of the batched forward: split K until both problems' tiles reach ~256 workgroups
         self._q_splitk = 1
         if self.batched_fwd:
@@ -501,13 +497,9 @@ class DeepDQN:
 
     def _dw(self, l: int, actsT) -> None:
         """Weight gradient of layer l: dW = G_l^T . A_l (long-K, few-tile product)."""
-        kind, arg = self._dw_plan[l]
-        if kind == "blaslt":
-            torch.mm(self.GT[l], actsT[l].t(), out_dtype=torch.float32, out=self.dW[l])
-        else:
-            tile, sk = arg
-            gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=tile, splitk=sk,
-                       prezeroed=sk > 1)   # zeroed by this update's replay gather
+        _, (tile, sk) = self._dw_plan[l]
+        gm.gemm_nt(self.GT[l], actsT[l], self.dW[l], gm.EPI_F32, tile=tile, splitk=sk,
+                   prezeroed=sk > 1)   # zeroed by this update's replay gather
 
     def update_step(self, with_act: bool = False, split: bool = False) -> None:
         """One DQN update: sample B transitions, Q(x) online / Q(x') target, TD, backward, Adam.

@@ -44,10 +44,10 @@ def test_replay_ring_and_env_step(native_built):
 
 
 @pytest.mark.parametrize("dw_gemm,concurrent,fused,batched,dual,dp", [("hip", True, True, True, True, False),
-                                                                       ("hipblaslt", True, True, True, False, False),
+                                                                       ("hip", True, True, True, False, False),
                                                                        ("hip", False, False, False, False, False),
-                                                                       ("hipblaslt", False, True, True, True, False),
-                                                                       ("hipblaslt", True, True, False, False, False),
+                                                                       ("hip", False, True, True, True, False),
+                                                                       ("hip", True, True, False, False, False),
                                                                        ("hip", True, True, True, True, True)])
 def test_update_gradients_match_torch(native_built, dw_gemm, concurrent, fused, batched, dual, dp):
     kw = dict(dw_gemm=dw_gemm, concurrent=concurrent, fused_adam=fused, batched_fwd=batched, dual_bwd=dual)
@@ -130,7 +130,7 @@ def test_batched_forward_equals_two_chains(native_built):
         assert torch.equal(a.ActT[l], b.ActT[l]), l
 
 
-@pytest.mark.parametrize("dw_gemm,concurrent", [("hip", True), ("hipblaslt", True), ("hipblaslt", False)])
+@pytest.mark.parametrize("dw_gemm,concurrent", [("hip", True), ("hip", False)])
 def test_graph_iteration_runs(native_built, dw_gemm, concurrent):
     d = _dqn(dw_gemm=dw_gemm, concurrent=concurrent)
     for _ in range(4):
@@ -153,7 +153,7 @@ def test_overlapped_act_matches_same_order_serial(native_built, fuse):
     summation order: identical env state and replay contents, same weights within 1e-5."""
     res = []
     for serial in (False, True):
-        d = _dqn(dw_gemm="hipblaslt", overlap_act=True, fuse_act=fuse and not serial)
+        d = _dqn(dw_gemm="hip", overlap_act=True, fuse_act=fuse and not serial)
         for _ in range(6):
             d.act_step()
         if serial:

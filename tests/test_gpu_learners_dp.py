@@ -132,7 +132,7 @@ def _rccl_worker(_rank, port, kind, fast, out):
     kw = dict(_DEEP if kind == "deep" else _REC, world_size=2)
     if kind == "deep" and not fast:
         # bit-reproducible weight gradients (no split-K atomics), as in tests/test_gpu_runs.py
-        kw.update(dw_gemm="hipblaslt", concurrent=False, batched_fwd=False, dual_bwd=False)
+        kw.update(dw_gemm="hip", concurrent=False, batched_fwd=False, dual_bwd=False)
     res = {}
     # eager; captured with the all-reduce between two graphs; captured with the all-reduce inside the
     # update graph (config 4: per layer on a comm stream)
