@@ -34,8 +34,16 @@
 // summation order differs (bias added first, k order pi inside MFMAs, per-16-env gradient sums).
 #include "qstep.h"
 
+#ifndef WS_STAMPS
+#define WS_STAMPS 0     // 1: s_memtime stamps per phase (the debug build csrc/qstep_ws_stamps.hip only: the stamp
+#endif                  // code costs the 256-register build its last free registers)
+#ifndef WS_NS
+#define WS_NS ws
+#define WS_API(name) name
+#endif
+
 namespace st {
-namespace ws {
+namespace WS_NS {
 
 constexpr int NW = 8, NT = 64 * NW;
 constexpr int ND = 4, NG = 4;    // data waves (0..3), gradient waves (4..7)
@@ -209,8 +217,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     WS_LOAD_PRICES(0, e_pos)
     WS_LOAD_ENV(1, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
 
-    unsigned long long* stamps = (p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0) ? p.stamps : nullptr;
-#define WS_STAMP(I) if (stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime();
+    unsigned long long* stamps = (WS_STAMPS && p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0)
+                                     ? p.stamps : nullptr;
+#define WS_STAMP(I) if (WS_STAMPS && stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime();
 #define WS_PIN(V) asm volatile("" ::"v"(V))
 #define WS_SB() __builtin_amdgcn_sched_barrier(0)
 
@@ -507,9 +516,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     const int nseq = ND * nmy;
     // debug stamps of gradient wave 0 of workgroup 0: per slot (wait begins, slot full, slot done) after the
     // data-wave rows ((nmy + 1) * 16 words in)
-    unsigned long long* gst = (p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
+    unsigned long long* gst = (WS_STAMPS && p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
                                   ? p.stamps + (size_t)(nmy + 1) * 16 : nullptr;
-#define WS_GST(I) if (gst) gst[8 * q + (I)] = __builtin_amdgcn_s_memtime();
+#define WS_GST(I) if (WS_STAMPS && gst) gst[8 * q + (I)] = __builtin_amdgcn_s_memtime();
     for (int q = 0; q < nseq; ++q) {
       const int sl = q % NSLOT;
       WS_GST(0);
@@ -639,19 +648,19 @@ static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
   return hipGetLastError();
 }
 
-}  // namespace ws
+}  // namespace WS_NS
 }  // namespace st
 
-extern "C" int st_qstep_ws_lds_bytes(int inp, int h1p, int h2p) {
-  if (inp == st::ws::INP && h1p == st::ws::HP && h2p == st::ws::HP) return st::ws::LDS_BYTES;
+extern "C" int WS_API(st_qstep_ws_lds_bytes)(int inp, int h1p, int h2p) {
+  if (inp == st::WS_NS::INP && h1p == st::WS_NS::HP && h2p == st::WS_NS::HP) return st::WS_NS::LDS_BYTES;
   return -1;
 }
 
 // Preconditions (checked here and by sharetrade/trainer/engine.py): E % 64 == 0, 1 <= grid <= E / 64,
 // H == 201, padded dims (224, 128, 128), static chunk schedule, 32-aligned weight offsets for bf16 slabs.
-extern "C" hipError_t st_qstep_ws_launch(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
-                                         hipStream_t stream) {
-  using namespace st::ws;
+extern "C" hipError_t WS_API(st_qstep_ws_launch)(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
+                                                 hipStream_t stream) {
+  using namespace st::WS_NS;
   if (inp != INP || h1p != HP || h2p != HP || p->H != HWIN) return hipErrorInvalidValue;
   if (p->E % C != 0 || grid < 1 || grid > p->E / C || p->chunk_heads != nullptr) return hipErrorInvalidValue;
   if (p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;

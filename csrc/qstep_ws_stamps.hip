@@ -1,0 +1,7 @@
+// Debug build of csrc/qstep_ws.hip with s_memtime stamps per phase (tools/stamp_qstep.py --kernel ws):
+// st_qstep_ws_launch_stamps, same contract.  Kept out of the production build: the stamp code costs the
+// 256-register kernel its last free registers (and with them the price prefetch's latency cover).
+#define WS_STAMPS 1
+#define WS_NS ws_stamps
+#define WS_API(name) name##_stamps
+#include "qstep_ws.hip"

@@ -100,6 +100,8 @@ def lib() -> C.CDLL:
     L.st_qstep_pair_lds_bytes.restype = C.c_int
     L.st_qstep_ws_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_qstep_ws_launch.restype = C.c_int
+    L.st_qstep_ws_launch_stamps.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_qstep_ws_launch_stamps.restype = C.c_int
     L.st_qstep_ws_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
     L.st_qstep_ws_lds_bytes.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]

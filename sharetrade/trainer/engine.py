@@ -352,7 +352,8 @@ class VectorEngine:
 
     def _launch_qstep(self, L, sh) -> None:
         if self.step_kernel == "ws":
-            fn = L.st_qstep_ws_launch
+            # the stamps build only when a stamp buffer is attached (tools/stamp_qstep.py)
+            fn = L.st_qstep_ws_launch_stamps if self._qp.stamps else L.st_qstep_ws_launch
         elif self.step_kernel == "pair":
             fn = L.st_qstep_pair_launch
         elif self.chunk == 64:
