@@ -111,13 +111,44 @@ ST_DEV s4v pk4(float a, float b, float c, float d) {
   v.y = pack_bf2(c, d);
   return __builtin_bit_cast(s4v, v);
 }
-ST_DEV s4v relu_bf(f4v v) { return pk4(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)); }
+// relu then bf16 == bf16 then relu on the bits: a bf16 with the sign bit set is a negative int16, and
+// rounding never changes a sign (-0 -> +0 is fine); one v_pk_max_i16 per two values instead of a
+// NaN-canonicalising v_max_f32 pair per value
+typedef short s2v __attribute__((ext_vector_type(2)));
+ST_DEV s4v relu_bf(f4v v) {
+  const s2v z = {0, 0};
+  const s2v a = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf2(v[0], v[1])), z);
+  const s2v b = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf2(v[2], v[3])), z);
+  s4v r = {a[0], a[1], b[0], b[1]};
+  return r;
+}
 // accumulator tile -> bf16 masked by (act > 0) (act: bf16 bits, a positive value has a positive short)
 ST_DEV s4v mask_bf(f4v v, s4v act) {
   return pk4(act[0] > 0 ? v[0] : 0.f, act[1] > 0 ? v[1] : 0.f, act[2] > 0 ? v[2] : 0.f, act[3] > 0 ? v[3] : 0.f);
 }
 ST_DEV s4v lo4(s8v v) { s4v r = {v[0], v[1], v[2], v[3]}; return r; }
 ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
+
+// acc[i] += W1 (rows 16 i .. 16 i + 15, pi-ordered columns) . H (B operands of 4 k-steps), 32 MFMAs with
+// the W1 fragment of pair j + PD2 read while pair j issues (j = 8 ks + i)
+ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc) {
+  constexpr int PD2 = 6, NB2 = PD2 + 1;
+  s8v A[NB2];
+#pragma unroll
+  for (int j = 0; j < PD2; ++j) A[j] = lds_ld8(W1p + w1_off(16 * (j & 7) + l16, 32 * (j >> 3) + 8 * g4));
+  __builtin_amdgcn_sched_group_barrier(0x100, PD2, 0);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    acc[j & 7] = mfma32(A[j % NB2], H[j >> 3], acc[j & 7]);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (j + PD2 < 32) {
+      const int jn = j + PD2;
+      A[jn % NB2] = lds_ld8(W1p + w1_off(16 * (jn & 7) + l16, 32 * (jn >> 3) + 8 * g4));
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // every ring wait is bounded (~1 s at s_sleep 1): a protocol bug ends the launch with an error bit in
 // p.err instead of leaving waves spinning on the GPU
@@ -268,13 +299,26 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v a1[8], a1n[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a1[i] = zero4(); a1n[i] = zero4(); }
+      {
+        // software pipeline: the W0 fragment of pair j + PD1 is read while pair j's two MFMAs issue
+        // (j = 8 ks + i; one fragment feeds Q(x) and Q(x')'s window)
+        constexpr int PD1 = 2, NB1 = PD1 + 1;
+        const bf16_t* w0b = W0p + l16 * KX + 8 * g4;
+        s8v A[NB1];
 #pragma unroll
-      for (int ks = 0; ks < 6; ++ks) {
+        for (int j = 0; j < PD1; ++j) A[j] = lds_ld8(w0b + (j & 7) * 16 * KX + 32 * (j >> 3));
+        __builtin_amdgcn_sched_group_barrier(0x100, PD1, 0);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const s8v a = lds_ld8(W0p + (16 * i + l16) * KX + 32 * ks + 8 * g4);
-          a1[i] = mfma32(a, X[ks], a1[i]);
-          a1n[i] = mfma32(a, Xn[ks], a1n[i]);
+        for (int j = 0; j < 48; ++j) {
+          const int ks = j >> 3, i = j & 7;
+          a1[i] = mfma32(A[j % NB1], X[ks], a1[i]);
+          a1n[i] = mfma32(A[j % NB1], Xn[ks], a1n[i]);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          if (j + PD1 < 48) {
+            const int jn = j + PD1;
+            A[jn % NB1] = lds_ld8(w0b + (jn & 7) * 16 * KX + 32 * (jn >> 3));
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
         }
         WS_SB();
       }
@@ -317,12 +361,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v a2[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a2[i] = mfma32(lds_ld8(W1p + w1_off(16 * i + l16, 32 * ks + 8 * g4)), H1[ks], a2[i]);
-        WS_SB();
-      }
+      layer2(W1p, l16, g4, H1, a2);
       s8v H2[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
@@ -388,12 +427,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_SB();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a2[i] = mfma32(lds_ld8(W1p + w1_off(16 * i + l16, 32 * ks + 8 * g4)), H1n[ks], a2[i]);
-        WS_SB();
-      }
+      layer2(W1p, l16, g4, H1n, a2);
       s8v H2n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2n[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));

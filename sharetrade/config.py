@@ -151,9 +151,10 @@ class EngineConfig:
     # 64 = csrc/qstep_wide.hip (layer-1 weights in VGPRs), 32 = csrc/qstep_fused.hip (weights in LDS)
     chunk: int = 0
     step_waves: int = 8             # 64-env-chunk kernel: 8 waves (two per SIMD, measured fastest) or 4
-    # fused bf16 step kernel: "auto" (by chunk), "wide" (csrc/qstep_wide.hip, 64-env chunks),
-    # "narrow" (csrc/qstep_fused.hip, 32-env chunks) or "pair" (csrc/qstep_pair.hip: two 32-env chunks
-    # in flight per workgroup, five phases apart; E % 64 == 0, static schedule)
+    # fused bf16 step kernel: "auto" (ws where its geometry fits, else by chunk), "ws" (csrc/qstep_ws.hip:
+    # wave-specialised, data waves run whole 16-env tiles, gradient waves consume them through an LDS ring;
+    # E % 64 == 0, history 201, dims 224-128-128, static schedule), "wide" (csrc/qstep_wide.hip, 64-env
+    # chunks), "narrow" (csrc/qstep_fused.hip, 32-env chunks) or "pair" (csrc/qstep_pair.hip)
     step_kernel: str = "auto"
     step_variant: str = ""          # tuning builds of the 64-env-chunk kernel (st_qstep_wide_launch_<v>); "" = default
     graph: bool = True              # capture the step in a HIP graph

@@ -146,7 +146,9 @@ class VectorEngine:
                 raise NotImplementedError(f"engine.step_kernel='pair' needs E % 64 == 0 and padded dims "
                                           f"(224, 128, 128); got E={self.E}, dims {L.pdims}")
             self.chunk, self.step_kernel = 64, "pair"
-        elif self.kernel == "bf16_fused" and sk == "ws":
+        elif self.kernel == "bf16_fused" and (sk == "ws" or (sk == "auto" and int(cfg.engine.chunk) == 0
+                                                            and not cfg.engine.step_variant
+                                                            and cfg.engine.step_waves == 8 and self.ws_ok(cfg, L))):
             if not self.ws_ok(cfg, L):
                 raise NotImplementedError(f"engine.step_kernel='ws' needs E % 64 == 0, history 201, padded dims "
                                           f"(224, 128, 128) and the static chunk schedule; got E={self.E}, "
