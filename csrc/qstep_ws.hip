@@ -37,6 +37,9 @@
 #ifndef WS_STAMPS
 #define WS_STAMPS 0     // 1: s_memtime stamps per phase (the debug build csrc/qstep_ws_stamps.hip only: the stamp
 #endif                  // code costs the 256-register build its last free registers)
+#ifndef WS_GSKIP
+#define WS_GSKIP 0      // 1: timing build (csrc/qstep_ws_gskip.hip), gradient waves skip their work
+#endif
 #ifndef WS_NS
 #define WS_NS ws
 #define WS_API(name) name
@@ -561,6 +564,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         if (spin > SPIN_LIMIT) { ws_fail(p); break; }
       }
       WS_GST(1);
+#if WS_GSKIP
+      // timing build: the gradient waves only hand the slots back (how fast do the data waves run alone?)
+      if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      continue;
+#endif
       const char* sb = smem + oSLOT + sl * SLOT_BYTES;
       const bf16_t* sx = reinterpret_cast<const bf16_t*>(sb + sX);
       const bf16_t* sh1 = reinterpret_cast<const bf16_t*>(sb + sH1);

@@ -71,6 +71,7 @@ def main(argv=None) -> int:
             p.add_argument("--stall-timeout", type=float, default=120.0, help="--elastic: seconds without progress")
             p.add_argument("--pg-timeout", type=float, default=120.0, help="--elastic: collective timeout (s)")
             p.add_argument("--final-dir", default=None, help="each rank writes its final state here")
+            p.add_argument("--same-device", action="store_true", help="--elastic: every rank on cuda:0 (rehearsal)")
             if name == "engine":
                 p.add_argument("--dist-backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
         if name in ("deep", "recurrent"):
@@ -126,7 +127,8 @@ def main(argv=None) -> int:
         dev = getattr(a, "device", None) or "cuda"
         dev = "cpu" if dev.startswith("cpu") else "cuda"
         kw = dict(device=dev, backend=a.dist_backend, metrics=a.metrics, log_every=a.log_every, ckpt_dir=a.ckpt_dir,
-                  ckpt_every=a.ckpt_every, graph=not a.no_graph, final_dir=a.final_dir, pg_timeout_s=a.pg_timeout)
+                  ckpt_every=a.ckpt_every, graph=not a.no_graph, final_dir=a.final_dir, pg_timeout_s=a.pg_timeout,
+                  same_device=a.same_device)
         if a.cmd == "engine":
             kw.update(steps=a.steps, envs=a.envs)
         else:

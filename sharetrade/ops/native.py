@@ -64,9 +64,9 @@ class OptimParams(C.Structure):
 ENV_ROWS = ("pos", "budget", "shares", "value", "ret_sum", "episodes", "last_final", "actions_out", "rewards_out")
 
 
-def variant_launch(suffix: str):
-    """``st_qstep_wide_launch_<suffix>`` of a tuning build of the 64-env-chunk kernel (same params)."""
-    fn = getattr(lib(), "st_qstep_wide_launch_" + suffix)
+def variant_launch(suffix: str, prefix: str = "st_qstep_wide_launch_"):
+    """``<prefix><suffix>`` of a tuning / timing build of a step kernel (same params)."""
+    fn = getattr(lib(), prefix + suffix)
     fn.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     fn.restype = C.c_int
     return fn

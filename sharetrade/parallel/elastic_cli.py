@@ -29,6 +29,8 @@ def cli_worker(rank: int, world: int, generation: int, kind: str, cfg_dict: Dict
 
     cfg = Config.from_dict(cfg_dict)
     device = kw.get("device", "cuda")
+    if kw.get("same_device"):
+        os.environ["LOCAL_RANK"] = "0"   # rehearsal: every rank on cuda:0
     if device == "cpu":
         torch.set_num_threads(1)
     ctx = D.init(backend=kw.get("backend"), device=device, timeout_s=float(kw.get("pg_timeout_s", 120.0)))

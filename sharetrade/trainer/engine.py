@@ -356,6 +356,8 @@ class VectorEngine:
         if self.step_kernel == "ws":
             # the stamps build only when a stamp buffer is attached (tools/stamp_qstep.py)
             fn = L.st_qstep_ws_launch_stamps if self._qp.stamps else L.st_qstep_ws_launch
+            if self.cfg.engine.step_variant:   # timing builds (csrc/qstep_ws_<v>.hip), same contract
+                fn = native.variant_launch(self.cfg.engine.step_variant, "st_qstep_ws_launch_")
         elif self.step_kernel == "pair":
             fn = L.st_qstep_pair_launch
         elif self.chunk == 64:
