@@ -40,6 +40,11 @@
 #ifndef WS_GSKIP
 #define WS_GSKIP 0      // 1: timing build (csrc/qstep_ws_gskip.hip), gradient waves skip their work
 #endif
+#if WS_MARKS   // tools/isa.py: assembly comments at the stamp points, to count instructions per phase
+#define WS_MARK(W, I) asm volatile(";@" #W " " #I);
+#else
+#define WS_MARK(W, I)
+#endif
 #ifndef WS_NS
 #define WS_NS ws
 #define WS_API(name) name
@@ -55,6 +60,7 @@ constexpr int INP = 224, HP = 128;
 constexpr int KX = 208;          // input slots used by layer 1
 constexpr int HWIN = 201;        // window length this kernel is built for
 constexpr int NSLOT = 4;
+static_assert(NSLOT % ND == 0, "a data wave reuses its own slots (sequence q = ND k + d)");
 
 // ---------------------------------------------------------------------------------- LDS layout (bytes)
 constexpr int oW0 = 0;                          // W0p [128][208] bf16: columns in slot order
@@ -129,13 +135,28 @@ ST_DEV s4v relu_bf(f4v v) {
 ST_DEV s4v mask_bf(f4v v, s4v act) {
   return pk4(act[0] > 0 ? v[0] : 0.f, act[1] > 0 ? v[1] : 0.f, act[2] > 0 ? v[2] : 0.f, act[3] > 0 ? v[3] : 0.f);
 }
+// same, on packed integer ops: bf16(v) bits * min(act, 1) (act >= 0 as a short: relu'd bf16 bits)
+// (inline asm: written in C, the compiler turns min(act, 1) * x back into a compare + select per value)
+ST_DEV unsigned mask2(unsigned x, unsigned act) {
+  unsigned m, r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(act), "v"(0x00010001u));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(x), "v"(m));
+  return r;
+}
+ST_DEV s4v mask_pk(f4v v, s4v act) {
+  const uint2 a = __builtin_bit_cast(uint2, act);
+  uint2 r;
+  r.x = mask2(pack_bf2(v[0], v[1]), a.x);
+  r.y = mask2(pack_bf2(v[2], v[3]), a.y);
+  return __builtin_bit_cast(s4v, r);
+}
 ST_DEV s4v lo4(s8v v) { s4v r = {v[0], v[1], v[2], v[3]}; return r; }
 ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
 
 // acc[i] += W1 (rows 16 i .. 16 i + 15, pi-ordered columns) . H (B operands of 4 k-steps), 32 MFMAs with
 // the W1 fragment of pair j + PD2 read while pair j issues (j = 8 ks + i)
 ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc) {
-  constexpr int PD2 = 6, NB2 = PD2 + 1;
+  constexpr int PD2 = 8, NB2 = PD2 + 1;
   s8v A[NB2];
 #pragma unroll
   for (int j = 0; j < PD2; ++j) A[j] = lds_ld8(W1p + w1_off(16 * (j & 7) + l16, 32 * (j >> 3) + 8 * g4));
@@ -234,6 +255,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
     const int sh_ = pc_ & 3;                                                                     \
     const float* b_ = p.prices4 + ((size_t)sh_ * p.E + (size_t)e_) * p.T4 + (size_t)(pc_ - sh_);  \
+    pl = *reinterpret_cast<const float4*>(b_ + 200);  /* first: the back edge copies it (see below) */ \
     _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
       const float* q_ = b_ + 32 * ks + 8 * g4;                                                   \
       pa[ks] = *reinterpret_cast<const float4*>(q_);                                             \
@@ -245,7 +267,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       pd = *reinterpret_cast<const float4*>(r_);                                                 \
       pe = r_[4];                                                                                \
     }                                                                                            \
-    pl = *reinterpret_cast<const float4*>(b_ + 200);                                             \
   }
     WS_LOAD_ENV(0, e_pos, e_b, e_sh, e_val, e_rs, e_ep)
     WS_LOAD_PRICES(0, e_pos)
@@ -253,7 +274,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 
     unsigned long long* stamps = (WS_STAMPS && p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0)
                                      ? p.stamps : nullptr;
-#define WS_STAMP(I) if (WS_STAMPS && stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime();
+#define WS_STAMP(I) if (WS_STAMPS && stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime(); WS_MARK(D, I)
 #define WS_PIN(V) asm volatile("" ::"v"(V))
 #define WS_SB() __builtin_amdgcn_sched_barrier(0)
 
@@ -298,6 +319,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
       WS_SB();
       WS_STAMP(1);
+      // the epsilon-greedy draw (Philox, ~70 VALU with quarter-rate multiplies) depends only on (env, step):
+      // issued here, the scheduler interleaves it with layer 1's MFMAs (VALU slots in the group pattern)
+      float u1, u2;
+      {
+        uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
+                 c2 = (uint32_t)(step >> 32), c3 = 0u;
+        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+        u1 = u24(c0);
+        u2 = u24(c1);
+      }
       // ---------------------------------------------------------------- layer 1 of Q(x) and of Q(x')'s window
       f4v a1[8], a1n[8];
 #pragma unroll
@@ -305,7 +336,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       {
         // software pipeline: the W0 fragment of pair j + PD1 is read while pair j's two MFMAs issue
         // (j = 8 ks + i; one fragment feeds Q(x) and Q(x')'s window)
-        constexpr int PD1 = 2, NB1 = PD1 + 1;
+        constexpr int PD1 = 6, NB1 = PD1 + 1;
         const bf16_t* w0b = W0p + l16 * KX + 8 * g4;
         s8v A[NB1];
 #pragma unroll
@@ -322,7 +353,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
             A[jn % NB1] = lds_ld8(w0b + (jn & 7) * 16 * KX + 32 * (jn >> 3));
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           }
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU (the Philox draw) between MFMAs
         }
+        WS_PIN(u1); WS_PIN(u2);   // (else the draw sinks into the env-step branch)
         WS_SB();
       }
       s4v w06[8];   // the last k-step's A fragments: used again after the env step (x')
@@ -334,13 +367,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s8v H1[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1[ks] = cat8(relu_bf(a1[2 * ks]), relu_bf(a1[2 * ks + 1]));
+      f4v a2[8];   // layer 2's accumulators start at the bias (read early: its latency is off the MFMA chain)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_PIN(H1[3]); WS_PIN(a1n[7]);
       WS_SB();
       WS_STAMP(2);
       // ---------------------------------------------------------------- claim a ring slot; X and H1 go in now
-      int q = 0;
-      if (lane == 0) q = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      q = __builtin_amdgcn_readfirstlane(q);
+      // sequence number fixed by (tile, wave): the gradient waves consume the tiles of a workgroup in one
+      // order on every run, so the fp32 gradient sums (and every replay of a captured step) are bit-exact
+      const int q = ND * k + d;
       const int sl = q % NSLOT, round = q / NSLOT;
       for (int spin = 0; lds_acq(ctl + 5 + sl) < NG * round; ++spin) {
         __builtin_amdgcn_s_sleep(1);
@@ -361,9 +397,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_SB();
       WS_STAMP(4);
       // ---------------------------------------------------------------- layer 2 + output of Q(x)
-      f4v a2[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       layer2(W1p, l16, g4, H1, a2);
       s8v H2[4];
 #pragma unroll
@@ -395,10 +428,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         float best = q0;
         if (q1 > best) { best = q1; greedy = 1; }
         if (q2 > best) { best = q2; greedy = 2; }
-        uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
-                 c2 = (uint32_t)(step >> 32), c3 = 0u;
-        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
-        const float u1 = u24(c0), u2 = u24(c1);
         const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
         int rnd = (int)(u2 * 3.0f);
         rnd = rnd > 2 ? 2 : rnd;
@@ -427,6 +456,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s8v H1n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1n[ks] = cat8(relu_bf(a1n[2 * ks]), relu_bf(a1n[2 * ks + 1]));
+      // the next tile's price windows, issued here (their registers are free from now to the next tile's
+      // features): half a tile of HBM latency hidden.  Unconditional (env_of clamps the last tile) so the
+      // loop-carried registers need no phi copy -- a copy of a register with a load in flight is a
+      // vmcnt(0) wait at the back edge.
+      WS_LOAD_PRICES(k + 1, e_pos)
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_SB();
@@ -487,25 +521,26 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         st_fsum += fdone;
         st_fsq += fdone * fdone;
       }
-      // the next tile's price windows (their registers are live from here to the next tile's features)
-      if (k + 1 < nmy) WS_LOAD_PRICES(k + 1, e_pos)
       WS_SB();
       WS_STAMP(9);
       // ---------------------------------------------------------------- dZ2 = (W2^T dQ) * [H2 > 0]
-      // dQ has one nonzero entry per env (its slot), so dZ2[env][u2] = bf16(dq) * W2[slot][u2]: an exact
-      // fp32 product, as the MFMA with the bf16 dQ row would give.  (slot, dq) live in lanes g4 == 0.
-      const int slot_b = __shfl(slot, l16, 64);
-      const float dq_b = bf2f(f2bf(__shfl(dq, l16, 64)));
-      s4v dz[8];
+      // on the matrix cores: A = W2^T tiles (lanes g4 == 0 hold W2[0..3][u2], a transposed read of W2p's 4
+      // rows), B = dQ^T (lanes g4 == 0 hold dQ[env][0..3], where TD left them); the result has the layout of
+      // layer 2's accumulators.  dQ has one nonzero entry per env, so every output is one exact fp32 product.
+      const bf16_t* zchunk = reinterpret_cast<const bf16_t*>(ctl + 10);   // 8 zero bytes
+      const s4v bq = g4 == 0 ? pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f, slot == 2 ? dq : 0.f, 0.f)
+                             : zero_s4();
+      s4v aw[8], h2m[8], dz[8];
+      f4v zt[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const s4v w = lds_ld4(W2p + slot_b * HP + pi_pos4(i, g4));
-        const s4v h = *reinterpret_cast<const s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4));
-        f4v v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = __fmul_rn(dq_b, bf2f((bf16_t)w[j]));
-        dz[i] = mask_bf(v, h);
+        aw[i] = lds_tr4(g4 == 0 ? W2p + (l16 >> 2) * HP + pi_pos4(i, l16 & 3) : zchunk);
+        h2m[i] = *reinterpret_cast<const s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4));
       }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zt[i] = mfma16(aw[i], bq, zero4());
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dz[i] = mask_pk(zt[i], h2m[i]);
       WS_PIN(dz[7]);
       WS_SB();
       WS_STAMP(10);
@@ -513,9 +548,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
         *reinterpret_cast<s8v*>(sz2 + w1_off(l16, 32 * ks + 8 * g4)) = cat8(dz[2 * ks], dz[2 * ks + 1]);
-      if (g4 == 0)
-        *reinterpret_cast<s4v*>(sx + l16 * KX + 204) = pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f,
-                                                          slot == 2 ? dq : 0.f, 0.f);
+      if (g4 == 0) *reinterpret_cast<s4v*>(sx + l16 * KX + 204) = bq;
       if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       WS_SB();
       WS_STAMP(11);
@@ -555,7 +588,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     // data-wave rows ((nmy + 1) * 16 words in)
     unsigned long long* gst = (WS_STAMPS && p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
                                   ? p.stamps + (size_t)(nmy + 1) * 16 : nullptr;
-#define WS_GST(I) if (WS_STAMPS && gst) gst[8 * q + (I)] = __builtin_amdgcn_s_memtime();
+#define WS_GST(I) if (WS_STAMPS && gst) gst[8 * q + (I)] = __builtin_amdgcn_s_memtime(); WS_MARK(G, I)
     for (int q = 0; q < nseq; ++q) {
       const int sl = q % NSLOT;
       WS_GST(0);
@@ -594,9 +627,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s4v bh[8];   // H1[env 4 g4 .. + 3][u1 = 16 n + l16]
 #pragma unroll
       for (int n = 0; n < 8; ++n) bh[n] = lds_tr4(sh1 + a_off(r4, 16 * n + 4 * qq));
-      s4v a0[2];
+      s4v a0[2];   // (own tiles read again: bh[2 gw + t] would be a dynamic index -> scratch)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) a0[t] = mask_bf(c1[t], bh[2 * gw + t]);
+      for (int t = 0; t < 2; ++t) a0[t] = mask_pk(c1[t], lds_tr4(sh1 + a_off(r4, 16 * (2 * gw + t) + 4 * qq)));
       WS_PIN(a0[1]);
       WS_SB();
       WS_GST(3);

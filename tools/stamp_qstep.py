@@ -161,10 +161,10 @@ def ws_stamps(a):
     assert int(eng.kernel_err.sum()) == 0
     raw = st.cpu()
     s = raw[: nmy * 16].view(nmy, 16).double()
-    names = ["features", "layer 1 of Q(x) + Q(x') window (56 + 48 MFMA)", "slot claim (wait for a free slot)",
+    names = ["features", "layer 1 of Q(x) + Q(x') window (56 + 48 MFMA) + Philox draw", "slot wait (own slot freed)",
              "X, H1 -> slot", "layer 2 of Q(x) (32 MFMA) + H2 -> slot", "output of Q(x) (4 MFMA chain)",
-             "epsilon-greedy + env step", "Q(x'): layer-1 tail, layer 2, output (8 + 32 + 4 MFMA)",
-             "TD + state write-back + next prices issued", "dZ2 (VALU rank-1 + mask)", "dZ2, dQ -> slot, publish"]
+             "epsilon-greedy + env step", "Q(x'): layer-1 tail, layer 2, output (8 + 32 + 4 MFMA) + next prices issued",
+             "TD + state write-back", "dZ2 (8 MFMA 16x16x16 + packed mask)", "dZ2, dQ -> slot, publish"]
     lines = [f"# ws step kernel: data wave 0 of workgroup 0 ({a.envs} envs, grid {eng.grid}, {nmy} tiles per data "
              f"wave; s_memtime ticks)\n", "| phase | ticks/tile | % |", "|---|---|---|"]
     tot = 0.0
