@@ -45,6 +45,12 @@
 #else
 #define WS_MARK(W, I)
 #endif
+#ifndef WS_L1REP
+#define WS_L1REP 1      // timing builds only (qstep_ws_l1x2.hip / _l2x2.hip): a phase run twice, to price it in
+#endif                  // context (wrong results)
+#ifndef WS_L2REP
+#define WS_L2REP 1
+#endif
 #ifndef WS_NS
 #define WS_NS ws
 #define WS_API(name) name
@@ -103,8 +109,12 @@ ST_DEV int pi_pos4(int i, int q) { return 32 * (i >> 1) + 8 * q + 4 * (i & 1); }
 // pi-ordered images (W1p, DZ2): 16-byte units of row R XOR-swizzled by 2 (R & 7) -- conflict-free 16-byte
 // row reads, 2-way transposed reads (the minimum for one half-unit per lane; tools/lds_bank_sim.py)
 ST_DEV int w1_off(int R, int s) { return R * HP + ((((s >> 3) ^ (2 * (R & 7)))) << 3) + (s & 7); }
-// natural-order 128-wide slot images (H1, H2): 8-byte chunk c8 of row r at c8 ^ 4 (r & 7)
-ST_DEV int a_off(int r, int c) { return r * HP + ((((c >> 2) ^ (4 * (r & 7)))) << 2) + (c & 3); }
+// natural-order 128-wide slot images (H1, H2): 8-byte chunk c8 of row r at c8 ^ (4 (r & 7) | ((r >> 2) & 3)) --
+// conflict-free for the data waves' 8-byte row writes / reads (16 rows of one chunk) and the gradient waves'
+// transposed reads (8 rows x 4 chunks per 32 lanes) alike (tools/lds_bank_sim.py --ws)
+ST_DEV int a_off(int r, int c) {
+  return r * HP + ((((c >> 2) ^ ((4 * (r & 7)) | ((r >> 2) & 3)))) << 2) + (c & 3);
+}
 
 ST_DEV s4v zero_s4() { s4v z = {0, 0, 0, 0}; return z; }
 ST_DEV s8v zero_s8() { s8v z = {0, 0, 0, 0, 0, 0, 0, 0}; return z; }
@@ -338,6 +348,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         // (j = 8 ks + i; one fragment feeds Q(x) and Q(x')'s window)
         constexpr int PD1 = 6, NB1 = PD1 + 1;
         const bf16_t* w0b = W0p + l16 * KX + 8 * g4;
+        for (int rep = 0; rep < WS_L1REP; ++rep) {
         s8v A[NB1];
 #pragma unroll
         for (int j = 0; j < PD1; ++j) A[j] = lds_ld8(w0b + (j & 7) * 16 * KX + 32 * (j >> 3));
@@ -354,6 +365,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           }
           __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU (the Philox draw) between MFMAs
+        }
         }
         WS_PIN(u1); WS_PIN(u2);   // (else the draw sinks into the env-step branch)
         WS_SB();
@@ -397,7 +409,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_SB();
       WS_STAMP(4);
       // ---------------------------------------------------------------- layer 2 + output of Q(x)
-      layer2(W1p, l16, g4, H1, a2);
+      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1, a2);
       s8v H2[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
@@ -464,7 +476,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_SB();
-      layer2(W1p, l16, g4, H1n, a2);
+      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1n, a2);
       s8v H2n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2n[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
