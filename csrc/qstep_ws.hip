@@ -45,6 +45,18 @@
 #else
 #define WS_MARK(W, I)
 #endif
+#ifndef WS_PF_POS
+#define WS_PF_POS 1     // where the next tile's price windows are issued: 0 at Q(x')'s layer 2, 1 after Q(x)'s
+#endif                  // layer 2, 2 right after this tile's features (a whole tile ahead; qstep_ws_pfe.hip)
+#ifndef WS_WB_DEFER
+#define WS_WB_DEFER 1   // 0 (timing build qstep_ws_old.hip): env-state stores issued at TD, not deferred
+#endif
+#ifndef WS_UNAL
+#define WS_UNAL 0       // 1 (qstep_ws_unal.hip): windows read unaligned from replica 0 (4-B aligned dwordx4)
+#endif
+#ifndef WS_NOPF
+#define WS_NOPF 0       // timing build qstep_ws_nopf.hip: no price prefetch in the loop (stale windows)
+#endif
 #ifndef WS_L1REP
 #define WS_L1REP 1      // timing builds only (qstep_ws_l1x2.hip / _l2x2.hip): a phase run twice, to price it in
 #endif                  // context (wrong results)
@@ -263,7 +275,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   {                                                                                              \
     const int e_ = env_of(K);                                                                    \
     const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
-    const int sh_ = pc_ & 3;                                                                     \
+    const int sh_ = WS_UNAL ? 0 : (pc_ & 3);                                                     \
     const float* b_ = p.prices4 + ((size_t)sh_ * p.E + (size_t)e_) * p.T4 + (size_t)(pc_ - sh_);  \
     pl = *reinterpret_cast<const float4*>(b_ + 200);  /* first: the back edge copies it (see below) */ \
     _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
@@ -287,6 +299,20 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #define WS_STAMP(I) if (WS_STAMPS && stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime(); WS_MARK(D, I)
 #define WS_PIN(V) asm volatile("" ::"v"(V))
 #define WS_SB() __builtin_amdgcn_sched_barrier(0)
+
+    // the env-state write-back of tile k is issued in tile k + 1, after its features have waited for their
+    // price windows: a store issued after the windows' loads would make that wait (in-order vmcnt) last
+    // until the store is acknowledged
+    int w_e = -1, w_s = 0, w_pos = 0, w_ep = 0, w_act = 0;
+    float w_b = 0.f, w_v = 0.f, w_rs = 0.f, w_fin = 0.f, w_rew = 0.f;
+    bool w_done = false;
+#define WS_WRITE_BACK()                                                                           \
+  if (g4 == 0 && w_e >= 0) {                                                                     \
+    ENV_F(ER_BUDGET, w_e) = w_b; ENV_I(ER_SHARES, w_e) = w_s; ENV_F(ER_VALUE, w_e) = w_v;        \
+    ENV_I(ER_POS, w_e) = w_pos; ENV_F(ER_RET_SUM, w_e) = w_rs;                                   \
+    ENV_I(ER_ACTION, w_e) = w_act; ENV_F(ER_REWARD, w_e) = w_rew;                                \
+    if (w_done) { ENV_F(ER_LAST_FINAL, w_e) = w_fin; ENV_I(ER_EPISODES, w_e) = w_ep; }           \
+  }
 
     for (int k = 0; k < nmy; ++k) {
       WS_STAMP(0);
@@ -325,10 +351,15 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
       // rotate the prefetched env state; load the one after next
       e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep;
-      WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+#if WS_PF_POS == 2
+      WS_LOAD_PRICES(k + 1, e_pos)
+#endif
       WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
       WS_SB();
       WS_STAMP(1);
+      // (after the features: a store or load issued before them would hold their window wait)
+      WS_WRITE_BACK()
+      WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
       // the epsilon-greedy draw (Philox, ~70 VALU with quarter-rate multiplies) depends only on (env, step):
       // issued here, the scheduler interleaves it with layer 1's MFMAs (VALU slots in the group pattern)
       float u1, u2;
@@ -417,6 +448,15 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int i = 0; i < 8; ++i)
         *reinterpret_cast<s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
       WS_PIN(H2[3]);
+#if WS_PF_POS == 1 && !WS_NOPF
+      // the next tile's price windows: their registers are free from here (the peak of Q(x')'s layer 2 is
+      // no higher with them) to the next tile's features -- over half a tile of HBM latency hidden.
+      // Unconditional (env_of clamps the last tile) so the loop-carried registers need no phi copy (a copy
+      // of a register with a load in flight is a vmcnt(0) wait at the back edge); no store is issued
+      // between here and the features' wait (the env-state write-back is deferred), so that wait is for
+      // the windows alone.
+      WS_LOAD_PRICES(k + 1, e_pos)
+#endif
       WS_SB();
       WS_STAMP(5);
       f4v qa = zero4();
@@ -456,8 +496,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
         Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fxn(vnew));
         st_explore += exploit ? 0.f : 1.f;
-        ENV_I(ER_ACTION, e) = act;
-        ENV_F(ER_REWARD, e) = rew;
       }
       WS_PIN(Xn6);
       WS_SB();
@@ -468,11 +506,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s8v H1n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1n[ks] = cat8(relu_bf(a1n[2 * ks]), relu_bf(a1n[2 * ks + 1]));
-      // the next tile's price windows, issued here (their registers are free from now to the next tile's
-      // features): half a tile of HBM latency hidden.  Unconditional (env_of clamps the last tile) so the
-      // loop-carried registers need no phi copy -- a copy of a register with a load in flight is a
-      // vmcnt(0) wait at the back edge.
+      // (WS_PF_POS 0: the next tile's price windows issued here)
+#if WS_PF_POS == 0 && !WS_NOPF
       WS_LOAD_PRICES(k + 1, e_pos)
+#endif
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_SB();
@@ -508,24 +545,24 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         const int np = pos + 1;
         const float rs = rs0 + rew;
         float fdone = 0.f, ndone = 0.f;
-        if (np >= p.T - HWIN) {
+        w_e = e;
+        w_act = act;
+        w_rew = rew;
+        w_done = np >= p.T - HWIN;
+        if (w_done) {
           const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
-          ENV_F(ER_LAST_FINAL, e) = fin;
-          ENV_I(ER_EPISODES, e) = ep0 + 1;
-          ENV_F(ER_BUDGET, e) = p.b0;
-          ENV_I(ER_SHARES, e) = p.s0;
-          ENV_F(ER_VALUE, e) = 0.f;
-          ENV_I(ER_POS, e) = 0;
-          ENV_F(ER_RET_SUM, e) = 0.f;
+          w_fin = fin;
+          w_ep = ep0 + 1;
+          w_b = p.b0; w_s = p.s0; w_v = 0.f; w_pos = 0; w_rs = 0.f;
           fdone = fin;
           ndone = 1.f;
         } else {
-          ENV_F(ER_BUDGET, e) = b2;
-          ENV_I(ER_SHARES, e) = s2;
-          ENV_F(ER_VALUE, e) = vnew;
-          ENV_I(ER_POS, e) = np;
-          ENV_F(ER_RET_SUM, e) = rs;
+          w_b = b2; w_s = s2; w_v = vnew; w_pos = np; w_rs = rs;
         }
+#if !WS_WB_DEFER
+        WS_WRITE_BACK()
+        w_e = -1;
+#endif
         st_reward += rew;
         st_loss += diff * diff;
         st_qslot += qs;
@@ -565,6 +602,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_SB();
       WS_STAMP(11);
     }
+    WS_WRITE_BACK()   // the last tile's
+#undef WS_WRITE_BACK
 #undef WS_LOAD_ENV
 #undef WS_LOAD_PRICES
 #undef WS_STAMP
