@@ -46,14 +46,11 @@
 #define WS_MARK(W, I)
 #endif
 #ifndef WS_PF_POS
-#define WS_PF_POS 1     // where the next tile's price windows are issued: 0 at Q(x')'s layer 2, 1 after Q(x)'s
-#endif                  // layer 2, 2 right after this tile's features (a whole tile ahead; qstep_ws_pfe.hip)
+#define WS_PF_POS 0     // where the next tile's price windows are issued: 0 at Q(x')'s layer 2, 1 after Q(x)'s
+#endif                  // layer 2, 2 right after this tile's features (a whole tile ahead: 59 VGPRs spill)
 #ifndef WS_WB_DEFER
-#define WS_WB_DEFER 1   // 0 (timing build qstep_ws_old.hip): env-state stores issued at TD, not deferred
-#endif
-#ifndef WS_UNAL
-#define WS_UNAL 0       // 1 (qstep_ws_unal.hip): windows read unaligned from replica 0 (4-B aligned dwordx4)
-#endif
+#define WS_WB_DEFER 0   // 1: env-state stores issued in the next tile after its window wait (qstep_ws_defer.hip:
+#endif                  // with WS_PF_POS 1, 2.6 % slower on one box, profiles/r3_ws_ab.md)
 #ifndef WS_NOPF
 #define WS_NOPF 0       // timing build qstep_ws_nopf.hip: no price prefetch in the loop (stale windows)
 #endif
@@ -275,8 +272,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   {                                                                                              \
     const int e_ = env_of(K);                                                                    \
     const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
-    const int sh_ = WS_UNAL ? 0 : (pc_ & 3);                                                     \
-    const float* b_ = p.prices4 + ((size_t)sh_ * p.E + (size_t)e_) * p.T4 + (size_t)(pc_ - sh_);  \
+    const float* b_ = p.prices4 + (size_t)e_ * p.T4 + (size_t)pc_;  /* 4-B aligned dwordx4 reads */   \
     pl = *reinterpret_cast<const float4*>(b_ + 200);  /* first: the back edge copies it (see below) */ \
     _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
       const float* q_ = b_ + 32 * ks + 8 * g4;                                                   \

@@ -41,8 +41,8 @@ __global__ void __launch_bounds__(256) random_walk_kernel(float* __restrict__ ou
 // ps & 3 — the fused step kernel's gather becomes one global_load_dwordx4 per lane per row
 // with no realignment.  4 x 1.6 GB for 65,536 envs: cheap on 288 GB of HBM3E.
 __global__ void __launch_bounds__(256) replicate4_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                                         int E, int T, int T4) {
-  const size_t n = (size_t)4 * E * T4;
+                                                         int E, int T, int T4, int reps) {
+  const size_t n = (size_t)reps * E * T4;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(idx % T4);
     const size_t se = idx / T4;
@@ -82,9 +82,12 @@ extern "C" hipError_t st_init_normal(float* out, int rows, int cols, int ld, flo
   return hipGetLastError();
 }
 
-extern "C" hipError_t st_replicate4(const float* src, float* dst, int E, int T, int T4, hipStream_t stream) {
-  if (T4 % 4 != 0 || T4 < T) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(st::replicate4_kernel, dim3(4096), dim3(256), 0, stream, src, dst, E, T, T4);
+// reps shifted copies (replica s = row shifted left by s): 4 for the 16-B-aligned window gathers of
+// qstep_wide / fused / pair, 1 (a padded copy) for qstep_ws, whose 4-B-aligned dwordx4 reads measured as
+// fast (profiles/r3_ws_ab.md)
+extern "C" hipError_t st_replicate4(const float* src, float* dst, int E, int T, int T4, int reps, hipStream_t stream) {
+  if (T4 % 4 != 0 || T4 < T || reps < 1 || reps > 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::replicate4_kernel, dim3(4096), dim3(256), 0, stream, src, dst, E, T, T4, reps);
   return hipGetLastError();
 }
 

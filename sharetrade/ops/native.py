@@ -115,7 +115,7 @@ def lib() -> C.CDLL:
     L.st_random_walk.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_uint32,
                                  C.c_uint32, C.c_void_p]
     L.st_random_walk.restype = C.c_int
-    L.st_replicate4.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_replicate4.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_replicate4.restype = C.c_int
     L.st_init_normal.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_uint32, C.c_uint32,
                                  C.c_uint32, C.c_void_p]
@@ -196,13 +196,13 @@ def replica_stride(T: int) -> int:
     return (T + 64 + 3) // 4 * 4
 
 
-def replicate4(src: torch.Tensor) -> torch.Tensor:
-    """[E, T] -> [4, E, T4] shifted replicas (csrc/series.hip: replicate4)."""
+def replicate4(src: torch.Tensor, reps: int = 4) -> torch.Tensor:
+    """[E, T] -> [reps, E, T4] shifted replicas (csrc/series.hip: replicate4); reps=1 is a padded copy."""
     E, T = src.shape
     T4 = replica_stride(T)
-    flat = torch.zeros(4 * E * T4 + 64, dtype=torch.float32, device=src.device)   # +64: last row's over-read
-    out = flat[: 4 * E * T4].view(4, E, T4)
-    check(lib().st_replicate4(ptr(src), ptr(out), E, T, T4, stream_handle()), "st_replicate4")
+    flat = torch.zeros(reps * E * T4 + 64, dtype=torch.float32, device=src.device)   # +64: last row's over-read
+    out = flat[: reps * E * T4].view(reps, E, T4)
+    check(lib().st_replicate4(ptr(src), ptr(out), E, T, T4, int(reps), stream_handle()), "st_replicate4")
     return out
 
 

@@ -255,7 +255,9 @@ class VectorEngine:
             self._f32 = F32EngineStep(self)
             return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
-        self.prices4 = native.replicate4(self.prices)   # aligned-gather replicas (4 x bank, HBM is plentiful)
+        # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide / pair
+        # kernels; one padded copy for ws (4-B-aligned dwordx4 reads, as fast: profiles/r3_ws_ab.md)
+        self.prices4 = native.replicate4(self.prices, 1 if self.step_kernel == "ws" else 4)
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
         self.grid = max(1, min(self.cfg.engine.grid or props.multi_processor_count, self.E // self.chunk))

@@ -344,21 +344,25 @@ def test_reward_modes_and_td_clip_match_oracle(native_built, chunk):
         assert _rel(grad, g_ref) < 3e-2, (mode, clip, _rel(grad, g_ref))
 
 
-def test_large_bank_gather_matches_oracle(native_built):
-    """131,072 envs x 6,047 days: the 4 aligned replicas hold 3.2e9 floats, so replica offsets of the
-    upper envs pass 2^31 elements (the bench runs 1,048,576 envs per GPU).  The last 512 envs
-    (windows spread over the whole series) must select the same greedy actions as the fp32 oracle on
-    their own rows and make bit-identical env transitions."""
+@pytest.mark.parametrize("kernel,E", [("wide", 131072), ("ws", 393216)])
+def test_large_bank_gather_matches_oracle(native_built, kernel, E):
+    """x 6,047 days: the wide kernel's 4 aligned replicas of 131,072 envs hold 3.2e9 floats, the ws
+    kernel's single padded copy of 393,216 envs 2.4e9, so the window offsets of the upper envs pass
+    2^31 elements (the bench runs 1,835,008 envs per GPU).  The last 512 envs (windows spread over the
+    whole series) must select the same greedy actions as the fp32 oracle on their own rows and make
+    bit-identical env transitions."""
     from sharetrade.env import trading as tr
     from sharetrade.trainer.engine import VectorEngine
 
     cfg = _cfg()
     cfg.agent.epsilon, cfg.agent.ramp = 1.0, 1.0   # exploit whenever pos >= 1: actions = argmax Q(x)
     cfg.data.source, cfg.data.length = "random_walk", 6047
-    E, S = 131072, 512
+    cfg.engine.step_kernel = kernel
+    S = 512
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=E)
-    assert eng.chunk == 64 and eng.prices4.numel() > 2 ** 31
+    assert eng.chunk == 64 and eng.step_kernel == kernel and eng.prices4.numel() > 2 ** 31
+    assert eng.prices4.shape[0] == (1 if kernel == "ws" else 4)
     idx = torch.arange(E, dtype=torch.int32, device=dev)
     eng.state.pos.copy_(1 + idx * 37 % (eng.T - cfg.model.history - 3))
     eng.state.shares.copy_(idx % 3)
@@ -481,6 +485,7 @@ def test_ofold_variant_matches_default(native_built):
         cfg = _cfg()
         cfg.agent.epsilon = 0.9
         cfg.engine.step_variant = variant
+        cfg.engine.step_kernel = "wide"   # the variants are builds of the 8-wave wide kernel (the default is ws)
         eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
         eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
         eng.ctrl.fill_(2000)
@@ -506,6 +511,7 @@ def test_wswz_variant_bit_identical(native_built):
         cfg = _cfg()
         cfg.agent.epsilon = 0.9
         cfg.engine.step_variant = variant
+        cfg.engine.step_kernel = "wide"   # the variants are builds of the 8-wave wide kernel (the default is ws)
         eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
         eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 150)
         eng.ctrl.fill_(3000)
