@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=64, help="acting steps to pre-fill the replay ring")
     ap.add_argument("--updates", type=int, default=1)
-    ap.add_argument("--dw-gemm", default="auto", help="weight-gradient GEMMs: auto | hip | hipblaslt")
+    ap.add_argument("--dw-gemm", default="auto", help="weight-gradient GEMMs: auto | hip (own split-K kernels)")
     ap.add_argument("--serial", action="store_true", help="one stream (no concurrent GEMM chains in the update)")
     ap.add_argument("--unfused-adam", action="store_true", help="per-layer Adam + row-sum + counter launches")
     ap.add_argument("--no-pingpong", action="store_true", help="no 256x256 ping-pong GEMM for the act-step layers")

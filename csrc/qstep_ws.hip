@@ -80,8 +80,8 @@ static_assert(NSLOT % ND == 0, "a data wave reuses its own slots (sequence q = N
 // ---------------------------------------------------------------------------------- LDS layout (bytes)
 constexpr int oW0 = 0;                          // W0p [128][208] bf16: columns in slot order
 constexpr int oW1 = oW0 + HP * KX * 2;          // W1p [128][128] bf16: columns in pi order, 16-B units swizzled
-constexpr int oW2 = oW1 + HP * HP * 2;          // W2p [4][128] bf16 (rows = actions, row 3 zero; pi order)
-constexpr int oB1 = oW2 + 4 * HP * 2;           // b1 [128] f32
+constexpr int oW2 = oW1 + HP * HP * 2;          // W2p [5][128] bf16 (rows = actions, rows 3, 4 zero; pi order)
+constexpr int oB1 = oW2 + 5 * HP * 2;           // b1 [128] f32
 constexpr int oB2 = oB1 + HP * 4;               // b2 [16] f32
 constexpr int oSLOT = oB2 + 64;
 // one ring slot: X [16][208] (slots 204..207 of each row carry dQ[env][0..3]), H1 / H2 [16][128]
@@ -203,6 +203,16 @@ ST_DEV int lds_acq(const int* w) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 
+// env-state rows addressed as a uniform row base + a 32-bit byte offset, so the loads / stores use the
+// SGPR-base form (no 64-bit VALU address add per access)
+ST_DEV int* env_ptr(const QStepParams& p, int R, int e) {
+  return reinterpret_cast<int*>(reinterpret_cast<char*>(p.env + (size_t)R * p.E) + (unsigned)e * 4u);
+}
+#undef ENV_I
+#undef ENV_F
+#define ENV_I(R, e) (*env_ptr(p, (R), (e)))
+#define ENV_F(R, e) (*reinterpret_cast<float*>(env_ptr(p, (R), (e))))
+
 // ---------------------------------------------------------------------------------- the kernel
 template <int FEAT>
 __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
@@ -234,7 +244,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       W1p[w1_off(R, s)] = w1[R * HP + pi_unit(s)];
     }
     const bf16_t* w2 = p.wq + p.off_w2;
-    for (int i = tid; i < 4 * HP; i += NT) {           // W2p[a][s] = W2^T[a][pi(s)] (row 3 = padding row)
+    for (int i = tid; i < 5 * HP; i += NT) {           // W2p[a][s] = W2^T[a][pi(s)] (rows 3, 4: padding rows)
       const int a = i >> 7, s = i & 127;
       W2p[i] = w2[a * HP + pi_unit(s)];
     }
@@ -458,7 +468,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v qa = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : zero_s8();
+        const s8v a = lds_ld8(W2p + min(l16, 4) * HP + 32 * ks + 8 * g4);   // rows >= 3 zero: no masked load
         qa = mfma32(a, H2[ks], qa);
       }
       WS_PIN(qa);
@@ -516,7 +526,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v qn = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = l16 < 4 ? lds_ld8(W2p + l16 * HP + 32 * ks + 8 * g4) : zero_s8();
+        const s8v a = lds_ld8(W2p + min(l16, 4) * HP + 32 * ks + 8 * g4);   // rows >= 3 zero: no masked load
         qn = mfma32(a, H2n[ks], qn);
       }
       WS_PIN(qn);

@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 200 python -u bench.py --steps 200 --warmup 10 --no-episode > gpurun_out/r3p_bench.log 2>&1 && echo "bench: $(tail -1 gpurun_out/r3p_bench.log | cut -c100-200)" && \
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/r3p_suite.log 2>&1 || { echo SUITE_FAIL; tail -60 gpurun_out/r3p_suite.log; exit 1; }
 tail -2 gpurun_out/r3p_suite.log

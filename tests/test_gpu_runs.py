@@ -19,7 +19,7 @@ def _deep(cfg):
     prices = torch.from_numpy(random_walk(400, 50.0, 0.02, 4, n_series=256).astype(np.float32))
     # hipBLASLt weight gradients, no split-K forward / dual launches: a run that is bit-reproducible
     return DeepDQN(cfg, torch.device("cuda", 0), envs=256, batch=256, replay_capacity=4096, prices=prices,
-                   dw_gemm="hipblaslt", concurrent=False, batched_fwd=False, dual_bwd=False, overlap_act=True,
+                   dw_gemm="hip", concurrent=False, batched_fwd=False, dual_bwd=False, overlap_act=True,
                    target_every=4)
 
 
