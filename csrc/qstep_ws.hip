@@ -51,6 +51,18 @@
 #ifndef WS_WB_DEFER
 #define WS_WB_DEFER 0   // 1: env-state stores issued in the next tile after its window wait (qstep_ws_defer.hip:
 #endif                  // with WS_PF_POS 1, 2.6 % slower on one box, profiles/r3_ws_ab.md)
+#ifndef WS_GPIPE
+#define WS_GPIPE 1      // gradient waves: fragments issued in latency order (0: qstep_ws_gold.hip, the v4 order)
+#endif
+#ifndef WS_GZ
+#define WS_GZ 1         // gradient waves: dZ1 fragments read this many k-steps ahead
+#endif
+#ifndef WS_GX
+#define WS_GX 3         // gradient waves: X fragments read this many dW0 steps ahead
+#endif
+#ifndef WS_GH
+#define WS_GH 12        // gradient waves: the dW1 / dW2 fragments issued after this dW0 step
+#endif
 #ifndef WS_NOPF
 #define WS_NOPF 0       // timing build qstep_ws_nopf.hip: no price prefetch in the loop (stale windows)
 #endif
@@ -667,6 +679,81 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---- dZ1 for this wave's u1 tiles i = 2 gw + t:  C[env][u1] = sum_u2 dZ2[env][u2] W1[u2][u1]
       //      (A = dZ2 rows in pi order, B = W1 read transposed from W1p); the result lane (u1, g4) holds envs
       //      4 g4 .. 4 g4 + 3 -- the A layout of the dW0 MFMA, no transpose needed
+#if WS_GPIPE
+      // issue order = latency order, within the ~68 VGPRs beside the accumulators: dZ1's fragments two
+      // k-steps ahead of its MFMAs; the mask's H1 tiles and all of X before the mask; the dW1 / dW2
+      // fragments under the second half of the dW0 MFMAs; the slot goes back once the last has landed
+      f4v c1[2] = {zero4(), zero4()};
+      {
+        s8v az[4];
+        s4v wt[4][2][2];
+        auto rd = [&](int ks) {
+          az[ks] = lds_ld8(sz2 + w1_off(l16, 32 * ks + 8 * g4));
+          const int R = 32 * ks + 4 * g4 + (l16 >> 2);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int col = pi_pos4(2 * gw + t, qq);
+            wt[ks][t][0] = lds_tr4(W1p + w1_off(R, col));
+            wt[ks][t][1] = lds_tr4(W1p + w1_off(R + 16, col));
+          }
+        };
+        constexpr int ZD = WS_GZ;   // k-steps of dZ1 fragments read ahead
+#pragma unroll
+        for (int ks = 0; ks < ZD; ++ks) rd(ks);
+        __builtin_amdgcn_sched_group_barrier(0x100, 5 * ZD, 0);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          if (ks + ZD < 4) rd(ks + ZD);
+          if (ks + ZD < 4) __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) c1[t] = mfma32(az[ks], cat8(wt[ks][t][0], wt[ks][t][1]), c1[t]);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+      }
+      s4v bown[2], bx[13];   // own H1 tiles; X^T fragments
+#pragma unroll
+      for (int t = 0; t < 2; ++t) bown[t] = lds_tr4(sh1 + a_off(r4, 16 * (2 * gw + t) + 4 * qq));
+      constexpr int XD = WS_GX;   // X fragments read ahead of the dW0 MFMAs
+#pragma unroll
+      for (int n = 0; n < XD; ++n) bx[n] = lds_tr4(sx + r4 * KX + 16 * n + 4 * qq);
+      WS_PIN(c1[0]); WS_PIN(c1[1]);
+      WS_SB();
+      WS_GST(2);
+      s4v a0[2];   // (own tiles read separately: bh[2 gw + t] would be a dynamic index -> scratch)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a0[t] = mask_pk(c1[t], bown[t]);
+      WS_PIN(a0[1]);
+      WS_SB();
+      WS_GST(3);
+      // ---- dW0^T[u1][slot] += dZ1^T . X; the dW1 / dW2 fragments issued half way
+      s4v bh[8], a1[2], aq, bh2[2];   // H1[env 4 g4 .. + 3][u1 = 16 n + l16], dZ2^T, dQ^T[a][env], H2 tiles
+#pragma unroll
+      for (int n = 0; n < 13; ++n) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma16(a0[m], bx[n], gW0[m][n]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (n + XD < 13) {
+          bx[n + XD] = lds_tr4(sx + r4 * KX + 16 * (n + XD) + 4 * qq);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if (n == WS_GH) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) bh[k] = lds_tr4(sh1 + a_off(r4, 16 * k + 4 * qq));
+#pragma unroll
+          for (int m = 0; m < 2; ++m) a1[m] = lds_tr4(sz2 + w1_off(r4, pi_pos4(2 * gw + m, qq)));
+          aq = lds_tr4(qq == 0 ? sx + r4 * KX + 204 : zchunk);   // a = l16 < 4
+#pragma unroll
+          for (int k = 0; k < 2; ++k) bh2[k] = lds_tr4(sh2 + a_off(r4, 16 * (2 * gw + k) + 4 * qq));
+          __builtin_amdgcn_sched_group_barrier(0x100, 13, 0);
+        }
+      }
+      WS_PIN(gW0[1][12]);
+      WS_SB();
+      WS_GST(4);
+      // every fragment of the slot is in registers: hand the slot back
+      if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      WS_GST(5);
+#else
       f4v c1[2] = {zero4(), zero4()};
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -711,6 +798,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // every fragment of the slot is in registers: hand the slot back before the MFMAs
       if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       WS_GST(5);
+#endif
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
 #pragma unroll
