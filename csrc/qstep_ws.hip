@@ -35,8 +35,8 @@
 #include "qstep.h"
 
 #ifndef WS_STAMPS
-#define WS_STAMPS 0     // 1: s_memtime stamps per phase (the debug build csrc/qstep_ws_stamps.hip only: the stamp
-#endif                  // code costs the 256-register build its last free registers)
+#define WS_STAMPS 0     // s_memtime stamps per phase, bit 0 data wave 0, bit 1 gradient wave 0 (debug builds
+#endif                  // csrc/qstep_ws_stamps*.hip only: the stamp code costs registers)
 #ifndef WS_GSKIP
 #define WS_GSKIP 0      // 1: timing build (csrc/qstep_ws_gskip.hip), gradient waves skip their work
 #endif
@@ -71,6 +71,9 @@
 #endif                  // context (wrong results)
 #ifndef WS_L2REP
 #define WS_L2REP 1
+#endif
+#ifndef WS_GST_MASK
+#define WS_GST_MASK 0x7F   // which gradient-wave stamps a stamps build takes
 #endif
 #ifndef WS_NS
 #define WS_NS ws
@@ -312,9 +315,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     WS_LOAD_PRICES(0, e_pos)
     WS_LOAD_ENV(1, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
 
-    unsigned long long* stamps = (WS_STAMPS && p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0)
+    unsigned long long* stamps = ((WS_STAMPS & 1) && p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0)
                                      ? p.stamps : nullptr;
-#define WS_STAMP(I) if (WS_STAMPS && stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime(); WS_MARK(D, I)
+#define WS_STAMP(I) if ((WS_STAMPS & 1) && stamps) stamps[k * 16 + (I)] = __builtin_amdgcn_s_memtime(); WS_MARK(D, I)
 #define WS_PIN(V) asm volatile("" ::"v"(V))
 #define WS_SB() __builtin_amdgcn_sched_barrier(0)
 
@@ -655,9 +658,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     const int nseq = ND * nmy;
     // debug stamps of gradient wave 0 of workgroup 0: per slot (wait begins, slot full, slot done) after the
     // data-wave rows ((nmy + 1) * 16 words in)
-    unsigned long long* gst = (WS_STAMPS && p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
+    unsigned long long* gst = ((WS_STAMPS & 2) && p.stamps != nullptr && blockIdx.x == 0 && gw == 0 && lane == 0)
                                   ? p.stamps + (size_t)(nmy + 1) * 16 : nullptr;
-#define WS_GST(I) if (WS_STAMPS && gst) gst[8 * q + (I)] = __builtin_amdgcn_s_memtime(); WS_MARK(G, I)
+    // (held in SGPRs and stored once per slot: the gradient wave has no VGPR to spare mid-slot)
+    unsigned long long gts[7] = {0, 0, 0, 0, 0, 0, 0};
+#define WS_GST(I) if ((WS_STAMPS & 2) && ((WS_GST_MASK >> (I)) & 1)) gts[I] = __builtin_amdgcn_s_memtime(); WS_MARK(G, I)
     for (int q = 0; q < nseq; ++q) {
       const int sl = q % NSLOT;
       WS_GST(0);
@@ -811,6 +816,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_PIN(gW1[1][7]); WS_PIN(gB2);
       WS_SB();
       WS_GST(6);
+      if ((WS_STAMPS & 2) && gst) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) gst[8 * q + i] = gts[i];
+      }
     }
     __syncthreads();
     // ------------------------------------------------------------------ gradient slab write-out

@@ -1,4 +1,5 @@
-// Debug build of csrc/qstep_ws.hip with s_memtime stamps per phase (tools/stamp_qstep.py --kernel ws):
+// Debug build of csrc/qstep_ws.hip with s_memtime stamps per phase of data wave 0 of workgroup 0
+// (tools/stamp_qstep.py --kernel ws; gradient-wave stamps: csrc/qstep_ws_gstamps.hip):
 // st_qstep_ws_launch_stamps, same contract.  Kept out of the production build: the stamp code costs the
 // 256-register kernel its last free registers (and with them the price prefetch's latency cover).
 #define WS_STAMPS 1

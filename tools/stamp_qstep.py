@@ -153,13 +153,21 @@ def ws_stamps(a):
     eng.run(3)
     torch.cuda.synchronize()
     nmy = (a.envs // 64 + eng.grid - 1) // eng.grid
-    st = torch.zeros((nmy + 1) * 16 + 8 * 4 * nmy + 16, dtype=torch.int64, device=dev)
-    eng._qp.stamps = st.data_ptr()
-    eng.step()
-    torch.cuda.synchronize()
-    eng._qp.stamps = None
-    assert int(eng.kernel_err.sum()) == 0
-    raw = st.cpu()
+
+    def stamped(variant):
+        # data-wave stamps from csrc/qstep_ws_stamps.hip, gradient-wave stamps from qstep_ws_gstamps.hip
+        st = torch.zeros((nmy + 1) * 16 + 8 * 4 * nmy + 16, dtype=torch.int64, device=dev)
+        eng.cfg.engine.step_variant = variant
+        eng._qp.stamps = st.data_ptr()
+        eng.step()
+        torch.cuda.synchronize()
+        eng._qp.stamps = None
+        eng.cfg.engine.step_variant = ""
+        assert int(eng.kernel_err.sum()) == 0
+        return st.cpu()
+
+    raw = stamped("")
+    graw = stamped("gstamps")
     s = raw[: nmy * 16].view(nmy, 16).double()
     names = ["features", "layer 1 of Q(x) + Q(x') window (56 + 48 MFMA) + Philox draw", "slot wait (own slot freed)",
              "X, H1 -> slot", "layer 2 of Q(x) (32 MFMA) + H2 -> slot", "output of Q(x) (4 MFMA chain)",
@@ -177,11 +185,11 @@ def ws_stamps(a):
         lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
     loop = float((s[1:, 0] - s[:-1, 0]).mean()) if nmy > 1 else tot
     lines.append(f"| tile loop (stamp0 -> stamp0) | {loop:.0f} | |")
-    g = raw[(nmy + 1) * 16: (nmy + 1) * 16 + 8 * 4 * nmy].view(4 * nmy, 8).double()
-    gn = ["wait for the next full slot", "dZ1 for own u1 tiles (8 MFMA 16x16x32, 16 transposed W1 reads)",
-          "H1 fragments + dZ1 mask", "dW0 (26 MFMA 16x16x16, 13 X reads)", "dZ2^T / dQ^T / H2 reads + release",
-          "dW1, db1, dW2, db2 (21 MFMA)"]
-    lines += ["", "| gradient wave 0, per ring slot | ticks | % |", "|---|---|---|"]
+    g = graw[(nmy + 1) * 16: (nmy + 1) * 16 + 8 * 4 * nmy].view(4 * nmy, 8).double()
+    gn = ["wait for the next full slot", "dZ1 for own u1 tiles (8 MFMA 16x16x32, 20 reads one k-step ahead) + "
+          "own H1 tiles / first X fragments issued", "dZ1 mask", "dW0 (26 MFMA 16x16x16, X 3 steps ahead) + "
+          "dW1 / dW2 fragments issued", "release", "dW1, db1, dW2, db2 (21 MFMA)"]
+    lines += ["", "| gradient wave 0, per ring slot (separate build) | ticks | % |", "|---|---|---|"]
     gt = float((g[:, 6] - g[:, 0]).mean())
     for i, n in enumerate(gn):
         d = float((g[:, i + 1] - g[:, i]).mean())
