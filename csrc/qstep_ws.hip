@@ -54,6 +54,12 @@
 #ifndef WS_GPIPE
 #define WS_GPIPE 1      // gradient waves: fragments issued in latency order (0: qstep_ws_gold.hip, the v4 order)
 #endif
+#ifndef WS_PD1
+#define WS_PD1 6        // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs
+#endif
+#ifndef WS_NOPHIL
+#define WS_NOPHIL 0     // timing build qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
+#endif
 #ifndef WS_GZ
 #define WS_GZ 1         // gradient waves: dZ1 fragments read this many k-steps ahead
 #endif
@@ -387,7 +393,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       {
         uint32_t c0 = (uint32_t)(p.env_offset + e), c1 = (uint32_t)(step & 0xFFFFFFFFull),
                  c2 = (uint32_t)(step >> 32), c3 = 0u;
-        philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+        if (!WS_NOPHIL) philox4x32(c0, c1, c2, c3, p.key0, p.key1);
         u1 = u24(c0);
         u2 = u24(c1);
       }
@@ -398,7 +404,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       {
         // software pipeline: the W0 fragment of pair j + PD1 is read while pair j's two MFMAs issue
         // (j = 8 ks + i; one fragment feeds Q(x) and Q(x')'s window)
-        constexpr int PD1 = 6, NB1 = PD1 + 1;
+        constexpr int PD1 = WS_PD1, NB1 = PD1 + 1;
         const bf16_t* w0b = W0p + l16 * KX + 8 * g4;
         for (int rep = 0; rep < WS_L1REP; ++rep) {
         s8v A[NB1];
