@@ -55,7 +55,13 @@
 #define WS_GPIPE 1      // gradient waves: fragments issued in latency order (0: qstep_ws_gold.hip, the v4 order)
 #endif
 #ifndef WS_PD1
-#define WS_PD1 6        // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs
+#define WS_PD1 10       // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs
+#endif
+#ifndef WS_DPRIO
+#define WS_DPRIO 0      // s_setprio of the data waves (qstep_ws_dprio.hip: 2)
+#endif
+#ifndef WS_GPRIO
+#define WS_GPRIO 0      // s_setprio of the gradient waves (qstep_ws_gprio.hip: 2)
 #endif
 #ifndef WS_NOPHIL
 #define WS_NOPHIL 0     // timing build qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
@@ -278,6 +284,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   if (wave < ND) {
     // ================================================================ DATA WAVE
     const int d = wave;
+    if (WS_DPRIO) __builtin_amdgcn_s_setprio(WS_DPRIO);   // issue priority over the gradient wave beside it
     float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
           st_qslot = 0.f;
     const float b2v[3] = {sB2[0], sB2[1], sB2[2]};
@@ -645,7 +652,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     __syncthreads();
   } else {
     // ================================================================ GRADIENT WAVE
-    const int gw = wave - ND;   // owns hidden units 32 gw .. 32 gw + 31 of both layers, dW2 columns likewise
+    const int gw = wave - ND;
+    if (WS_GPRIO) __builtin_amdgcn_s_setprio(WS_GPRIO);   // owns hidden units 32 gw .. 32 gw + 31 of both layers, dW2 columns likewise
     f4v gW0[2][13], gW1[2][8], gB1[2], gW2[2], gB2 = zero4();
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
