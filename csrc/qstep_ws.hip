@@ -57,6 +57,12 @@
 #ifndef WS_PD1
 #define WS_PD1 10       // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs
 #endif
+#ifndef WS_W2_EARLY
+#define WS_W2_EARLY 1   // the output layers' W2 fragments read in layer 2's last read slots (0: qstep_ws_w2late.hip)
+#endif
+#ifndef WS_DZ_EARLY
+#define WS_DZ_EARLY 1   // dZ2's LDS fragments read before TD (0: after it, qstep_ws_dzlate.hip)
+#endif
 #ifndef WS_DPRIO
 #define WS_DPRIO 0      // s_setprio of the data waves (qstep_ws_dprio.hip: 2)
 #endif
@@ -201,7 +207,7 @@ ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
 
 // acc[i] += W1 (rows 16 i .. 16 i + 15, pi-ordered columns) . H (B operands of 4 k-steps), 32 MFMAs with
 // the W1 fragment of pair j + PD2 read while pair j issues (j = 8 ks + i)
-ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc) {
+ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc, const bf16_t* w2row, s8v* w2f) {
   constexpr int PD2 = 8, NB2 = PD2 + 1;
   s8v A[NB2];
 #pragma unroll
@@ -214,6 +220,9 @@ ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc) {
     if (j + PD2 < 32) {
       const int jn = j + PD2;
       A[jn % NB2] = lds_ld8(W1p + w1_off(16 * (jn & 7) + l16, 32 * (jn >> 3) + 8 * g4));
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    } else if (WS_W2_EARLY && j >= 32 - 4) {   // the output layer's W2 fragments, in the last read slots
+      w2f[j - 28] = lds_ld8(w2row + 32 * (j - 28));
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
   }
@@ -474,7 +483,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_SB();
       WS_STAMP(4);
       // ---------------------------------------------------------------- layer 2 + output of Q(x)
-      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1, a2);
+      const bf16_t* w2row = W2p + min(l16, 4) * HP + 8 * g4;   // rows >= 3 zero: no masked load
+      s8v w2f[4];
+      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1, a2, w2row, w2f);
       s8v H2[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
@@ -496,7 +507,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v qa = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = lds_ld8(W2p + min(l16, 4) * HP + 32 * ks + 8 * g4);   // rows >= 3 zero: no masked load
+        const s8v a = WS_W2_EARLY ? w2f[ks] : lds_ld8(w2row + 32 * ks);
         qa = mfma32(a, H2[ks], qa);
       }
       WS_PIN(qa);
@@ -547,20 +558,31 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_SB();
-      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1n, a2);
+      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1n, a2, w2row, w2f);
       s8v H2n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2n[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
       f4v qn = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = lds_ld8(W2p + min(l16, 4) * HP + 32 * ks + 8 * g4);   // rows >= 3 zero: no masked load
+        const s8v a = WS_W2_EARLY ? w2f[ks] : lds_ld8(w2row + 32 * ks);
         qn = mfma32(a, H2n[ks], qn);
       }
       WS_PIN(qn);
       WS_SB();
       WS_STAMP(8);
       // ---------------------------------------------------------------- TD target, dQ, state write-back
+      // (dZ2's fragments -- W2^T tiles and the H2 mask -- are read first: their latency runs under TD)
+      const bf16_t* zchunk = reinterpret_cast<const bf16_t*>(ctl + 10);   // 8 zero bytes
+      s4v aw[8], h2m[8];
+      auto dz_reads = [&]() {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          aw[i] = lds_tr4(g4 == 0 ? W2p + (l16 >> 2) * HP + pi_pos4(i, l16 & 3) : zchunk);
+          h2m[i] = *reinterpret_cast<const s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4));
+        }
+      };
+      if (WS_DZ_EARLY) dz_reads();
       float dq = 0.f;
       int slot = 0;
       if (g4 == 0) {
@@ -610,16 +632,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // on the matrix cores: A = W2^T tiles (lanes g4 == 0 hold W2[0..3][u2], a transposed read of W2p's 4
       // rows), B = dQ^T (lanes g4 == 0 hold dQ[env][0..3], where TD left them); the result has the layout of
       // layer 2's accumulators.  dQ has one nonzero entry per env, so every output is one exact fp32 product.
-      const bf16_t* zchunk = reinterpret_cast<const bf16_t*>(ctl + 10);   // 8 zero bytes
       const s4v bq = g4 == 0 ? pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f, slot == 2 ? dq : 0.f, 0.f)
                              : zero_s4();
-      s4v aw[8], h2m[8], dz[8];
+      if (!WS_DZ_EARLY) dz_reads();
+      s4v dz[8];
       f4v zt[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        aw[i] = lds_tr4(g4 == 0 ? W2p + (l16 >> 2) * HP + pi_pos4(i, l16 & 3) : zchunk);
-        h2m[i] = *reinterpret_cast<const s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4));
-      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) zt[i] = mfma16(aw[i], bq, zero4());
 #pragma unroll

@@ -3,6 +3,7 @@
 // st_qstep_ws_launch_stamps, same contract.  Kept out of the production build: the stamp code costs the
 // 256-register kernel its last free registers (and with them the price prefetch's latency cover).
 #define WS_STAMPS 1
+#define WS_PD1 6   // (production reads 10 ahead; at 10 the stamp code spills)
 #define WS_NS ws_stamps
 #define WS_API(name) name##_stamps
 #include "qstep_ws.hip"

@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 3: dZ2 fragments read before TD, W2 fragments in layer 2's tail (A/B: dzlate, w2late)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_qstep_ws.py -x -q --timeout 120 --timeout-method thread \
+  > gpurun_out/r3v_ws.log 2>&1 || { echo WS_FAIL; tail -60 gpurun_out/r3v_ws.log; exit 1; }
+tail -1 gpurun_out/r3v_ws.log
+for rep in 1 2; do
+for v in "" dzlate w2late; do
+  extra="--step-kernel ws"; [ -n "$v" ] && extra="--step-kernel ws --step-variant $v"
+  timeout -k 10 150 python -u bench.py --steps 200 --warmup 10 --no-episode $extra > gpurun_out/r3v_bench_${v}_$rep.log 2>&1 \
+    || { echo BENCH_FAIL $v; tail -30 gpurun_out/r3v_bench_${v}_$rep.log; exit 1; }
+  echo "$v $rep: $(tail -1 gpurun_out/r3v_bench_${v}_$rep.log | cut -c100-200)"
+done
+done
