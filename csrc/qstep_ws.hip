@@ -444,6 +444,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         WS_PIN(u1); WS_PIN(u2);   // (else the draw sinks into the env-step branch)
         WS_SB();
       }
+      WS_STAMP(12);   // (sub-phase: layer 1's k-steps 0..5 done)
       s4v w06[8];   // the last k-step's A fragments: used again after the env step (x')
 #pragma unroll
       for (int i = 0; i < 8; ++i) {

@@ -183,6 +183,8 @@ def ws_stamps(a):
         tot += d
     for n, v in rows:
         lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
+    sub = float((s[:, 12] - s[:, 1]).mean())
+    lines.append(f"| (of layer 1: philox + k-steps 0..5, 96 MFMA 16x16x32) | {sub:.0f} | |")
     loop = float((s[1:, 0] - s[:-1, 0]).mean()) if nmy > 1 else tot
     lines.append(f"| tile loop (stamp0 -> stamp0) | {loop:.0f} | |")
     g = graw[(nmy + 1) * 16: (nmy + 1) * 16 + 8 * 4 * nmy].view(4 * nmy, 8).double()
