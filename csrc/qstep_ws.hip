@@ -57,6 +57,9 @@
 #ifndef WS_PD1
 #define WS_PD1 10       // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs
 #endif
+#ifndef WS_ENV_AT_L1
+#define WS_ENV_AT_L1 0  // 1 (qstep_ws_envl1.hip): the env-state prefetch issued at layer 1's start
+#endif
 #ifndef WS_W2_EARLY
 #define WS_W2_EARLY 1   // the output layers' W2 fragments read in layer 2's last read slots (0: qstep_ws_w2late.hip)
 #endif
@@ -402,7 +405,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_STAMP(1);
       // (after the features: a store or load issued before them would hold their window wait)
       WS_WRITE_BACK()
+#if WS_ENV_AT_L1
       WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+#endif
       // the epsilon-greedy draw (Philox, ~70 VALU with quarter-rate multiplies) depends only on (env, step):
       // issued here, the scheduler interleaves it with layer 1's MFMAs (VALU slots in the group pattern)
       float u1, u2;
@@ -470,6 +475,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         if (spin > SPIN_LIMIT) { ws_fail(p); break; }   // never expected: report, do not hang the GPU
       }
       WS_STAMP(3);
+#if !WS_ENV_AT_L1
+      // the env state of the tile after next: its 6 loads issued here, away from layer 1's MFMA stream
+      WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+#endif
       char* sb = smem + oSLOT + sl * SLOT_BYTES;
       bf16_t* sx = reinterpret_cast<bf16_t*>(sb + sX);
       bf16_t* sh1 = reinterpret_cast<bf16_t*>(sb + sH1);

@@ -13,3 +13,6 @@ for v in "" dzlate w2late; do
   echo "$v $rep: $(tail -1 gpurun_out/r3v_bench_${v}_$rep.log | cut -c100-200)"
 done
 done
+timeout -k 10 150 python -u tools/stamp_qstep.py --kernel ws --envs 1835008 --out gpurun_out/r3v_stamps_ws.md \
+  > gpurun_out/r3v_stamps.log 2>&1 || { echo STAMP_FAIL; tail -30 gpurun_out/r3v_stamps.log; exit 1; }
+cat gpurun_out/r3v_stamps_ws.md

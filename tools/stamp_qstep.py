@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="0 = engine default, 32 or 64")
     ap.add_argument("--variant", default="", help="tuning build suffix (st_qstep_wide_launch_<v>)")
     ap.add_argument("--waves", type=int, default=8, help="64-env-chunk kernel: 4 or 8 waves")
-    ap.add_argument("--kernel", default="auto", help="engine.step_kernel: auto | wide | narrow | pair")
+    ap.add_argument("--kernel", default="auto", help="engine.step_kernel: auto | wide | narrow | pair | ws")
+    ap.add_argument("--ws-dvariant", default="", help="ws: data-wave stamps build suffix ('' = stamps, gskipst)")
     a = ap.parse_args()
     if a.kernel == "pair":
         return pair_stamps(a)
@@ -166,7 +167,7 @@ def ws_stamps(a):
         assert int(eng.kernel_err.sum()) == 0
         return st.cpu()
 
-    raw = stamped("")
+    raw = stamped(a.ws_dvariant)
     graw = stamped("gstamps")
     s = raw[: nmy * 16].view(nmy, 16).double()
     names = ["features", "layer 1 of Q(x) + Q(x') window (56 + 48 MFMA) + Philox draw", "slot wait (own slot freed)",
@@ -174,7 +175,7 @@ def ws_stamps(a):
              "epsilon-greedy + env step", "Q(x'): layer-1 tail, layer 2, output (8 + 32 + 4 MFMA) + next prices issued",
              "TD + state write-back", "dZ2 (8 MFMA 16x16x16 + packed mask)", "dZ2, dQ -> slot, publish"]
     lines = [f"# ws step kernel: data wave 0 of workgroup 0 ({a.envs} envs, grid {eng.grid}, {nmy} tiles per data "
-             f"wave; s_memtime ticks)\n", "| phase | ticks/tile | % |", "|---|---|---|"]
+             f"wave; s_memtime ticks; build {a.ws_dvariant or 'stamps'})\n", "| phase | ticks/tile | % |", "|---|---|---|"]
     tot = 0.0
     rows = []
     for ph in range(11):
