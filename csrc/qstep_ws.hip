@@ -58,7 +58,7 @@
 #define WS_PD1 10       // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs
 #endif
 #ifndef WS_ENV_AT_L1
-#define WS_ENV_AT_L1 0  // 1 (qstep_ws_envl1.hip): the env-state prefetch issued at layer 1's start
+#define WS_ENV_AT_L1 1  // the env-state prefetch issued at layer 1's start (0: after the slot claim, qstep_ws_envslot.hip)
 #endif
 #ifndef WS_W2_EARLY
 #define WS_W2_EARLY 1   // the output layers' W2 fragments read in layer 2's last read slots (0: qstep_ws_w2late.hip)
@@ -74,6 +74,12 @@
 #endif
 #ifndef WS_NOPHIL
 #define WS_NOPHIL 0     // timing build qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
+#endif
+#ifndef WS_GPAIR
+#define WS_GPAIR 1      // gradient waves take ring slots in pairs: K = 32 MFMAs (0: one slot, K = 16; qstep_ws_gsingle.hip)
+#endif
+#ifndef WS_GXP
+#define WS_GXP 1        // paired slots: X fragment pairs read this many dW0 steps ahead (2 spills 1 VGPR)
 #endif
 #ifndef WS_GZ
 #define WS_GZ 1         // gradient waves: dZ1 fragments read this many k-steps ahead
@@ -704,6 +710,130 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     // (held in SGPRs and stored once per slot: the gradient wave has no VGPR to spare mid-slot)
     unsigned long long gts[7] = {0, 0, 0, 0, 0, 0, 0};
 #define WS_GST(I) if ((WS_STAMPS & 2) && ((WS_GST_MASK >> (I)) & 1)) gts[I] = __builtin_amdgcn_s_memtime(); WS_MARK(G, I)
+#if WS_GPAIR
+    // slots in pairs (q, q + 1): the weight-gradient MFMAs run with K = 32 envs -- v_mfma_f32_16x16x32_bf16
+    // at the cost of the K = 16 form for twice the work.  K index 8 g4 + j of lane group g4 is env
+    // 4 g4 + (j & 3) of slot q (j < 4) or of slot q + 1 (j >= 4): the A and B fragments are the two slots'
+    // 4-element fragments side by side (cat8), no data moves between lanes.  dZ1 stays per slot (K = u2);
+    // its W1^T fragments are read once for both.
+    s8v ones8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones8[j] = (l16 == 0) ? (short)0x3F80 : (short)0;
+    for (int q = 0; q < nseq; q += 2) {
+      const int sa = q % NSLOT, sb = (q + 1) % NSLOT;
+      WS_GST(0);
+      for (int spin = 0; lds_acq(ctl + 1 + sa) != q + 1; ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > SPIN_LIMIT) { ws_fail(p); break; }
+      }
+      for (int spin = 0; lds_acq(ctl + 1 + sb) != q + 2; ++spin) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spin > SPIN_LIMIT) { ws_fail(p); break; }
+      }
+      WS_GST(1);
+#if WS_GSKIP
+      if (lane == 0) {
+        __hip_atomic_fetch_add(ctl + 5 + sa, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(ctl + 5 + sb, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      continue;
+#endif
+      const char* pa_ = smem + oSLOT + sa * SLOT_BYTES;
+      const char* pb_ = smem + oSLOT + sb * SLOT_BYTES;
+      const bf16_t *xa = reinterpret_cast<const bf16_t*>(pa_ + sX), *xb = reinterpret_cast<const bf16_t*>(pb_ + sX);
+      const bf16_t *h1a = reinterpret_cast<const bf16_t*>(pa_ + sH1), *h1b = reinterpret_cast<const bf16_t*>(pb_ + sH1);
+      const bf16_t *h2a = reinterpret_cast<const bf16_t*>(pa_ + sH2), *h2b = reinterpret_cast<const bf16_t*>(pb_ + sH2);
+      const bf16_t *z2a = reinterpret_cast<const bf16_t*>(pa_ + sDZ2), *z2b = reinterpret_cast<const bf16_t*>(pb_ + sDZ2);
+      // both slots' tr4 fragments at one offset, side by side: K = 32 envs
+      auto tr8 = [&](const bf16_t* a, const bf16_t* b, int off) { return cat8(lds_tr4(a + off), lds_tr4(b + off)); };
+      // ---- dZ1 of both slots for this wave's u1 tiles (result lane (u1, g4): envs 4 g4 .. 4 g4 + 3)
+      f4v c1a[2] = {zero4(), zero4()}, c1b[2] = {zero4(), zero4()};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const s8v aza = lds_ld8(z2a + w1_off(l16, 32 * ks + 8 * g4));
+        const s8v azb = lds_ld8(z2b + w1_off(l16, 32 * ks + 8 * g4));
+        const int R = 32 * ks + 4 * g4 + (l16 >> 2);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int col = pi_pos4(2 * gw + t, qq);
+          const s8v wt = cat8(lds_tr4(W1p + w1_off(R, col)), lds_tr4(W1p + w1_off(R + 16, col)));
+          c1a[t] = mfma32(aza, wt, c1a[t]);
+          c1b[t] = mfma32(azb, wt, c1b[t]);
+        }
+      }
+      s4v bowna[2], bownb[2];   // own H1 tiles of both slots (the dZ1 mask)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        bowna[t] = lds_tr4(h1a + a_off(r4, 16 * (2 * gw + t) + 4 * qq));
+        bownb[t] = lds_tr4(h1b + a_off(r4, 16 * (2 * gw + t) + 4 * qq));
+      }
+      constexpr int XD = WS_GXP;   // X fragment pairs read ahead of the dW0 MFMAs
+      s8v bx[13];
+#pragma unroll
+      for (int n = 0; n < XD; ++n) bx[n] = tr8(xa, xb, r4 * KX + 16 * n + 4 * qq);
+      WS_PIN(c1a[1]); WS_PIN(c1b[1]);
+      WS_SB();
+      WS_GST(2);
+      s8v a0[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a0[t] = cat8(mask_pk(c1a[t], bowna[t]), mask_pk(c1b[t], bownb[t]));
+      WS_PIN(a0[1]);
+      WS_SB();
+      WS_GST(3);
+      // ---- dW0^T[u1][slot col] += dZ1^T . X (K = 32 envs)
+#pragma unroll
+      for (int n = 0; n < 13; ++n) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma32(a0[m], bx[n], gW0[m][n]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (n + XD < 13) {
+          bx[n + XD] = tr8(xa, xb, r4 * KX + 16 * (n + XD) + 4 * qq);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+      }
+      WS_PIN(gW0[1][12]);
+      WS_SB();
+      WS_GST(4);
+      // ---- dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
+      //      (H1 fragments in two halves; both slots go back once the last fragment has landed)
+      s8v a1[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) a1[m] = tr8(z2a, z2b, w1_off(r4, pi_pos4(2 * gw + m, qq)));
+#pragma unroll
+      for (int m = 0; m < 2; ++m) gB1[m] = mfma32(a1[m], ones8, gB1[m]);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        s8v bh[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bh[k] = tr8(h1a, h1b, a_off(r4, 16 * (4 * half + k) + 4 * qq));
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) gW1[m][4 * half + k] = mfma32(a1[m], bh[k], gW1[m][4 * half + k]);
+      }
+      {
+        const s8v aq = qq == 0 ? tr8(xa, xb, r4 * KX + 204) : cat8(lds_tr4(zchunk), lds_tr4(zchunk));   // a = l16 < 4
+        s8v bh2[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
+        if (lane == 0) {
+          __hip_atomic_fetch_add(ctl + 5 + sa, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(ctl + 5 + sb, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        WS_GST(5);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) gW2[n] = mfma32(aq, bh2[n], gW2[n]);
+        gB2 = mfma32(aq, ones8, gB2);
+      }
+      WS_PIN(gW1[1][7]); WS_PIN(gB2);
+      WS_SB();
+      WS_GST(6);
+      if ((WS_STAMPS & 2) && gst) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) gst[8 * q + i] = gts[i];
+      }
+    }
+#else
     for (int q = 0; q < nseq; ++q) {
       const int sl = q % NSLOT;
       WS_GST(0);
@@ -862,6 +992,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         for (int i = 0; i < 7; ++i) gst[8 * q + i] = gts[i];
       }
     }
+#endif
     __syncthreads();
     // ------------------------------------------------------------------ gradient slab write-out
     // this wave's rows: dW0^T / dW1^T rows 32 gw + 16 m + 4 g4 + j; dW2^T u2 columns 16 (2 gw + n) + l16

@@ -189,10 +189,11 @@ def ws_stamps(a):
     loop = float((s[1:, 0] - s[:-1, 0]).mean()) if nmy > 1 else tot
     lines.append(f"| tile loop (stamp0 -> stamp0) | {loop:.0f} | |")
     g = graw[(nmy + 1) * 16: (nmy + 1) * 16 + 8 * 4 * nmy].view(4 * nmy, 8).double()
-    gn = ["wait for the next full slot", "dZ1 for own u1 tiles (8 MFMA 16x16x32, 20 reads one k-step ahead) + "
-          "own H1 tiles / first X fragments issued", "dZ1 mask", "dW0 (26 MFMA 16x16x16, X 3 steps ahead) + "
-          "dW1 / dW2 fragments issued", "release", "dW1, db1, dW2, db2 (21 MFMA)"]
-    lines += ["", "| gradient wave 0, per ring slot (separate build) | ticks | % |", "|---|---|---|"]
+    g = g[g[:, 6] > 0]   # paired slots: one row per pair
+    gn = ["wait for the next two full slots", "dZ1 of both slots (16 MFMA 16x16x32, W1^T read once) + "
+          "own H1 tiles / first X fragments issued", "dZ1 mask", "dW0 (26 MFMA 16x16x32, K = 32 envs)",
+          "dW1, db1 (18 MFMA 16x16x32) + dW2 fragments, release", "dW2, db2 (3 MFMA 16x16x32)"]
+    lines += ["", "| gradient wave 0, per PAIR of ring slots (separate build) | ticks | % |", "|---|---|---|"]
     gt = float((g[:, 6] - g[:, 0]).mean())
     for i, n in enumerate(gn):
         d = float((g[:, i + 1] - g[:, i]).mean())
