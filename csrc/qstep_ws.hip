@@ -79,7 +79,13 @@
 #define WS_GPAIR 1      // gradient waves take ring slots in pairs: K = 32 MFMAs (0: one slot, K = 16; qstep_ws_gsingle.hip)
 #endif
 #ifndef WS_GXP
-#define WS_GXP 1        // paired slots: X fragment pairs read this many dW0 steps ahead (2 spills 1 VGPR)
+#define WS_GXP 2        // paired slots: X fragment pairs read this many dW0 steps ahead
+#endif
+#ifndef WS_GDZ
+#define WS_GDZ 1        // the gradient waves form dZ2 from dQ + H2 (0: the data waves do, qstep_ws_ddz.hip)
+#endif
+#if WS_GDZ && !WS_GPAIR
+#error "WS_GDZ needs the paired-slot gradient waves"
 #endif
 #ifndef WS_GZ
 #define WS_GZ 1         // gradient waves: dZ1 fragments read this many k-steps ahead
@@ -508,6 +514,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         *reinterpret_cast<s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
+#if WS_GDZ
+      // H2 again in pi order (the DZ2 area's layout): the gradient waves' dZ2 mask, one 16-byte read per k-step
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) *reinterpret_cast<s8v*>(sz2 + w1_off(l16, 32 * ks + 8 * g4)) = H2[ks];
+#endif
       WS_PIN(H2[3]);
 #if WS_PF_POS == 1 && !WS_NOPF
       // the next tile's price windows: their registers are free from here (the peak of Q(x')'s layer 2 is
@@ -592,6 +603,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       const bf16_t* zchunk = reinterpret_cast<const bf16_t*>(ctl + 10);   // 8 zero bytes
       s4v aw[8], h2m[8];
       auto dz_reads = [&]() {
+        if (WS_GDZ) return;   // (the gradient waves form dZ2)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           aw[i] = lds_tr4(g4 == 0 ? W2p + (l16 >> 2) * HP + pi_pos4(i, l16 & 3) : zchunk);
@@ -650,6 +662,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // layer 2's accumulators.  dQ has one nonzero entry per env, so every output is one exact fp32 product.
       const s4v bq = g4 == 0 ? pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f, slot == 2 ? dq : 0.f, 0.f)
                              : zero_s4();
+#if !WS_GDZ
       if (!WS_DZ_EARLY) dz_reads();
       s4v dz[8];
       f4v zt[8];
@@ -658,12 +671,15 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) dz[i] = mask_pk(zt[i], h2m[i]);
       WS_PIN(dz[7]);
+#endif
       WS_SB();
       WS_STAMP(10);
-      // publish: dZ2 (pi order: tiles 2 ks, 2 ks + 1 form k-step ks), dQ in the X row's pad slots
+      // publish: (WS_GDZ 0: dZ2, pi order: tiles 2 ks, 2 ks + 1 form k-step ks) dQ in the X row's pad slots
+#if !WS_GDZ
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
         *reinterpret_cast<s8v*>(sz2 + w1_off(l16, 32 * ks + 8 * g4)) = cat8(dz[2 * ks], dz[2 * ks + 1]);
+#endif
       if (g4 == 0) *reinterpret_cast<s4v*>(sx + l16 * KX + 204) = bq;
       if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       WS_SB();
@@ -687,14 +703,29 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     // ================================================================ GRADIENT WAVE
     const int gw = wave - ND;
     if (WS_GPRIO) __builtin_amdgcn_s_setprio(WS_GPRIO);   // owns hidden units 32 gw .. 32 gw + 31 of both layers, dW2 columns likewise
-    f4v gW0[2][13], gW1[2][8], gB1[2], gW2[2], gB2 = zero4();
+    f4v gW0[2][13], gW1[2][8], gW2[2];
+#if WS_GPAIR
+    // bias gradients as per-lane fp32 sums of the dZ2^T / dQ^T fragments (each lane's 8 envs per slot
+    // pair), folded over the 4 lane groups at the write-out: 3 VGPRs instead of 12 + a ones operand
+    float gB1s[2] = {0.f, 0.f}, gB2s = 0.f;
+    auto sum8 = [](const s8v& v) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += bf2f((bf16_t)v[j]);
+      return acc;
+    };
+#else
+    f4v gB1[2], gB2 = zero4();
+#endif
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
 #pragma unroll
       for (int n = 0; n < 13; ++n) gW0[m][n] = zero4();
 #pragma unroll
       for (int n = 0; n < 8; ++n) gW1[m][n] = zero4();
+#if !WS_GPAIR
       gB1[m] = zero4();
+#endif
       gW2[m] = zero4();
     }
     s4v ones;
@@ -716,9 +747,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     // 4 g4 + (j & 3) of slot q (j < 4) or of slot q + 1 (j >= 4): the A and B fragments are the two slots'
     // 4-element fragments side by side (cat8), no data moves between lanes.  dZ1 stays per slot (K = u2);
     // its W1^T fragments are read once for both.
-    s8v ones8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ones8[j] = (l16 == 0) ? (short)0x3F80 : (short)0;
     for (int q = 0; q < nseq; q += 2) {
       const int sa = q % NSLOT, sb = (q + 1) % NSLOT;
       WS_GST(0);
@@ -748,10 +776,32 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto tr8 = [&](const bf16_t* a, const bf16_t* b, int off) { return cat8(lds_tr4(a + off), lds_tr4(b + off)); };
       // ---- dZ1 of both slots for this wave's u1 tiles (result lane (u1, g4): envs 4 g4 .. 4 g4 + 3)
       f4v c1a[2] = {zero4(), zero4()}, c1b[2] = {zero4(), zero4()};
+#if WS_GDZ
+      // dZ2 = (W2^T dQ) * [H2 > 0] formed here from the slot's dQ (the X rows' pad slots) and H2: A = W2^T
+      // tiles (lanes g4 == 0 hold W2[0..3][u2]), B = dQ^T (lanes g4 == 0 hold dQ[env][0..3]); the result
+      // tiles 2 ks, 2 ks + 1 side by side are dZ1's A operand for k-step ks (pi order), one exact fp32
+      // product per output as in the data wave's version
+      const s4v bqa = lds_ld4(g4 == 0 ? xa + l16 * KX + 204 : zchunk);
+      const s4v bqb = lds_ld4(g4 == 0 ? xb + l16 * KX + 204 : zchunk);
+      // (one address register for all W2^T reads: the other lane groups read zero row 4 at the same offsets;
+      //  the mask is H2 in pi order, which the data wave writes into the slot's DZ2 area for this)
+      const bf16_t* w2base = W2p + (g4 == 0 ? (l16 >> 2) * HP + 8 * (l16 & 3) : 4 * HP);
+      auto w2t = [&](int i) { return lds_tr4(w2base + 32 * (i >> 1) + 4 * (i & 1)); };
+      auto dzks = [&](const bf16_t* h2p, const s4v& bq, const s4v& aw0, const s4v& aw1, int ks) {
+        const s8v m = lds_ld8(h2p + w1_off(l16, 32 * ks + 8 * g4));
+        return cat8(mask_pk(mfma16(aw0, bq, zero4()), lo4(m)), mask_pk(mfma16(aw1, bq, zero4()), hi4(m)));
+      };
+#endif
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
+#if WS_GDZ
+        const s4v aw0 = w2t(2 * ks), aw1 = w2t(2 * ks + 1);
+        const s8v aza = dzks(z2a, bqa, aw0, aw1, ks);
+        const s8v azb = dzks(z2b, bqb, aw0, aw1, ks);
+#else
         const s8v aza = lds_ld8(z2a + w1_off(l16, 32 * ks + 8 * g4));
         const s8v azb = lds_ld8(z2b + w1_off(l16, 32 * ks + 8 * g4));
+#endif
         const int R = 32 * ks + 4 * g4 + (l16 >> 2);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -760,6 +810,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
           c1a[t] = mfma32(aza, wt, c1a[t]);
           c1b[t] = mfma32(azb, wt, c1b[t]);
         }
+        if (WS_GDZ) WS_SB();   // (one k-step's fragments live at a time)
       }
       s4v bowna[2], bownb[2];   // own H1 tiles of both slots (the dZ1 mask)
 #pragma unroll
@@ -769,8 +820,75 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       constexpr int XD = WS_GXP;   // X fragment pairs read ahead of the dW0 MFMAs
       s8v bx[13];
+#if !WS_GDZ
 #pragma unroll
       for (int n = 0; n < XD; ++n) bx[n] = tr8(xa, xb, r4 * KX + 16 * n + 4 * qq);
+#endif
+#if WS_GDZ
+      // order: mask -> dW2 / db2, dW1 / db1 (their fragments live with a0 only) -> dW0 with the X reads ->
+      // both slots go back
+      WS_PIN(c1a[1]); WS_PIN(c1b[1]);
+      WS_SB();
+      WS_GST(2);
+      s8v a0[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a0[t] = cat8(mask_pk(c1a[t], bowna[t]), mask_pk(c1b[t], bownb[t]));
+      WS_PIN(a0[1]);
+      WS_SB();
+      WS_GST(3);
+      s8v a1[2];
+      {
+        // dZ2^T tiles of this wave's u2 (the dW1 A operand, lane (u2, g4): envs 4 g4 ..): A = dQ (the same
+        // registers as dZ2's B), B = W2 (the same registers as dZ2's A), masked by H2 read transposed
+        s8v bh2[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const s4v aw = w2t(2 * gw + m);
+          a1[m] = cat8(mask_pk(mfma16(bqa, aw, zero4()), lo4(bh2[m])), mask_pk(mfma16(bqb, aw, zero4()), hi4(bh2[m])));
+        }
+        const s8v aq = qq == 0 ? tr8(xa, xb, r4 * KX + 204) : cat8(lds_tr4(zchunk), lds_tr4(zchunk));   // a = l16 < 4
+#pragma unroll
+        for (int n = 0; n < 2; ++n) gW2[n] = mfma32(aq, bh2[n], gW2[n]);
+        gB2s += sum8(aq);
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) gB1s[m] += sum8(a1[m]);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        s8v bh[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bh[k] = tr8(h1a, h1b, a_off(r4, 16 * (4 * half + k) + 4 * qq));
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) gW1[m][4 * half + k] = mfma32(a1[m], bh[k], gW1[m][4 * half + k]);
+      }
+      WS_SB();
+      WS_GST(4);
+      // ---- dW0^T[u1][slot col] += dZ1^T . X (K = 32 envs)
+#pragma unroll
+      for (int n = 0; n < XD; ++n) bx[n] = tr8(xa, xb, r4 * KX + 16 * n + 4 * qq);
+#pragma unroll
+      for (int n = 0; n < 13; ++n) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma32(a0[m], bx[n], gW0[m][n]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (n + XD < 13) {
+          bx[n + XD] = tr8(xa, xb, r4 * KX + 16 * (n + XD) + 4 * qq);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        if (n + XD == 12) {   // the last X fragment is in flight: nothing else of the slots is read
+          if (lane == 0) {
+            __hip_atomic_fetch_add(ctl + 5 + sa, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(ctl + 5 + sb, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          WS_GST(5);
+        }
+      }
+      WS_PIN(gW0[1][12]);
+#else
       WS_PIN(c1a[1]); WS_PIN(c1b[1]);
       WS_SB();
       WS_GST(2);
@@ -797,10 +915,28 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---- dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
       //      (H1 fragments in two halves; both slots go back once the last fragment has landed)
       s8v a1[2];
+#if WS_GDZ
+      // dZ2^T tiles of this wave's u2 (the dW1 A operand, lane (u2, g4): envs 4 g4 ..): A = dQ (the same
+      // registers as dZ2's B), B = W2 (the same registers as dZ2's A), masked by H2 read transposed
+      s8v bh2[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
+      {
+        // (dQ re-read: holding it through dW0 costs the registers of an accumulator tile)
+        const s4v bqa2 = lds_ld4(g4 == 0 ? xa + l16 * KX + 204 : zchunk);
+        const s4v bqb2 = lds_ld4(g4 == 0 ? xb + l16 * KX + 204 : zchunk);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const s4v aw = w2t(2 * gw + m);
+          a1[m] = cat8(mask_pk(mfma16(bqa2, aw, zero4()), lo4(bh2[m])), mask_pk(mfma16(bqb2, aw, zero4()), hi4(bh2[m])));
+        }
+      }
+#else
 #pragma unroll
       for (int m = 0; m < 2; ++m) a1[m] = tr8(z2a, z2b, w1_off(r4, pi_pos4(2 * gw + m, qq)));
+#endif
 #pragma unroll
-      for (int m = 0; m < 2; ++m) gB1[m] = mfma32(a1[m], ones8, gB1[m]);
+      for (int m = 0; m < 2; ++m) gB1s[m] += sum8(a1[m]);
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         s8v bh[4];
@@ -813,9 +949,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       {
         const s8v aq = qq == 0 ? tr8(xa, xb, r4 * KX + 204) : cat8(lds_tr4(zchunk), lds_tr4(zchunk));   // a = l16 < 4
+#if !WS_GDZ
         s8v bh2[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
+#endif
         if (lane == 0) {
           __hip_atomic_fetch_add(ctl + 5 + sa, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_fetch_add(ctl + 5 + sb, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -823,9 +961,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         WS_GST(5);
 #pragma unroll
         for (int n = 0; n < 2; ++n) gW2[n] = mfma32(aq, bh2[n], gW2[n]);
-        gB2 = mfma32(aq, ones8, gB2);
+        gB2s += sum8(aq);
       }
-      WS_PIN(gW1[1][7]); WS_PIN(gB2);
+#endif
+      WS_PIN(gW1[1][7]); WS_PIN(gB2s);
       WS_SB();
       WS_GST(6);
       if ((WS_STAMPS & 2) && gst) {
@@ -1013,15 +1152,35 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         for (int n = 0; n < 13; ++n) put(p.off_w0 + u * INP + slot_col(16 * n + l16), gW0[m][n][j]);
 #pragma unroll
         for (int n = 0; n < 8; ++n) put(p.off_w1 + u * HP + 16 * n + l16, gW1[m][n][j]);
+#if !WS_GPAIR
         if (l16 == 0) put(p.off_b1 + u, gB1[m][j]);
+#endif
       }
+#if WS_GPAIR
+    // bias gradients: fold the 4 lane groups' partial sums (lane (l16, g4): 8 envs of each slot pair)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      float v = gB1s[m];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g4 == 0) put(p.off_b1 + 32 * gw + 16 * m + l16, v);
+    }
+    {
+      float v = gB2s;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (gw == 0 && g4 == 0 && l16 < 4) put(p.off_b2 + l16, v);
+    }
+#endif
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int j = 0; j < 4; ++j) put(p.off_w2 + (4 * g4 + j) * HP + 16 * (2 * gw + n) + l16, gW2[n][j]);
+#if !WS_GPAIR
     if (gw == 0 && l16 == 0)
 #pragma unroll
       for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
+#endif
   }
 #undef WS_SB
 #undef WS_PIN
