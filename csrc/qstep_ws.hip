@@ -82,7 +82,8 @@
 #define WS_GXP 2        // paired slots: X fragment pairs read this many dW0 steps ahead
 #endif
 #ifndef WS_GDZ
-#define WS_GDZ 1        // the gradient waves form dZ2 from dQ + H2 (0: the data waves do, qstep_ws_ddz.hip)
+#define WS_GDZ 0        // 1: the gradient waves form dZ2 from dQ + a pi-order H2 copy (qstep_ws_gdz.hip: they
+                        // become the bottleneck, 13 % slower; profiles/r3_ws_ab.md)
 #endif
 #if WS_GDZ && !WS_GPAIR
 #error "WS_GDZ needs the paired-slot gradient waves"
