@@ -190,9 +190,9 @@ def ws_stamps(a):
     lines.append(f"| tile loop (stamp0 -> stamp0) | {loop:.0f} | |")
     g = graw[(nmy + 1) * 16: (nmy + 1) * 16 + 8 * 4 * nmy].view(4 * nmy, 8).double()
     g = g[g[:, 6] > 0]   # paired slots: one row per pair
-    gn = ["wait for the next two full slots", "dZ2 formed (16 MFMA 16x16x16) + dZ1 of both slots (16 MFMA "
-          "16x16x32, W1^T read once)", "dZ1 mask", "dZ2^T own tiles (4 MFMA 16x16x16), dW2 (2), dW1 (16 MFMA "
-          "16x16x32), bias sums", "dW0 up to the last X read (K = 32 envs), release", "dW0 tail"]
+    gn = ["wait for the next two full slots", "dZ1 of both slots (16 MFMA 16x16x32, W1^T read once) + "
+          "own H1 tiles / first X fragments issued", "dZ1 mask", "dW0 (26 MFMA 16x16x32, K = 32 envs)",
+          "dW1 (16 MFMA 16x16x32), bias sums, dW2 fragments, release", "dW2 (2 MFMA 16x16x32)"]
     lines += ["", "| gradient wave 0, per PAIR of ring slots (separate build) | ticks | % |", "|---|---|---|"]
     gt = float((g[:, 6] - g[:, 0]).mean())
     for i, n in enumerate(gn):
