@@ -97,6 +97,15 @@
 #ifndef WS_GH
 #define WS_GH 12        // gradient waves: the dW1 / dW2 fragments issued after this dW0 step
 #endif
+#ifndef WS_FMA_FEAT
+#define WS_FMA_FEAT 1   // window features w / last - 1 as one fma per value, one rounding (0: multiply then subtract,
+#endif                  // two roundings as qstep_wide.hip; qstep_ws_fsub.hip, 1.2 % slower; profiles/r3_ws_ab.md)
+#ifndef WS_WBE
+#define WS_WBE 1        // the env-state write-back issued right after the env step, before Q(x') and the next tile's
+#endif                  // window loads (0: at TD, qstep_ws_wbtd.hip, 0.5 % slower; profiles/r3_ws_ab.md)
+#ifndef WS_NOWB
+#define WS_NOWB 0       // timing build qstep_ws_nowb.hip: no env-state write-back (wrong results)
+#endif
 #ifndef WS_NOPF
 #define WS_NOPF 0       // timing build qstep_ws_nopf.hip: no price prefetch in the loop (stale windows)
 #endif
@@ -366,11 +375,27 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     float w_b = 0.f, w_v = 0.f, w_rs = 0.f, w_fin = 0.f, w_rew = 0.f;
     bool w_done = false;
 #define WS_WRITE_BACK()                                                                           \
-  if (g4 == 0 && w_e >= 0) {                                                                     \
+  if (!WS_NOWB && g4 == 0 && w_e >= 0) {                                                         \
     ENV_F(ER_BUDGET, w_e) = w_b; ENV_I(ER_SHARES, w_e) = w_s; ENV_F(ER_VALUE, w_e) = w_v;        \
     ENV_I(ER_POS, w_e) = w_pos; ENV_F(ER_RET_SUM, w_e) = w_rs;                                   \
     ENV_I(ER_ACTION, w_e) = w_act; ENV_F(ER_REWARD, w_e) = w_rew;                                \
     if (w_done) { ENV_F(ER_LAST_FINAL, w_e) = w_fin; ENV_I(ER_EPISODES, w_e) = w_ep; }           \
+  }
+    // the env's next state from this tile's env step (pos, bud0 ... of the tile; act, rew, b2, s2 of its step),
+    // then the write-back unless it is deferred to the next tile
+#define WS_WB_SET()                                                                               \
+  {                                                                                              \
+    const int np_ = pos + 1;                                                                     \
+    w_e = e; w_act = act; w_rew = rew;                                                           \
+    w_done = np_ >= p.T - HWIN;                                                                  \
+    w_ep = w_done ? ep0 + 1 : ep0;                                                               \
+    if (w_done) {                                                                                \
+      w_fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));                                         \
+      w_b = p.b0; w_s = p.s0; w_v = 0.f; w_pos = 0; w_rs = 0.f;                                  \
+    } else {                                                                                     \
+      w_b = b2; w_s = s2; w_v = vnew; w_pos = np_; w_rs = rs0 + rew;                             \
+    }                                                                                            \
+    if (!WS_WB_DEFER) { WS_WRITE_BACK() w_e = -1; }                                              \
   }
 
     for (int k = 0; k < nmy; ++k) {
@@ -384,8 +409,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         inv = __fdiv_rn(1.0f, last);
         invn = __fdiv_rn(1.0f, vnew);
       }
-      auto fx = [&](float w) { return FEAT ? __fsub_rn(__fmul_rn(w, inv), 1.0f) : w; };
-      auto fxn = [&](float w) { return FEAT ? __fsub_rn(__fmul_rn(w, invn), 1.0f) : w; };
+      auto fx = [&](float w) {
+        return FEAT ? (WS_FMA_FEAT ? __fmaf_rn(w, inv, -1.0f) : __fsub_rn(__fmul_rn(w, inv), 1.0f)) : w;
+      };
+      auto fxn = [&](float w) {
+        return FEAT ? (WS_FMA_FEAT ? __fmaf_rn(w, invn, -1.0f) : __fsub_rn(__fmul_rn(w, invn), 1.0f)) : w;
+      };
       s8v X[6], Xn[6];
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
@@ -570,6 +599,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fxn(vnew));
         st_explore += exploit ? 0.f : 1.f;
       }
+#if WS_WBE
+      WS_WB_SET()
+#endif
       WS_PIN(Xn6);
       WS_SB();
       WS_STAMP(7);
@@ -627,26 +659,13 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         const float diff = __fsub_rn(qs, y);
         dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
         if (p.output_relu && !(qs > 0.f)) dq = 0.f;
-        const int np = pos + 1;
-        const float rs = rs0 + rew;
         float fdone = 0.f, ndone = 0.f;
-        w_e = e;
-        w_act = act;
-        w_rew = rew;
-        w_done = np >= p.T - HWIN;
-        if (w_done) {
-          const float fin = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
-          w_fin = fin;
-          w_ep = ep0 + 1;
-          w_b = p.b0; w_s = p.s0; w_v = 0.f; w_pos = 0; w_rs = 0.f;
-          fdone = fin;
+        if (pos + 1 >= p.T - HWIN) {
+          fdone = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
           ndone = 1.f;
-        } else {
-          w_b = b2; w_s = s2; w_v = vnew; w_pos = np; w_rs = rs;
         }
-#if !WS_WB_DEFER
-        WS_WRITE_BACK()
-        w_e = -1;
+#if !WS_WBE
+        WS_WB_SET()
 #endif
         st_reward += rew;
         st_loss += diff * diff;
@@ -688,6 +707,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     }
     WS_WRITE_BACK()   // the last tile's
 #undef WS_WRITE_BACK
+#undef WS_WB_SET
 #undef WS_LOAD_ENV
 #undef WS_LOAD_PRICES
 #undef WS_STAMP

@@ -7,6 +7,8 @@ MFMAs differs); with the kernel's actions forced into the oracle, env transition
 exactly and the gradient within a relative-norm tolerance.  Small ``engine.grid`` values make every
 workgroup run many tiles, so the LDS ring of the kernel wraps around many times.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,8 @@ def _cfg(compat=False):
 
     cfg = preset_config("flagship")
     cfg.engine.step_kernel = "ws"
+    # a tuning build of the same kernel (csrc/qstep_ws_<v>.hip) under the same checks, for A/B candidates
+    cfg.engine.step_variant = os.environ.get("SHARETRADE_WS_VARIANT", "")
     if compat:
         cfg.env.compat_decisions = True
         cfg.agent.target_slot = "compat"
@@ -135,6 +139,8 @@ def test_ws_and_wide_agree_over_steps(native_built):
     for kern in ("wide", "ws"):
         cfg = _cfg()
         cfg.engine.step_kernel = kern
+        if kern != "ws":
+            cfg.engine.step_variant = ""
         cfg.agent.epsilon = 0.0          # every action a uniform draw: identical trajectories
         eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
         assert eng.step_kernel == kern
