@@ -103,6 +103,9 @@
 #ifndef WS_WBE
 #define WS_WBE 1        // the env-state write-back issued right after the env step, before Q(x') and the next tile's
 #endif                  // window loads (0: at TD, qstep_ws_wbtd.hip, 0.5 % slower; profiles/r3_ws_ab.md)
+#ifndef WS_L2PRE
+#define WS_L2PRE 4      // Q(x)'s first n layer-2 W1 fragments read before the slot claim: their LDS latency runs
+#endif                  // under the slot wait and the slot stores (0: qstep_ws_l2pre0.hip; 6: _l2pre6.hip)
 #ifndef WS_NOWB
 #define WS_NOWB 0       // timing build qstep_ws_nowb.hip: no env-state write-back (wrong results)
 #endif
@@ -232,12 +235,22 @@ ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
 
 // acc[i] += W1 (rows 16 i .. 16 i + 15, pi-ordered columns) . H (B operands of 4 k-steps), 32 MFMAs with
 // the W1 fragment of pair j + PD2 read while pair j issues (j = 8 ks + i)
-ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc, const bf16_t* w2row, s8v* w2f) {
-  constexpr int PD2 = 8, NB2 = PD2 + 1;
+// (pre: the first PD2 fragments were read by layer2_pre, earlier in the chain -- their LDS latency off it)
+constexpr int PD2 = 8, NB2 = PD2 + 1;
+template <int NPRE>
+ST_DEV void layer2_pre(const bf16_t* W1p, int l16, int g4, s8v* A) {
+#pragma unroll
+  for (int j = 0; j < NPRE; ++j) A[j] = lds_ld8(W1p + w1_off(16 * (j & 7) + l16, 32 * (j >> 3) + 8 * g4));
+}
+template <int NPRE = 0>
+ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc, const bf16_t* w2row, s8v* w2f,
+                   const s8v* Apre = nullptr) {
   s8v A[NB2];
 #pragma unroll
-  for (int j = 0; j < PD2; ++j) A[j] = lds_ld8(W1p + w1_off(16 * (j & 7) + l16, 32 * (j >> 3) + 8 * g4));
-  __builtin_amdgcn_sched_group_barrier(0x100, PD2, 0);
+  for (int j = 0; j < NPRE; ++j) A[j] = Apre[j];
+#pragma unroll
+  for (int j = NPRE; j < PD2; ++j) A[j] = lds_ld8(W1p + w1_off(16 * (j & 7) + l16, 32 * (j >> 3) + 8 * g4));
+  if (NPRE < PD2) __builtin_amdgcn_sched_group_barrier(0x100, PD2 - NPRE, 0);
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     acc[j & 7] = mfma32(A[j % NB2], H[j >> 3], acc[j & 7]);
@@ -510,6 +523,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---------------------------------------------------------------- claim a ring slot; X and H1 go in now
       // sequence number fixed by (tile, wave): the gradient waves consume the tiles of a workgroup in one
       // order on every run, so the fp32 gradient sums (and every replay of a captured step) are bit-exact
+#if WS_L2PRE
+      s8v A2pre[WS_L2PRE];
+      layer2_pre<WS_L2PRE>(W1p, l16, g4, A2pre);
+#endif
       const int q = ND * k + d;
       const int sl = q % NSLOT, round = q / NSLOT;
       for (int spin = 0; lds_acq(ctl + 5 + sl) < NG * round; ++spin) {
@@ -537,7 +554,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---------------------------------------------------------------- layer 2 + output of Q(x)
       const bf16_t* w2row = W2p + min(l16, 4) * HP + 8 * g4;   // rows >= 3 zero: no masked load
       s8v w2f[4];
+#if WS_L2PRE
+      layer2<WS_L2PRE>(W1p, l16, g4, H1, a2, w2row, w2f, A2pre);
+#else
       for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1, a2, w2row, w2f);
+#endif
       s8v H2[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
