@@ -105,7 +105,7 @@
 #endif                  // window loads (0: at TD, qstep_ws_wbtd.hip, 0.5 % slower; profiles/r3_ws_ab.md)
 #ifndef WS_L2PRE
 #define WS_L2PRE 4      // Q(x)'s first n layer-2 W1 fragments read before the slot claim: their LDS latency runs
-#endif                  // under the slot wait and the slot stores (0: qstep_ws_l2pre0.hip; 6: _l2pre6.hip)
+#endif                  // under the slot wait and the slot stores (0: qstep_ws_l2pre0.hip, 1 % slower; 6: 0.8 % slower)
 #ifndef WS_NOWB
 #define WS_NOWB 0       // timing build qstep_ws_nowb.hip: no env-state write-back (wrong results)
 #endif
