@@ -106,15 +106,6 @@
 #ifndef WS_L2PRE
 #define WS_L2PRE 4      // Q(x)'s first n layer-2 W1 fragments read before the slot claim: their LDS latency runs
 #endif                  // under the slot wait and the slot stores (0: qstep_ws_l2pre0.hip, 1 % slower; 6: 0.8 % slower)
-#ifndef WS_B2E
-#define WS_B2E 0        // 1: Q(x')'s layer-2 bias accumulators read before the env step (qstep_ws_b2e.hip)
-#endif
-#ifndef WS_L2NPRE
-#define WS_L2NPRE 0     // n: Q(x')'s first n layer-2 W1 fragments read before the env step (qstep_ws_b2e4.hip)
-#endif
-#ifndef WS_EXPRE
-#define WS_EXPRE 0      // 1: the explore / exploit test and the random action formed before Q(x)'s output (qstep_ws_expre.hip)
-#endif
 #ifndef WS_NOWB
 #define WS_NOWB 0       // timing build qstep_ws_nowb.hip: no env-state write-back (wrong results)
 #endif
@@ -591,11 +582,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #endif
       WS_SB();
       WS_STAMP(5);
-#if WS_EXPRE
-      // (off the chain from Q(x)'s output to the env step: they depend on the draw and the position only)
-      const bool exploit_pre = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
-      const int rnd_pre = min((int)(u2 * 3.0f), 2);
-#endif
       f4v qa = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -605,14 +591,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       WS_PIN(qa);
       WS_SB();
       WS_STAMP(6);
-#if WS_B2E
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
-#endif
-#if WS_L2NPRE
-      s8v A2npre[WS_L2NPRE];
-      layer2_pre<WS_L2NPRE>(W1p, l16, g4, A2npre);
-#endif
       // ---------------------------------------------------------------- epsilon-greedy + env step (lanes g4 == 0)
       float b2 = 0.f, rew = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f;
       int s2 = 0, act = 0;
@@ -625,14 +603,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         float best = q0;
         if (q1 > best) { best = q1; greedy = 1; }
         if (q2 > best) { best = q2; greedy = 2; }
-#if WS_EXPRE
-        const bool exploit = exploit_pre;
-        const int rnd = rnd_pre;
-#else
         const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
         int rnd = (int)(u2 * 3.0f);
         rnd = rnd > 2 ? 2 : rnd;
-#endif
         act = exploit ? greedy : rnd;
         const float bd = p.compat_env ? p.b0 : bud0;
         const int sd = p.compat_env ? p.s0 : sh0;
@@ -663,16 +636,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #if WS_PF_POS == 0 && !WS_NOPF
       WS_LOAD_PRICES(k + 1, e_pos)
 #endif
-#if !WS_B2E
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
-#endif
       WS_SB();
-#if WS_L2NPRE
-      layer2<WS_L2NPRE>(W1p, l16, g4, H1n, a2, w2row, w2f, A2npre);
-#else
       for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1n, a2, w2row, w2f);
-#endif
       s8v H2n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2n[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
