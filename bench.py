@@ -132,7 +132,7 @@ def main() -> int:
     # capture -> vote (all ranks agree on graphs vs eager) -> prime with the same step counts on every
     # rank (each step holds the DP all-reduce); untimed, reported as "graph_prime_steps"
     use_graph, _ = benchkit.prepare_steps(eng, not args.no_graph and not cfg.engine.dp_overlap, rank, world,
-                                          group, prime_reps=4 if world == 1 else 6)
+                                          group, prime_reps=8)
     prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()
