@@ -18,6 +18,16 @@ class AskTimeoutException(TimeoutError):
     """An ``ask`` got no reply in time (akka.pattern.AskTimeoutException)."""
 
 
+class _Inline:
+    __slots__ = ("fn",)
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self, f):
+        self.fn(f)
+
+
 class Future:
     __slots__ = ("_cond", "_done", "_value", "_exc", "_callbacks", "_executor")
 
@@ -60,7 +70,7 @@ class Future:
         return self._complete(None, exc)
 
     def _run(self, cb: Callable[["Future"], None]) -> None:
-        if self._executor is not None:
+        if self._executor is not None and not isinstance(cb, _Inline):
             self._executor(lambda: cb(self))
         else:
             cb(self)
@@ -96,7 +106,11 @@ class Future:
         return ("err", self._exc) if self._exc is not None else ("ok", self._value)
 
     # ------------------------------------------------------------ combinators
-    def on_complete(self, cb: Callable[["Future"], None]) -> None:
+    def on_complete(self, cb: Callable[["Future"], None], inline: bool = False) -> None:
+        """``cb(self)`` once completed, on the executor -- or ``inline`` on the completing thread (for
+        trivial, thread-safe callbacks such as cancelling a timer: no dispatcher hop)."""
+        if inline:
+            cb = _Inline(cb)
         with self._cond:
             if not self._done:
                 self._callbacks.append(cb)

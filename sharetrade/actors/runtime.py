@@ -781,8 +781,10 @@ class Scheduler:
                 fn()
 
         with self._cv:
-            heapq.heappush(self._heap, (time.monotonic() + max(0.0, delay_s), next(self._seq), run))
-            self._cv.notify()
+            item = (time.monotonic() + max(0.0, delay_s), next(self._seq), run)
+            heapq.heappush(self._heap, item)
+            if self._heap[0] is item:   # a new earliest deadline: the timer thread must re-arm (else no wake-up:
+                self._cv.notify()       # an ask's 10 s timeout is almost never the earliest)
 
         def cancel():
             entry[0] = False
@@ -941,7 +943,7 @@ class ActorSystem:
                 timeout, lambda: p.set_exception(AskTimeoutException(
                     f"Ask timed out on [{target.path}] after [{int(timeout * 1000)} ms]. "
                     f"Message of type [{type(msg).__name__}]")))
-            p.on_complete(lambda _f: cancel())
+            p.on_complete(lambda _f: cancel(), inline=True)
         target.tell(msg, ref)
         return p
 
