@@ -110,10 +110,11 @@ class _Scratch:
 
 
 class _Staging:
-    """Pinned host image of one call's inputs -- padded rows of x (and x'), rewards, actions -- and
-    its device twin: host-side inputs (the actor path's [1, 203] states) reach the GPU in ONE
+    """Pinned host images of one call's inputs -- padded rows of x (and x'), rewards, actions -- and
+    their device twins: host-side inputs (the actor path's [1, 203] states) reach the GPU in ONE
     asynchronous copy instead of a copy + three pad kernels per tensor.  The bias column and the
-    zero padding are written once; the host image is reused after the previous copy's event."""
+    zero padding are written once.  Two images alternate (``_StagingPair``): an image is rewritten two
+    calls later, after its copy's event, so the host runs up to two calls ahead of the GPU."""
 
     def __init__(self, layout: qn.QNetLayout, B: int, device):
         self.B, self.in_p = B, layout.in_p
@@ -142,12 +143,25 @@ class _Staging:
         if act is not None:
             self.act[:] = act.numpy()
         self.d.copy_(self.h, non_blocking=True)
-        self.ev = torch.cuda.Event()
+        if self.ev is None:
+            self.ev = torch.cuda.Event()
         self.ev.record()
 
     def ptr(self, what: str) -> int:
         off = {"x": 0, "xn": self.B * self.in_p, "r": self.n_x, "act": self.n_x + self.B}[what]
         return self.d.data_ptr() + 4 * off
+
+
+class _StagingPair:
+    """Two :class:`_Staging` images used in turn (the device copies stay in stream order)."""
+
+    def __init__(self, layout: qn.QNetLayout, B: int, device):
+        self.imgs = (_Staging(layout, B, device), _Staging(layout, B, device))
+        self.i = 1
+
+    def next(self) -> _Staging:
+        self.i ^= 1
+        return self.imgs[self.i]
 
 
 class F32Learner:
@@ -158,12 +172,14 @@ class F32Learner:
         self.L = _bind()
         self._scratch = {}
         self._staging = {}
+        self._td_cache = {}
+        self._fwd_cache = {}
 
     def _stage(self, B: int) -> _Staging:
         st = self._staging.get(B)
         if st is None:
-            st = self._staging[B] = _Staging(self.layout, B, self.l.device)
-        return st
+            st = self._staging[B] = _StagingPair(self.layout, B, self.l.device)
+        return st.next()
 
     def _s(self, B: int) -> _Scratch:
         s = self._scratch.get(B)
@@ -180,7 +196,10 @@ class F32Learner:
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = x.shape[0]
         s = self._s(B)
-        r = F32Rows()
+        r = self._fwd_cache.get(B)
+        if r is None:
+            r = self._fwd_cache[B] = F32Rows()
+            r.q_out, r.B, r.mode = s.q.data_ptr(), B, 0
         if x.device.type == "cpu":
             st = self._stage(B)
             st.put(x.float())
@@ -188,7 +207,7 @@ class F32Learner:
         else:
             xp = self._pad(x)
             xptr = xp.data_ptr()
-        r.params, r.x, r.q_out, r.B, r.mode = self.l.params.data_ptr(), xptr, s.q.data_ptr(), B, 0
+        r.params, r.x = self.l.params.data_ptr(), xptr
         native.check(self.L.st_f32_rows(self.net, r, native.stream_handle()), "st_f32_rows(fwd)")
         return s.q.clone()
 
@@ -198,7 +217,7 @@ class F32Learner:
         B = x.shape[0]
         s = self._s(B)
         a = self.l.cfg.agent
-        r = F32Rows()
+        r, o = self._td_structs(B, s, coef)
         if x.device.type == "cpu" and xn.device.type == "cpu" and r_.device.type == "cpu" and \
                 (act is None or act.device.type == "cpu"):
             st = self._stage(B)
@@ -211,23 +230,42 @@ class F32Learner:
             acti = act.to(self.l.device, torch.int32).contiguous() if act is not None else None
             r.params, r.x, r.xn, r.reward = self.l.params.data_ptr(), xp.data_ptr(), xnp.data_ptr(), rew.data_ptr()
             r.action = acti.data_ptr() if acti is not None else None
-        r.q_out, r.qn_out, r.acts, r.dz, r.loss = (s.q.data_ptr(), s.qn.data_ptr(), s.acts.data_ptr(),
-                                                   s.dz.data_ptr(), s.loss.data_ptr())
-        r.B, r.mode, r.gamma, r.coef = B, 1, float(a.gamma), float(coef)
-        r.td_clip = float(a.td_clip)
         sh = native.stream_handle()
         native.check(self.L.st_f32_rows(self.net, r, sh), "st_f32_rows(td)")
         opt = self.l.opt
         opt.t += 1
-        o = F32Optim()
-        o.params, o.mask = self.l.params.data_ptr(), self.l.mask.data_ptr()
-        o.s1 = opt.s1.data_ptr() if opt.s1.numel() else None
-        o.s2 = opt.s2.data_ptr() if opt.s2.numel() else None
-        o.acts, o.dz, o.ctrl, o.B, o.kind, o.t = s.acts.data_ptr(), s.dz.data_ptr(), None, B, OPT_KIND[opt.kind], opt.t
-        o.mode, o.grad = 0, None
-        o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+        o.params = self.l.params.data_ptr()
+        o.t = opt.t
         native.check(self.L.st_f32_grad_optim(self.net, o, sh), "st_f32_grad_optim")
         return float(s.loss.sum()) if want_loss else s.loss
+
+    def _td_structs(self, B: int, s: "_Scratch", coef: float):
+        """The launch structs of a TD update of batch B, built once (the actor path calls this per
+        ``UpdateQ``: constructing and filling two ctypes structs per call cost more than the launches).
+        Per call only the input pointers, the parameter pointer and the step counter change."""
+        key = (B, float(coef))
+        c = self._td_cache.get(key)
+        a, opt = self.l.cfg.agent, self.l.opt
+        if c is None:
+            r = F32Rows()
+            r.q_out, r.qn_out, r.acts, r.dz, r.loss = (s.q.data_ptr(), s.qn.data_ptr(), s.acts.data_ptr(),
+                                                       s.dz.data_ptr(), s.loss.data_ptr())
+            r.B, r.mode, r.gamma, r.coef = B, 1, float(a.gamma), float(coef)
+            r.td_clip = float(a.td_clip)
+            o = F32Optim()
+            o.mask = self.l.mask.data_ptr()
+            o.s1 = opt.s1.data_ptr() if opt.s1.numel() else None
+            o.s2 = opt.s2.data_ptr() if opt.s2.numel() else None
+            o.acts, o.dz, o.ctrl, o.B, o.kind = s.acts.data_ptr(), s.dz.data_ptr(), None, B, OPT_KIND[opt.kind]
+            o.mode, o.grad = 0, None
+            o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+            c = self._td_cache[key] = (r, o)
+        r, o = c
+        if o.mask != self.l.mask.data_ptr() or (opt.s1.numel() and o.s1 != opt.s1.data_ptr()) or \
+                (opt.s2.numel() and o.s2 != opt.s2.data_ptr()):
+            del self._td_cache[key]            # optimizer state re-allocated (load_state_dict): rebuild
+            return self._td_structs(B, s, coef)
+        return r, o
 
 
 class F32EngineStep:
