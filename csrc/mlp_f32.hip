@@ -37,6 +37,7 @@ struct F32Net {
   int dz_off[F_MAXL];            // offset of dz_l inside a row's dz record
   int act_stride, dz_stride;     // floats per row
   int bias_col, input_dim, output_relu, P;
+  int gemv_legacy;               // 1: every layer in the wave-per-neuron form (A/B of the thread-per-neuron form)
 };
 
 struct F32Rows {
@@ -65,8 +66,33 @@ struct F32Rows {
 };
 
 // out[n] = act(sum_k W^T[n][k] * in[k] + b[n]) for n < N (padded N); rows of W^T are contiguous.
+// Wide layers (N >= 64): a thread per output neuron, 16-byte weight loads along its W^T row (the 64 rows of a
+// wave-instruction are distinct L1 lines, each reused by the lane's next 3 loads) against the input vector
+// broadcast from LDS, 4 partial sums -- no cross-lane reduction.  The wave-per-neuron form below did ~N/4
+// dependent wave reductions per layer and made a batch-1 TD update ~100 us of kernel time.
 ST_DEV void gemv_layer(const float* __restrict__ W, const float* __restrict__ b, const float* in, float* out,
-                       int N, int K, int nreal, bool relu) {
+                       int N, int K, int nreal, bool relu, bool legacy = false) {
+  if (!legacy && N >= 64 && (K & 3) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(in);
+    for (int n = threadIdx.x; n < N; n += F_NT) {
+      float v = 0.f;
+      if (n < nreal) {
+        const float4* w = reinterpret_cast<const float4*>(W + (size_t)n * K);
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        for (int k = 0; k < (K >> 2); ++k) {
+          const float4 a = w[k], x = x4[k];
+          s0 = fmaf(a.x, x.x, s0);
+          s1 = fmaf(a.y, x.y, s1);
+          s2 = fmaf(a.z, x.z, s2);
+          s3 = fmaf(a.w, x.w, s3);
+        }
+        v = ((s0 + s1) + (s2 + s3)) + (b ? b[n] : 0.f);
+      }
+      out[n] = relu ? fmaxf(v, 0.f) : v;
+    }
+    return;
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int n = wave; n < N; n += F_NT / 64) {
     float s = 0.f;
@@ -90,7 +116,7 @@ ST_DEV void forward_row(const F32Net& net, const float* __restrict__ P, float* a
     const float* b = net.off_b[l] >= 0 ? P + net.off_b[l] : nullptr;
     float* out = last ? q : a + aoff[l + 1];
     gemv_layer(P + net.off_w[l], b, a + aoff[l], out, net.pd[l + 1], net.pd[l], net.dims[l + 1],
-               last ? (bool)net.output_relu : true);
+               last ? (bool)net.output_relu : true, net.gemv_legacy != 0);
     __syncthreads();
   }
 }

@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import numpy as np
@@ -29,6 +30,7 @@ class F32Net(C.Structure):
         ("off_w", C.c_int * F_MAXL), ("off_b", C.c_int * F_MAXL), ("act_off", C.c_int * F_MAXL),
         ("dz_off", C.c_int * F_MAXL), ("act_stride", C.c_int), ("dz_stride", C.c_int),
         ("bias_col", C.c_int), ("input_dim", C.c_int), ("output_relu", C.c_int), ("P", C.c_int),
+        ("gemv_legacy", C.c_int),
     ]
 
 
@@ -93,6 +95,8 @@ def make_net(layout: qn.QNetLayout, output_relu: bool) -> F32Net:
         dz += layout.pdims[l + 1]
     n.act_stride, n.dz_stride = ao, dz
     n.bias_col, n.input_dim, n.output_relu, n.P = layout.bias_col, layout.input_dim, int(output_relu), layout.numel
+    # A/B switch for csrc/mlp_f32.hip gemv_layer: "legacy" = the wave-per-neuron form everywhere
+    n.gemv_legacy = int(os.environ.get("SHARETRADE_F32_GEMV", "") == "legacy")
     return n
 
 

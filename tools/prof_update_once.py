@@ -1,0 +1,15 @@
+import cProfile, pstats, sys, os
+sys.path.insert(0, os.getcwd())
+import numpy as np, torch
+from sharetrade.config import preset_config
+from sharetrade.policy.learner import QLearner
+lr = QLearner(preset_config("reference_compat"), device=torch.device("cuda"))
+rng = np.random.default_rng(0)
+s = torch.from_numpy(rng.random((1, 203), dtype=np.float32)); ns = torch.from_numpy(rng.random((1, 203), dtype=np.float32))
+for _ in range(100): lr.update(s, 0.5, ns, None, return_loss=False)
+torch.cuda.synchronize()
+pr = cProfile.Profile(); pr.enable()
+for _ in range(2000): lr.update(s, 0.5, ns, None, return_loss=False)
+torch.cuda.synchronize()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(18)
