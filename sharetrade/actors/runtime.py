@@ -396,6 +396,10 @@ class ActorContext:
     def self_ref(self) -> ActorRef:
         return self._cell.ref
 
+    def mailbox_size(self) -> int:
+        """User messages queued behind the current one (a hint: others may enqueue concurrently)."""
+        return len(self._cell.mailbox)
+
     @property
     def parent(self) -> Optional[ActorRef]:
         p = self._cell.parent

@@ -10,7 +10,8 @@ MI355X-first differences (semantics preserved):
 
 * **Mailbox micro-batching.**  ``SelectionAction``s that are already queued
   are answered with ONE batched forward: a selection is held until a ``_Flush``
-  the actor sends itself, which lands behind everything queued so far; any
+  the actor sends itself, which lands behind everything queued so far (with an
+  empty mailbox it is answered at once: nothing could join the batch); any
   ``UpdateQ`` first flushes the pending selections, so every selection still
   sees exactly the weights it would have seen one-message-at-a-time.
 * **Real snapshots.**  Every ``snapshot_interval`` updates the learner state is
@@ -71,8 +72,11 @@ class QDecisionPolicyActor(Actor):
                 return None
             self._pending.append((st, float(msg.step), self.sender))
             if not self._flush_scheduled:
-                self._flush_scheduled = True
-                self.self_ref.tell(_Flush, self.self_ref)
+                if self.context.mailbox_size() == 0:
+                    self._flush()        # nothing queued to batch with: answer now (no _Flush round trip)
+                else:
+                    self._flush_scheduled = True
+                    self.self_ref.tell(_Flush, self.self_ref)
             return None
         if msg is _Flush:
             self._flush_scheduled = False
