@@ -72,25 +72,26 @@ def main() -> int:
     dev = torch.device(a.device)
     kinds = a.kinds.split(",")
     res = {k: run(k, a.steps, a.envs, a.every, a.phi, dev, a.set) for k in kinds}
-    if kinds != ["learned", "random", "frozen"]:
-        return 0
     lines = [f"# Learning curve: flagship online DQN (2x128 MLP, bf16 fused step) on an AR(1)-momentum "
              f"price bank (phi = {a.phi}, vol 0.02, 6,047 days), {a.envs} envs", "",
              "Reward = the portfolio's one-step return (`agent.reward_mode = relative`, flagship preset), "
-             f"mean per env-step in basis points, per window of {a.every} steps; same bank and seed for all "
-             "three runs (`tools/learning_curve.py`).  All envs start together, so every env ends an "
+             f"mean per env-step in basis points, per window of {a.every} steps; same bank and seed for every "
+             "run (`tools/learning_curve.py`).  All envs start together, so every env ends an "
              "episode (5,846 steps) in the same window: the final-portfolio columns (budget 2,400 at the "
-             "start of each episode) are filled there.", "",
-             "| step | learned bp/step | random bp/step | frozen bp/step | learned final $ | random final $ | "
-             "frozen final $ | learned TD loss | learned explore |",
-             "|---|---|---|---|---|---|---|---|---|"]
+             "start of each episode) are filled there." + (f"  Overrides: {' '.join(a.set)}." if a.set else ""), ""]
+    head = ["step"] + [f"{k} bp/step" for k in kinds] + [f"{k} final $" for k in kinds]
+    if "learned" in kinds:
+        head += ["learned TD loss", "learned explore"]
+    lines += ["| " + " | ".join(head) + " |", "|" + "---|" * len(head)]
     fp = lambda r: f"{r['final_portfolio_mean']:.1f}" if "final_portfolio_mean" in r else ""
-    for i, r in enumerate(res["learned"]):
-        rr, rf = res["random"][i], res["frozen"][i]
-        lines.append(f"| {r['step']} | {r['mean_reward'] * 1e4:.3f} | {rr['mean_reward'] * 1e4:.3f} | "
-                     f"{rf['mean_reward'] * 1e4:.3f} | {fp(r)} | {fp(rr)} | {fp(rf)} | "
-                     f"{r['mean_td_loss']:.2e} | {r['explore_rate']:.3f} |")
-    for k in ("learned", "random", "frozen"):
+    for i, r0 in enumerate(res[kinds[0]]):
+        rows = [res[k][i] for k in kinds]
+        cells = [str(r0["step"])] + [f"{r['mean_reward'] * 1e4:.3f}" for r in rows] + [fp(r) for r in rows]
+        if "learned" in kinds:
+            rl = res["learned"][i]
+            cells += [f"{rl['mean_td_loss']:.2e}", f"{rl['explore_rate']:.3f}"]
+        lines.append("| " + " | ".join(cells) + " |")
+    for k in kinds:
         m = sum(r["mean_reward"] for r in res[k]) / max(1, len(res[k]))
         lines.append(f"\n{k}: mean {m * 1e4:.3f} bp per env-step over {a.steps} steps")
     txt = "\n".join(lines) + "\n"
