@@ -1,3 +1,8 @@
+"""cProfile of the batch-1 learner update's host path (``QLearner.update`` on the GPU, reference_compat
+preset): where the ~116 us per UpdateQ went before the thread-per-neuron GEMV (profiles/r3_secondary_benches.md).
+
+    python tools/prof_update_once.py
+"""
 import cProfile, pstats, sys, os
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch
