@@ -236,7 +236,10 @@ ST_DEV s4v hi4(s8v v) { s4v r = {v[4], v[5], v[6], v[7]}; return r; }
 // acc[i] += W1 (rows 16 i .. 16 i + 15, pi-ordered columns) . H (B operands of 4 k-steps), 32 MFMAs with
 // the W1 fragment of pair j + PD2 read while pair j issues (j = 8 ks + i)
 // (pre: the first PD2 fragments were read by layer2_pre, earlier in the chain -- their LDS latency off it)
-constexpr int PD2 = 8, NB2 = PD2 + 1;
+#ifndef WS_PD2
+#define WS_PD2 8        // data waves: layer-2 W1 fragments read ahead of their MFMAs (6 and 10: 0.6-0.8 % slower)
+#endif
+constexpr int PD2 = WS_PD2, NB2 = PD2 + 1;
 template <int NPRE>
 ST_DEV void layer2_pre(const bf16_t* W1p, int l16, int g4, s8v* A) {
 #pragma unroll
