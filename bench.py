@@ -53,9 +53,9 @@ def main() -> int:
                     help="all ranks on cuda:0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace here")
     ap.add_argument("--step-kernel", default="auto",
-                    help="fused step kernel: auto | wide (64-env chunks) | pair (two 32-env slots in flight) | narrow")
+                    help="fused step kernel: auto | ws (flagship) | wide (64-env chunks) | narrow")
     ap.add_argument("--step-waves", type=int, default=8, help="64-env-chunk kernel: waves per workgroup (4 or 8)")
-    ap.add_argument("--step-variant", default="", help="tuning build of the 64-env-chunk kernel (suffix)")
+    ap.add_argument("--step-variant", default="", help="timing / debug build of the ws kernel (csrc/ab/qstep_ws_<v>.hip; needs SHARETRADE_AB_BUILDS=1)")
     ap.add_argument("--chunk", type=int, default=0,
                     help="envs per chunk of the fused step kernel: 0 = auto (64 when envs %% 64 == 0), 32, 64")
     ap.add_argument("--dp-overlap", action="store_true",
@@ -71,8 +71,8 @@ def main() -> int:
                     help="N>1: collective timeout (s); with TORCH_NCCL_ASYNC_ERROR_HANDLING=1 a dead peer fails "
                          "the job instead of hanging it")
     ap.add_argument("--no-episode", action="store_true",
-                    help="skip the untimed full-episode returns (learned policy + random-policy baseline) "
-                         "after the timed window")
+                    help="skip the untimed full-episode returns after the timed window (greedy learned policy, "
+                         "greedy random-init policy, buy-and-hold, online learned episode, random policy)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,6 +123,7 @@ def main() -> int:
         cfg.engine.graph_steps = args.graph_steps
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
+    init_params = None if args.no_episode else eng.params.detach().clone()   # the frozen-init baseline
 
     # load the (lazily loaded) torch kernels of the start-of-window portfolio snapshot before the graphs
     # are primed: loading them between the warm-up and the timed window idled the GPU for >= 10 ms,
@@ -185,12 +186,20 @@ def main() -> int:
     st = stats.cpu().tolist()
     episodes = None
     if not args.no_episode:
-        # untimed, after the timed window: every env plays one complete episode over its series
-        # (T - H = 5,846 online-learning steps), first with the policy being learned, then with a
-        # uniformly random policy on the same banks (the baseline)
+        # untimed, after the timed window, every env plays complete episodes over its series
+        # (T - H = 5,846 steps each) on the same banks:
+        #  * greedy: the parameters learned so far, frozen, exploit-only (the policy itself);
+        #  * init_greedy: the same with the random-init parameters (what learning has to improve on);
+        #  * buy_hold: Buy at every step (budget into shares at the start, then held);
+        #  * learned: the online epsilon-greedy episode with learning on (the training regime);
+        #  * random: uniformly random actions.
+        greedy = benchkit.greedy_episode_returns(eng, world, group)
+        init_greedy = benchkit.greedy_episode_returns(eng, world, group, params=init_params)
+        buy_hold = benchkit.buy_and_hold_returns(eng, world, group)
         learned = benchkit.full_episode_returns(eng, world, group)
         rnd = benchkit.full_episode_returns(eng, world, group, random_policy=True)
-        episodes = {"learned": learned, "random": rnd}
+        episodes = {"learned": learned, "random": rnd, "greedy": greedy, "init_greedy": init_greedy,
+                    "buy_hold": buy_hold}
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -238,15 +247,21 @@ def main() -> int:
         if allreduce_ms is not None:
             out["allreduce_ms_per_step"] = allreduce_ms
         if episodes is not None:
-            lr_, rd_ = episodes["learned"], episodes["random"]
-            out["episode_return"] = {
+            lr_ = episodes["learned"]
+            er = {
                 "what": "final portfolio - initial budget, one complete episode per env (untimed, after the "
-                        "timed window), mean / population std over all envs of all ranks",
+                        "timed window), mean / population std over all envs of all ranks. greedy: the learned "
+                        "parameters frozen, exploit-only; init_greedy: the same at the random init; buy_hold: "
+                        "Buy every step (budget into shares, then held); learned: online epsilon-greedy episode "
+                        "with learning on; random: uniform actions",
                 "episode_steps": lr_["steps"],
-                "learned_mean": round(lr_["mean"], 4), "learned_std": round(lr_["std"], 4),
-                "random_mean": round(rd_["mean"], 4), "random_std": round(rd_["std"], 4),
-                "episodes": lr_["n"], "complete_frac": round(lr_["complete_frac"], 6),
             }
+            for k in ("greedy", "init_greedy", "buy_hold", "learned", "random"):
+                er[f"{k}_mean"] = round(episodes[k]["mean"], 4)
+                er[f"{k}_std"] = round(episodes[k]["std"], 4)
+            er["episodes"] = lr_["n"]
+            er["complete_frac"] = round(min(episodes[k]["complete_frac"] for k in episodes), 6)
+            out["episode_return"] = er
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

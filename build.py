@@ -9,7 +9,11 @@ Produces (next to the Python package, so they travel with the repo snapshot):
 * ``sharetrade/_native/libsharetrade_rt.so`` — the host-side C++ runtime
   (journal / snapshot store / checkpoint writer), built with g++.
 
-Usage: ``python build.py [--force] [-j N]``.  Rebuilds only when a source is
+The timing / debug builds of the flagship kernel (``csrc/ab/``) are not part of the production
+library; ``python build.py --ab`` (or ``SHARETRADE_AB_BUILDS=1``) builds them into
+``libsharetrade_ab.so``.
+
+Usage: ``python build.py [--force] [--ab] [-j N]``.  Rebuilds only when a source is
 newer than the library.
 """
 from __future__ import annotations
@@ -33,6 +37,7 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contr
 CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter"]
 
 HIP_LIB = os.path.join(OUT, "libsharetrade_hip.so")
+AB_LIB = os.path.join(OUT, "libsharetrade_ab.so")   # opt-in timing / debug builds (csrc/ab/)
 RT_LIB = os.path.join(OUT, "libsharetrade_rt.so")
 
 
@@ -76,25 +81,30 @@ def _run(cmd):
     return r.stdout
 
 
-def build_hip(force: bool = False, jobs: int = 8) -> str:
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+def build_hip(force: bool = False, jobs: int = 8, ab: bool = False) -> str:
+    """Production kernels: every ``csrc/*.hip`` -> libsharetrade_hip.so.  With ``ab``: the timing / debug
+    builds of the flagship kernel (``csrc/ab/*.hip``: per-phase stamps, phases skipped or run twice, several
+    computing wrong results by design) -> their own libsharetrade_ab.so, which only an opted-in process
+    (SHARETRADE_AB_BUILDS=1) loads."""
+    lib_path = AB_LIB if ab else HIP_LIB
+    srcs = sorted(glob.glob(os.path.join(CSRC, "ab" if ab else "", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "*.h")))
-    if not force and not _newer(HIP_LIB, srcs + hdrs):
-        return HIP_LIB   # library newer than every source: nothing to do (the object dir need not exist)
+    if not force and not _newer(lib_path, srcs + hdrs + ([os.path.join(CSRC, "qstep_ws.hip")] if ab else [])):
+        return lib_path   # library newer than every source: nothing to do (the object dir need not exist)
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(OUT, exist_ok=True)
     objs = []
     todo = []
     for s in srcs:
-        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        o = os.path.join(OBJ, ("ab_" if ab else "") + os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(o, [s] + hdrs + sorted(_includes(s))):
             todo.append((s, o))
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(lambda so: _run([HIPCC] + HIP_FLAGS + ["-c", so[0], "-o", so[1]]), todo))
-    if force or todo or _newer(HIP_LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_LIB] + objs)
-    return HIP_LIB
+    if force or todo or _newer(lib_path, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path] + objs)
+    return lib_path
 
 
 def build_rt(force: bool = False) -> str:
@@ -109,7 +119,7 @@ def build_rt(force: bool = False) -> str:
     return RT_LIB
 
 
-def build_all(force: bool = False, jobs: int = 8):
+def build_all(force: bool = False, jobs: int = 8, ab: bool = False):
     """Build (or confirm up to date) both libraries.  Serialised across processes by an exclusive
     lock on ``build/.lock``: the ranks of a multi-GPU job all call this before they initialise the
     process group, the first one builds, the others wait on the lock and find the libraries current
@@ -121,6 +131,8 @@ def build_all(force: bool = False, jobs: int = 8):
         fcntl.flock(lk, fcntl.LOCK_EX)
         try:
             libs = [build_hip(force, jobs)]
+            if ab or os.environ.get("SHARETRADE_AB_BUILDS", "") not in ("", "0"):
+                libs.append(build_hip(force, jobs, ab=True))
             rt = build_rt(force)
             if rt:
                 libs.append(rt)
@@ -132,7 +144,8 @@ def build_all(force: bool = False, jobs: int = 8):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--ab", action="store_true", help="also build the opt-in timing / debug kernels (csrc/ab/)")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     a = ap.parse_args()
-    for lib in build_all(a.force, a.j):
+    for lib in build_all(a.force, a.j, a.ab):
         print(lib)

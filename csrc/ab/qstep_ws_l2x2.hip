@@ -1,0 +1,7 @@
+// Timing build of csrc/qstep_ws.hip (wrong results; never used for training): both layer-2 passes
+// run twice per tile -- the time over the production build is that phase's cost in context.
+// st_qstep_ws_launch_l2x2 (engine.step_variant = "l2x2" with step_kernel "ws").
+#define WS_L2REP 2
+#define WS_NS ws_l2x2
+#define WS_API(name) name##_l2x2
+#include "../qstep_ws.hip"

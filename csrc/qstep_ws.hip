@@ -36,84 +36,43 @@
 
 #ifndef WS_STAMPS
 #define WS_STAMPS 0     // s_memtime stamps per phase, bit 0 data wave 0, bit 1 gradient wave 0 (debug builds
-#endif                  // csrc/qstep_ws_stamps*.hip only: the stamp code costs registers)
+#endif                  // csrc/ab/qstep_ws_*stamps*.hip only: the stamp code costs registers)
 #ifndef WS_GSKIP
-#define WS_GSKIP 0      // 1: timing build (csrc/qstep_ws_gskip.hip), gradient waves skip their work
+#define WS_GSKIP 0      // 1: timing build (csrc/ab/qstep_ws_gskip.hip), gradient waves skip their work
 #endif
 #if WS_MARKS   // tools/isa.py: assembly comments at the stamp points, to count instructions per phase
 #define WS_MARK(W, I) asm volatile(";@" #W " " #I);
 #else
 #define WS_MARK(W, I)
 #endif
-#ifndef WS_PF_POS
-#define WS_PF_POS 0     // where the next tile's price windows are issued: 0 at Q(x')'s layer 2, 1 after Q(x)'s
-#endif                  // layer 2, 2 right after this tile's features (a whole tile ahead: 59 VGPRs spill)
-#ifndef WS_WB_DEFER
-#define WS_WB_DEFER 0   // 1: env-state stores issued in the next tile after its window wait (qstep_ws_defer.hip:
-#endif                  // with WS_PF_POS 1, 2.6 % slower on one box, profiles/r3_ws_ab.md)
-#ifndef WS_GPIPE
-#define WS_GPIPE 1      // gradient waves: fragments issued in latency order (0: qstep_ws_gold.hip, the v4 order)
-#endif
 #ifndef WS_PD1
 #define WS_PD1 8        // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs (10: 0.5 % slower, 12: 1 %)
 #endif
-#ifndef WS_ENV_AT_L1
-#define WS_ENV_AT_L1 1  // the env-state prefetch issued at layer 1's start (0: after the slot claim, qstep_ws_envslot.hip)
-#endif
-#ifndef WS_W2_EARLY
-#define WS_W2_EARLY 1   // the output layers' W2 fragments read in layer 2's last read slots (0: qstep_ws_w2late.hip)
-#endif
-#ifndef WS_DZ_EARLY
-#define WS_DZ_EARLY 1   // dZ2's LDS fragments read before TD (0: after it, qstep_ws_dzlate.hip)
-#endif
-#ifndef WS_DPRIO
-#define WS_DPRIO 0      // s_setprio of the data waves (qstep_ws_dprio.hip: 2)
-#endif
-#ifndef WS_GPRIO
-#define WS_GPRIO 0      // s_setprio of the gradient waves (qstep_ws_gprio.hip: 2)
-#endif
 #ifndef WS_NOPHIL
-#define WS_NOPHIL 0     // timing build qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
+#define WS_NOPHIL 0     // timing build csrc/ab/qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
 #endif
-#ifndef WS_GPAIR
-#define WS_GPAIR 1      // gradient waves take ring slots in pairs: K = 32 MFMAs (0: one slot, K = 16; qstep_ws_gsingle.hip)
-#endif
-#ifndef WS_GXP
-#define WS_GXP 2        // paired slots: X fragment pairs read this many dW0 steps ahead
-#endif
-#ifndef WS_GDZ
-#define WS_GDZ 0        // 1: the gradient waves form dZ2 from dQ + a pi-order H2 copy (qstep_ws_gdz.hip: they
-                        // become the bottleneck, 13 % slower; profiles/r3_ws_ab.md)
-#endif
-#if WS_GDZ && !WS_GPAIR
-#error "WS_GDZ needs the paired-slot gradient waves"
-#endif
-#ifndef WS_GZ
-#define WS_GZ 1         // gradient waves: dZ1 fragments read this many k-steps ahead
-#endif
-#ifndef WS_GX
-#define WS_GX 3         // gradient waves: X fragments read this many dW0 steps ahead
-#endif
-#ifndef WS_GH
-#define WS_GH 12        // gradient waves: the dW1 / dW2 fragments issued after this dW0 step
-#endif
-#ifndef WS_FMA_FEAT
-#define WS_FMA_FEAT 1   // window features w / last - 1 as one fma per value, one rounding (0: multiply then subtract,
-#endif                  // two roundings as qstep_wide.hip; qstep_ws_fsub.hip, 1.2 % slower; profiles/r3_ws_ab.md)
-#ifndef WS_WBE
-#define WS_WBE 1        // the env-state write-back issued right after the env step, before Q(x') and the next tile's
-#endif                  // window loads (0: at TD, qstep_ws_wbtd.hip, 0.5 % slower; profiles/r3_ws_ab.md)
+// Production schedule choices, each A/B'd in round 3 (profiles/r3_ws_ab.md; the losing builds were retired):
+//  - the next tile's price windows are issued at Q(x')'s layer 2 (earlier issue loses 1.3-2 %, a whole tile
+//    ahead spills);
+//  - the env-state write-back is issued right after the env step (at TD: 0.5 % slower; deferred: 2.6 %);
+//  - the env-state prefetch of the tile after next is issued at layer 1's start;
+//  - the output layers' W2 fragments are read in layer 2's last read slots, dZ2's fragments before TD;
+//  - window features are w / last - 1 as one fma per value (multiply + subtract: 1.2 % slower);
+//  - Q(x)'s first WS_L2PRE layer-2 W1 fragments are read before the slot claim;
+//  - gradient waves take ring slots in pairs (K = 32 weight-gradient MFMAs; single slots: 3.4 % slower), the
+//    data waves form dZ2 (gradient waves forming it: 13 % slower), no issue priorities (gradient priority: +25 %).
+constexpr int WS_GXP = 2;       // paired slots: X fragment pairs read this many dW0 steps ahead
 #ifndef WS_L2PRE
-#define WS_L2PRE 4      // Q(x)'s first n layer-2 W1 fragments read before the slot claim: their LDS latency runs
-#endif                  // under the slot wait and the slot stores (0: qstep_ws_l2pre0.hip, 1 % slower; 6: 0.8 % slower)
+#define WS_L2PRE 4
+#endif
 #ifndef WS_NOWB
-#define WS_NOWB 0       // timing build qstep_ws_nowb.hip: no env-state write-back (wrong results)
+#define WS_NOWB 0       // timing build csrc/ab/qstep_ws_nowb.hip: no env-state write-back (wrong results)
 #endif
 #ifndef WS_NOPF
-#define WS_NOPF 0       // timing build qstep_ws_nopf.hip: no price prefetch in the loop (stale windows)
+#define WS_NOPF 0       // timing build csrc/ab/qstep_ws_nopf.hip: no price prefetch in the loop (stale windows)
 #endif
 #ifndef WS_L1REP
-#define WS_L1REP 1      // timing builds only (qstep_ws_l1x2.hip / _l2x2.hip): a phase run twice, to price it in
+#define WS_L1REP 1      // timing builds only (csrc/ab/qstep_ws_l1x2.hip / _l2x2.hip): a phase run twice, to price it in
 #endif                  // context (wrong results)
 #ifndef WS_L2REP
 #define WS_L2REP 1
@@ -149,7 +108,8 @@ constexpr int oSLOT = oB2 + 64;
 // (8-byte chunks swizzled), DZ2 [16][128] (pi order, 16-byte units swizzled like W1p)
 constexpr int sX = 0, sH1 = sX + 16 * KX * 2, sH2 = sH1 + 16 * HP * 2, sDZ2 = sH2 + 16 * HP * 2,
               SLOT_BYTES = sDZ2 + 16 * HP * 2;
-constexpr int oCTL = oSLOT + NSLOT * SLOT_BYTES;   // ints: [0] claim, [1..4] full, [5..8] freed, [10..11] zero
+constexpr int oCTL = oSLOT + NSLOT * SLOT_BYTES;   // ints: [0] claim, [1..4] full, [5..8] freed, [10..11] zero,
+                                                   // [12] abort (sticky)
 constexpr int oST = oCTL + 64;                     // [ND][NSTAT] f32
 constexpr int LDS_BYTES = oST + ND * NSTAT * 4;
 static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -262,7 +222,7 @@ ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc, c
       const int jn = j + PD2;
       A[jn % NB2] = lds_ld8(W1p + w1_off(16 * (jn & 7) + l16, 32 * (jn >> 3) + 8 * g4));
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    } else if (WS_W2_EARLY && j >= 32 - 4) {   // the output layer's W2 fragments, in the last read slots
+    } else if (j >= 32 - 4) {   // the output layer's W2 fragments, in the last read slots
       w2f[j - 28] = lds_ld8(w2row + 32 * (j - 28));
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
@@ -271,13 +231,30 @@ ST_DEV void layer2(const bf16_t* W1p, int l16, int g4, const s8v* H, f4v* acc, c
 }
 
 // every ring wait is bounded (~1 s at s_sleep 1): a protocol bug ends the launch with an error bit in
-// p.err instead of leaving waves spinning on the GPU
+// p.err instead of leaving waves spinning on the GPU.  The first wait that gives up also sets a sticky
+// abort word in the workgroup's control block (ctl[12]); every wait checks it before sleeping, so the
+// rest of the launch falls through its waits at once (results are garbage, p.err says so) instead of
+// spinning a full SPIN_LIMIT per wait.  The host checks p.err at its synchronisation points
+// (VectorEngine.check_kernel_err).
 constexpr int SPIN_LIMIT = 1 << 24;
-ST_DEV void ws_fail(const QStepParams& p) {
-  if (p.err != nullptr && (threadIdx.x & 63) == 0) atomicOr(p.err, 1u);
-}
+constexpr int CTL_ABORT = 12;
 ST_DEV int lds_acq(const int* w) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+ST_DEV void ws_fail(const QStepParams& p, int* ctl) {
+  if ((threadIdx.x & 63) == 0) {
+    __hip_atomic_store(ctl + CTL_ABORT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (p.err != nullptr) atomicOr(p.err, 1u);
+  }
+}
+// wait until pred(*w) holds: bounded, and abandoned at once once the workgroup has aborted
+template <typename Pred>
+ST_DEV void ring_wait(const QStepParams& p, int* ctl, const int* w, Pred pred) {
+  for (int spin = 0; !pred(lds_acq(w)); ++spin) {
+    if (lds_acq(ctl + CTL_ABORT)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (spin > SPIN_LIMIT) { ws_fail(p, ctl); break; }   // never expected: report, do not hang the GPU
+  }
 }
 
 // env-state rows addressed as a uniform row base + a 32-bit byte offset, so the loads / stores use the
@@ -334,7 +311,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   if (wave < ND) {
     // ================================================================ DATA WAVE
     const int d = wave;
-    if (WS_DPRIO) __builtin_amdgcn_s_setprio(WS_DPRIO);   // issue priority over the gradient wave beside it
     float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
           st_qslot = 0.f;
     const float b2v[3] = {sB2[0], sB2[1], sB2[2]};
@@ -411,7 +387,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     } else {                                                                                     \
       w_b = b2; w_s = s2; w_v = vnew; w_pos = np_; w_rs = rs0 + rew;                             \
     }                                                                                            \
-    if (!WS_WB_DEFER) { WS_WRITE_BACK() w_e = -1; }                                              \
+    WS_WRITE_BACK() w_e = -1;                                                                    \
   }
 
     for (int k = 0; k < nmy; ++k) {
@@ -426,10 +402,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         invn = __fdiv_rn(1.0f, vnew);
       }
       auto fx = [&](float w) {
-        return FEAT ? (WS_FMA_FEAT ? __fmaf_rn(w, inv, -1.0f) : __fsub_rn(__fmul_rn(w, inv), 1.0f)) : w;
+        return FEAT ? __fmaf_rn(w, inv, -1.0f) : w;
       };
       auto fxn = [&](float w) {
-        return FEAT ? (WS_FMA_FEAT ? __fmaf_rn(w, invn, -1.0f) : __fsub_rn(__fmul_rn(w, invn), 1.0f)) : w;
+        return FEAT ? __fmaf_rn(w, invn, -1.0f) : w;
       };
       s8v X[6], Xn[6];
 #pragma unroll
@@ -455,17 +431,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
       // rotate the prefetched env state; load the one after next
       e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep;
-#if WS_PF_POS == 2
-      WS_LOAD_PRICES(k + 1, e_pos)
-#endif
       WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
       WS_SB();
       WS_STAMP(1);
       // (after the features: a store or load issued before them would hold their window wait)
       WS_WRITE_BACK()
-#if WS_ENV_AT_L1
       WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
-#endif
       // the epsilon-greedy draw (Philox, ~70 VALU with quarter-rate multiplies) depends only on (env, step):
       // issued here, the scheduler interleaves it with layer 1's MFMAs (VALU slots in the group pattern)
       float u1, u2;
@@ -526,21 +497,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---------------------------------------------------------------- claim a ring slot; X and H1 go in now
       // sequence number fixed by (tile, wave): the gradient waves consume the tiles of a workgroup in one
       // order on every run, so the fp32 gradient sums (and every replay of a captured step) are bit-exact
-#if WS_L2PRE
       s8v A2pre[WS_L2PRE];
       layer2_pre<WS_L2PRE>(W1p, l16, g4, A2pre);
-#endif
       const int q = ND * k + d;
       const int sl = q % NSLOT, round = q / NSLOT;
-      for (int spin = 0; lds_acq(ctl + 5 + sl) < NG * round; ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin > SPIN_LIMIT) { ws_fail(p); break; }   // never expected: report, do not hang the GPU
-      }
+      ring_wait(p, ctl, ctl + 5 + sl, [&](int v) { return v >= NG * round; });
       WS_STAMP(3);
-#if !WS_ENV_AT_L1
-      // the env state of the tile after next: its 6 loads issued here, away from layer 1's MFMA stream
-      WS_LOAD_ENV(k + 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
-#endif
       char* sb = smem + oSLOT + sl * SLOT_BYTES;
       bf16_t* sx = reinterpret_cast<bf16_t*>(sb + sX);
       bf16_t* sh1 = reinterpret_cast<bf16_t*>(sb + sH1);
@@ -557,38 +519,20 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---------------------------------------------------------------- layer 2 + output of Q(x)
       const bf16_t* w2row = W2p + min(l16, 4) * HP + 8 * g4;   // rows >= 3 zero: no masked load
       s8v w2f[4];
-#if WS_L2PRE
       layer2<WS_L2PRE>(W1p, l16, g4, H1, a2, w2row, w2f, A2pre);
-#else
-      for (int rep = 0; rep < WS_L2REP; ++rep) layer2(W1p, l16, g4, H1, a2, w2row, w2f);
-#endif
       s8v H2[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H2[ks] = cat8(relu_bf(a2[2 * ks]), relu_bf(a2[2 * ks + 1]));
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         *reinterpret_cast<s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4)) = (i & 1) ? hi4(H2[i >> 1]) : lo4(H2[i >> 1]);
-#if WS_GDZ
-      // H2 again in pi order (the DZ2 area's layout): the gradient waves' dZ2 mask, one 16-byte read per k-step
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) *reinterpret_cast<s8v*>(sz2 + w1_off(l16, 32 * ks + 8 * g4)) = H2[ks];
-#endif
       WS_PIN(H2[3]);
-#if WS_PF_POS == 1 && !WS_NOPF
-      // the next tile's price windows: their registers are free from here (the peak of Q(x')'s layer 2 is
-      // no higher with them) to the next tile's features -- over half a tile of HBM latency hidden.
-      // Unconditional (env_of clamps the last tile) so the loop-carried registers need no phi copy (a copy
-      // of a register with a load in flight is a vmcnt(0) wait at the back edge); no store is issued
-      // between here and the features' wait (the env-state write-back is deferred), so that wait is for
-      // the windows alone.
-      WS_LOAD_PRICES(k + 1, e_pos)
-#endif
       WS_SB();
       WS_STAMP(5);
       f4v qa = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = WS_W2_EARLY ? w2f[ks] : lds_ld8(w2row + 32 * ks);
+        const s8v a = w2f[ks];
         qa = mfma32(a, H2[ks], qa);
       }
       WS_PIN(qa);
@@ -623,9 +567,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fxn(vnew));
         st_explore += exploit ? 0.f : 1.f;
       }
-#if WS_WBE
       WS_WB_SET()
-#endif
       WS_PIN(Xn6);
       WS_SB();
       WS_STAMP(7);
@@ -635,10 +577,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       s8v H1n[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1n[ks] = cat8(relu_bf(a1n[2 * ks]), relu_bf(a1n[2 * ks + 1]));
-      // (WS_PF_POS 0: the next tile's price windows issued here)
-#if WS_PF_POS == 0 && !WS_NOPF
+      // the next tile's price windows issued here
       WS_LOAD_PRICES(k + 1, e_pos)
-#endif
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);
       WS_SB();
@@ -649,7 +589,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       f4v qn = zero4();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const s8v a = WS_W2_EARLY ? w2f[ks] : lds_ld8(w2row + 32 * ks);
+        const s8v a = w2f[ks];
         qn = mfma32(a, H2n[ks], qn);
       }
       WS_PIN(qn);
@@ -660,14 +600,13 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       const bf16_t* zchunk = reinterpret_cast<const bf16_t*>(ctl + 10);   // 8 zero bytes
       s4v aw[8], h2m[8];
       auto dz_reads = [&]() {
-        if (WS_GDZ) return;   // (the gradient waves form dZ2)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           aw[i] = lds_tr4(g4 == 0 ? W2p + (l16 >> 2) * HP + pi_pos4(i, l16 & 3) : zchunk);
           h2m[i] = *reinterpret_cast<const s4v*>(sh2 + a_off(l16, 16 * i + 4 * g4));
         }
       };
-      if (WS_DZ_EARLY) dz_reads();
+      dz_reads();
       float dq = 0.f;
       int slot = 0;
       if (g4 == 0) {
@@ -688,9 +627,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
           fdone = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
           ndone = 1.f;
         }
-#if !WS_WBE
-        WS_WB_SET()
-#endif
         st_reward += rew;
         st_loss += diff * diff;
         st_qslot += qs;
@@ -706,8 +642,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // layer 2's accumulators.  dQ has one nonzero entry per env, so every output is one exact fp32 product.
       const s4v bq = g4 == 0 ? pk4(slot == 0 ? dq : 0.f, slot == 1 ? dq : 0.f, slot == 2 ? dq : 0.f, 0.f)
                              : zero_s4();
-#if !WS_GDZ
-      if (!WS_DZ_EARLY) dz_reads();
       s4v dz[8];
       f4v zt[8];
 #pragma unroll
@@ -715,15 +649,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) dz[i] = mask_pk(zt[i], h2m[i]);
       WS_PIN(dz[7]);
-#endif
       WS_SB();
       WS_STAMP(10);
-      // publish: (WS_GDZ 0: dZ2, pi order: tiles 2 ks, 2 ks + 1 form k-step ks) dQ in the X row's pad slots
-#if !WS_GDZ
+      // publish: (dZ2, pi order: tiles 2 ks, 2 ks + 1 form k-step ks) dQ in the X row's pad slots
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
         *reinterpret_cast<s8v*>(sz2 + w1_off(l16, 32 * ks + 8 * g4)) = cat8(dz[2 * ks], dz[2 * ks + 1]);
-#endif
       if (g4 == 0) *reinterpret_cast<s4v*>(sx + l16 * KX + 204) = bq;
       if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       WS_SB();
@@ -747,9 +678,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   } else {
     // ================================================================ GRADIENT WAVE
     const int gw = wave - ND;
-    if (WS_GPRIO) __builtin_amdgcn_s_setprio(WS_GPRIO);   // owns hidden units 32 gw .. 32 gw + 31 of both layers, dW2 columns likewise
+    // owns hidden units 32 gw .. 32 gw + 31 of both layers, dW2 columns likewise
     f4v gW0[2][13], gW1[2][8], gW2[2];
-#if WS_GPAIR
     // bias gradients as per-lane fp32 sums of the dZ2^T / dQ^T fragments (each lane's 8 envs per slot
     // pair), folded over the 4 lane groups at the write-out: 3 VGPRs instead of 12 + a ones operand
     float gB1s[2] = {0.f, 0.f}, gB2s = 0.f;
@@ -759,18 +689,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       for (int j = 0; j < 8; ++j) acc += bf2f((bf16_t)v[j]);
       return acc;
     };
-#else
-    f4v gB1[2], gB2 = zero4();
-#endif
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
 #pragma unroll
       for (int n = 0; n < 13; ++n) gW0[m][n] = zero4();
 #pragma unroll
       for (int n = 0; n < 8; ++n) gW1[m][n] = zero4();
-#if !WS_GPAIR
-      gB1[m] = zero4();
-#endif
       gW2[m] = zero4();
     }
     s4v ones;
@@ -786,7 +710,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     // (held in SGPRs and stored once per slot: the gradient wave has no VGPR to spare mid-slot)
     unsigned long long gts[7] = {0, 0, 0, 0, 0, 0, 0};
 #define WS_GST(I) if ((WS_STAMPS & 2) && ((WS_GST_MASK >> (I)) & 1)) gts[I] = __builtin_amdgcn_s_memtime(); WS_MARK(G, I)
-#if WS_GPAIR
     // slots in pairs (q, q + 1): the weight-gradient MFMAs run with K = 32 envs -- v_mfma_f32_16x16x32_bf16
     // at the cost of the K = 16 form for twice the work.  K index 8 g4 + j of lane group g4 is env
     // 4 g4 + (j & 3) of slot q (j < 4) or of slot q + 1 (j >= 4): the A and B fragments are the two slots'
@@ -795,14 +718,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     for (int q = 0; q < nseq; q += 2) {
       const int sa = q % NSLOT, sb = (q + 1) % NSLOT;
       WS_GST(0);
-      for (int spin = 0; lds_acq(ctl + 1 + sa) != q + 1; ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin > SPIN_LIMIT) { ws_fail(p); break; }
-      }
-      for (int spin = 0; lds_acq(ctl + 1 + sb) != q + 2; ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin > SPIN_LIMIT) { ws_fail(p); break; }
-      }
+      ring_wait(p, ctl, ctl + 1 + sa, [&](int v) { return v == q + 1; });
+      ring_wait(p, ctl, ctl + 1 + sb, [&](int v) { return v == q + 2; });
       WS_GST(1);
 #if WS_GSKIP
       if (lane == 0) {
@@ -821,32 +738,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto tr8 = [&](const bf16_t* a, const bf16_t* b, int off) { return cat8(lds_tr4(a + off), lds_tr4(b + off)); };
       // ---- dZ1 of both slots for this wave's u1 tiles (result lane (u1, g4): envs 4 g4 .. 4 g4 + 3)
       f4v c1a[2] = {zero4(), zero4()}, c1b[2] = {zero4(), zero4()};
-#if WS_GDZ
-      // dZ2 = (W2^T dQ) * [H2 > 0] formed here from the slot's dQ (the X rows' pad slots) and H2: A = W2^T
-      // tiles (lanes g4 == 0 hold W2[0..3][u2]), B = dQ^T (lanes g4 == 0 hold dQ[env][0..3]); the result
-      // tiles 2 ks, 2 ks + 1 side by side are dZ1's A operand for k-step ks (pi order), one exact fp32
-      // product per output as in the data wave's version
-      const s4v bqa = lds_ld4(g4 == 0 ? xa + l16 * KX + 204 : zchunk);
-      const s4v bqb = lds_ld4(g4 == 0 ? xb + l16 * KX + 204 : zchunk);
-      // (one address register for all W2^T reads: the other lane groups read zero row 4 at the same offsets;
-      //  the mask is H2 in pi order, which the data wave writes into the slot's DZ2 area for this)
-      const bf16_t* w2base = W2p + (g4 == 0 ? (l16 >> 2) * HP + 8 * (l16 & 3) : 4 * HP);
-      auto w2t = [&](int i) { return lds_tr4(w2base + 32 * (i >> 1) + 4 * (i & 1)); };
-      auto dzks = [&](const bf16_t* h2p, const s4v& bq, const s4v& aw0, const s4v& aw1, int ks) {
-        const s8v m = lds_ld8(h2p + w1_off(l16, 32 * ks + 8 * g4));
-        return cat8(mask_pk(mfma16(aw0, bq, zero4()), lo4(m)), mask_pk(mfma16(aw1, bq, zero4()), hi4(m)));
-      };
-#endif
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-#if WS_GDZ
-        const s4v aw0 = w2t(2 * ks), aw1 = w2t(2 * ks + 1);
-        const s8v aza = dzks(z2a, bqa, aw0, aw1, ks);
-        const s8v azb = dzks(z2b, bqb, aw0, aw1, ks);
-#else
         const s8v aza = lds_ld8(z2a + w1_off(l16, 32 * ks + 8 * g4));
         const s8v azb = lds_ld8(z2b + w1_off(l16, 32 * ks + 8 * g4));
-#endif
         const int R = 32 * ks + 4 * g4 + (l16 >> 2);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -855,7 +750,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
           c1a[t] = mfma32(aza, wt, c1a[t]);
           c1b[t] = mfma32(azb, wt, c1b[t]);
         }
-        if (WS_GDZ) WS_SB();   // (one k-step's fragments live at a time)
       }
       s4v bowna[2], bownb[2];   // own H1 tiles of both slots (the dZ1 mask)
 #pragma unroll
@@ -865,75 +759,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       constexpr int XD = WS_GXP;   // X fragment pairs read ahead of the dW0 MFMAs
       s8v bx[13];
-#if !WS_GDZ
 #pragma unroll
       for (int n = 0; n < XD; ++n) bx[n] = tr8(xa, xb, r4 * KX + 16 * n + 4 * qq);
-#endif
-#if WS_GDZ
-      // order: mask -> dW2 / db2, dW1 / db1 (their fragments live with a0 only) -> dW0 with the X reads ->
-      // both slots go back
-      WS_PIN(c1a[1]); WS_PIN(c1b[1]);
-      WS_SB();
-      WS_GST(2);
-      s8v a0[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) a0[t] = cat8(mask_pk(c1a[t], bowna[t]), mask_pk(c1b[t], bownb[t]));
-      WS_PIN(a0[1]);
-      WS_SB();
-      WS_GST(3);
-      s8v a1[2];
-      {
-        // dZ2^T tiles of this wave's u2 (the dW1 A operand, lane (u2, g4): envs 4 g4 ..): A = dQ (the same
-        // registers as dZ2's B), B = W2 (the same registers as dZ2's A), masked by H2 read transposed
-        s8v bh2[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const s4v aw = w2t(2 * gw + m);
-          a1[m] = cat8(mask_pk(mfma16(bqa, aw, zero4()), lo4(bh2[m])), mask_pk(mfma16(bqb, aw, zero4()), hi4(bh2[m])));
-        }
-        const s8v aq = qq == 0 ? tr8(xa, xb, r4 * KX + 204) : cat8(lds_tr4(zchunk), lds_tr4(zchunk));   // a = l16 < 4
-#pragma unroll
-        for (int n = 0; n < 2; ++n) gW2[n] = mfma32(aq, bh2[n], gW2[n]);
-        gB2s += sum8(aq);
-      }
-#pragma unroll
-      for (int m = 0; m < 2; ++m) gB1s[m] += sum8(a1[m]);
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        s8v bh[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) bh[k] = tr8(h1a, h1b, a_off(r4, 16 * (4 * half + k) + 4 * qq));
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) gW1[m][4 * half + k] = mfma32(a1[m], bh[k], gW1[m][4 * half + k]);
-      }
-      WS_SB();
-      WS_GST(4);
-      // ---- dW0^T[u1][slot col] += dZ1^T . X (K = 32 envs)
-#pragma unroll
-      for (int n = 0; n < XD; ++n) bx[n] = tr8(xa, xb, r4 * KX + 16 * n + 4 * qq);
-#pragma unroll
-      for (int n = 0; n < 13; ++n) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma32(a0[m], bx[n], gW0[m][n]);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        if (n + XD < 13) {
-          bx[n + XD] = tr8(xa, xb, r4 * KX + 16 * (n + XD) + 4 * qq);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        if (n + XD == 12) {   // the last X fragment is in flight: nothing else of the slots is read
-          if (lane == 0) {
-            __hip_atomic_fetch_add(ctl + 5 + sa, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(ctl + 5 + sb, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          WS_GST(5);
-        }
-      }
-      WS_PIN(gW0[1][12]);
-#else
       WS_PIN(c1a[1]); WS_PIN(c1b[1]);
       WS_SB();
       WS_GST(2);
@@ -960,26 +787,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // ---- dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
       //      (H1 fragments in two halves; both slots go back once the last fragment has landed)
       s8v a1[2];
-#if WS_GDZ
-      // dZ2^T tiles of this wave's u2 (the dW1 A operand, lane (u2, g4): envs 4 g4 ..): A = dQ (the same
-      // registers as dZ2's B), B = W2 (the same registers as dZ2's A), masked by H2 read transposed
-      s8v bh2[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
-      {
-        // (dQ re-read: holding it through dW0 costs the registers of an accumulator tile)
-        const s4v bqa2 = lds_ld4(g4 == 0 ? xa + l16 * KX + 204 : zchunk);
-        const s4v bqb2 = lds_ld4(g4 == 0 ? xb + l16 * KX + 204 : zchunk);
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const s4v aw = w2t(2 * gw + m);
-          a1[m] = cat8(mask_pk(mfma16(bqa2, aw, zero4()), lo4(bh2[m])), mask_pk(mfma16(bqb2, aw, zero4()), hi4(bh2[m])));
-        }
-      }
-#else
 #pragma unroll
       for (int m = 0; m < 2; ++m) a1[m] = tr8(z2a, z2b, w1_off(r4, pi_pos4(2 * gw + m, qq)));
-#endif
 #pragma unroll
       for (int m = 0; m < 2; ++m) gB1s[m] += sum8(a1[m]);
 #pragma unroll
@@ -994,11 +803,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       {
         const s8v aq = qq == 0 ? tr8(xa, xb, r4 * KX + 204) : cat8(lds_tr4(zchunk), lds_tr4(zchunk));   // a = l16 < 4
-#if !WS_GDZ
         s8v bh2[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) bh2[k] = tr8(h2a, h2b, a_off(r4, 16 * (2 * gw + k) + 4 * qq));
-#endif
         if (lane == 0) {
           __hip_atomic_fetch_add(ctl + 5 + sa, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_fetch_add(ctl + 5 + sb, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1008,7 +815,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         for (int n = 0; n < 2; ++n) gW2[n] = mfma32(aq, bh2[n], gW2[n]);
         gB2s += sum8(aq);
       }
-#endif
       WS_PIN(gW1[1][7]); WS_PIN(gB2s);
       WS_SB();
       WS_GST(6);
@@ -1017,166 +823,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         for (int i = 0; i < 7; ++i) gst[8 * q + i] = gts[i];
       }
     }
-#else
-    for (int q = 0; q < nseq; ++q) {
-      const int sl = q % NSLOT;
-      WS_GST(0);
-      for (int spin = 0; lds_acq(ctl + 1 + sl) != q + 1; ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin > SPIN_LIMIT) { ws_fail(p); break; }
-      }
-      WS_GST(1);
-#if WS_GSKIP
-      // timing build: the gradient waves only hand the slots back (how fast do the data waves run alone?)
-      if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      continue;
-#endif
-      const char* sb = smem + oSLOT + sl * SLOT_BYTES;
-      const bf16_t* sx = reinterpret_cast<const bf16_t*>(sb + sX);
-      const bf16_t* sh1 = reinterpret_cast<const bf16_t*>(sb + sH1);
-      const bf16_t* sh2 = reinterpret_cast<const bf16_t*>(sb + sH2);
-      const bf16_t* sz2 = reinterpret_cast<const bf16_t*>(sb + sDZ2);
-      // ---- dZ1 for this wave's u1 tiles i = 2 gw + t:  C[env][u1] = sum_u2 dZ2[env][u2] W1[u2][u1]
-      //      (A = dZ2 rows in pi order, B = W1 read transposed from W1p); the result lane (u1, g4) holds envs
-      //      4 g4 .. 4 g4 + 3 -- the A layout of the dW0 MFMA, no transpose needed
-#if WS_GPIPE
-      // issue order = latency order, within the ~68 VGPRs beside the accumulators: dZ1's fragments two
-      // k-steps ahead of its MFMAs; the mask's H1 tiles and all of X before the mask; the dW1 / dW2
-      // fragments under the second half of the dW0 MFMAs; the slot goes back once the last has landed
-      f4v c1[2] = {zero4(), zero4()};
-      {
-        s8v az[4];
-        s4v wt[4][2][2];
-        auto rd = [&](int ks) {
-          az[ks] = lds_ld8(sz2 + w1_off(l16, 32 * ks + 8 * g4));
-          const int R = 32 * ks + 4 * g4 + (l16 >> 2);
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const int col = pi_pos4(2 * gw + t, qq);
-            wt[ks][t][0] = lds_tr4(W1p + w1_off(R, col));
-            wt[ks][t][1] = lds_tr4(W1p + w1_off(R + 16, col));
-          }
-        };
-        constexpr int ZD = WS_GZ;   // k-steps of dZ1 fragments read ahead
-#pragma unroll
-        for (int ks = 0; ks < ZD; ++ks) rd(ks);
-        __builtin_amdgcn_sched_group_barrier(0x100, 5 * ZD, 0);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          if (ks + ZD < 4) rd(ks + ZD);
-          if (ks + ZD < 4) __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
-#pragma unroll
-          for (int t = 0; t < 2; ++t) c1[t] = mfma32(az[ks], cat8(wt[ks][t][0], wt[ks][t][1]), c1[t]);
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
-      }
-      s4v bown[2], bx[13];   // own H1 tiles; X^T fragments
-#pragma unroll
-      for (int t = 0; t < 2; ++t) bown[t] = lds_tr4(sh1 + a_off(r4, 16 * (2 * gw + t) + 4 * qq));
-      constexpr int XD = WS_GX;   // X fragments read ahead of the dW0 MFMAs
-#pragma unroll
-      for (int n = 0; n < XD; ++n) bx[n] = lds_tr4(sx + r4 * KX + 16 * n + 4 * qq);
-      WS_PIN(c1[0]); WS_PIN(c1[1]);
-      WS_SB();
-      WS_GST(2);
-      s4v a0[2];   // (own tiles read separately: bh[2 gw + t] would be a dynamic index -> scratch)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) a0[t] = mask_pk(c1[t], bown[t]);
-      WS_PIN(a0[1]);
-      WS_SB();
-      WS_GST(3);
-      // ---- dW0^T[u1][slot] += dZ1^T . X; the dW1 / dW2 fragments issued half way
-      s4v bh[8], a1[2], aq, bh2[2];   // H1[env 4 g4 .. + 3][u1 = 16 n + l16], dZ2^T, dQ^T[a][env], H2 tiles
-#pragma unroll
-      for (int n = 0; n < 13; ++n) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma16(a0[m], bx[n], gW0[m][n]);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        if (n + XD < 13) {
-          bx[n + XD] = lds_tr4(sx + r4 * KX + 16 * (n + XD) + 4 * qq);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        if (n == WS_GH) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) bh[k] = lds_tr4(sh1 + a_off(r4, 16 * k + 4 * qq));
-#pragma unroll
-          for (int m = 0; m < 2; ++m) a1[m] = lds_tr4(sz2 + w1_off(r4, pi_pos4(2 * gw + m, qq)));
-          aq = lds_tr4(qq == 0 ? sx + r4 * KX + 204 : zchunk);   // a = l16 < 4
-#pragma unroll
-          for (int k = 0; k < 2; ++k) bh2[k] = lds_tr4(sh2 + a_off(r4, 16 * (2 * gw + k) + 4 * qq));
-          __builtin_amdgcn_sched_group_barrier(0x100, 13, 0);
-        }
-      }
-      WS_PIN(gW0[1][12]);
-      WS_SB();
-      WS_GST(4);
-      // every fragment of the slot is in registers: hand the slot back
-      if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      WS_GST(5);
-#else
-      f4v c1[2] = {zero4(), zero4()};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const s8v az = lds_ld8(sz2 + w1_off(l16, 32 * ks + 8 * g4));
-        const int R = 32 * ks + 4 * g4 + (l16 >> 2);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int col = pi_pos4(2 * gw + t, qq);
-          c1[t] = mfma32(az, cat8(lds_tr4(W1p + w1_off(R, col)), lds_tr4(W1p + w1_off(R + 16, col))), c1[t]);
-        }
-      }
-      WS_PIN(c1[0]); WS_PIN(c1[1]);
-      WS_SB();
-      WS_GST(2);
-      s4v bh[8];   // H1[env 4 g4 .. + 3][u1 = 16 n + l16]
-#pragma unroll
-      for (int n = 0; n < 8; ++n) bh[n] = lds_tr4(sh1 + a_off(r4, 16 * n + 4 * qq));
-      s4v a0[2];   // (own tiles read again: bh[2 gw + t] would be a dynamic index -> scratch)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) a0[t] = mask_pk(c1[t], lds_tr4(sh1 + a_off(r4, 16 * (2 * gw + t) + 4 * qq)));
-      WS_PIN(a0[1]);
-      WS_SB();
-      WS_GST(3);
-      // ---- dW0^T[u1][slot] += dZ1^T . X
-#pragma unroll
-      for (int n = 0; n < 13; ++n) {
-        const s4v b = lds_tr4(sx + r4 * KX + 16 * n + 4 * qq);
-#pragma unroll
-        for (int m = 0; m < 2; ++m) gW0[m][n] = mfma16(a0[m], b, gW0[m][n]);
-      }
-      WS_PIN(gW0[1][12]);
-      WS_SB();
-      WS_GST(4);
-      // ---- dW1^T[u2][u1] += dZ2^T . H1, db1 += dZ2^T . 1 ; dW2^T[a][u2] += dQ^T . H2, db2 += dQ^T . 1
-      s4v a1[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) a1[m] = lds_tr4(sz2 + w1_off(r4, pi_pos4(2 * gw + m, qq)));
-      const s4v aq = lds_tr4(qq == 0 ? sx + r4 * KX + 204 : zchunk);   // dQ^T[a][env]: a = l16 < 4
-      s4v bh2[2];
-#pragma unroll
-      for (int n = 0; n < 2; ++n) bh2[n] = lds_tr4(sh2 + a_off(r4, 16 * (2 * gw + n) + 4 * qq));
-      // every fragment of the slot is in registers: hand the slot back before the MFMAs
-      if (lane == 0) __hip_atomic_fetch_add(ctl + 5 + sl, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      WS_GST(5);
-#endif
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-#pragma unroll
-        for (int n = 0; n < 8; ++n) gW1[m][n] = mfma16(a1[m], bh[n], gW1[m][n]);
-        gB1[m] = mfma16(a1[m], ones, gB1[m]);
-      }
-#pragma unroll
-      for (int n = 0; n < 2; ++n) gW2[n] = mfma16(aq, bh2[n], gW2[n]);
-      gB2 = mfma16(aq, ones, gB2);
-      WS_PIN(gW1[1][7]); WS_PIN(gB2);
-      WS_SB();
-      WS_GST(6);
-      if ((WS_STAMPS & 2) && gst) {
-#pragma unroll
-        for (int i = 0; i < 7; ++i) gst[8 * q + i] = gts[i];
-      }
-    }
-#endif
     __syncthreads();
     // ------------------------------------------------------------------ gradient slab write-out
     // this wave's rows: dW0^T / dW1^T rows 32 gw + 16 m + 4 g4 + j; dW2^T u2 columns 16 (2 gw + n) + l16
@@ -1197,11 +843,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         for (int n = 0; n < 13; ++n) put(p.off_w0 + u * INP + slot_col(16 * n + l16), gW0[m][n][j]);
 #pragma unroll
         for (int n = 0; n < 8; ++n) put(p.off_w1 + u * HP + 16 * n + l16, gW1[m][n][j]);
-#if !WS_GPAIR
-        if (l16 == 0) put(p.off_b1 + u, gB1[m][j]);
-#endif
       }
-#if WS_GPAIR
     // bias gradients: fold the 4 lane groups' partial sums (lane (l16, g4): 8 envs of each slot pair)
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -1216,16 +858,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       v += __shfl_xor(v, 32, 64);
       if (gw == 0 && g4 == 0 && l16 < 4) put(p.off_b2 + l16, v);
     }
-#endif
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int j = 0; j < 4; ++j) put(p.off_w2 + (4 * g4 + j) * HP + 16 * (2 * gw + n) + l16, gW2[n][j]);
-#if !WS_GPAIR
-    if (gw == 0 && l16 == 0)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) put(p.off_b2 + 4 * g4 + j, gB2[j]);
-#endif
   }
 #undef WS_SB
 #undef WS_PIN

@@ -154,9 +154,10 @@ class EngineConfig:
     # fused bf16 step kernel: "auto" (ws where its geometry fits, else by chunk), "ws" (csrc/qstep_ws.hip:
     # wave-specialised, data waves run whole 16-env tiles, gradient waves consume them through an LDS ring;
     # E % 64 == 0, history 201, dims 224-128-128, static schedule), "wide" (csrc/qstep_wide.hip, 64-env
-    # chunks), "narrow" (csrc/qstep_fused.hip, 32-env chunks) or "pair" (csrc/qstep_pair.hip)
+    # chunks) or "narrow" (csrc/qstep_fused.hip, 32-env chunks)
     step_kernel: str = "auto"
-    step_variant: str = ""          # tuning builds of the 64-env-chunk kernel (st_qstep_wide_launch_<v>); "" = default
+    step_variant: str = ""          # timing / debug build of the ws kernel (csrc/ab/qstep_ws_<v>.hip); opt-in only
+                                    # (SHARETRADE_AB_BUILDS=1, several compute wrong results); "" = production
     graph: bool = True              # capture the step in a HIP graph
     graph_steps: int = 16           # steps per graph replay in VectorEngine.run (fewer launch boundaries)
     backend: str = "auto"           # auto | native | torch

@@ -118,9 +118,13 @@ def env_transition(a: torch.Tensor, b: torch.Tensor, s: torch.Tensor, v_prev: to
 
 def select_actions(q: torch.Tensor, pos: torch.Tensor, env_ids: np.ndarray, step: int, seed: int,
                    rank: int, epsilon: float, ramp: float, n_actions: int = 3):
-    """Epsilon-greedy with the exploit ramp ``min(eps, i/ramp)`` (QDecisionPolicyActor.scala:58-62)."""
+    """Epsilon-greedy with the exploit ramp ``min(eps, i/ramp)`` (QDecisionPolicyActor.scala:58-62).
+    ``epsilon = inf``: the greedy policy (exploit at every position, as the kernels' eps = inv_ramp = inf)."""
     u1, u2 = rng.uniforms(seed, rank, env_ids, step)
-    thr = np.minimum(np.float32(epsilon), pos.cpu().numpy().astype(np.float32) * np.float32(1.0 / ramp))
+    if np.isinf(epsilon):
+        thr = np.full(u1.shape, np.inf, dtype=np.float32)
+    else:
+        thr = np.minimum(np.float32(epsilon), pos.cpu().numpy().astype(np.float32) * np.float32(1.0 / ramp))
     exploit = torch.from_numpy(u1 < thr)
     greedy = torch.argmax(q[:, :n_actions].cpu(), dim=1)  # first max on ties (like TF ArgMax)
     rnd = torch.from_numpy(np.minimum((u2 * np.float32(n_actions)).astype(np.int64), n_actions - 1))

@@ -64,9 +64,40 @@ class OptimParams(C.Structure):
 ENV_ROWS = ("pos", "budget", "shares", "value", "ret_sum", "episodes", "last_final", "actions_out", "rewards_out")
 
 
-def variant_launch(suffix: str, prefix: str = "st_qstep_wide_launch_"):
-    """``<prefix><suffix>`` of a tuning / timing build of a step kernel (same params)."""
-    fn = getattr(lib(), prefix + suffix)
+# Timing / debug builds of the flagship step kernel (csrc/ab/*.hip: per-phase stamps, phases skipped or
+# run twice to price them).  They are NOT in the production library: `python build.py --ab` (or
+# SHARETRADE_AB_BUILDS=1) builds them into their own libsharetrade_ab.so, and nothing loads it unless
+# SHARETRADE_AB_BUILDS=1 is set.  Builds in WRONG_RESULT_VARIANTS compute wrong results by design.
+AB_LIB_PATH = os.path.join(LIB_DIR, "libsharetrade_ab.so")
+WRONG_RESULT_VARIANTS = frozenset({"gskip", "gskipst", "l1x2", "l2x2", "nopf", "nowb", "nophil"})
+_ab_lib: Optional[C.CDLL] = None
+
+
+def ab_builds_enabled() -> bool:
+    return os.environ.get("SHARETRADE_AB_BUILDS", "") not in ("", "0")
+
+
+def ab_lib() -> C.CDLL:
+    global _ab_lib
+    if not ab_builds_enabled():
+        raise RuntimeError("timing / debug kernel builds are opt-in: set SHARETRADE_AB_BUILDS=1 and run "
+                           "`python build.py --ab` (csrc/ab/*.hip -> libsharetrade_ab.so)")
+    if _ab_lib is None:
+        if not os.path.exists(AB_LIB_PATH):
+            raise NativeUnavailable(f"{AB_LIB_PATH} not built: run `SHARETRADE_AB_BUILDS=1 python build.py`")
+        lib()   # the production library first (HIP runtime, shared entry points)
+        _ab_lib = C.CDLL(AB_LIB_PATH)
+    return _ab_lib
+
+
+def variant_launch(suffix: str, prefix: str = "st_qstep_ws_launch_"):
+    """``<prefix><suffix>`` of a timing / debug build of a step kernel (same params), from the opt-in
+    A/B library.  Refused unless SHARETRADE_AB_BUILDS=1: several of these builds compute wrong results
+    on purpose (WRONG_RESULT_VARIANTS) and must never be selected by a production config."""
+    if not ab_builds_enabled():
+        bad = " (computes WRONG results by design)" if suffix in WRONG_RESULT_VARIANTS else ""
+        raise RuntimeError(f"engine.step_variant={suffix!r}{bad} needs SHARETRADE_AB_BUILDS=1")
+    fn = getattr(ab_lib(), prefix + suffix)
     fn.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     fn.restype = C.c_int
     return fn
@@ -94,14 +125,8 @@ def lib() -> C.CDLL:
     L.st_qstep_wide_lds_bytes.restype = C.c_int
     L.st_qstep_wide_launch_w8.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_qstep_wide_launch_w8.restype = C.c_int
-    L.st_qstep_pair_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
-    L.st_qstep_pair_launch.restype = C.c_int
-    L.st_qstep_pair_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
-    L.st_qstep_pair_lds_bytes.restype = C.c_int
     L.st_qstep_ws_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_qstep_ws_launch.restype = C.c_int
-    L.st_qstep_ws_launch_stamps.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
-    L.st_qstep_ws_launch_stamps.restype = C.c_int
     L.st_qstep_ws_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
     L.st_qstep_ws_lds_bytes.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
@@ -167,13 +192,6 @@ def qstep_wide_supported(inp: int, h1p: int, h2p: int) -> bool:
     if not available():
         return False
     return lib().st_qstep_wide_lds_bytes(inp, h1p, h2p) > 0
-
-
-def qstep_pair_supported(inp: int, h1p: int, h2p: int) -> bool:
-    """Two-slot pipelined variant (csrc/qstep_pair.hip: two 32-env chunks in flight per workgroup)."""
-    if not available():
-        return False
-    return lib().st_qstep_pair_lds_bytes(inp, h1p, h2p) > 0
 
 
 def qstep_ws_supported(inp: int, h1p: int, h2p: int) -> bool:

@@ -93,13 +93,24 @@ def _train_episode(rank, world, gen, ctx, cfg, prices: np.ndarray, envs: int, ck
         start = eng.step_count
     eng.sync_params_from(0)          # re-dispatch: every rank continues from rank 0's learner state
     if eng.backend == "native" and cfg.engine.graph:
-        # the synchronous DP step (kernel, slab reduce, RCCL all-reduce, optimizer) as one HIP graph;
-        # every rank captures (no collective runs during a capture), gloo groups stay eager
-        eng.capture_graph(warmup=0)
-    for step in range(start, steps):
-        fail_point(rank, step, gen)
-        eng.step()
-        s = step + 1
+        # the synchronous DP step (kernel, slab reduce, RCCL all-reduce, optimizer) in HIP graphs; every
+        # rank captures (no collective runs during a capture) and the ranks vote: a capture failure on
+        # one rank sends every rank down the eager path (gloo groups stay eager)
+        from ..trainer.benchkit import capture_with_vote
+
+        capture_with_vote(eng, rank, world, ctx.group, warmup=0)
+    step = start
+    while step < steps:
+        # one multi-step graph replay at a time (VectorEngine.run), never across a progress / checkpoint
+        # point; the fault-injection points of every step of it are checked before it runs
+        nxt = min(steps, step + max(1, int(cfg.engine.graph_steps)))
+        for every in (progress_every, ckpt_every):
+            if every:
+                nxt = min(nxt, (step // every + 1) * every)
+        for s_ in range(step, nxt):
+            fail_point(rank, s_, gen)
+        eng.run(nxt - step)
+        step = s = nxt
         if progress_every and s % progress_every == 0:
             conn.send(("progress", rank, s))
         if ckpt_every and s % ckpt_every == 0 and s < steps:

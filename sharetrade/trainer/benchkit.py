@@ -16,6 +16,7 @@ reference's equivalent invariant: ``router.route(Train(d))`` reaches every route
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import sys
@@ -93,6 +94,30 @@ def prepare_steps(eng, want_graph: bool, rank: int, world: int, group=None, prim
     return use_graph, eng.step_count - start
 
 
+def capture_with_vote(eng, rank: int, world: int, group=None, warmup: int = 0, log=None) -> bool:
+    """Capture ``eng``'s step graphs and agree across ranks (all-reduce MIN) whether to replay them.
+
+    A rank whose capture raises or returns False drops its graphs with ``_drop_graphs`` (the HIP
+    runtime's sticky capture error cleared and the device synchronised, so its first eager launch does
+    not report the failed capture); if any rank failed, every rank drops its graphs and runs eager
+    steps -- the same collectives everywhere.  ``SHARETRADE_FAIL_CAPTURE`` injects the failure."""
+    log = log or (lambda m: print(m, file=sys.stderr))
+    ok = False
+    try:
+        if _fail_capture_here(rank):
+            raise RuntimeError("injected capture failure (SHARETRADE_FAIL_CAPTURE)")
+        ok = bool(eng.capture_graph(warmup=warmup))
+    except Exception as e:  # noqa: BLE001 -- eager launches, same math
+        log(f"rank {rank}: HIP graph capture failed ({str(e).splitlines()[0] if str(e) else type(e).__name__})")
+        ok = False
+    if not ok:
+        _drop_graphs(eng)
+    use = agree(ok, world, group, getattr(eng, "device", None))
+    if not use:
+        _drop_graphs(eng)
+    return use
+
+
 def _drop_graphs(eng) -> None:
     eng._graph, eng._graph_k = None, None
     if getattr(eng, "device", torch.device("cpu")).type == "cuda":
@@ -119,42 +144,34 @@ def reset_episodes(eng) -> torch.Tensor:
     return st.episodes.clone()
 
 
-def full_episode_returns(eng, world: int = 1, group=None, random_policy: bool = False) -> Dict[str, float]:
-    """One complete episode per env (``T - H`` steps, online learning on), then mean / population
-    std of (final portfolio - initial budget) over every env of every rank.
-
-    ``random_policy``: the epsilon-greedy exploit probability is forced to 0 for this episode (every
-    action uniform over Buy / Sell / Hold, same draws, same banks): the baseline a learned policy has
-    to beat.  Native engines run it with eager launches (the captured graphs hold the old
-    parameters struct); the learner still updates, which does not change a random policy's actions."""
-    steps = int(eng.T - eng.H)
-    ep0 = reset_episodes(eng)
-    if random_policy:
-        if eng.backend == "native":
-            qp = eng._qp
-            saved = qp.eps
-            qp.eps = 0.0
-            try:
-                for _ in range(steps):
-                    eng._native_step()
-                    eng.step_count += 1
-            finally:
-                qp.eps = saved
-        else:
-            saved = eng.cfg.agent.epsilon
-            eng.cfg.agent.epsilon = 0.0
-            try:
-                eng.run(steps)
-            finally:
-                eng.cfg.agent.epsilon = saved
-    else:
-        eng.run(steps)
+@contextlib.contextmanager
+def evaluation_snapshot(eng):
+    """Run an evaluation on the engine and put everything back afterwards: parameters, optimizer state,
+    step counters, env state and the step-statistics accumulators (an evaluation episode moves the env
+    positions, the optimizer moments -- even at lr 0 -- and the statistics)."""
     eng.synchronize()
+    snap = eng.state_dict()
+    acc = [t.clone() for t in (getattr(eng, "stat_acc", None), getattr(eng, "stats", None)) if torch.is_tensor(t)]
+    try:
+        yield eng
+    finally:
+        eng.synchronize(check=False)
+        eng.load_state_dict(snap)
+        for t, c in zip([t for t in (getattr(eng, "stat_acc", None), getattr(eng, "stats", None))
+                         if torch.is_tensor(t)], acc):
+            t.copy_(c)
+        eng.synchronize()
+
+
+def _episode_summary(eng, ep0: torch.Tensor, world: int, group, steps: int) -> Dict[str, float]:
     st = eng.state
     done = st.episodes > ep0
     fin = st.last_final.double() - float(eng.cfg.env.budget)
     fin = torch.where(done, fin, torch.zeros_like(fin))
-    dev = fin.device
+    return _reduce_returns(done, fin, eng.E, world, group, steps)
+
+
+def _reduce_returns(done: torch.Tensor, fin: torch.Tensor, E: int, world: int, group, steps: int) -> Dict[str, float]:
     s = torch.stack([done.double().sum(), fin.sum(), (fin * fin).sum()])
     if world > 1:
         dist = _dist()
@@ -162,9 +179,70 @@ def full_episode_returns(eng, world: int = 1, group=None, random_policy: bool = 
             s = s.cpu()
         dist.all_reduce(s, group=group)
     n, sx, sxx = (float(v) for v in s.cpu())
-    n_total = float(eng.E * world)
+    n_total = float(E * world)
     if n == 0:
         return {"n": 0, "mean": math.nan, "std": math.nan, "steps": steps, "complete_frac": 0.0}
     m = sx / n
     return {"n": int(n), "mean": m, "std": math.sqrt(max(0.0, sxx / n - m * m)), "steps": steps,
             "complete_frac": n / n_total}
+
+
+def greedy_episode_returns(eng, world: int = 1, group=None, params: Optional[torch.Tensor] = None) -> Dict[str, float]:
+    """One complete episode per env with the CURRENT parameters (or ``params``, e.g. the random init)
+    frozen and the greedy policy (exploit at every step, no exploration, no learning: the optimizer runs
+    at lr 0), on a snapshot of the engine that is restored afterwards.  This measures the learned policy
+    itself, without the epsilon-greedy schedule of the online episodes (whose first ~1,000 steps are
+    mostly random)."""
+    steps = int(eng.T - eng.H)
+    with evaluation_snapshot(eng):
+        if params is not None:
+            eng.set_params(params)
+        ep0 = reset_episodes(eng)
+        with eng.policy_overrides(epsilon=math.inf, lr=0.0):
+            p0 = eng.params.detach().clone()
+            eng.run(steps)
+            eng.synchronize()
+            if not torch.equal(p0, eng.params):
+                raise RuntimeError("greedy evaluation changed the parameters (lr 0 expected to freeze them)")
+        out = _episode_summary(eng, ep0, world, group, steps)
+    return out
+
+
+def buy_and_hold_returns(eng, world: int = 1, group=None) -> Dict[str, float]:
+    """The buy-and-hold baseline on the engine's own price banks, within its action space: Buy at every
+    step (one share whenever the budget covers the price, as the env's Buy does), so the budget goes
+    into shares at the start of the episode and the position is then held to the end.  Same arithmetic
+    as the env step (fp32, one rounding per operation); returns final portfolio - initial budget."""
+    c = eng.cfg.env
+    P = eng.prices
+    H, T = int(eng.H), int(eng.T)
+    steps = T - H
+    b = torch.full((P.shape[0],), float(c.budget), dtype=torch.float32, device=P.device)
+    sh = torch.full((P.shape[0],), int(c.shares), dtype=torch.int32, device=P.device)
+    for pos in range(steps):
+        v = P[:, pos + H]
+        buy = b >= v
+        b = torch.where(buy, b - v, b)
+        sh = sh + buy.to(torch.int32)
+    fin = (b + sh.to(torch.float32) * P[:, T - 1]).double() - float(c.budget)
+    done = torch.ones_like(fin, dtype=torch.bool)
+    return _reduce_returns(done, fin, P.shape[0], world, group, steps)
+
+
+def full_episode_returns(eng, world: int = 1, group=None, random_policy: bool = False) -> Dict[str, float]:
+    """One complete episode per env (``T - H`` steps, online learning on), then mean / population
+    std of (final portfolio - initial budget) over every env of every rank.
+
+    ``random_policy``: the epsilon-greedy exploit probability is forced to 0 for this episode (every
+    action uniform over Buy / Sell / Hold, same draws, same banks): the baseline a learned policy has
+    to beat.  It runs with eager launches (``policy_overrides``); the learner still updates, which does
+    not change a random policy's actions."""
+    steps = int(eng.T - eng.H)
+    ep0 = reset_episodes(eng)
+    if random_policy:
+        with eng.policy_overrides(epsilon=0.0):
+            eng.run(steps)
+    else:
+        eng.run(steps)
+    eng.synchronize()
+    return _episode_summary(eng, ep0, world, group, steps)

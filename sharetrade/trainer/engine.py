@@ -22,6 +22,8 @@ rehearsal) and as the numerics reference; it is never chosen silently on a GPU.
 """
 from __future__ import annotations
 
+import contextlib
+
 import math
 import time
 from typing import Dict, Optional
@@ -133,21 +135,19 @@ class VectorEngine:
             # bf16: the fused MFMA step kernel (csrc/qstep_fused.hip);
             # fp32: the exact-fp32 row kernels (csrc/mlp_f32.hip) — any MLP up to 6 layers x 1024
             self.kernel = "bf16_fused" if fused_ok else "fp32_rows"
-        # envs per chunk of the fused kernel: 64 -> csrc/qstep_wide.hip, 32 -> csrc/qstep_fused.hip;
-        # step_kernel "pair" -> csrc/qstep_pair.hip (two 32-env slots per workgroup: chunk = 64 envs of
-        # work per workgroup and cycle)
+        # envs per chunk of the fused kernel: 64 -> csrc/qstep_wide.hip / csrc/qstep_ws.hip, 32 ->
+        # csrc/qstep_fused.hip
         self.chunk = 32
         self.step_kernel = "narrow"
         sk = cfg.engine.step_kernel
-        if sk not in ("auto", "wide", "narrow", "pair", "ws"):
+        if sk not in ("auto", "wide", "narrow", "ws"):
             raise ValueError(f"engine.step_kernel: {sk!r}")
-        if self.kernel == "bf16_fused" and sk == "pair":
-            if not (self.E % 64 == 0 and native.qstep_pair_supported(L.pdims[0], L.pdims[1], L.pdims[2])):
-                raise NotImplementedError(f"engine.step_kernel='pair' needs E % 64 == 0 and padded dims "
-                                          f"(224, 128, 128); got E={self.E}, dims {L.pdims}")
-            self.chunk, self.step_kernel = 64, "pair"
-        elif self.kernel == "bf16_fused" and (sk == "ws" or (sk == "auto" and int(cfg.engine.chunk) == 0
-                                                            and not cfg.engine.step_variant
+        if cfg.engine.step_variant:
+            # timing / debug builds of the ws kernel only; refused unless SHARETRADE_AB_BUILDS=1
+            if sk not in ("auto", "ws"):
+                raise ValueError("engine.step_variant selects a build of the ws kernel (step_kernel 'ws')")
+            native.variant_launch(cfg.engine.step_variant)
+        if self.kernel == "bf16_fused" and (sk == "ws" or (sk == "auto" and int(cfg.engine.chunk) == 0
                                                             and cfg.engine.step_waves == 8 and self.ws_ok(cfg, L))):
             if not self.ws_ok(cfg, L):
                 raise NotImplementedError(f"engine.step_kernel='ws' needs E % 64 == 0, history 201, padded dims "
@@ -255,7 +255,7 @@ class VectorEngine:
             self._f32 = F32EngineStep(self)
             return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
-        # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide / pair
+        # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide
         # kernels; one padded copy for ws (4-B-aligned dwordx4 reads, as fast: profiles/r3_ws_ab.md)
         self.prices4 = native.replicate4(self.prices, 1 if self.step_kernel == "ws" else 4)
         native.to_bf16(self.params, self.params_bf)
@@ -356,16 +356,13 @@ class VectorEngine:
 
     def _launch_qstep(self, L, sh) -> None:
         if self.step_kernel == "ws":
-            # the stamps build only when a stamp buffer is attached (tools/stamp_qstep.py)
-            fn = L.st_qstep_ws_launch_stamps if self._qp.stamps else L.st_qstep_ws_launch
-            if self.cfg.engine.step_variant:   # timing builds (csrc/qstep_ws_<v>.hip), same contract
-                fn = native.variant_launch(self.cfg.engine.step_variant, "st_qstep_ws_launch_")
-        elif self.step_kernel == "pair":
-            fn = L.st_qstep_pair_launch
+            fn = L.st_qstep_ws_launch
+            if self._qp.stamps:   # tools/stamp_qstep.py: the debug stamps build (opt-in A/B library)
+                fn = native.variant_launch(self.cfg.engine.step_variant or "stamps")
+            elif self.cfg.engine.step_variant:   # timing builds (csrc/ab/qstep_ws_<v>.hip), same contract
+                fn = native.variant_launch(self.cfg.engine.step_variant)
         elif self.chunk == 64:
             fn = L.st_qstep_wide_launch_w8 if self.cfg.engine.step_waves == 8 else L.st_qstep_wide_launch
-            if self.cfg.engine.step_variant:   # tuning builds (csrc/qstep_wide8_<v>.hip), same contract
-                fn = native.variant_launch(self.cfg.engine.step_variant)
         else:
             fn = L.st_qstep_launch
         d = self.layout.pdims
@@ -473,6 +470,46 @@ class VectorEngine:
     def serving_params(self) -> torch.Tensor:
         """The weights to serve: the Polyak average when engine.ema_decay > 0, else the live ones."""
         return self.params_ema if self.params_ema is not None else self.params
+
+    @contextlib.contextmanager
+    def policy_overrides(self, epsilon: Optional[float] = None, lr: Optional[float] = None):
+        """Temporarily change the behaviour policy / learning rate of the eager step (evaluation
+        episodes).  ``epsilon = inf`` is the greedy policy: every kernel's exploit test is
+        ``u < min(eps, pos * inv_ramp)``, and with eps = inv_ramp = +inf the threshold is +inf at every
+        position (at pos 0, 0 * inf is NaN and min(inf, NaN) = inf).  ``epsilon = 0``: uniform random
+        actions.  ``lr = 0``: the optimizer's update is exactly zero (frozen weights; its moment
+        estimates still move -- restore them from a snapshot).  Captured graphs hold the original
+        parameter structs, so they are set aside while the overrides are active: steps run eagerly."""
+        saved_graphs = (self._graph, getattr(self, "_graph_k", None))
+        self._graph, self._graph_k = None, None
+        a = self.cfg.agent
+        undo = []
+        inv = None if epsilon is None else (math.inf if math.isinf(epsilon) else float(np.float32(1.0 / a.ramp)))
+        if self.backend == "native" and self.kernel == "fp32_rows":
+            r, o = self._f32.rows, self._f32.optim
+            undo.append((r, "eps", r.eps)); undo.append((r, "inv_ramp", r.inv_ramp)); undo.append((o, "lr", o.lr))
+            if epsilon is not None:
+                r.eps, r.inv_ramp = float(epsilon), inv
+            if lr is not None:
+                o.lr = float(lr)
+        elif self.backend == "native":
+            q, o = self._qp, self._op
+            undo.append((q, "eps", q.eps)); undo.append((q, "inv_ramp", q.inv_ramp)); undo.append((o, "lr", o.lr))
+            if epsilon is not None:
+                q.eps, q.inv_ramp = float(epsilon), inv
+            if lr is not None:
+                o.lr = float(lr)
+        undo.append((a, "epsilon", a.epsilon)); undo.append((a, "lr", a.lr))
+        if epsilon is not None:
+            a.epsilon = float(epsilon)
+        if lr is not None:
+            a.lr = float(lr)
+        try:
+            yield self
+        finally:
+            for obj, k, v in reversed(undo):
+                setattr(obj, k, v)
+            self._graph, self._graph_k = saved_graphs
 
     def step(self) -> None:
         if self.backend == "native":
@@ -626,6 +663,13 @@ class VectorEngine:
             return self.step_count
         return self.opt.t
 
+    def set_params(self, params: torch.Tensor) -> None:
+        """Overwrite the live parameters (fp32 master copy and, for the bf16 kernels, its bf16 image)."""
+        self.params.copy_(params.to(self.device))
+        self.params.mul_(self._real)
+        if self.backend == "native" and self.kernel == "bf16_fused":
+            native.to_bf16(self.params, self.params_bf)
+
     def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
         self.params.copy_(d["params"].to(self.device))
         self.params.mul_(self._real)
@@ -656,6 +700,20 @@ class VectorEngine:
         if self.backend == "native" and self.kernel == "bf16_fused":
             native.to_bf16(self.params, self.params_bf)
 
-    def synchronize(self) -> None:
+    def synchronize(self, check: bool = True) -> None:
+        """Wait for the device; then (``check``) raise if a step kernel reported a protocol error."""
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+            if check:
+                self.check_kernel_err()
+
+    def check_kernel_err(self) -> None:
+        """The ws kernel's error word (csrc/qstep_ws.hip ``ws_fail``: a bounded ring wait gave up and the
+        workgroup aborted -- that launch's gradients are garbage).  Reads 16 bytes from the device: call
+        it where the host already synchronises (logging, checkpoints, end of a run)."""
+        err = getattr(self, "kernel_err", None)
+        if err is not None and err.device.type == "cuda":
+            v = int(err.abs().max())
+            if v:
+                raise RuntimeError(f"step kernel reported error word {v:#x} (ws ring protocol wait gave up; "
+                                   f"gradients of the failing launch are invalid)")

@@ -22,9 +22,10 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
           rank: int = 0, world_size: int = 1, group=None, until: Optional[int] = None,
           on_step: Optional[Callable[[int], None]] = None, final_dir: Optional[str] = None) -> Dict[str, Any]:
     """``steps`` more steps (or, with ``until``, up to that total step count -- a resumed elastic
-    generation finishes the same job).  ``on_step(step)`` runs before every step (fault injection and
-    the heartbeat's progress mark of ``--elastic`` jobs); without it the steps between two logging /
-    checkpoint points run as whole multi-step graph replays (``VectorEngine.run``).  ``final_dir``: each
+    generation finishes the same job).  The steps between two logging / checkpoint points run as whole
+    multi-step graph replays (``VectorEngine.run``).  ``on_step(step)`` (fault injection and the
+    heartbeat's progress mark of ``--elastic`` jobs) is called for every step of the next replay before
+    that replay runs; with it, one replay (``engine.graph_steps`` steps) runs at a time.  ``final_dir``: each
     rank writes its final state there (``final-rank-<r>.stck``).
 
     Several ranks (one process per GPU, RCCL): the synchronous DP step -- kernel, slab reduce, all-reduce,
@@ -45,14 +46,9 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
             eng.load_state_dict(st)
     eng.sync_params_from(0)
     if graph and eng.backend == "native":
-        from .benchkit import agree
+        from .benchkit import capture_with_vote
 
-        try:
-            ok = bool(eng.capture_graph(warmup=0 if world_size > 1 else 1))
-        except Exception:  # noqa: BLE001 -- eager launches, same math
-            ok = False
-        if not agree(ok, world_size, group, eng.device):
-            eng._graph, eng._graph_k = None, None
+        capture_with_vote(eng, rank, world_size, group, warmup=0 if world_size > 1 else 1)
     if eng._sync is not None:
         eng._sync.enable_timing()          # metrics: mean all-reduce ms per logging window
     ml = MetricsLogger(metrics_path)
@@ -69,16 +65,18 @@ def train(cfg: Config, steps: int, device: Optional[torch.device] = None, envs: 
     start = eng.step_count
     target = int(until) if until is not None else start + steps
     while eng.step_count < target:
+        # whole graph replays up to the next logging / checkpoint point; with ``on_step`` (the heartbeat's
+        # progress mark and the fault-injection points of --elastic jobs) at most one multi-step replay
+        # at a time, on_step called for every step of it before it runs
+        nxt = target
+        for every in (log_every, ckpt_every):
+            if every:
+                nxt = min(nxt, (eng.step_count // every + 1) * every)
         if on_step is not None:
-            on_step(eng.step_count)
-            eng.step()
-        else:
-            # whole graph replays up to the next logging / checkpoint point
-            nxt = target
-            for every in (log_every, ckpt_every):
-                if every:
-                    nxt = min(nxt, (eng.step_count // every + 1) * every)
-            eng.run(nxt - eng.step_count)
+            nxt = min(nxt, eng.step_count + max(1, int(eng.cfg.engine.graph_steps)))
+            for s_ in range(eng.step_count, nxt):
+                on_step(s_)
+        eng.run(nxt - eng.step_count)
         s = eng.step_count
         if log_every and s % log_every == 0:
             eng.synchronize()

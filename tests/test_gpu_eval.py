@@ -1,0 +1,148 @@
+"""Policy evaluation on the GPU engine (bench.py's episode returns, VERDICT r3 'measure the policy'):
+the greedy override really exploits at every position and freezes the weights, evaluations run on a
+snapshot that is restored, the buy-and-hold baseline matches a host re-simulation of the env, and a
+policy learned on a predictable bank beats the random policy greedily.  Also the capture-failure
+fallback of the training loop."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _prices(E, T=400, seed=3):
+    from sharetrade.data.prices import random_walk
+
+    return torch.from_numpy(random_walk(T, 50.0, 0.02, seed, n_series=E).astype(np.float32))
+
+
+def _engine(E=4096, T=400, **over):
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    for k, v in over.items():
+        sec, key = k.split("__")
+        setattr(getattr(cfg, sec), key, v)
+    return VectorEngine(cfg, prices=_prices(E, T), device=torch.device("cuda", 0), envs=E)
+
+
+def test_greedy_override_exploits_everywhere_and_freezes(native_built):
+    eng = _engine()
+    assert eng.step_kernel == "ws"
+    eng.state.pos.zero_()                         # the ramp min(eps, pos / ramp) is 0 here: all explore
+    s0 = eng.stats_dict()
+    eng.step()
+    eng.synchronize()
+    s1 = eng.stats_dict()
+    assert s1["explore"] - s0["explore"] == eng.E  # normal schedule: every env explores at pos 0
+    eng.state.pos.zero_()
+    p0 = eng.params.clone()
+    with eng.policy_overrides(epsilon=math.inf, lr=0.0):
+        eng.step()
+        eng.step()
+        eng.synchronize()
+    s2 = eng.stats_dict()
+    assert s2["explore"] == s1["explore"], "greedy policy explored"
+    assert torch.equal(eng.params, p0), "lr 0 changed the weights"
+    # the overrides are undone: the next eager step explores again at pos 0 and learns
+    eng.state.pos.zero_()
+    eng.step()
+    eng.synchronize()
+    assert eng.stats_dict()["explore"] - s2["explore"] == eng.E
+    assert not torch.equal(eng.params, p0)
+
+
+def test_evaluation_snapshot_restores_engine(native_built):
+    from sharetrade.trainer import benchkit
+
+    eng = _engine(E=2048, T=300)
+    eng.capture_graph(warmup=1)
+    eng.run(20)
+    eng.synchronize()
+    before = eng.state_dict()
+    acc = eng.stat_acc.clone()
+    res = benchkit.greedy_episode_returns(eng)
+    assert res["n"] == eng.E and res["complete_frac"] == 1.0
+    after = eng.state_dict()
+    for k in before:
+        assert torch.equal(before[k].nan_to_num(-7.0), after[k].nan_to_num(-7.0)), k
+    assert torch.equal(acc, eng.stat_acc)
+    # the graphs still replay the original step (same trajectory as an untouched engine)
+    eng2 = _engine(E=2048, T=300)
+    eng2.capture_graph(warmup=1)
+    eng2.run(20)
+    eng.run(5)
+    eng2.run(5)
+    eng.synchronize()
+    eng2.synchronize()
+    assert torch.equal(eng.params, eng2.params)
+    assert torch.equal(eng.state.budget, eng2.state.budget)
+
+
+def test_buy_and_hold_matches_host_simulation(native_built):
+    from sharetrade.trainer import benchkit
+
+    E, T = 1024, 320
+    eng = _engine(E=E, T=T)
+    res = benchkit.buy_and_hold_returns(eng)
+    P = eng.prices[:, :T].cpu().numpy()
+    H = eng.H
+    b = np.full(E, np.float32(eng.cfg.env.budget), np.float32)
+    s = np.zeros(E, np.int64)
+    for pos in range(T - H):
+        v = P[:, pos + H]
+        buy = b >= v
+        b = np.where(buy, (b - v).astype(np.float32), b)
+        s += buy
+    fin = (b + s.astype(np.float32) * P[:, T - 1]).astype(np.float64) - eng.cfg.env.budget
+    assert res["n"] == E
+    assert abs(res["mean"] - fin.mean()) < 1e-6 * max(1.0, abs(fin.mean()))
+    assert abs(res["std"] - fin.std()) < 1e-4 * max(1.0, fin.std())
+
+
+def test_greedy_learned_beats_random(native_built):
+    """On an AR(1)-momentum bank the learned policy, evaluated greedily with frozen weights, earns more
+    than the uniform-random policy (and than its own random init) -- the policy, not the schedule."""
+    from sharetrade.config import preset_config
+    from sharetrade.trainer import benchkit
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    cfg.data.source = "ar1"
+    cfg.data.length = 1401
+    eng = VectorEngine(cfg, device=torch.device("cuda", 0), envs=65536)
+    init = eng.params.detach().clone()
+    eng.capture_graph(warmup=1)
+    eng.run(3 * (eng.T - eng.H))
+    eng.synchronize()
+    g = benchkit.greedy_episode_returns(eng)
+    g0 = benchkit.greedy_episode_returns(eng, params=init)
+    r = benchkit.full_episode_returns(eng, random_policy=True)
+    assert g["complete_frac"] == 1.0 and r["complete_frac"] == 1.0
+    assert g["mean"] > r["mean"] + 0.25 * abs(r["mean"]) + 50.0, (g, r)
+    assert math.isfinite(g0["mean"])
+
+
+def test_train_falls_back_to_eager_when_capture_fails(native_built, monkeypatch):
+    """SHARETRADE_FAIL_CAPTURE on this rank: train() drops the graphs (sticky HIP error cleared) and
+    runs eager steps to the same result as the captured run."""
+    from sharetrade.config import preset_config
+    from sharetrade.trainer.loop import train
+
+    def run(fail):
+        if fail:
+            monkeypatch.setenv("SHARETRADE_FAIL_CAPTURE", "0")
+        else:
+            monkeypatch.delenv("SHARETRADE_FAIL_CAPTURE", raising=False)
+        cfg = preset_config("flagship")
+        cfg.data.length = 400
+        return train(cfg, 40, device=torch.device("cuda", 0), envs=2048, log_every=16)
+
+    a = run(False)
+    b = run(True)
+    assert a["steps"] == b["steps"] == 40
+    assert a["mean"] == b["mean"] and a["std"] == b["std"]     # same portfolios (graph replay == eager)
+    assert a["reward_sum"] == b["reward_sum"] and a["explore"] == b["explore"]

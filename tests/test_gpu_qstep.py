@@ -391,67 +391,6 @@ def test_large_bank_gather_matches_oracle(native_built, kernel, E):
         assert torch.equal(getattr(ns, k), getattr(eng.state, k)[sub].cpu()), k
 
 
-@pytest.mark.parametrize("compat", [False, True])
-@pytest.mark.parametrize("E,grid", [(512, 0), (448, 3), (64 * 20, 4), (4096, 0)])
-def test_pair_kernel_matches_wide(native_built, compat, E, grid):
-    """csrc/qstep_pair.hip (two 32-env chunk slots in flight, five phases apart) vs csrc/qstep_wide.hip
-    on the same state: identical env transitions, actions and rewards, gradients and statistics equal
-    up to fp32 summation order.  Small grids give several pipeline cycles per workgroup and slots
-    with unequal chunk counts (pipeline fill and drain)."""
-    from sharetrade.trainer.engine import VectorEngine
-
-    prices = _prices(E)
-    dev = torch.device("cuda", 0)
-    out = {}
-    for sk in ("wide", "pair"):
-        cfg = _cfg(compat)
-        cfg.agent.epsilon = 0.5
-        cfg.engine.step_kernel = sk
-        cfg.engine.grid = grid
-        cfg.engine.slab_dtype = "fp32"
-        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
-        assert eng.step_kernel == sk
-        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
-        eng.state.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
-        eng.state.pos[::97] = prices.shape[1] - cfg.model.history - 1    # some episodes end this step
-        eng.ctrl.fill_(9)
-        g = eng.native_grad().detach().cpu().clone()
-        torch.cuda.synchronize()
-        out[sk] = (g, eng.actions_out.cpu().clone(), eng.rewards_out.cpu().clone(),
-                   {k: v.cpu().clone() for k, v in eng.state.as_dict().items()}, eng.stat_slab.sum(0).cpu())
-    gw, aw, rw, sw, stw = out["wide"]
-    gp, ap, rp, sp, stp = out["pair"]
-    assert torch.equal(aw, ap) and torch.equal(rw, rp)
-    for k in sw:
-        assert torch.equal(sw[k].nan_to_num(-1.0), sp[k].nan_to_num(-1.0)), k
-    assert _rel(gp, gw) < 1e-4, _rel(gp, gw)
-    assert torch.allclose(stp, stw, rtol=1e-4, atol=1e-3), (stp, stw)
-
-
-def test_pair_kernel_multi_step_bf16_slabs(native_built):
-    """Pair kernel through the default bf16 slabs and the optimizer over several graph-replayed steps:
-    tracks the wide kernel (same actions every step while the parameters agree to bf16 rounding)."""
-    from sharetrade.trainer.engine import VectorEngine
-
-    E = 64 * 64
-    prices = _prices(E)
-    dev = torch.device("cuda", 0)
-    res = {}
-    for sk in ("wide", "pair"):
-        cfg = _cfg(False)
-        cfg.engine.step_kernel = sk
-        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
-        eng.capture_graph(warmup=1, graph_steps=4)
-        eng.run(9)
-        torch.cuda.synchronize()
-        res[sk] = (eng.params.cpu().clone(), eng.state.pos.cpu().clone(), eng.stats_dict())
-    pw, posw, stw = res["wide"]
-    pp, posp, stp = res["pair"]
-    assert torch.equal(posw, posp)
-    assert _rel(pp, pw) < 1e-3, _rel(pp, pw)
-    assert abs(stp["explore"] - stw["explore"]) <= 0.01 * max(1.0, stw["explore"])
-
-
 def test_graph_priming_is_rank_uniform(native_built):
     """prime_graph: one process stops once two consecutive replays agree; with world_size > 1 it
     replays exactly min_reps times on every rank (each replay holds the DP all-reduce, so a
@@ -469,54 +408,3 @@ def test_graph_priming_is_rank_uniform(native_built):
     s1 = eng.step_count
     assert eng.prime_graph(5) == 5 and eng.step_count == s1 + 20
     eng.world_size = 1
-
-
-def test_ofold_variant_matches_default(native_built):
-    """engine.step_variant = "ofold" (Q(x)'s output layer folded into layer 2's epilogue) vs the default
-    8-wave kernel: same operands, fp32 summation order of q differs -> actions equal except near-ties,
-    gradients equal to fp32 rounding."""
-    from sharetrade.trainer.engine import VectorEngine
-
-    E = 256
-    prices = _prices(E, seed=9)
-    dev = torch.device("cuda", 0)
-    out = []
-    for variant in ("", "ofold"):
-        cfg = _cfg()
-        cfg.agent.epsilon = 0.9
-        cfg.engine.step_variant = variant
-        cfg.engine.step_kernel = "wide"   # the variants are builds of the 8-wave wide kernel (the default is ws)
-        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
-        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 150)
-        eng.ctrl.fill_(2000)
-        g = eng.native_grad().detach().cpu().clone()
-        torch.cuda.synchronize()
-        out.append((eng.actions_out.cpu().clone(), g))
-    (a0, g0), (a1, g1) = out
-    assert (a0 != a1).float().mean().item() <= 0.02
-    if torch.equal(a0, a1):
-        assert _rel(g1, g0) < 1e-3
-
-
-def test_wswz_variant_bit_identical(native_built):
-    """engine.step_variant = "wswz" (XOR-swizzled weight images) reorders LDS addresses only: actions,
-    rewards and gradients bit-identical to the default 8-wave kernel."""
-    from sharetrade.trainer.engine import VectorEngine
-
-    E = 256
-    prices = _prices(E, seed=4)
-    dev = torch.device("cuda", 0)
-    out = []
-    for variant in ("", "wswz"):
-        cfg = _cfg()
-        cfg.agent.epsilon = 0.9
-        cfg.engine.step_variant = variant
-        cfg.engine.step_kernel = "wide"   # the variants are builds of the 8-wave wide kernel (the default is ws)
-        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
-        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 150)
-        eng.ctrl.fill_(3000)
-        g = eng.native_grad().detach().cpu().clone()
-        torch.cuda.synchronize()
-        out.append((eng.actions_out.cpu().clone(), eng.rewards_out.cpu().clone(), g))
-    for a, b in zip(out[0], out[1]):
-        assert torch.equal(a, b)

@@ -23,13 +23,10 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--out", default="")
     ap.add_argument("--chunk", type=int, default=0, help="0 = engine default, 32 or 64")
-    ap.add_argument("--variant", default="", help="tuning build suffix (st_qstep_wide_launch_<v>)")
     ap.add_argument("--waves", type=int, default=8, help="64-env-chunk kernel: 4 or 8 waves")
-    ap.add_argument("--kernel", default="auto", help="engine.step_kernel: auto | wide | narrow | pair | ws")
+    ap.add_argument("--kernel", default="auto", help="engine.step_kernel: auto | wide | narrow | ws")
     ap.add_argument("--ws-dvariant", default="", help="ws: data-wave stamps build suffix ('' = stamps, gskipst)")
     a = ap.parse_args()
-    if a.kernel == "pair":
-        return pair_stamps(a)
     if a.kernel == "ws":
         return ws_stamps(a)
     import build
@@ -42,7 +39,6 @@ def main():
     cfg = preset_config("flagship")
     cfg.engine.chunk = a.chunk
     cfg.engine.step_waves = a.waves
-    cfg.engine.step_variant = a.variant
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=a.envs)
     eng.run(3)
@@ -92,58 +88,13 @@ def main():
         open(a.out, "w").write(txt)
 
 
-PAIR_INTERVALS = ["I0 A.P0 gather | B.P5 L2 Q(x')", "I1 B.P6 TD | A.P1 L1 Q(x)", "I2 B.P7 bwd L2+dW2 | A.P2 L2 Q(x)",
-                  "I3 A.P3 env | B.P8 bwd L1+dW1", "I4 B.P9 dW0 | A.P4 L1 Q(x')", "I5 B.P0 gather | A.P5 L2 Q(x')",
-                  "I6 A.P6 TD | B.P1 L1 Q(x)", "I7 A.P7 bwd L2+dW2 | B.P2 L2 Q(x)", "I8 B.P3 env | A.P8 bwd L1+dW1",
-                  "I9 A.P9 dW0 | B.P4 L1 Q(x')"]
-
-
-def pair_stamps(a):
-    """csrc/qstep_pair.hip: one stamp per barrier interval (10 per cycle = 2 x 32 envs)."""
-    import build
-
-    build.build_all()
-    from sharetrade.config import preset_config
-    from sharetrade.trainer.engine import VectorEngine
-
-    cfg = preset_config("flagship")
-    cfg.engine.step_kernel = "pair"
-    dev = torch.device("cuda", 0)
-    eng = VectorEngine(cfg, device=dev, envs=a.envs)
-    eng.run(3)
-    torch.cuda.synchronize()
-    nch = a.envs // 32
-    ncyc = (nch + 2 * eng.grid - 1) // (2 * eng.grid)
-    st = torch.zeros((ncyc + 2) * 16, dtype=torch.int64, device=dev)
-    eng._qp.stamps = st.data_ptr()
-    eng.step()
-    torch.cuda.synchronize()
-    eng._qp.stamps = None
-    s = st.cpu().view(-1, 16)
-    full = s[1:ncyc - 1] if ncyc > 2 else s[:ncyc]     # steady-state cycles (no fill / drain)
-    lines = [f"# two-slot step kernel (csrc/qstep_pair.hip) interval breakdown (workgroup 0, {a.envs} envs, "
-             f"grid {eng.grid}, {ncyc} cycles/WG of 2 x 32 envs; s_memtime ticks)\n",
-             "| interval | ticks/cycle | % |", "|---|---|---|"]
-    ds = [float((full[:, i + 1] - full[:, i]).double().mean()) for i in range(10)]
-    tot = sum(ds)
-    for n, v in zip(PAIR_INTERVALS, ds):
-        lines.append(f"| {n} | {v:.0f} | {100 * v / tot:.1f} |")
-    lines.append(f"| cycle (64 envs) | {tot:.0f} | |")
-    x = s[ncyc + 1, 8:13].double()
-    lines.append(f"| prologue | {float(x[1] - x[0]):.0f} | |")
-    lines.append(f"| chunk loop, all cycles | {float(x[2] - x[1]):.0f} | |")
-    lines.append(f"| step statistics + gradient slab write-out | {float(x[3] - x[2]):.0f} | |")
-    txt = "\n".join(lines) + "\n"
-    print(txt)
-    if a.out:
-        open(a.out, "w").write(txt)
-
-
 def ws_stamps(a):
-    """csrc/qstep_ws.hip: data wave 0 of workgroup 0 per 16-env tile, gradient wave 0 per ring slot."""
+    """csrc/qstep_ws.hip: data wave 0 of workgroup 0 per 16-env tile, gradient wave 0 per ring slot (the
+    stamps builds live in the opt-in A/B library, csrc/ab/)."""
     import build
 
-    build.build_all()
+    os.environ["SHARETRADE_AB_BUILDS"] = "1"
+    build.build_all(ab=True)
     from sharetrade.config import preset_config
     from sharetrade.trainer.engine import VectorEngine
 
@@ -156,7 +107,7 @@ def ws_stamps(a):
     nmy = (a.envs // 64 + eng.grid - 1) // eng.grid
 
     def stamped(variant):
-        # data-wave stamps from csrc/qstep_ws_stamps.hip, gradient-wave stamps from qstep_ws_gstamps.hip
+        # data-wave stamps from csrc/ab/qstep_ws_stamps.hip, gradient-wave stamps from csrc/ab/qstep_ws_gstamps.hip
         st = torch.zeros((nmy + 1) * 16 + 8 * 4 * nmy + 16, dtype=torch.int64, device=dev)
         eng.cfg.engine.step_variant = variant
         eng._qp.stamps = st.data_ptr()
