@@ -250,11 +250,20 @@ ST_DEV void ws_fail(const QStepParams& p, int* ctl) {
 // wait until pred(*w) holds: bounded, and abandoned at once once the workgroup has aborted
 template <typename Pred>
 ST_DEV void ring_wait(const QStepParams& p, int* ctl, const int* w, Pred pred) {
+#pragma clang loop unroll(disable)
   for (int spin = 0; !pred(lds_acq(w)); ++spin) {
     if (lds_acq(ctl + CTL_ABORT)) break;
     __builtin_amdgcn_s_sleep(1);
     if (spin > SPIN_LIMIT) { ws_fail(p, ctl); break; }   // never expected: report, do not hang the GPU
   }
+}
+
+// 16-byte loads from 4-byte-aligned addresses (the one padded bank copy is read at every shift): a memcpy
+// from a float pointer promises the compiler only 4-byte alignment; it is still one dwordx4 load
+ST_DEV float4 ldu4(const float* a) {
+  float4 v;
+  __builtin_memcpy(&v, a, sizeof(v));
+  return v;
 }
 
 // env-state rows addressed as a uniform row base + a 32-bit byte offset, so the loads / stores use the
@@ -337,16 +346,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     const int e_ = env_of(K);                                                                    \
     const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
     const float* b_ = p.prices4 + (size_t)e_ * p.T4 + (size_t)pc_;  /* 4-B aligned dwordx4 reads */   \
-    pl = *reinterpret_cast<const float4*>(b_ + 200);  /* first: the back edge copies it (see below) */ \
+    pl = ldu4(b_ + 200);  /* first: the back edge copies it (see below) */                         \
     _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
       const float* q_ = b_ + 32 * ks + 8 * g4;                                                   \
-      pa[ks] = *reinterpret_cast<const float4*>(q_);                                             \
-      pb[ks] = *reinterpret_cast<const float4*>(q_ + 4);                                         \
+      pa[ks] = ldu4(q_);                                                                         \
+      pb[ks] = ldu4(q_ + 4);                                                                     \
       pc[ks] = q_[8];                                                                            \
     }                                                                                            \
     if (g4 == 1 || g4 == 2) {                                                                    \
       const float* r_ = b_ + 188 + 4 * g4;                                                       \
-      pd = *reinterpret_cast<const float4*>(r_);                                                 \
+      pd = ldu4(r_);                                                                             \
       pe = r_[4];                                                                                \
     }                                                                                            \
   }

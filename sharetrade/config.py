@@ -101,7 +101,7 @@ class EnvConfig:
 
 @dataclass
 class DataConfig:
-    source: str = "csv"             # csv | linear | random_walk | ar1 (momentum walk: a learnable signal)
+    source: str = "csv"             # csv | linear | random_walk | ar1 (one-day momentum) | trend (persistent drift)
     ticker: str = "MSFT"
     start: str = "1992-01-01"
     end: str = "2015-01-01"
@@ -111,6 +111,11 @@ class DataConfig:
     start_price: float = 50.0
     volatility: float = 0.02
     ar_phi: float = 0.3             # ar1 source: log-return autocorrelation
+    # trend source: log-return = mu_t + volatility * eps_t with a persistent, zero-mean drift
+    # mu_t = rho mu_{t-1} + trend_sd sqrt(1 - rho^2) eta_t (regimes lasting ~1 / (1 - rho) days): a signal
+    # that a policy moving one share per step can follow, unlike ar1's one-day momentum
+    trend_rho: float = 0.995
+    trend_sd: float = 0.002
     seed: int = 7
 
 

@@ -90,6 +90,23 @@ def make_price_bank(cfg: Config, E: int, device: torch.device, seed: int = 0) ->
             logp.add_(r)
             out[:, t] = d.start_price * torch.exp(logp)
         return out
+    if d.source == "trend":
+        # persistent zero-mean drift regimes (AR(1) on the drift, not on the returns), on the device
+        g = torch.Generator(device=device)
+        g.manual_seed(d.seed + 7919 * seed)
+        out = padded_bank(E, d.length, device)
+        eps = torch.empty(E, device=device)
+        mu = torch.empty(E, device=device).normal_(0.0, d.trend_sd, generator=g)   # stationary start
+        logp = torch.zeros(E, device=device)
+        out[:, 0] = d.start_price
+        k = float(d.trend_sd * math.sqrt(max(0.0, 1.0 - d.trend_rho ** 2)))
+        for t in range(1, d.length):
+            eps.normal_(0.0, 1.0, generator=g)
+            mu.mul_(d.trend_rho).add_(eps, alpha=k)
+            eps.normal_(0.0, d.volatility, generator=g)
+            logp.add_(mu).add_(eps)
+            out[:, t] = d.start_price * torch.exp(logp)
+        return out
     from ..data import prices as pr
 
     src = pr.make_source(d)

@@ -68,6 +68,24 @@ def test_full_length_compat_run_vector_engine():
     assert time.perf_counter() - t0 < 600
 
 
+@pytest.mark.slow
+def test_full_length_compat_run_actors_engine():
+    """Message-level parity at full length: the `actors` engine runs the reference app exactly as
+    `ShareTradeHelper.scala:20-48` wires it -- 10 TrainerChildActor FSMs, each asking ONE shared
+    QDecisionPolicyActor `SelectionAction` and `UpdateQ` per step (`TrainerChildActor.scala:87-102`), over
+    the whole MSFT series (5,846 steps each: 116,920 round trips) -- and ends at exactly avg 2400.0,
+    std 0.0 (quirk Q1)."""
+    from sharetrade.app import run
+
+    cfg = _cfg()
+    cfg.router.poll_interval_s = 2.0     # the app's 201 polls then span 402 s
+    t0 = time.perf_counter()
+    res = run(cfg, engine="actors", device="cpu", quiet=True)
+    assert res["completed"] == 1.0, res
+    assert res["avg"] == 2400.0 and res["std"] == 0.0, res
+    assert time.perf_counter() - t0 < 900
+
+
 def test_intended_semantics_trade():
     from sharetrade.app import run
 

@@ -90,6 +90,10 @@ def test_ws_matches_oracle(native_built, compat, E, grid):
         assert _rel(gw, rw) < 3e-2, (l, _rel(gw, rw))
         if l > 0:
             assert _rel(L.b(grad, l), L.b(g_ref, l)) < 3e-2, l
+    # and vs the pure fp32 oracle (no bf16 emulation, same actions): the bound the wide kernel meets
+    _, g32, _ = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=False,
+                        forced_actions=acts)
+    assert _rel(grad, g32) < 0.1, _rel(grad, g32)
     # statistics slab: reward sum and the number of explore draws
     st = eng.stat_slab.sum(0).cpu()
     assert abs(float(st[0]) - float(info["reward"].sum())) < 1e-3 + 1e-4 * float(info["reward"].abs().sum())
@@ -157,3 +161,51 @@ def test_ws_and_wide_agree_over_steps(native_built):
     assert _rel(pv, pw) < 1e-2, _rel(pv, pw)
     assert torch.allclose(stv[0], stw[0], rtol=1e-5, atol=1e-5)     # reward sums
     assert torch.allclose(stv[1], stw[1], rtol=2e-2)                # TD loss sums
+
+
+@pytest.mark.parametrize("compat", [False, True])
+def test_ws_trajectory_matches_torch_oracle(native_built, compat):
+    """Ten eager ws steps against the plain-PyTorch oracle engine (engine_step_ref + optimizer_step_ref)
+    driven with the kernel's actions: env transitions and rewards exact at every step, the learned
+    parameter change within bf16 tolerance of the oracle's (bf16-emulating forward / backward) and
+    within a looser bound of the pure-fp32 oracle's.  SGD, so the parameter change is linear in the
+    gradients (Adam's first steps are ~lr * sign(g): elements with near-zero gradients would flip)."""
+    from sharetrade.models import qnet as qn
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 1024
+    cfg = _cfg(compat)
+    cfg.agent.epsilon = 0.6
+    cfg.agent.optimizer = "sgd"
+    cfg.agent.lr = 0.01
+    prices = _prices(E, T=320, seed=11)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    assert eng.step_kernel == "ws"
+    eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 100)
+    refs = {}
+    for emulate in (True, False):
+        ref = VectorEngine(cfg, prices=prices, device=torch.device("cpu"), envs=E, backend="torch")
+        ref.params.copy_(eng.params.detach().cpu())
+        refs[emulate] = ref
+    p0 = eng.params.detach().cpu().clone()
+    a = cfg.agent
+    for t in range(10):
+        st0 = eng.state.clone().to("cpu")
+        eng.step()
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        acts = eng.actions_out.cpu().clone()
+        rew = eng.rewards_out.cpu().clone()
+        for emulate, ref in refs.items():
+            ns, g, info = _oracle(cfg, prices, st0, ref.params, ref.layout, t, eng.loss_coef,
+                                  emulate_bf16=emulate, forced_actions=acts)
+            qn.optimizer_step_ref(ref.params, g, ref.opt, ref.mask, a.lr, a.adam_betas, a.adam_eps)
+            if emulate:
+                assert torch.equal(info["reward"], rew), t
+                for k in ("budget", "shares", "value", "pos", "episodes"):
+                    assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (t, k)
+    d = eng.params.detach().cpu() - p0
+    for emulate, tol in ((True, 3e-2), (False, 0.1)):
+        dr = refs[emulate].params - p0
+        assert _rel(d, dr) < tol, (emulate, _rel(d, dr))
