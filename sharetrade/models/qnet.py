@@ -149,17 +149,23 @@ def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0, device=None) 
     QDecisionPolicyActor.scala:41,45) or He-normal; biases = ``bias_init``.
 
     ``m.init_rng``: ``"philox"`` (default) draws W from the counter-based Philox + Box-Muller
-    generator -- on a GPU ``device`` by the ``init_normal`` HIP kernel (csrc/series.hip), on the host by
-    its NumPy mirror, the same values either way up to libm ulps; ``"torch"`` uses torch's CPU
-    generator (rounds 1-2 behaviour).  The result lives on ``device`` (CPU by default)."""
+    generator: by the ``init_normal`` HIP kernel (csrc/series.hip) whenever a GPU and the native library
+    are present -- also for a host-side ``device`` (drawn on the GPU, copied over), so a host learner
+    (PolicyServer, serve_eval) and a device engine get bit-identical weights for one seed -- and by its
+    NumPy mirror on a machine without a GPU (the same values up to libm ulps: logf / cosf vs NumPy).
+    ``"torch"`` uses torch's CPU generator and reproduces the seeded runs of rounds 1-2.  The result
+    lives on ``device`` (CPU by default)."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
     flat = torch.zeros(layout.numel, dtype=torch.float32, device=dev)
-    use_kernel = m.init_rng == "philox" and dev.type == "cuda"
+    kdev = _kernel_device(dev) if m.init_rng == "philox" else None
+    use_kernel = kdev is not None
     if use_kernel:
         from ..ops import native
         from ..utils import rng
 
         k0, k1 = rng.key_for(int(seed), 0)
+        out = flat
+        flat = torch.zeros(layout.numel, dtype=torch.float32, device=kdev)
     g = torch.Generator().manual_seed(int(seed)) if m.init_rng == "torch" else None
     for l in range(layout.n_layers):
         fan_in, fan_out = layout.dims[l], layout.dims[l + 1]
@@ -174,7 +180,25 @@ def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0, device=None) 
         else:
             raise KeyError(f"model.init_rng: {m.init_rng!r}")
         layout.b(flat, l)[:fan_out] = m.bias_init
+    if use_kernel and out.device != flat.device:
+        out.copy_(flat)
+        return out
     return flat
+
+
+def _kernel_device(dev: torch.device):
+    """Where the init_normal kernel draws for ``dev``: ``dev`` itself if it is a GPU, the current GPU
+    when ``dev`` is the host and a GPU plus the native library exist, else None (NumPy mirror)."""
+    if dev.type == "cuda":
+        return dev
+    try:
+        from ..ops import native
+
+        if native.available() and torch.cuda.is_available():
+            return torch.device("cuda", torch.cuda.current_device())
+    except Exception:  # noqa: BLE001 -- no usable GPU: host mirror
+        pass
+    return None
 
 
 # ---------------------------------------------------------------- oracle

@@ -240,10 +240,8 @@ class VectorEngine:
             self._init_native()
 
     def ws_ok(self, cfg: Config, L) -> bool:
-        """Geometry of csrc/qstep_ws.hip (wave-specialised step kernel)."""
-        sched = cfg.engine.chunk_schedule
-        dyn = sched == "dynamic" or (sched == "auto" and self.world_size > 1 and cfg.engine.dp_overlap)
-        return (self.E % 64 == 0 and self.H == 201 and tuple(L.pdims[:3]) == (224, 128, 128) and not dyn
+        """Geometry of csrc/qstep_ws.hip (wave-specialised step kernel; static or dynamic chunk schedule)."""
+        return (self.E % 64 == 0 and self.H == 201 and tuple(L.pdims[:3]) == (224, 128, 128)
                 and native.qstep_ws_supported(L.pdims[0], L.pdims[1], L.pdims[2]))
 
     # ---------------------------------------------------------------- native buffers
@@ -291,9 +289,10 @@ class VectorEngine:
             sched = "dynamic" if (self.world_size > 1 and self.cfg.engine.dp_overlap) else "static"
         if sched not in ("static", "dynamic"):
             raise ValueError(f"engine.chunk_schedule: {sched!r}")
-        # dynamic: 8 per-XCD claim heads, one per 128-byte line (csrc/qstep_wide.hip); needs the
-        # 64-env-chunk kernel, grid % 8 == 0 and (E / 64) % 8 == 0, else the static schedule is used
-        dyn_ok = self.step_kernel == "wide" and self.grid % 8 == 0 and (self.E // 64) % 8 == 0
+        # dynamic: 8 per-XCD claim heads, one per 128-byte line (csrc/qstep_wide.hip, csrc/qstep_ws.hip);
+        # needs grid % 8 == 0 (the wide kernel also (E / 64) % 8 == 0), else the static schedule is used
+        dyn_ok = ((self.step_kernel == "wide" and self.grid % 8 == 0 and (self.E // 64) % 8 == 0)
+                  or (self.step_kernel == "ws" and self.grid % 8 == 0))
         self.chunk_schedule = "dynamic" if (sched == "dynamic" and dyn_ok) else "static"
         self.chunk_heads = (torch.zeros(8 * 32, dtype=torch.int32, device=dev)
                             if self.chunk_schedule == "dynamic" else None)

@@ -104,26 +104,28 @@ def test_buy_and_hold_matches_host_simulation(native_built):
 
 
 def test_greedy_learned_beats_random(native_built):
-    """On an AR(1)-momentum bank the learned policy, evaluated greedily with frozen weights, earns more
-    than the uniform-random policy (and than its own random init) -- the policy, not the schedule."""
+    """On an AR(1)-momentum bank the learned policy, evaluated greedily with frozen weights after two
+    online episodes, earns well above the uniform-random policy (mean final portfolio) -- the policy,
+    not the schedule (profiles/r4_learning_eval_65k.md: the same deterministic run, episode 2)."""
     from sharetrade.config import preset_config
     from sharetrade.trainer import benchkit
     from sharetrade.trainer.engine import VectorEngine
 
     cfg = preset_config("flagship")
     cfg.data.source = "ar1"
-    cfg.data.length = 1401
+    cfg.data.length = 1601
     eng = VectorEngine(cfg, device=torch.device("cuda", 0), envs=65536)
-    init = eng.params.detach().clone()
-    eng.capture_graph(warmup=1)
-    eng.run(3 * (eng.T - eng.H))
+    eng.capture_graph(warmup=0)
+    for _ in range(2):
+        benchkit.reset_episodes(eng)
+        eng.run(eng.T - eng.H)
     eng.synchronize()
     g = benchkit.greedy_episode_returns(eng)
-    g0 = benchkit.greedy_episode_returns(eng, params=init)
     r = benchkit.full_episode_returns(eng, random_policy=True)
+    bh = benchkit.buy_and_hold_returns(eng)
     assert g["complete_frac"] == 1.0 and r["complete_frac"] == 1.0
-    assert g["mean"] > r["mean"] + 0.25 * abs(r["mean"]) + 50.0, (g, r)
-    assert math.isfinite(g0["mean"])
+    assert g["mean"] > 2.0 * r["mean"] + 100.0, (g, r)
+    assert g["mean"] <= 1.05 * bh["mean"] + 50.0, (g, bh)   # one-share trades: holding is near-optimal here
 
 
 def test_train_falls_back_to_eager_when_capture_fails(native_built, monkeypatch):
@@ -147,3 +149,16 @@ def test_train_falls_back_to_eager_when_capture_fails(native_built, monkeypatch)
     assert a["steps"] == 39 and b["steps"] == 40     # (a: one of the 40 was capture_graph's warm-up)
     assert a["mean"] == b["mean"] and a["std"] == b["std"]     # same portfolios (graph replay == eager)
     assert a["reward_sum"] == b["reward_sum"] and a["explore"] == b["explore"]
+
+
+def test_philox_init_identical_on_host_and_device(native_built):
+    """model.init_rng = "philox": a host-side learner (PolicyServer, serve_eval) gets the same initial
+    weights as the device engine for one seed -- both drawn by the init_normal kernel."""
+    from sharetrade.config import preset_config
+    from sharetrade.models import qnet as qn
+
+    cfg = preset_config("flagship")
+    layout = qn.QNetLayout(cfg.model.history + 2, cfg.model.hidden)
+    a = qn.init_params(layout, cfg.model, seed=5, device="cpu")
+    b = qn.init_params(layout, cfg.model, seed=5, device=torch.device("cuda", 0))
+    assert a.device.type == "cpu" and torch.equal(a, b.cpu())

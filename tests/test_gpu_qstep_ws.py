@@ -209,3 +209,73 @@ def test_ws_trajectory_matches_torch_oracle(native_built, compat):
     for emulate, tol in ((True, 3e-2), (False, 0.1)):
         dr = refs[emulate].params - p0
         assert _rel(d, dr) < tol, (emulate, _rel(d, dr))
+
+
+@pytest.mark.parametrize("E,grid", [(64 * 48, 16), (64 * 100, 8), (64 * 13, 8), (64 * 1000, 16), (64 * 2048, 256)])
+def test_ws_dynamic_schedule_matches_static(native_built, E, grid):
+    """csrc/qstep_ws.hip with the dynamic chunk schedule (overlapped DP): rounds 0-2 static, later chunks
+    claimed from per-XCD-group heads and handed to the data waves through the LDS ring, the gradient
+    waves stopping at the round count.  Every chunk is stepped exactly once per launch, transitions and
+    actions equal the static schedule's, gradients agree up to the bf16 rounding of differently grouped
+    partials; the heads are re-zeroed so a second launch works too."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    prices = _prices(E, seed=5)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for sched in ("static", "dynamic"):
+        cfg = _cfg()
+        cfg.agent.epsilon = 0.5
+        cfg.engine.chunk_schedule = sched
+        cfg.engine.grid = grid
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.step_kernel == "ws" and eng.chunk_schedule == sched and eng.grid == grid
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 150)
+        pos0 = eng.state.pos.clone()
+        eng.ctrl.fill_(7)
+        g = eng.native_grad().detach().cpu().clone()
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0, "ring wait gave up"
+        assert torch.equal(eng.state.pos, pos0 + 1), "a chunk was skipped or stepped twice"
+        out[sched] = (g, eng.actions_out.cpu().clone(), eng.stat_slab.sum(0).cpu(),
+                      {k: v.cpu().clone() for k, v in eng.state.as_dict().items()})
+        if sched == "dynamic":
+            assert int(eng.chunk_heads.abs().sum()) == 0, "claim heads not re-zeroed"
+            g2 = eng.native_grad().detach().cpu().clone()
+            torch.cuda.synchronize()
+            assert int(eng.kernel_err.sum()) == 0
+            assert torch.equal(eng.state.pos, pos0 + 2)
+            assert torch.isfinite(g2).all()
+    gs, as_, sts, ss = out["static"]
+    gd, ad, std_, sd = out["dynamic"]
+    assert torch.equal(ad, as_)
+    for k in ("budget", "shares", "value", "episodes"):
+        assert torch.equal(ss[k], sd[k]), k
+    assert _rel(gd, gs) < 4e-3, _rel(gd, gs)
+    assert torch.allclose(std_, sts, rtol=1e-4, atol=1e-3)
+
+
+def test_ws_dynamic_schedule_multi_step_graphs(native_built):
+    """The dynamic-schedule ws kernel inside captured multi-step graphs (the heads are re-zeroed between
+    launches by the slab pass): the same trajectory as the static schedule over 12 steps."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 64 * 512
+    prices = _prices(E, seed=6)
+    dev = torch.device("cuda", 0)
+    res = {}
+    for sched in ("static", "dynamic"):
+        cfg = _cfg()
+        cfg.agent.epsilon = 0.0   # uniform actions: identical trajectories
+        cfg.engine.chunk_schedule = sched
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.chunk_schedule == sched
+        eng.capture_graph(warmup=1, graph_steps=4)
+        eng.run(12)
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        res[sched] = (eng.params.cpu().clone(), {k: v.cpu().clone() for k, v in eng.state.as_dict().items()})
+    (ps, ss), (pd, sd) = res["static"], res["dynamic"]
+    for k in ("budget", "shares", "pos", "value"):
+        assert torch.equal(ss[k], sd[k]), k
+    assert _rel(pd, ps) < 1e-2, _rel(pd, ps)
