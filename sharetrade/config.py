@@ -161,6 +161,9 @@ class EngineConfig:
     # E % 64 == 0, history 201, dims 224-128-128, static schedule), "wide" (csrc/qstep_wide.hip, 64-env
     # chunks) or "narrow" (csrc/qstep_fused.hip, 32-env chunks)
     step_kernel: str = "auto"
+    # fp32 engine (engine.dtype = "fp32": the reference geometry): "auto" = the batched MFMA step
+    # (csrc/mlp_f32_mfma.hip) from 1,024 envs up, the per-env row kernels (csrc/mlp_f32.hip) below; "on" / "off"
+    f32_batched: str = "auto"
     step_variant: str = ""          # timing / debug build of the ws kernel (csrc/ab/qstep_ws_<v>.hip); opt-in only
                                     # (SHARETRADE_AB_BUILDS=1, several compute wrong results); "" = production
     graph: bool = True              # capture the step in a HIP graph

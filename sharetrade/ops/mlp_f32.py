@@ -346,3 +346,195 @@ class F32EngineStep:
             self.optim.mode, self.optim.grad = 2, grad_buf.data_ptr()
             native.check(self.L.st_f32_grad_optim(self.net, self.optim, sh), "st_f32_update(engine)")
         native.check(self.L.st_f32_advance(self.eng.ctrl.data_ptr(), sh), "st_f32_advance")
+
+
+# ---------------------------------------------------------------------------------- batched (MFMA) fp32 step
+class GemmF32(C.Structure):
+    _fields_ = [
+        ("A", C.c_void_p), ("B", C.c_void_p), ("C", C.c_void_p), ("bias", C.c_void_p), ("aux", C.c_void_p),
+        ("M", C.c_int), ("N", C.c_int), ("K", C.c_int),
+        ("am", C.c_longlong), ("ak", C.c_longlong), ("bk", C.c_longlong), ("bn", C.c_longlong),
+        ("ldc", C.c_longlong), ("ldaux", C.c_longlong),
+        ("epi", C.c_int), ("relu", C.c_int), ("kchunk", C.c_int),
+    ]
+
+
+class F32Batch(C.Structure):
+    _fields_ = [
+        ("E", C.c_int), ("in_p", C.c_int), ("H", C.c_int), ("T", C.c_int), ("bias_col", C.c_int),
+        ("feat_mode", C.c_int),
+        ("X", C.c_void_p), ("XN", C.c_void_p), ("Q", C.c_void_p), ("QN", C.c_void_p), ("DQ", C.c_void_p),
+        ("loss", C.c_void_p),
+        ("s_b2", C.c_void_p), ("s_s2", C.c_void_p), ("s_rew", C.c_void_p), ("s_act", C.c_void_p),
+        ("prices", C.c_void_p), ("budget", C.c_void_p), ("shares", C.c_void_p), ("value", C.c_void_p),
+        ("pos", C.c_void_p), ("episodes", C.c_void_p), ("last_final", C.c_void_p), ("ret_sum", C.c_void_p),
+        ("actions_out", C.c_void_p), ("rewards_out", C.c_void_p), ("ctrl", C.c_void_p),
+        ("compat_env", C.c_int), ("target_compat", C.c_int), ("output_relu", C.c_int), ("s0", C.c_int),
+        ("env_offset", C.c_int), ("reward_mode", C.c_int),
+        ("eps", C.c_float), ("inv_ramp", C.c_float), ("b0", C.c_float), ("inv_b0", C.c_float),
+        ("gamma", C.c_float), ("coef", C.c_float), ("td_clip", C.c_float),
+        ("key0", C.c_uint32), ("key1", C.c_uint32),
+    ]
+
+
+F32B_STORE, F32B_MASK, F32B_ATOMIC = 0, 1, 2
+
+
+def _bind_batched():
+    L = _bind()
+    if not getattr(L, "_f32b_bound", False):
+        L.st_f32b_gemm.argtypes = [C.POINTER(GemmF32), C.c_int, C.c_void_p]
+        L.st_f32b_gemm.restype = C.c_int
+        for n in ("st_f32b_gather", "st_f32b_env", "st_f32b_td"):
+            getattr(L, n).argtypes = [C.POINTER(F32Batch), C.c_void_p]
+            getattr(L, n).restype = C.c_int
+        L.st_f32b_colsum.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.st_f32b_colsum.restype = C.c_int
+        L._f32b_bound = True
+    return L
+
+
+class _BatchedScratch:
+    def __init__(self, layout: qn.QNetLayout, E: int, device):
+        f = dict(dtype=torch.float32, device=device)
+        pd = layout.pdims
+        self.X = torch.zeros(E, pd[0], **f)
+        self.XN = torch.zeros(E, pd[0], **f)
+        # activations of x (inputs of layers 1 .. L-1) and of x' (one buffer per layer, reused)
+        self.A = [self.X] + [torch.zeros(E, pd[l], **f) for l in range(1, layout.n_layers)]
+        self.AN = [self.XN] + [torch.zeros(E, pd[l], **f) for l in range(1, layout.n_layers)]
+        self.q = torch.zeros(E, 16, **f)
+        self.qn = torch.zeros(E, 16, **f)
+        # dL/dz of every layer's output: dz[l] is [E][pd[l + 1]] (dz[L - 1] = dQ)
+        self.dz = [torch.zeros(E, pd[l + 1], **f) for l in range(layout.n_layers)]
+        self.loss = torch.zeros(E, **f)
+        self.b2 = torch.zeros(E, **f)
+        self.s2 = torch.zeros(E, dtype=torch.int32, device=device)
+        self.rew = torch.zeros(E, **f)
+        self.act = torch.zeros(E, dtype=torch.int32, device=device)
+
+
+class F32BatchedStep:
+    """Batched fp32 step of :class:`~sharetrade.trainer.engine.VectorEngine` on the matrix cores
+    (csrc/mlp_f32_mfma.hip): the reference network's 203->200->3 geometry -- and any fp32 MLP of the
+    flat layout -- over many envs.  Same interface as :class:`F32EngineStep` (``step``, ``grad``,
+    ``s.loss``, ``rows`` / ``optim`` for ``policy_overrides``); the optimizer is csrc/mlp_f32.hip's
+    ``f32_grad_optim`` applied to the reduced gradient (mode 2), so AdaGrad / Adam / SGD are unchanged."""
+
+    def __init__(self, eng, splits: int = 0):
+        self.eng = eng
+        cfg = eng.cfg
+        self.layout = lay = eng.layout
+        self.net = make_net(lay, cfg.model.output_relu)
+        self.L = _bind_batched()
+        E = eng.E
+        self.s = _BatchedScratch(lay, E, eng.device)
+        self.grad_local = torch.zeros(lay.numel, dtype=torch.float32, device=eng.device)
+        # split-K of the weight-gradient products (K = envs): enough workgroups to fill the chip
+        self.splits = splits or max(1, min(256, E // 256))
+        st, s = eng.state, self.s
+        r = F32Batch()
+        r.E, r.in_p, r.H, r.T, r.bias_col = E, lay.in_p, eng.H, eng.T, lay.bias_col
+        from ..env.trading import FEATURES
+
+        r.feat_mode = FEATURES[cfg.env.features]
+        r.X, r.XN, r.Q, r.QN, r.DQ = (s.X.data_ptr(), s.XN.data_ptr(), s.q.data_ptr(), s.qn.data_ptr(),
+                                      s.dz[-1].data_ptr())
+        r.loss = s.loss.data_ptr()
+        r.s_b2, r.s_s2, r.s_rew, r.s_act = s.b2.data_ptr(), s.s2.data_ptr(), s.rew.data_ptr(), s.act.data_ptr()
+        r.prices = eng.prices.data_ptr()
+        r.budget, r.shares, r.value, r.pos = (st.budget.data_ptr(), st.shares.data_ptr(), st.value.data_ptr(),
+                                              st.pos.data_ptr())
+        r.episodes, r.last_final, r.ret_sum = st.episodes.data_ptr(), st.last_final.data_ptr(), st.ret_sum.data_ptr()
+        r.actions_out, r.rewards_out, r.ctrl = (eng.actions_out.data_ptr(), eng.rewards_out.data_ptr(),
+                                                eng.ctrl.data_ptr())
+        r.compat_env = int(cfg.env.compat_decisions)
+        r.target_compat = int(cfg.agent.target_slot == "compat")
+        r.output_relu = int(cfg.model.output_relu)
+        r.s0, r.env_offset = int(cfg.env.shares), int(eng.env_offset)
+        r.reward_mode = int(cfg.agent.reward_mode == "relative")
+        r.eps = float(cfg.agent.epsilon)
+        r.inv_ramp = float(np.float32(1.0 / cfg.agent.ramp))
+        r.b0 = float(cfg.env.budget)
+        r.inv_b0 = float(np.float32(1.0 / cfg.env.budget))
+        r.gamma, r.coef, r.td_clip = float(cfg.agent.gamma), float(eng.loss_coef), float(cfg.agent.td_clip)
+        r.key0, r.key1 = int(eng.key0), int(eng.key1)
+        self.rows = r          # (policy_overrides edits eps / inv_ramp here)
+        a = cfg.agent
+        o = F32Optim()
+        opt = eng.opt
+        o.params, o.mask = eng.params.data_ptr(), eng.mask.data_ptr()
+        o.s1 = opt.s1.data_ptr() if opt.s1.numel() else None
+        o.s2 = opt.s2.data_ptr() if opt.s2.numel() else None
+        o.acts, o.dz, o.ctrl, o.B, o.kind = None, None, eng.ctrl.data_ptr(), E, OPT_KIND[opt.kind]
+        o.lr, o.beta1, o.beta2, o.eps, o.scale = a.lr, a.adam_betas[0], a.adam_betas[1], a.adam_eps, 1.0
+        o.mode = 2
+        self.optim = o
+        self._fwd = [self._fwd_structs(s.A, s.q), self._fwd_structs(s.AN, s.qn)]
+
+    def _gemm(self, A, B, Cp, M, N, K, am, ak, bk, bn, ldc, epi, bias=None, relu=False, aux=None, ldaux=0, splits=1):
+        g = GemmF32()
+        g.A, g.B, g.C, g.bias, g.aux = A, B, Cp, bias, aux
+        g.M, g.N, g.K = M, N, K
+        g.am, g.ak, g.bk, g.bn, g.ldc, g.ldaux = am, ak, bk, bn, ldc, ldaux
+        g.epi, g.relu, g.kchunk = epi, int(relu), 0
+        return (g, splits)
+
+    def _fwd_structs(self, acts, q):
+        lay, net, E = self.layout, self.net, self.eng.E
+        P = self.eng.params
+        out = []
+        for l in range(lay.n_layers):
+            K, N = lay.pdims[l], lay.pdims[l + 1]
+            last = l == lay.n_layers - 1
+            dst = q if last else acts[l + 1]
+            bias = P.data_ptr() + 4 * net.off_b[l] if net.off_b[l] >= 0 else None
+            relu = (not last) or bool(net.output_relu)
+            # Z = A_l . W_l^T: A(m = env, k = in) row-major, B(k = in, n = out) = W^T[out][in]
+            out.append(self._gemm(acts[l].data_ptr(), P.data_ptr() + 4 * net.off_w[l], dst.data_ptr(), E, N, K,
+                                  K, 1, 1, K, N, F32B_STORE, bias=bias, relu=relu))
+        return out
+
+    def _run(self, structs, sh):
+        for g, splits in structs:
+            native.check(self.L.st_f32b_gemm(C.byref(g), splits, sh), "st_f32b_gemm")
+
+    def grad(self, out: torch.Tensor) -> torch.Tensor:
+        """One env step of every env and the local gradient into ``out`` (no update)."""
+        sh = native.stream_handle()
+        L, r, s, lay, net = self.L, self.rows, self.s, self.layout, self.net
+        E = self.eng.E
+        P = self.eng.params
+        out.zero_()
+        native.check(L.st_f32b_gather(C.byref(r), sh), "st_f32b_gather")
+        self._run(self._fwd[0], sh)
+        native.check(L.st_f32b_env(C.byref(r), sh), "st_f32b_env")
+        self._run(self._fwd[1], sh)
+        native.check(L.st_f32b_td(C.byref(r), sh), "st_f32b_td")
+        for l in reversed(range(lay.n_layers)):
+            Kin, Nout = lay.pdims[l], lay.pdims[l + 1]
+            dz = s.dz[l]
+            # dW_l^T[out][in] += sum_e dZ_l[e][out] A_l[e][in]  (K = envs, split over workgroups)
+            g = self._gemm(dz.data_ptr(), s.A[l].data_ptr(), out.data_ptr() + 4 * net.off_w[l], Nout, Kin, E,
+                           1, Nout, Kin, 1, Kin, F32B_ATOMIC, splits=self.splits)
+            self._run([g], sh)
+            if net.off_b[l] >= 0:
+                native.check(L.st_f32b_colsum(dz.data_ptr(), Nout, E, Nout, out.data_ptr() + 4 * net.off_b[l], sh),
+                             "st_f32b_colsum")
+            if l > 0:
+                # dZ_{l-1} = (dZ_l . W_l) * [A_l > 0]: B(k = out, n = in) = W^T[out][in]
+                g = self._gemm(dz.data_ptr(), P.data_ptr() + 4 * net.off_w[l], s.dz[l - 1].data_ptr(), E, Kin, Nout,
+                               Nout, 1, Kin, 1, Kin, F32B_MASK, aux=s.A[l].data_ptr(), ldaux=Kin)
+                self._run([g], sh)
+        return out
+
+    def step(self, grad_buf: Optional[torch.Tensor] = None, allreduce=None) -> None:
+        """One engine step: batched step + local gradient -> (DP: all-reduce) -> optimizer -> counter."""
+        sh = native.stream_handle()
+        g = grad_buf if grad_buf is not None else self.grad_local
+        self.grad(g)
+        if allreduce is not None:
+            allreduce(g)
+        self.optim.grad = g.data_ptr()
+        native.check(self.L.st_f32_grad_optim(self.net, self.optim, sh), "st_f32_update(batched)")
+        native.check(self.L.st_f32_advance(self.eng.ctrl.data_ptr(), sh), "st_f32_advance")

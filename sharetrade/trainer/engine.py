@@ -265,9 +265,14 @@ class VectorEngine:
         self.grad = torch.zeros(L.numel, dtype=torch.float32, device=dev)
         self.stat_acc = torch.zeros(NSTAT, dtype=torch.float64, device=dev)
         if self.kernel == "fp32_rows":
-            from ..ops.mlp_f32 import F32EngineStep
+            from ..ops.mlp_f32 import F32BatchedStep, F32EngineStep
 
-            self._f32 = F32EngineStep(self)
+            # many envs: the batched MFMA step (csrc/mlp_f32_mfma.hip); few: the per-env row kernels
+            fb = cfg.engine.f32_batched
+            if fb not in ("auto", "on", "off"):
+                raise ValueError(f"engine.f32_batched: {fb!r}")
+            self.f32_path = "batched" if (fb == "on" or (fb == "auto" and self.E >= 1024)) else "rows"
+            self._f32 = F32BatchedStep(self) if self.f32_path == "batched" else F32EngineStep(self)
             return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
         # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide

@@ -167,3 +167,80 @@ def test_init_normal_kernel_matches_host_mirror(native_built):
         dev = qn.init_params(L, cfg.model, seed=5, device="cuda:0").cpu()
         assert torch.equal(dev == 0, host == 0)                 # same padding pattern
         assert torch.allclose(dev, host, rtol=2e-5, atol=2e-6), float((dev - host).abs().max())
+
+
+@pytest.mark.parametrize("preset", ["reference_compat", "intended"])
+def test_fp32_batched_engine_matches_torch_engine(dev, preset):
+    """The batched fp32 MFMA step (csrc/mlp_f32_mfma.hip, the reference's 203->200->3 net over 1,024 envs)
+    vs the plain-PyTorch fp32 oracle engine for 5 steps: the same env transitions, parameters within
+    fp32 summation-order tolerance."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config(preset)
+    cfg.engine.dtype = "fp32"
+    cfg.agent.epsilon = 0.5
+    cfg.agent.ramp = 4.0
+    E, T = 1024, 260
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 5, n_series=E).astype(np.float32))
+    g = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    c = VectorEngine(cfg, prices=prices, device=torch.device("cpu"), envs=E, backend="torch")
+    assert g.kernel == "fp32_rows" and g.f32_path == "batched"
+    for _ in range(5):
+        g.step()
+        c.step()
+        torch.cuda.synchronize()
+        for k in ("budget", "shares", "pos"):
+            assert torch.equal(getattr(g.state, k).cpu(), getattr(c.state, k)), k
+        assert _rel(g.params.cpu(), c.params) < 1e-5, _rel(g.params.cpu(), c.params)
+
+
+@pytest.mark.parametrize("preset", ["reference_compat", "intended"])
+def test_fp32_batched_matches_row_kernels(dev, preset):
+    """Batched MFMA step vs the per-env row kernels on the same engine state (uniform actions): equal
+    transitions, gradients equal up to fp32 summation order, in captured graphs."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, T = 2048, 300
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 8, n_series=E).astype(np.float32))
+    out = {}
+    for path in ("on", "off"):
+        cfg = preset_config(preset)
+        cfg.engine.dtype = "fp32"
+        cfg.engine.f32_batched = path
+        cfg.agent.epsilon = 0.0
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng.f32_path == ("batched" if path == "on" else "rows")
+        g = eng.native_grad().detach().cpu().clone()
+        eng.capture_graph(warmup=1)
+        eng.run(6)
+        torch.cuda.synchronize()
+        out[path] = (g, eng.params.cpu().clone(), {k: v.cpu().clone() for k, v in eng.state.as_dict().items()})
+    (gb, pb, sb), (gr, pr, sr) = out["on"], out["off"]
+    assert _rel(gb, gr) < 1e-5, _rel(gb, gr)
+    for k in ("budget", "shares", "pos", "value"):
+        assert torch.equal(sb[k], sr[k]), k
+    assert _rel(pb, pr) < 1e-5, _rel(pb, pr)
+
+
+def test_fp32_batched_compat_reproduces_reference_portfolio(dev):
+    """Quirk Q1 through the batched path: 1,024 envs of the reference run, reward 0, every final
+    portfolio exactly the 2,400 budget."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("reference_compat")
+    E, T = 1024, 320
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 9, n_series=1).astype(np.float32)).expand(E, -1)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    assert eng.f32_path == "batched"
+    eng.capture_graph(warmup=1)
+    eng.run(T - 201 - 1)
+    torch.cuda.synchronize()
+    assert float(eng.stat_acc[0]) == 0.0
+    fin = eng.final_portfolios().cpu()
+    assert torch.all(fin == 2400.0), fin
