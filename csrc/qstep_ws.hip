@@ -71,6 +71,9 @@ constexpr int WS_GXP = 2;       // paired slots: X fragment pairs read this many
 #ifndef WS_LDU_CAST
 #define WS_LDU_CAST 0
 #endif
+#ifndef WS_PC_PERM
+#define WS_PC_PERM 0      // 1: x''s extra window values by ds_bpermute from the neighbour lane group (csrc/ab/qstep_ws_pcperm.hip)
+#endif
 #ifndef WS_NOWB
 #define WS_NOWB 0       // timing build csrc/ab/qstep_ws_nowb.hip: no env-state write-back (wrong results)
 #endif
@@ -417,7 +420,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       const float* q_ = b_ + 32 * ks + 8 * g4;                                                   \
       pa[ks] = ldu4(q_);                                                                         \
       pb[ks] = ldu4(q_ + 4);                                                                     \
-      pc[ks] = q_[8];                                                                            \
+      if (!WS_PC_PERM || ks == 5) pc[ks] = q_[8];                                                 \
     }                                                                                            \
     if (g4 == 1 || g4 == 2) {                                                                    \
       const float* r_ = b_ + 188 + 4 * g4;                                                       \
@@ -484,6 +487,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         return FEAT ? __fmaf_rn(w, invn, -1.0f) : w;
       };
       s8v X[6], Xn[6];
+#if WS_PC_PERM
+      // x' needs the window value after each lane group's 8: lane group g4 + 1's first value of the same
+      // k-step, or for g4 = 3 lane group 0's first value of the next k-step -- one ds_bpermute per k-step
+      // instead of a 4-byte HBM load (k-step 5's is still loaded: it is lane group 1's pd.x)
+#pragma unroll
+      for (int ks = 0; ks < 5; ++ks) {
+        const float src = g4 == 0 ? pa[ks + 1].x : pa[ks].x;
+        pc[ks] = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 16) & 63) << 2, __float_as_int(src)));
+      }
+#endif
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
         X[ks] = cat8(pk4(fx(pa[ks].x), fx(pa[ks].y), fx(pa[ks].z), fx(pa[ks].w)),

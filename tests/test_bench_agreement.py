@@ -149,12 +149,17 @@ def _episode_worker(rank, world, port, out_dir):
                        world_size=world, group=dist.group.WORLD, envs=E, backend="torch")
     eng.sync_params_from(0)
     eng.run(3)
+    p_before, pos_before = eng.params.clone(), eng.state.pos.clone()
+    greedy = benchkit.greedy_episode_returns(eng, world, dist.group.WORLD)
+    bh = benchkit.buy_and_hold_returns(eng, world, dist.group.WORLD)
+    restored = bool(torch.equal(p_before, eng.params) and torch.equal(pos_before, eng.state.pos))
     learned = benchkit.full_episode_returns(eng, world, dist.group.WORLD)
     rnd = benchkit.full_episode_returns(eng, world, dist.group.WORLD, random_policy=True)
     # the random-policy episode: every action is the uniform draw (exploit prob forced to 0)
     with open(os.path.join(out_dir, f"e{rank}.txt"), "w") as f:
         f.write(f"{learned['n']} {learned['steps']} {learned['mean']!r} {learned['std']!r} "
-                f"{rnd['n']} {rnd['mean']!r} {rnd['std']!r} {cfg.agent.epsilon!r}")
+                f"{rnd['n']} {rnd['mean']!r} {rnd['std']!r} {cfg.agent.epsilon!r} "
+                f"{greedy['n']} {greedy['mean']!r} {bh['n']} {bh['mean']!r} {int(restored)} {cfg.agent.lr!r}")
     dist.destroy_process_group()
 
 
@@ -165,9 +170,37 @@ def test_full_episode_returns_two_ranks():
                            start_method="spawn")
         res = [open(os.path.join(d, f"e{r}.txt")).read().split() for r in range(world)]
     assert res[0] == res[1]                          # the reduced statistics agree on every rank
-    n, steps, m, s, n_r, m_r, s_r, eps = res[0]
+    n, steps, m, s, n_r, m_r, s_r, eps, n_g, m_g, n_bh, m_bh, restored, lr = res[0]
     assert int(n) == 12 and int(steps) == 215 - 201  # every env of both ranks completed one episode
-    assert int(n_r) == 12
-    for v in (m, s, m_r, s_r):
+    assert int(n_r) == 12 and int(n_g) == 12 and int(n_bh) == 12
+    for v in (m, s, m_r, s_r, m_g, m_bh):
         assert np.isfinite(float(v))
     assert float(eps) == 0.9                         # the epsilon override was restored
+    assert restored == "1" and float(lr) == 1e-3     # the greedy evaluation ran on a snapshot
+
+
+def _vote_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SHARETRADE_FAIL_CAPTURE="1")
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=20))
+    from sharetrade.trainer import benchkit
+
+    eng = _FakeEngine()
+    use = benchkit.capture_with_vote(eng, rank, world, dist.group.WORLD, warmup=0, log=lambda m: None)
+    eng.run(10)
+    with open(os.path.join(out_dir, f"v{rank}.txt"), "w") as f:
+        f.write(f"{int(use)} {int(eng._graph is None and eng._graph_k is None)} {eng.calls}")
+    dist.destroy_process_group()
+
+
+def test_capture_with_vote_drops_graphs_on_every_rank():
+    """The train() / rank-group capture path: rank 1's capture fails, so both ranks drop
+    their graphs and step eagerly with the same collectives."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_vote_worker, args=(world, _free_port(), d), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [open(os.path.join(d, f"v{r}.txt")).read().split() for r in range(world)]
+    assert res[0] == res[1] == ["0", "1", "10"], res
