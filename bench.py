@@ -253,12 +253,14 @@ def main() -> int:
                         "timed window), mean / population std over all envs of all ranks. greedy: the learned "
                         "parameters frozen, exploit-only; init_greedy: the same at the random init; buy_hold: "
                         "Buy every step (budget into shares, then held); learned: online epsilon-greedy episode "
-                        "with learning on; random: uniform actions",
+                        "with learning on; random: uniform actions. median: exact at one rank, the mean of the "
+                        "ranks' medians at several",
                 "episode_steps": lr_["steps"],
             }
             for k in ("greedy", "init_greedy", "buy_hold", "learned", "random"):
                 er[f"{k}_mean"] = round(episodes[k]["mean"], 4)
                 er[f"{k}_std"] = round(episodes[k]["std"], 4)
+                er[f"{k}_median"] = round(episodes[k]["median"], 4)
             er["episodes"] = lr_["n"]
             er["complete_frac"] = round(min(episodes[k]["complete_frac"] for k in episodes), 6)
             out["episode_return"] = er

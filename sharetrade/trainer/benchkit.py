@@ -172,19 +172,24 @@ def _episode_summary(eng, ep0: torch.Tensor, world: int, group, steps: int) -> D
 
 
 def _reduce_returns(done: torch.Tensor, fin: torch.Tensor, E: int, world: int, group, steps: int) -> Dict[str, float]:
-    s = torch.stack([done.double().sum(), fin.sum(), (fin * fin).sum()])
+    """Mean / population std over every completed env of every rank, and the median: exact with one rank,
+    the mean of the ranks' medians with several (a geometric bank's mean is carried by the few series
+    that compound; the median is the typical env)."""
+    sel = fin[done]
+    med = sel.median().double() if sel.numel() else torch.tensor(0.0, dtype=torch.float64, device=fin.device)
+    s = torch.stack([done.double().sum(), fin.sum(), (fin * fin).sum(), med.to(fin.device)])
     if world > 1:
         dist = _dist()
         if dist.get_backend(group) == "gloo":
             s = s.cpu()
         dist.all_reduce(s, group=group)
-    n, sx, sxx = (float(v) for v in s.cpu())
+    n, sx, sxx, smed = (float(v) for v in s.cpu())
     n_total = float(E * world)
     if n == 0:
-        return {"n": 0, "mean": math.nan, "std": math.nan, "steps": steps, "complete_frac": 0.0}
+        return {"n": 0, "mean": math.nan, "std": math.nan, "median": math.nan, "steps": steps, "complete_frac": 0.0}
     m = sx / n
-    return {"n": int(n), "mean": m, "std": math.sqrt(max(0.0, sxx / n - m * m)), "steps": steps,
-            "complete_frac": n / n_total}
+    return {"n": int(n), "mean": m, "std": math.sqrt(max(0.0, sxx / n - m * m)), "median": smed / max(1, world),
+            "steps": steps, "complete_frac": n / n_total}
 
 
 def greedy_episode_returns(eng, world: int = 1, group=None, params: Optional[torch.Tensor] = None) -> Dict[str, float]:
