@@ -570,8 +570,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       // (after the features: a store or load issued before them would hold their window wait)
       WS_WRITE_BACK()
       WS_LOAD_ENV(k + 2, 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
-      if (DYN && d == 0 && lane == 0 && !ended) {   // the chunk of round k + 3 (used from tile k + 1 on)
-        claim_v = atomicAdd(head, 1u);
+      if (DYN && d == 0 && !ended) {   // the chunk of round k + 3 (used from tile k + 1 on); flags wave-uniform
+        if (lane == 0) claim_v = atomicAdd(head, 1u);
         claim_out = true;
       }
       // the epsilon-greedy draw (Philox, ~70 VALU with quarter-rate multiplies) depends only on (env, step):
@@ -795,20 +795,23 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       if (g4 == 0) *reinterpret_cast<s4v*>(sx + l16 * KX + 204) = bq;
       if (lane == 0) __hip_atomic_store(ctl + 1 + sl, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (DYN) {
-        if (d == 0 && lane == 0) {
+        if (d == 0) {
           // round k + 3's chunk into the ring; the first missing round also fixes the round count
           int c = -1;
           if (claim_out) {
-            const long long cc = 8ll * (3ll * gx + (long long)claim_v) + xg;
+            const unsigned cv = (unsigned)__builtin_amdgcn_readfirstlane((int)claim_v);
+            const long long cc = 8ll * (3ll * gx + (long long)cv) + xg;
             c = cc < nchunks ? (int)cc : -1;
             claim_out = false;
           }
-          if (c < 0 && !ended) {
-            ended = true;
-            if (ck2 >= 0) __hip_atomic_store(ctl + CTL_NROUNDS, k + 3 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const bool first_end = c < 0 && !ended;
+          if (c < 0) ended = true;
+          if (lane == 0) {
+            if (first_end && ck2 >= 0)
+              __hip_atomic_store(ctl + CTL_NROUNDS, k + 3 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(ctl + cid_word(k + 3), (((k + 3) & 0x3FF) << CID_SHIFT) | (c + 1), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
           }
-          __hip_atomic_store(ctl + cid_word(k + 3), (((k + 3) & 0x3FF) << CID_SHIFT) | (c + 1), __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         ck0 = ck1;
         ck1 = ck2;
