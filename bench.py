@@ -185,6 +185,7 @@ def main() -> int:
     n_trans = eng.E * world * eng.step_count   # every step taken (prime + warmup + timed)
     st = stats.cpu().tolist()
     episodes = None
+    episode_error = None
     if not args.no_episode:
         # untimed, after the timed window, every env plays complete episodes over its series
         # (T - H = 5,846 steps each) on the same banks:
@@ -193,13 +194,19 @@ def main() -> int:
         #  * buy_hold: Buy at every step (budget into shares at the start, then held);
         #  * learned: the online epsilon-greedy episode with learning on (the training regime);
         #  * random: uniformly random actions.
-        greedy = benchkit.greedy_episode_returns(eng, world, group)
-        init_greedy = benchkit.greedy_episode_returns(eng, world, group, params=init_params)
-        buy_hold = benchkit.buy_and_hold_returns(eng, world, group)
-        learned = benchkit.full_episode_returns(eng, world, group)
-        rnd = benchkit.full_episode_returns(eng, world, group, random_policy=True)
-        episodes = {"learned": learned, "random": rnd, "greedy": greedy, "init_greedy": init_greedy,
-                    "buy_hold": buy_hold}
+        try:
+            greedy = benchkit.greedy_episode_returns(eng, world, group)
+            init_greedy = benchkit.greedy_episode_returns(eng, world, group, params=init_params)
+            buy_hold = benchkit.buy_and_hold_returns(eng, world, group)
+            learned = benchkit.full_episode_returns(eng, world, group)
+            rnd = benchkit.full_episode_returns(eng, world, group, random_policy=True)
+            episodes = {"learned": learned, "random": rnd, "greedy": greedy, "init_greedy": init_greedy,
+                        "buy_hold": buy_hold}
+        except Exception as e:  # noqa: BLE001 -- the timed measurement above stands; report what failed
+            if world > 1:
+                raise          # (a rank that stops mid-collective would hang its peers: fail the job)
+            episode_error = f"{type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}"
+            print(f"bench.py: episode evaluation failed: {episode_error}", file=sys.stderr)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -246,6 +253,8 @@ def main() -> int:
             out["hbm_total_gb"] = round(total / 1e9, 1)
         if allreduce_ms is not None:
             out["allreduce_ms_per_step"] = allreduce_ms
+        if episode_error is not None:
+            out["episode_return_error"] = episode_error
         if episodes is not None:
             lr_ = episodes["learned"]
             er = {
