@@ -104,16 +104,19 @@ def test_buy_and_hold_matches_host_simulation(native_built):
 
 
 def test_greedy_learned_beats_random(native_built):
-    """On an AR(1)-momentum bank the learned policy, evaluated greedily with frozen weights after two
-    online episodes, earns well above the uniform-random policy (mean final portfolio) -- the policy,
-    not the schedule (profiles/r4_learning_eval_65k.md: the same deterministic run, episode 2)."""
+    """On a bank with a learnable signal (persistent drift regimes, ``data.source = trend``; gamma 0.99)
+    the learned policy, evaluated greedily with frozen weights after two online episodes, earns well
+    above the uniform-random policy in mean and median -- the policy, not the schedule
+    (profiles/r4_learning_eval_65k.md, run trend_g99: greedy 3.2-5.8k mean / 320-648 median over six
+    episodes vs random 1.1k / 46)."""
     from sharetrade.config import preset_config
     from sharetrade.trainer import benchkit
     from sharetrade.trainer.engine import VectorEngine
 
     cfg = preset_config("flagship")
-    cfg.data.source = "ar1"
+    cfg.data.source = "trend"
     cfg.data.length = 1601
+    cfg.agent.gamma = 0.99
     eng = VectorEngine(cfg, device=torch.device("cuda", 0), envs=65536)
     eng.capture_graph(warmup=0)
     for _ in range(2):
@@ -122,10 +125,9 @@ def test_greedy_learned_beats_random(native_built):
     eng.synchronize()
     g = benchkit.greedy_episode_returns(eng)
     r = benchkit.full_episode_returns(eng, random_policy=True)
-    bh = benchkit.buy_and_hold_returns(eng)
     assert g["complete_frac"] == 1.0 and r["complete_frac"] == 1.0
     assert g["mean"] > 2.0 * r["mean"] + 100.0, (g, r)
-    assert g["mean"] <= 1.05 * bh["mean"] + 50.0, (g, bh)   # one-share trades: holding is near-optimal here
+    assert g["median"] > r["median"] + 50.0, (g, r)
 
 
 def test_train_falls_back_to_eager_when_capture_fails(native_built, monkeypatch):
