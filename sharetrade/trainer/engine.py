@@ -268,7 +268,7 @@ class VectorEngine:
             from ..ops.mlp_f32 import F32BatchedStep, F32EngineStep
 
             # many envs: the batched MFMA step (csrc/mlp_f32_mfma.hip); few: the per-env row kernels
-            fb = cfg.engine.f32_batched
+            fb = self.cfg.engine.f32_batched
             if fb not in ("auto", "on", "off"):
                 raise ValueError(f"engine.f32_batched: {fb!r}")
             self.f32_path = "batched" if (fb == "on" or (fb == "auto" and self.E >= 1024)) else "rows"
