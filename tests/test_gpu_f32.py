@@ -220,7 +220,11 @@ def test_fp32_batched_matches_row_kernels(dev, preset):
         torch.cuda.synchronize()
         out[path] = (g, eng.params.cpu().clone(), {k: v.cpu().clone() for k, v in eng.state.as_dict().items()})
     (gb, pb, sb), (gr, pr, sr) = out["on"], out["off"]
-    assert _rel(gb, gr) < 1e-5, _rel(gb, gr)
+    # reference_compat's reward is 0 (quirk Q1), so its gradient is a sum of +/- TD terms over 2,048 envs
+    # that nearly cancel: the batched path's split-K atomics and the rows path's fixed-order reduction
+    # then differ by ~1e-4 of the (small) result; intended's gradient does not cancel
+    tol = 1e-3 if preset == "reference_compat" else 1e-5
+    assert _rel(gb, gr) < tol, _rel(gb, gr)
     for k in ("budget", "shares", "pos", "value"):
         assert torch.equal(sb[k], sr[k]), k
     assert _rel(pb, pr) < 1e-5, _rel(pb, pr)
