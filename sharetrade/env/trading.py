@@ -137,11 +137,19 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
                     target_slot: str, gamma: float, output_relu: bool, epsilon: float, ramp: float,
                     seed: int, rank: int, step: int, loss_coef: float, env_offset: int = 0,
                     emulate_bf16: bool = False, forced_actions: Optional[torch.Tensor] = None,
-                    reward_mode: str = "absolute", td_clip: float = 0.0):
+                    reward_mode: str = "absolute", td_clip: float = 0.0,
+                    target_params: Optional[torch.Tensor] = None, double_dqn: bool = False,
+                    reward_scale: float = 1.0, ramp_pos: Optional[torch.Tensor] = None):
     """One fused engine step for all envs.  Returns ``(new_state, grad, info)``.
 
     ``loss_coef`` multiplies ``(q_slot - y)`` (2.0 for the reference's summed
-    squared error, ``2/E_total`` for a batch mean)."""
+    squared error, ``2/E_total`` for a batch mean).
+
+    Learning-quality experiments (not in the reference, which bootstraps from the online net at the
+    episode position's ramp, QDecisionPolicyActor.scala:58-71): ``target_params`` values Q(x') with a
+    target copy of the parameters; ``double_dqn`` picks the max-Q(x') action with the online net and values
+    it with the target; ``reward_scale`` multiplies the reward in the TD target; ``ramp_pos`` replaces the
+    episode position in the exploit ramp (e.g. the global step count)."""
     E, T = prices.shape
     H = history
     pos = st.pos
@@ -150,7 +158,8 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
     x = features(win, st.budget, st.shares, feature_mode, budget0)
     q, acts, xp = qn.forward(params, layout, x, output_relu, emulate_bf16)
     env_ids = np.arange(env_offset, env_offset + E, dtype=np.uint32)
-    a, exploit = select_actions(q, pos, env_ids, step, seed, rank, epsilon, ramp, layout.n_actions)
+    a, exploit = select_actions(q, pos if ramp_pos is None else ramp_pos, env_ids, step, seed, rank, epsilon, ramp,
+                                layout.n_actions)
     if forced_actions is not None:
         a = forced_actions.to(torch.int32)
     b2, s2, r = env_transition(a, st.budget, st.shares, st.value, v_new, compat_env, budget0, shares0,
@@ -159,12 +168,20 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
     x2 = features(win2, b2, s2, feature_mode, budget0)
     q2, _, _ = qn.forward(params, layout, x2, output_relu, emulate_bf16)
     qa = q2[:, : layout.n_actions]
+    qv = qa
+    if target_params is not None:
+        qt, _, _ = qn.forward(target_params, layout, x2, output_relu, emulate_bf16)
+        qv = qt[:, : layout.n_actions]
+    rs = r * reward_scale if reward_scale != 1.0 else r
     if target_slot == "compat":
         slot = torch.argmax(qa, dim=1)
-        y = r + gamma * qa.gather(1, slot[:, None])[:, 0]
+        y = rs + gamma * qv.gather(1, slot[:, None])[:, 0]
     else:
         slot = a.long()
-        y = r + gamma * qa.max(dim=1).values
+        if double_dqn:
+            y = rs + gamma * qv.gather(1, torch.argmax(qa, dim=1)[:, None])[:, 0]
+        else:
+            y = rs + gamma * qv.max(dim=1).values
     qs = q.gather(1, slot[:, None])[:, 0]
     dq = torch.zeros_like(q)
     d = qs - y

@@ -138,6 +138,15 @@ class VectorEngine:
         if be == "auto":
             be = "native" if self.device.type == "cuda" else "torch"
         self.backend = be
+        a = cfg.agent
+        if be != "torch" and (a.target_every or a.double_dqn or a.reward_scale != 1.0 or a.ramp_mode != "position"):
+            raise NotImplementedError("agent.target_every / double_dqn / reward_scale / ramp_mode are learning "
+                                      "experiments of the torch backend (engine.backend='torch')")
+        if a.ramp_mode not in ("position", "global"):
+            raise ValueError(f"agent.ramp_mode: {a.ramp_mode!r}")
+        if a.double_dqn and not a.target_every:
+            raise ValueError("agent.double_dqn needs agent.target_every > 0")
+        self.params_target = None
         L = self.layout
         self.kernel = None
         if be == "native":
@@ -465,11 +474,15 @@ class VectorEngine:
             epsilon=cfg.agent.epsilon, ramp=cfg.agent.ramp, seed=cfg.agent.seed, rank=0,
             step=self.step_count, loss_coef=self.loss_coef, env_offset=self.env_offset,
             emulate_bf16=(cfg.engine.dtype == "bf16"), reward_mode=cfg.agent.reward_mode,
-            td_clip=cfg.agent.td_clip)
+            td_clip=cfg.agent.td_clip, target_params=self._target_params(), double_dqn=cfg.agent.double_dqn,
+            reward_scale=cfg.agent.reward_scale,
+            ramp_pos=(torch.full_like(self.state.pos, self.step_count) if cfg.agent.ramp_mode == "global" else None))
         if self.world_size > 1:
             self._sync.all_reduce(grad)
         qn.optimizer_step_ref(self.params, grad, self.opt, self.mask, cfg.agent.lr, cfg.agent.adam_betas,
                               cfg.agent.adam_eps)
+        if cfg.agent.target_every and (self.step_count + 1) % int(cfg.agent.target_every) == 0:
+            self.params_target.copy_(self.params)
         self._ema_update()
         done = ns.episodes > self.state.episodes
         fin = torch.where(done, ns.last_final, torch.zeros_like(ns.last_final)).double()
@@ -480,6 +493,13 @@ class VectorEngine:
         self.state = ns
         self._last_actions = info["actions"]
         self.grad_last = grad
+
+    def _target_params(self) -> Optional[torch.Tensor]:
+        if not self.cfg.agent.target_every:
+            return None
+        if self.params_target is None:
+            self.params_target = self.params.detach().clone()
+        return self.params_target
 
     def _ema_update(self) -> None:
         """ema <- ema + (1 - decay) (w - ema) in fp32, as csrc/optim.hip does it (host-side paths)."""
@@ -674,6 +694,8 @@ class VectorEngine:
             d["env_" + k] = v
         if self.params_ema is not None:
             d["params_ema"] = self.params_ema
+        if self.params_target is not None:
+            d["params_target"] = self.params_target
         return {k: v.detach().cpu().clone() for k, v in d.items()}
 
     def _opt_count(self) -> int:
@@ -700,6 +722,9 @@ class VectorEngine:
             self.opt.s1.copy_(d["opt_s1"].to(self.device))
         if self.opt.s2.numel():
             self.opt.s2.copy_(d["opt_s2"].to(self.device))
+        if "params_target" in d:
+            self._target_params()
+            self.params_target.copy_(d["params_target"].to(self.device))
         self.opt.t = int(d["opt_t"][0])
         self.step_count = int(d["step"][0])
         for k in self.state.as_dict():

@@ -8,7 +8,9 @@ gradient).  Modes:
 * ``sync``    -- synchronous DP (bench.py's default at N > 1): step kernel, slab reduce, RCCL all-reduce,
                  Adam, all captured in the HIP graphs;
 * ``overlap`` -- ``--dp-overlap``: this step's all-reduce on RCCL's stream beside the next step's kernel
-                 (one-step-delayed gradient, eager launches).
+                 (one-step-delayed gradient, eager launches, dynamic chunk schedule);
+* ``single_dyn`` / ``overlap_static`` -- the same with the other chunk schedule (separates the schedule's
+                 cost from the overlapped path's).
 
     python tools/bench_flagship_dp.py --steps 200 --warmup 20 [--modes single,sync,overlap] [--out x.md]
 """
@@ -29,8 +31,12 @@ def _time(mode, steps, warm, envs, group):
 
     cfg = preset_config("flagship")
     cfg.engine.envs_per_rank = envs
-    world = 1 if mode == "single" else 2
-    cfg.engine.dp_overlap = mode == "overlap"
+    world = 1 if mode.startswith("single") else 2
+    cfg.engine.dp_overlap = mode.startswith("overlap")
+    if mode.endswith("_dyn"):
+        cfg.engine.chunk_schedule = "dynamic"
+    elif mode.endswith("_static"):
+        cfg.engine.chunk_schedule = "static"
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, rank=0, world_size=world, group=group if world > 1 else None)
     use_graph, _ = benchkit.prepare_steps(eng, not cfg.engine.dp_overlap, 0, 1, None, prime_reps=4)

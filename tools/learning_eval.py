@@ -89,7 +89,7 @@ def run_one(name: str, sets, a, device):
     cfg = preset_config("flagship")
     cfg.data.length = a.length
     cfg.override(list(sets))
-    eng = VectorEngine(cfg, device=device, envs=a.envs)
+    eng = VectorEngine(cfg, device=device, envs=a.envs, backend=a.backend)
     init = eng.params.detach().clone()
     if eng.backend == "native":
         eng.capture_graph(warmup=0)
@@ -124,6 +124,8 @@ def main() -> int:
     ap.add_argument("--episodes", type=int, default=5)
     ap.add_argument("--run", action="append", default=[], help="name:key=val,key=val (config overrides)")
     ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--backend", default=None, help="engine backend: native (default on a GPU) | torch (the "
+                    "oracle; needed for agent.target_every / double_dqn / reward_scale / ramp_mode runs)")
     ap.add_argument("-o", "--out", default="")
     a = ap.parse_args()
     if a.device == "cuda":
@@ -138,7 +140,8 @@ def main() -> int:
         sets = [s for s in rest.split(",") if s]
         res.append(run_one(name, sets, a, dev))
     lines = [f"# Greedy evaluation of the learned policy: {a.envs} envs, series length {a.length} "
-             f"({a.length - 201} steps per episode), {a.episodes} online episodes per run", "",
+             f"({a.length - 201} steps per episode), {a.episodes} online episodes per run"
+             + (f", `{a.backend}` backend" if a.backend else ""), "",
              "Each cell: mean / median over envs of (final portfolio - initial budget $2,400) for one complete "
              "episode.  `online` = the training episode itself (epsilon-greedy ramp, learning on); `greedy` = "
              "the parameters after that episode, frozen, exploit-only, replayed from the start of the series "
