@@ -64,7 +64,7 @@ def main() -> int:
                          "measured faster, tools/dp_host_overhead.py)")
     ap.add_argument("--sync-dp", action="store_true", help="(default) strict synchronous DP")
     ap.add_argument("--chunk-schedule", default="auto",
-                    help="step-kernel chunk schedule: auto (dynamic for overlapped DP) | static | dynamic")
+                    help="step-kernel chunk schedule: auto (static; dynamic for the wide kernel under overlapped DP) | static | dynamic")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per HIP-graph replay in the timed loop (0 = engine.graph_steps)")
     ap.add_argument("--pg-timeout", type=float, default=300.0,

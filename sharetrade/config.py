@@ -186,7 +186,8 @@ class EngineConfig:
     # chunk schedule of the 64-env-chunk step kernel: "static" (chunk k of workgroup i = i + k*grid,
     # bit-reproducible), "dynamic" (per-XCD claim heads: workgroups whose CU is still held by the
     # overlapped RCCL all-reduce take fewer chunks instead of stretching the launch), or "auto"
-    # (dynamic for overlapped DP with world_size > 1, else static)
+    # (dynamic for the wide kernel under overlapped DP with world_size > 1, else static: the ws kernel's
+    # dynamic build is 14 % slower, profiles/r4_flagship_dp.md)
     chunk_schedule: str = "auto"
     grid: int = 0                   # step-kernel workgroups: 0 = one per CU (capped at the chunk count)
     # > 0: keep a Polyak (exponential moving) average of the parameters, updated by the optimizer pass

@@ -300,7 +300,11 @@ class VectorEngine:
         self.stat_slab = torch.zeros(self.grid, NSTAT, dtype=torch.float32, device=dev)
         sched = self.cfg.engine.chunk_schedule
         if sched == "auto":
-            sched = "dynamic" if (self.world_size > 1 and self.cfg.engine.dp_overlap) else "static"
+            # ws: static even under overlapped DP -- its dynamic build costs +14 % per step on one GPU (a
+            # 256-VGPR data wave with 36 B of spills), the static one +0.0 % beside the overlapped
+            # all-reduce (tools/bench_flagship_dp.py, profiles/r4_flagship_dp.md)
+            sched = ("dynamic" if (self.world_size > 1 and self.cfg.engine.dp_overlap and self.step_kernel != "ws")
+                     else "static")
         if sched not in ("static", "dynamic"):
             raise ValueError(f"engine.chunk_schedule: {sched!r}")
         # dynamic: 8 per-XCD claim heads, one per 128-byte line (csrc/qstep_wide.hip, csrc/qstep_ws.hip);
