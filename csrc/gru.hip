@@ -104,10 +104,11 @@ __global__ void __launch_bounds__(256) gru_pack_kernel(GruPack p) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid < RH) {
     const int u = tid;
-    p.bias4[u] = p.b_ih[u] + p.b_hh[u];
-    p.bias4[RH + u] = p.b_ih[RH + u] + p.b_hh[RH + u];
-    p.bias4[2 * RH + u] = p.b_ih[2 * RH + u];
-    p.bias4[3 * RH + u] = p.b_hh[2 * RH + u];
+    // pre-scaled gate biases (gru_common.h GS_RZ / GS_N)
+    p.bias4[u] = (p.b_ih[u] + p.b_hh[u]) * GS_RZ;
+    p.bias4[RH + u] = (p.b_ih[RH + u] + p.b_hh[RH + u]) * GS_RZ;
+    p.bias4[2 * RH + u] = p.b_ih[2 * RH + u] * GS_N;
+    p.bias4[3 * RH + u] = p.b_hh[2 * RH + u] * GS_N;
     for (int a = 0; a < 3; ++a) p.wq[a * RH + u] = p.w_q[a * RH + u];
     p.wq[3 * RH + u] = u < 3 ? p.b_q[u] : 0.f;
   }
@@ -117,10 +118,11 @@ __global__ void __launch_bounds__(256) gru_pack_kernel(GruPack p) {
   const int row = g * RH + 32 * w + 16 * m + (lane & 15);
   const int gl = lane >> 4;
   const float* wr = p.w_hh + (size_t)row * RH + 128 * ks;
+  const float gs = g == 2 ? GS_N : GS_RZ;   // the gate's pre-scale, applied before quantization
   // block exponent of K-block b (32 columns) of this row within the K step
   auto blk_e = [&](int b) {
     float amax = 0.f;
-    for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(wr[32 * b + j]));
+    for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(wr[32 * b + j] * gs));
     return mx_exp(amax);
   };
   const int e_lo = blk_e(gl >> 1), e_hi = blk_e(2 + (gl >> 1));   // blocks of this lane's two 16-byte halves
@@ -129,10 +131,10 @@ __global__ void __launch_bounds__(256) gru_pack_kernel(GruPack p) {
   i8v frag;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    frag[j] = (int)fp8x4(ldexpf(lo[4 * j], -e_lo), ldexpf(lo[4 * j + 1], -e_lo), ldexpf(lo[4 * j + 2], -e_lo),
-                         ldexpf(lo[4 * j + 3], -e_lo));
-    frag[4 + j] = (int)fp8x4(ldexpf(hi[4 * j], -e_hi), ldexpf(hi[4 * j + 1], -e_hi), ldexpf(hi[4 * j + 2], -e_hi),
-                             ldexpf(hi[4 * j + 3], -e_hi));
+    frag[j] = (int)fp8x4(ldexpf(lo[4 * j] * gs, -e_lo), ldexpf(lo[4 * j + 1] * gs, -e_lo),
+                         ldexpf(lo[4 * j + 2] * gs, -e_lo), ldexpf(lo[4 * j + 3] * gs, -e_lo));
+    frag[4 + j] = (int)fp8x4(ldexpf(hi[4 * j] * gs, -e_hi), ldexpf(hi[4 * j + 1] * gs, -e_hi),
+                             ldexpf(hi[4 * j + 2] * gs, -e_hi), ldexpf(hi[4 * j + 3] * gs, -e_hi));
   }
   p.whh8[tid] = frag;
   p.whhs[tid] = blk_e(gl) + 127;      // the scale slot of lane i + 16g belongs to K-block g
@@ -163,7 +165,7 @@ __global__ void __launch_bounds__(256) gru_pack_kernel(GruPack p) {
   if (ks == 0) {
     s8v x;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = (short)f2bf(p.w_ih[(size_t)row * RFL + 8 * (lane >> 4) + j]);
+    for (int j = 0; j < 8; ++j) x[j] = (short)f2bf(p.w_ih[(size_t)row * RFL + 8 * (lane >> 4) + j] * gs);
     p.wih[((w * 3 + g) * 2 + m) * 64 + lane] = x;
   }
 }
@@ -397,9 +399,9 @@ __global__ void __launch_bounds__(RT, 1) gru_act_kernel(GruAct p) {
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float r = sigm2(ar[m][i]);
-            const float z = sigm2(az[m][i]);
-            const float nn = tanh2(__builtin_fmaf(r, anh[m][i], anx[m][i]));
+            const float r = sigm_ps(ar[m][i]);
+            const float z = sigm_ps(az[m][i]);
+            const float nn = tanh_ps(__builtin_fmaf(r, anh[m][i], anx[m][i]));
             hr[m][n][i] = __builtin_fmaf(z, hr[m][n][i] - nn, nn);
           }
         // Q partials of this wave's units: one MFMA, h (bf16) taken straight from the accumulator layout
@@ -761,9 +763,9 @@ __global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float r = sigm2(ar[m][i]);
-          const float z = sigm2(az[m][i]);
-          const float nn = tanh2(__builtin_fmaf(r, anh[m][i], anx[m][i]));
+          const float r = sigm_ps(ar[m][i]);
+          const float z = sigm_ps(az[m][i]);
+          const float nn = tanh_ps(__builtin_fmaf(r, anh[m][i], anx[m][i]));
           hr[K][m][n][i] = __builtin_fmaf(z, hr[K][m][n][i] - nn, nn);
         }
       {

@@ -52,6 +52,13 @@ ST_DEV float tanh2(float x) {
   return __builtin_fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -2.88539008f)), -1.f);
 }
 ST_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
+// gate pre-activations arrive pre-scaled (gru_pack_kernel folds -log2(e) into the r / z rows of W_hh, W_ih and
+// their biases, -2 log2(e) into the n rows): sigmoid / tanh are then exp2 + add + rcp with no scaling
+// multiply -- 48 fewer VALU per wave-step of the actor (profiles/r4_gru_prescale.md)
+constexpr float GS_RZ = -1.44269504f;
+constexpr float GS_N = -2.88539008f;
+ST_DEV float sigm_ps(float y) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y)); }
+ST_DEV float tanh_ps(float y) { return __builtin_fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(y)), -1.f); }
 
 // max over the 4 rows of 16 lanes (lanes l, l^16, l^32, l^48) of a non-negative value: two VALU
 // row swaps (v_permlane16/32_swap) instead of two LDS round trips (ds_bpermute); unsigned max of

@@ -278,10 +278,11 @@ __global__ void __launch_bounds__(RT, 1) gru_seq_fwd_kernel(GruSeqFwd p) {
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float r = sigm2(ar[m][i]);
-          const float z = sigm2(az[m][i]);
-          const float nn = tanh2(__builtin_fmaf(r, anh[m][i], anx[m][i]));
-          vr[4 * m + i] = r; vz[4 * m + i] = z; vn[4 * m + i] = nn; vg[4 * m + i] = anh[m][i];
+          const float r = sigm_ps(ar[m][i]);
+          const float z = sigm_ps(az[m][i]);
+          const float nn = tanh_ps(__builtin_fmaf(r, anh[m][i], anx[m][i]));
+          // gh_n un-scaled for the backward (the packed weights are pre-scaled, gru_common.h)
+          vr[4 * m + i] = r; vz[4 * m + i] = z; vn[4 * m + i] = nn; vg[4 * m + i] = anh[m][i] * (1.f / GS_N);
           vh[4 * m + i] = hr[m][n][i];
           hr[m][n][i] = __builtin_fmaf(z, hr[m][n][i] - nn, nn);
         }

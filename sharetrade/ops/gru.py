@@ -22,6 +22,7 @@ from __future__ import annotations
 import ctypes as C
 from typing import Tuple
 
+import numpy as np
 import torch
 
 from . import native
@@ -137,8 +138,20 @@ def mx_roundtrip(x: torch.Tensor, block: int = 32) -> torch.Tensor:
     return mx_dequantize(q, e, block)
 
 
-def unpack_whh(whh8: torch.Tensor, whhs: torch.Tensor) -> torch.Tensor:
-    """Packed actor fragments -> the dequantized W_hh [768, 256] the actor multiplies with."""
+# gate pre-scales folded into the packed weights and biases (csrc/gru_common.h GS_RZ / GS_N): the kernels
+# evaluate sigmoid / tanh as exp2 + add + rcp on the pre-scaled pre-activations
+GS_RZ = float(np.float32(-1.44269504))
+GS_N = float(np.float32(-2.88539008))
+
+
+def gate_prescale() -> torch.Tensor:
+    """Per gate row (r, z, n blocks of 256) scale the packed W_hh / W_ih rows and biases carry, fp32 [768]."""
+    return torch.cat([torch.full((2 * HID,), GS_RZ), torch.full((HID,), GS_N)]).float()
+
+
+def unpack_whh(whh8: torch.Tensor, whhs: torch.Tensor, unscale: bool = True) -> torch.Tensor:
+    """Packed actor fragments -> the dequantized W_hh [768, 256] the actor multiplies with; ``unscale``
+    divides out the gate pre-scale (:func:`gate_prescale`), else the raw pre-scaled values."""
     b = whh8.detach().cpu().contiguous().view(torch.uint8).view(RW, 3, 2, 2, 64, 32)
     e = whhs.detach().cpu().view(RW, 3, 2, 2, 64).to(torch.int32) - 127
     vals = b.view(torch.float8_e4m3fn).float()
@@ -154,6 +167,8 @@ def unpack_whh(whh8: torch.Tensor, whhs: torch.Tensor) -> torch.Tensor:
                             blk = k0 // 32
                             sc = 2.0 ** float(e[w, g, m, ks, i + 16 * blk])
                             W[r, 128 * ks + k0:128 * ks + k0 + 16] = vals[w, g, m, ks, l, 16 * half:16 * half + 16] * sc
+    if unscale:
+        W = (W.double() / gate_prescale().double()[:, None]).float()
     return W
 
 

@@ -60,26 +60,29 @@ def _small(E=64, S=4, eps=0.9, **kw):
 
 
 def test_pack_is_exact_mx_quantization(native_built):
-    from sharetrade.ops.gru import mx_roundtrip, unpack_whh
+    from sharetrade.ops.gru import gate_prescale, mx_roundtrip, unpack_whh
 
     d = _small()
     torch.cuda.synchronize()
     W = d.P["w_hh"].cpu()
-    deq = unpack_whh(d.whh8, d.whhs)
-    assert torch.equal(deq, mx_roundtrip(W))   # 32-element blocks along K, same scale rule as the kernel
-    assert torch.allclose(deq, W, rtol=0.07, atol=1e-6)
+    Ws = W * gate_prescale()[:, None]          # the gate pre-scale, applied in fp32 before quantization
+    raw = unpack_whh(d.whh8, d.whhs, unscale=False)
+    assert torch.equal(raw, mx_roundtrip(Ws))  # 32-element blocks along K, same scale rule as the kernel
+    assert torch.allclose(unpack_whh(d.whh8, d.whhs), W, rtol=0.07, atol=1e-6)
 
 
 def _ref_actor(d, steps, eps_exploit):
     """Host replay of one actor launch: env in float32 (bit-exact), GRU in fp32 with the
     actor's quantization points (MX-fp8 W_hh and h, bf16 W_ih and x)."""
     from sharetrade.env import minute as me
-    from sharetrade.ops.gru import mx_roundtrip, unpack_whh
+    from sharetrade.ops.gru import gate_prescale, mx_roundtrip, unpack_whh
     from sharetrade.utils import rng
 
     E, S, T = d.E, d.S, d.T
     Whh = unpack_whh(d.whh8, d.whhs).double()
-    Wih = d.P["w_ih"].cpu()[:, :32].to(torch.bfloat16).double()
+    gs = gate_prescale()
+    # the actor's bf16 W_ih rows carry the gate pre-scale (rounded after scaling): undo it in double
+    Wih = (d.P["w_ih"].cpu()[:, :32] * gs[:, None]).to(torch.bfloat16).double() / gs.double()[:, None]
     b_ih, b_hh = d.P["b_ih"].cpu().view(-1).double(), d.P["b_hh"].cpu().view(-1).double()
     Wq, bq = d.P["w_q"].cpu().double(), d.P["b_q"].cpu().view(-1).double()
     close = d.close.cpu().numpy()
