@@ -760,10 +760,13 @@ class VectorEngine:
     def check_kernel_err(self) -> None:
         """The ws kernel's error word (csrc/qstep_ws.hip ``ws_fail``: a bounded ring wait gave up and the
         workgroup aborted -- that launch's gradients are garbage).  Reads 16 bytes from the device: call
-        it where the host already synchronises (logging, checkpoints, end of a run)."""
+        it where the host already synchronises (logging, checkpoints, end of a run).  The word is copied to
+        the host and tested there: a device-side reduction would load torch's reduction kernels on first use
+        and idle the GPU for >= 10 ms, which drops its clock for the next ~40 steps (bench.py calls this
+        right before its timed window; profiles/r2_dvfs_probe.md, profiles/r4_bench_window.md)."""
         err = getattr(self, "kernel_err", None)
         if err is not None and err.device.type == "cuda":
-            v = int(err.abs().max())
+            v = max(abs(int(x)) for x in err.cpu().tolist())
             if v:
                 raise RuntimeError(f"step kernel reported error word {v:#x} (ws ring protocol wait gave up; "
                                    f"gradients of the failing launch are invalid)")
