@@ -65,6 +65,11 @@ constexpr int WS_GXP = 2;       // paired slots: X fragment pairs read this many
 #ifndef WS_L2PRE
 #define WS_L2PRE 4
 #endif
+#ifndef WS_WAIT_UNROLL
+#define WS_WAIT_UNROLL -1 // ring-wait poll loops: 0 not unrolled, > 0 unrolled by this count, -1 the compiler's
+                          // choice (production: 6x, the round-3 form; not unrolled is 0.8-0.9 % slower,
+                          // profiles/r4_ws_ab.md; csrc/ab/qstep_ws_wunroll*.hip)
+#endif
 #ifndef WS_ABORT_WORD
 #define WS_ABORT_WORD 1   // ring waits check the workgroup's sticky abort word (0: csrc/ab/qstep_ws_noabort.hip)
 #endif
@@ -277,7 +282,11 @@ ST_DEV void ws_fail(const QStepParams& p, int* ctl) {
 // wait until pred(*w) holds: bounded, and abandoned at once once the workgroup has aborted
 template <typename Pred>
 ST_DEV void ring_wait(const QStepParams& p, int* ctl, const int* w, Pred pred) {
+#if WS_WAIT_UNROLL > 0
+#pragma clang loop unroll_count(WS_WAIT_UNROLL)
+#elif WS_WAIT_UNROLL == 0
 #pragma clang loop unroll(disable)
+#endif
   for (int spin = 0; !pred(lds_acq(w)); ++spin) {
     if (WS_ABORT_WORD && lds_acq(ctl + CTL_ABORT)) break;
     __builtin_amdgcn_s_sleep(1);
