@@ -156,6 +156,7 @@ def main() -> int:
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(args.trace)
+    eng.check_kernel_err()   # (untimed) a ws ring-protocol abort in the window would make its gradients invalid
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     pf1 = eng.current_portfolios().double()
     # per-env return over the window (episode resets inside the window are rare: 5,846-step episodes)
