@@ -194,15 +194,18 @@ def main() -> int:
         #  * init_greedy: the same with the random-init parameters (what learning has to improve on);
         #  * buy_hold: Buy at every step (budget into shares at the start, then held);
         #  * learned: the online epsilon-greedy episode with learning on (the training regime);
+        #  * greedy_trained: greedy + frozen again, with the parameters at the end of that online episode;
         #  * random: uniformly random actions.
         try:
             greedy = benchkit.greedy_episode_returns(eng, world, group)
             init_greedy = benchkit.greedy_episode_returns(eng, world, group, params=init_params)
             buy_hold = benchkit.buy_and_hold_returns(eng, world, group)
             learned = benchkit.full_episode_returns(eng, world, group)
+            # the parameters after that whole online episode (~6,000 Adam steps in all), greedy and frozen
+            greedy_trained = benchkit.greedy_episode_returns(eng, world, group)
             rnd = benchkit.full_episode_returns(eng, world, group, random_policy=True)
             episodes = {"learned": learned, "random": rnd, "greedy": greedy, "init_greedy": init_greedy,
-                        "buy_hold": buy_hold}
+                        "buy_hold": buy_hold, "greedy_trained": greedy_trained}
         except Exception as e:  # noqa: BLE001 -- the timed measurement above stands; report what failed
             if world > 1:
                 raise          # (a rank that stops mid-collective would hang its peers: fail the job)
@@ -263,11 +266,12 @@ def main() -> int:
                         "timed window), mean / population std over all envs of all ranks. greedy: the learned "
                         "parameters frozen, exploit-only; init_greedy: the same at the random init; buy_hold: "
                         "Buy every step (budget into shares, then held); learned: online epsilon-greedy episode "
-                        "with learning on; random: uniform actions. median: exact at one rank, the mean of the "
-                        "ranks' medians at several",
+                        "with learning on; greedy_trained: greedy + frozen with the parameters after that online "
+                        "episode; random: uniform actions. median: exact at one rank, the mean of the ranks' "
+                        "medians at several",
                 "episode_steps": lr_["steps"],
             }
-            for k in ("greedy", "init_greedy", "buy_hold", "learned", "random"):
+            for k in ("greedy", "init_greedy", "buy_hold", "learned", "greedy_trained", "random"):
                 er[f"{k}_mean"] = round(episodes[k]["mean"], 4)
                 er[f"{k}_std"] = round(episodes[k]["std"], 4)
                 er[f"{k}_median"] = round(episodes[k]["median"], 4)
