@@ -449,6 +449,8 @@ class VectorEngine:
         ov["pending"] = None
 
     def _f32_stats(self) -> None:
+        if getattr(self._f32, "stats_in_kernel", False):   # the batched path's TD kernel accumulates them
+            return
         r = self.rewards_out.double()
         self.stat_acc[0] += r.sum()
         self.stat_acc[1] += self._f32.s.loss.double().sum()
