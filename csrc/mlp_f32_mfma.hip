@@ -211,29 +211,41 @@ struct F32Batch {
 ST_DEV float f32b_feat(float w, float inv, int mode) { return mode ? __fsub_rn(__fmul_rn(w, inv), 1.0f) : w; }
 
 // one thread per element of X / X' (the divisions are per env but cheap beside the traffic)
+// one thread per (env, 4 consecutive columns) of X / X': the window's reciprocals once per thread and
+// float4 stores (one thread per element with 64-bit index math and two IEEE divisions each ran at
+// ~1.5 TB/s: 73 us at 65,536 envs)
 __global__ void __launch_bounds__(256) f32b_gather_kernel(F32Batch r) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)r.E * r.in_p) return;
-  const int e = (int)(i / r.in_p), k = (int)(i % r.in_p);
+  const int q4 = r.in_p >> 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= r.E * q4) return;
+  const int e = i / q4, k0 = 4 * (i - e * q4);
   const int ps = r.pos[e];
   const float* pr = r.prices + (size_t)e * r.T + ps;
   const float last = pr[r.H - 1], vnew = pr[r.H];
-  float v = 0.f, vn = 0.f;
-  if (k < r.H) {
-    v = f32b_feat(pr[k], __fdiv_rn(1.0f, last), r.feat_mode);
-    vn = f32b_feat(pr[k + 1], __fdiv_rn(1.0f, vnew), r.feat_mode);
-  } else if (k == r.H) {
-    const float b = r.budget[e];
-    v = r.feat_mode ? __fmul_rn(b, r.inv_b0) : b;
-  } else if (k == r.H + 1) {
-    const int s = r.shares[e];
-    v = r.feat_mode ? __fmul_rn(__fmul_rn((float)s, last), r.inv_b0) : (float)s;
-  } else if (k == r.bias_col) {
-    v = 1.f;
-    vn = 1.f;
+  const float inv = __fdiv_rn(1.0f, last), invn = __fdiv_rn(1.0f, vnew);
+  float v[4], vn[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int k = k0 + t;
+    v[t] = 0.f;
+    vn[t] = 0.f;
+    if (k < r.H) {
+      v[t] = f32b_feat(pr[k], inv, r.feat_mode);
+      vn[t] = f32b_feat(pr[k + 1], invn, r.feat_mode);
+    } else if (k == r.H) {
+      const float b = r.budget[e];
+      v[t] = r.feat_mode ? __fmul_rn(b, r.inv_b0) : b;
+    } else if (k == r.H + 1) {
+      const int s = r.shares[e];
+      v[t] = r.feat_mode ? __fmul_rn(__fmul_rn((float)s, last), r.inv_b0) : (float)s;
+    } else if (k == r.bias_col) {
+      v[t] = 1.f;
+      vn[t] = 1.f;
+    }
   }
-  r.X[i] = v;
-  r.XN[i] = vn;   // budget / shares columns of x' come from the env step
+  const size_t o = (size_t)e * r.in_p + k0;
+  *reinterpret_cast<float4*>(r.X + o) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(r.XN + o) = make_float4(vn[0], vn[1], vn[2], vn[3]);   // budget / shares of x': env step
 }
 
 // epsilon-greedy + the trading env, one thread per env (the row kernel's arithmetic, mlp_f32.hip)
@@ -282,8 +294,9 @@ __global__ void __launch_bounds__(256) f32b_env_kernel(F32Batch r) {
 }
 
 // TD target, one-hot dQ, loss, env write-back, one thread per env
-__global__ void __launch_bounds__(256) f32b_td_kernel(F32Batch r) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+__global__ void __launch_bounds__(1024) f32b_td_kernel(F32Batch r) {
+  __shared__ double red[2][16];
+  const int e = blockIdx.x * 1024 + threadIdx.x;
   double st_r = 0.0, st_l = 0.0;
   if (e < r.E) {
   const float* qn = r.QN + (size_t)e * 16;
@@ -326,36 +339,65 @@ __global__ void __launch_bounds__(256) f32b_td_kernel(F32Batch r) {
     r.ret_sum[e] = r.ret_sum[e] + rew;
   }
   }
-  if (r.stat != nullptr) {   // wave sums, one double atomic per wave and statistic
+  if (r.stat != nullptr) {   // block sums, one double atomic per block and statistic (per-wave atomics on
+                             // two addresses serialised: 30 us at 65,536 envs)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       st_r += __shfl_xor(st_r, o);
       st_l += __shfl_xor(st_l, o);
     }
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-      atomicAdd(r.stat, st_r);
-      atomicAdd(r.stat + 1, st_l);
+      red[0][w] = st_r;
+      red[1][w] = st_l;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      double t = 0.0;
+      for (int j = 0; j < (int)(blockDim.x >> 6); ++j) t += red[threadIdx.x][j];
+      atomicAdd(r.stat + threadIdx.x, t);
     }
   }
 }
 
 // out[n] += sum over rows e of D[e][n] (n < N): a bias gradient; 256 columns x 256 rows per block
-// column sums of D[E][N] (bias gradients): 64 columns x 4 row lanes per block, 256 rows per block, the
-// 4 lanes folded in LDS and one atomic per column per block (rows are read as coalesced runs; the first
-// form -- one thread per column looping over its rows -- ran 16 active lanes per block and took 37 us at
-// 65,536 x 16)
-constexpr int CS_ROWS = 256;
-__global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long long ld, int E, int N, float* out) {
-  __shared__ float part[4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + tx;
-  const int e0 = blockIdx.y * CS_ROWS, e1 = min(E, e0 + CS_ROWS);
-  float s = 0.f;
-  if (n < N)
-    for (int e = e0 + ty; e < e1; e += 4) s += D[(long long)e * ld + n];
-  part[ty][tx] = s;
+// column sums of D[E][N] (bias gradients), N % 4 == 0 and N <= 256: a block reads 256 / (N / 4) rows per
+// pass as float4 runs (N / 4 threads per row), sums `rows` rows (~E / 256: one block per CU), folds its row
+// groups in LDS and adds one atomic per column.  Other shapes: one thread per column and row group of 256.
+__global__ void __launch_bounds__(256) f32b_colsum4_kernel(const float* D, long long ld, int E, int N, int rows,
+                                                           float* out) {
+  __shared__ float4 part[256];
+  const int tr = N >> 2, rpi = 256 / tr;
+  const int t = threadIdx.x, c4 = t % tr, rg = t / tr;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rg < rpi) {
+    const int e0 = blockIdx.x * rows, e1 = min(E, e0 + rows);
+    for (int e = e0 + rg; e < e1; e += rpi) {
+      const float4 v = *reinterpret_cast<const float4*>(D + (long long)e * ld + 4 * c4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  part[t] = s;
   __syncthreads();
-  if (ty == 0 && n < N) atomicAdd(out + n, (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]));
+  if (t < tr) {
+    float4 a = part[t];
+    for (int g = 1; g < rpi; ++g) {
+      const float4 b = part[g * tr + t];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    atomicAdd(out + 4 * t, a.x);
+    atomicAdd(out + 4 * t + 1, a.y);
+    atomicAdd(out + 4 * t + 2, a.z);
+    atomicAdd(out + 4 * t + 3, a.w);
+  }
+}
+__global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long long ld, int E, int N, float* out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int e0 = blockIdx.y * 256, e1 = min(E, e0 + 256);
+  float s = 0.f;
+  for (int e = e0; e < e1; ++e) s += D[(long long)e * ld + n];
+  atomicAdd(out + n, s);
 }
 
 }  // namespace st
@@ -380,7 +422,10 @@ extern "C" hipError_t st_f32b_gemm(const st::GemmF32* g, int splits, hipStream_t
 }
 
 extern "C" hipError_t st_f32b_gather(const st::F32Batch* r, hipStream_t stream) {
-  const long long n = (long long)r->E * r->in_p;
+  if (r->in_p % 4 || (reinterpret_cast<uintptr_t>(r->X) & 15) || (reinterpret_cast<uintptr_t>(r->XN) & 15) ||
+      (long long)r->E * (r->in_p / 4) >= (1ll << 31))
+    return hipErrorInvalidValue;
+  const long long n = (long long)r->E * (r->in_p / 4);
   hipLaunchKernelGGL(st::f32b_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, *r);
   return hipGetLastError();
 }
@@ -391,13 +436,22 @@ extern "C" hipError_t st_f32b_env(const st::F32Batch* r, hipStream_t stream) {
 }
 
 extern "C" hipError_t st_f32b_td(const st::F32Batch* r, hipStream_t stream) {
-  hipLaunchKernelGGL(st::f32b_td_kernel, dim3((r->E + 255) / 256), dim3(256), 0, stream, *r);
+  hipLaunchKernelGGL(st::f32b_td_kernel, dim3((r->E + 1023) / 1024), dim3(1024), 0, stream, *r);
   return hipGetLastError();
 }
 
 extern "C" hipError_t st_f32b_colsum(const float* D, long long ld, int E, int N, float* out, hipStream_t stream) {
   if (E <= 0 || N <= 0) return hipErrorInvalidValue;
-  dim3 grid((N + 63) / 64, (E + st::CS_ROWS - 1) / st::CS_ROWS);
+  if (N % 4 == 0 && N <= 256 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(D) & 15) == 0) {
+    const int rpi = 256 / (N / 4);
+    int rows = (E + 255) / 256;
+    rows = (rows + rpi - 1) / rpi * rpi;
+    if (rows < 4 * rpi) rows = 4 * rpi;
+    hipLaunchKernelGGL(st::f32b_colsum4_kernel, dim3((E + rows - 1) / rows), dim3(256), 0, stream, D, ld, E, N, rows,
+                       out);
+    return hipGetLastError();
+  }
+  dim3 grid((N + 255) / 256, (E + 255) / 256);
   if (grid.y > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(st::f32b_colsum_kernel, grid, dim3(256), 0, stream, D, ld, E, N, out);
   return hipGetLastError();
