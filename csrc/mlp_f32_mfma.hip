@@ -176,6 +176,124 @@ __global__ void __launch_bounds__(GB_T) f32b_gemm_kernel(GemmF32 g) {
     }
 }
 
+// ------------------------------------------------------------------------------- fused 2-layer forward
+// Q = [relu](relu(A W1^T + b1) W2^T + b2) for a two-layer net with N1 <= 256 hidden units and <= 16 outputs,
+// 64 rows per workgroup: the first product on 64 x 256 tiles (the A tile is read once, not once per 64
+// hidden units), H written for the backward, and the second product from H in registers (per-lane
+// partials over the lane's 4 hidden units, 16-lane shuffles, 4-wave LDS fold) -- one launch and no
+// re-read of H instead of two GEMM launches.  A: [M][K] (row stride lda), W1: [N1][K], W2: [16][N1] (rows >=
+// nout zero), H: [M][N1], Q: [M][16].
+struct Fwd2F32 {
+  const float* A; const float* W1; const float* b1; const float* W2; const float* b2;
+  float* H; float* Q;
+  int M, K, N1, nout, relu_out;
+  long long lda;
+};
+constexpr int F2_N = 256;
+__global__ void __launch_bounds__(GB_T) f32b_fwd2_kernel(Fwd2F32 p) {
+  __shared__ __attribute__((aligned(16))) float As[GB_K][GB_M + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[GB_K][F2_N + 4];
+  __shared__ float red[4][GB_M][3];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, g4 = lane >> 4;
+  const int m0 = blockIdx.x * GB_M, wn = 64 * wave;
+  f4v acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = f4v{0.f, 0.f, 0.f, 0.f};
+  float va[8], vb[4][8];
+  auto load = [&](int k0) {
+    tile_ld<LD_KF>(p.A, p.lda, 1, m0, p.M, k0, p.K, va);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile_ld<LD_KF>(p.W1, p.K, 1, 64 * q, p.N1, k0, p.K, vb[q]);
+  };
+  load(0);
+  for (int k0 = 0; k0 < p.K; k0 += GB_K) {
+    tile_st<LD_KF>(As, va);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // column block q of Bs: the 64 x 32 loader's layout shifted by 64 q columns
+      const int tid2 = threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = tid2 + GB_T * j, r = i >> 3, k = 4 * (i & 7);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) Bs[k + t][64 * q + r] = vb[q][4 * j + t];
+      }
+    }
+    __syncthreads();
+    if (k0 + GB_K < p.K) load(k0 + GB_K);
+#pragma unroll
+    for (int ks = 0; ks < GB_K / 4; ++ks) {
+      const int kk = 4 * ks + g4;
+      float a[4], b[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = As[kk][16 * r + l16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) b[c] = Bs[kk][wn + 16 * c + l16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r], b[c], acc[r][c], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // epilogue: H = relu(acc + b1) -> global; per-lane layer-2 partials over this lane's 4 hidden units
+  float w2[4][3], bb[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int n = wn + 16 * c + l16;
+    const bool ok = n < p.N1;
+    bb[c] = ok && p.b1 ? p.b1[n] : 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) w2[c][a] = (ok && a < p.nout) ? p.W2[a * p.N1 + n] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mr = 16 * r + 4 * g4 + i, m = m0 + mr;
+      float part[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int n = wn + 16 * c + l16;
+        const float h = fmaxf(acc[r][c][i] + bb[c], 0.f);
+        if (m < p.M && n < p.N1) p.H[(long long)m * p.N1 + n] = h;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) part[a] = __builtin_fmaf(h, w2[c][a], part[a]);
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) part[a] += __shfl_xor(part[a], o);
+      }
+      if (l16 == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) red[wave][mr][a] = part[a];
+      }
+    }
+  __syncthreads();
+  {
+    const int mr = tid >> 2, a0 = 4 * (tid & 3), m = m0 + mr;   // 64 rows x 16 outputs, 4 per thread
+    if (m < p.M) {
+      float4 o;
+      float* ov = reinterpret_cast<float*>(&o);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int a = a0 + t;
+        float v = 0.f;
+        if (a < p.nout && a < 3) {
+          v = (red[0][mr][a] + red[1][mr][a]) + (red[2][mr][a] + red[3][mr][a]);
+          if (p.b2) v = v + p.b2[a];
+          if (p.relu_out) v = fmaxf(v, 0.f);
+        }
+        ov[t] = v;
+      }
+      *reinterpret_cast<float4*>(p.Q + (long long)m * 16 + a0) = o;
+    }
+  }
+}
+
 // loader mode of an operand with row stride sr / k stride sk
 inline int ld_mode(const float* P, long long sr, long long sk) {
   const bool al = (reinterpret_cast<uintptr_t>(P) & 15) == 0;
@@ -418,6 +536,15 @@ extern "C" hipError_t st_f32b_gemm(const st::GemmF32* g, int splits, hipStream_t
       {f32b_gemm_kernel<LD_RF, LD_KF>, f32b_gemm_kernel<LD_RF, LD_RF>, f32b_gemm_kernel<LD_RF, LD_SC>},
       {f32b_gemm_kernel<LD_SC, LD_KF>, f32b_gemm_kernel<LD_SC, LD_RF>, f32b_gemm_kernel<LD_SC, LD_SC>}};
   hipLaunchKernelGGL(tab[am][bm], grid, dim3(GB_T), 0, stream, a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_f32b_fwd2(const st::Fwd2F32* p, hipStream_t stream) {
+  using namespace st;
+  if (p->M <= 0 || p->K <= 0 || p->N1 <= 0 || p->N1 > F2_N || p->nout < 1 || p->nout > 3 || p->K % 4 || p->lda % 4 ||
+      ((reinterpret_cast<uintptr_t>(p->A) | reinterpret_cast<uintptr_t>(p->W1) | reinterpret_cast<uintptr_t>(p->Q)) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(f32b_fwd2_kernel, dim3((p->M + GB_M - 1) / GB_M), dim3(GB_T), 0, stream, *p);
   return hipGetLastError();
 }
 

@@ -378,6 +378,15 @@ class F32Batch(C.Structure):
     ]
 
 
+class Fwd2F32(C.Structure):
+    _fields_ = [
+        ("A", C.c_void_p), ("W1", C.c_void_p), ("b1", C.c_void_p), ("W2", C.c_void_p), ("b2", C.c_void_p),
+        ("H", C.c_void_p), ("Q", C.c_void_p),
+        ("M", C.c_int), ("K", C.c_int), ("N1", C.c_int), ("nout", C.c_int), ("relu_out", C.c_int),
+        ("lda", C.c_longlong),
+    ]
+
+
 F32B_STORE, F32B_MASK, F32B_ATOMIC = 0, 1, 2
 
 
@@ -386,6 +395,8 @@ def _bind_batched():
     if not getattr(L, "_f32b_bound", False):
         L.st_f32b_gemm.argtypes = [C.POINTER(GemmF32), C.c_int, C.c_void_p]
         L.st_f32b_gemm.restype = C.c_int
+        L.st_f32b_fwd2.argtypes = [C.POINTER(Fwd2F32), C.c_void_p]
+        L.st_f32b_fwd2.restype = C.c_int
         for n in ("st_f32b_gather", "st_f32b_env", "st_f32b_td"):
             getattr(L, n).argtypes = [C.POINTER(F32Batch), C.c_void_p]
             getattr(L, n).restype = C.c_int
@@ -486,9 +497,28 @@ class F32BatchedStep:
         g.epi, g.relu, g.kchunk = epi, int(relu), 0
         return (g, splits)
 
+    def _fwd2_ok(self) -> bool:
+        """The fused two-layer forward (csrc/mlp_f32_mfma.hip f32b_fwd2_kernel): 2 layers, <= 256 hidden,
+        <= 3 actions on a 16-wide output, from 8,192 envs (one workgroup per 64 envs: at 1,024 envs its 16
+        workgroups ran 14 % slower than the two GEMMs; ``SHARETRADE_F32_FWD2=0``: always two GEMM launches)."""
+        lay = self.layout
+        return (os.environ.get("SHARETRADE_F32_FWD2", "1") != "0" and self.eng.E >= 8192 and lay.n_layers == 2
+                and lay.pdims[1] <= 256
+                and lay.pdims[2] == 16 and lay.n_actions <= 3 and lay.pdims[0] % 4 == 0
+                and self.net.off_w[0] % 4 == 0)
+
     def _fwd_structs(self, acts, q):
         lay, net, E = self.layout, self.net, self.eng.E
         P = self.eng.params
+        if self._fwd2_ok():
+            f = Fwd2F32()
+            f.A, f.W1, f.W2 = acts[0].data_ptr(), P.data_ptr() + 4 * net.off_w[0], P.data_ptr() + 4 * net.off_w[1]
+            f.b1 = P.data_ptr() + 4 * net.off_b[0] if net.off_b[0] >= 0 else None
+            f.b2 = P.data_ptr() + 4 * net.off_b[1] if net.off_b[1] >= 0 else None
+            f.H, f.Q = acts[1].data_ptr(), q.data_ptr()
+            f.M, f.K, f.N1, f.nout = E, lay.pdims[0], lay.pdims[1], lay.n_actions
+            f.relu_out, f.lda = int(bool(net.output_relu)), lay.pdims[0]
+            return [("fwd2", f)]
         out = []
         for l in range(lay.n_layers):
             K, N = lay.pdims[l], lay.pdims[l + 1]
@@ -509,7 +539,10 @@ class F32BatchedStep:
 
     def _run(self, structs, sh):
         for g, splits in structs:
-            native.check(self.L.st_f32b_gemm(C.byref(g), splits, sh), "st_f32b_gemm")
+            if g == "fwd2":
+                native.check(self.L.st_f32b_fwd2(C.byref(splits), sh), "st_f32b_fwd2")
+            else:
+                native.check(self.L.st_f32b_gemm(C.byref(g), splits, sh), "st_f32b_gemm")
 
     def grad(self, out: torch.Tensor) -> torch.Tensor:
         """One env step of every env and the local gradient into ``out`` (no update)."""
