@@ -248,3 +248,40 @@ def test_fp32_batched_compat_reproduces_reference_portfolio(dev):
     assert float(eng.stat_acc[0]) == 0.0
     fin = eng.final_portfolios().cpu()
     assert torch.all(fin == 2400.0), fin
+
+
+@pytest.mark.parametrize("preset", ["reference_compat", "intended"])
+def test_fp32_fused_forward_matches_two_gemm_forward(dev, preset, monkeypatch):
+    """From 8,192 envs the batched step's forward is one launch (csrc/mlp_f32_mfma.hip f32b_fwd2_kernel:
+    hidden layer on 64 x 256 tiles, the 3-action output from registers); vs the two-GEMM forward
+    (SHARETRADE_F32_FWD2=0) over 4 captured steps: same transitions, Q / H / parameters within fp32
+    summation-order tolerance."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, T = 8192, 260
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 11, n_series=E).astype(np.float32))
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SHARETRADE_F32_FWD2", fused)
+        cfg = preset_config(preset)
+        cfg.engine.dtype = "fp32"
+        cfg.engine.f32_batched = "on"
+        cfg.agent.epsilon = 0.5
+        cfg.agent.ramp = 4.0
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert eng._f32._fwd2_ok() == (fused == "1")
+        eng.capture_graph(warmup=1)
+        eng.run(4)
+        torch.cuda.synchronize()
+        s = eng._f32.s
+        out[fused] = (s.q.cpu().clone(), s.A[1].cpu().clone(), eng.params.cpu().clone(),
+                      {k: v.cpu().clone() for k, v in eng.state.as_dict().items()})
+    (qf, hf, pf, sf), (qg, hg, pg, sg) = out["1"], out["0"]
+    for k in ("budget", "shares", "pos", "value"):
+        assert torch.equal(sf[k], sg[k]), k
+    assert _rel(hf, hg) < 1e-5, _rel(hf, hg)
+    assert _rel(qf, qg) < 1e-5, _rel(qf, qg)
+    assert _rel(pf, pg) < 1e-5, _rel(pf, pg)
+    assert torch.all(qf[:, 3:] == 0)
