@@ -89,8 +89,9 @@ ST_DEV void tile_ld(const float* P, long long sr, long long sk, int r0, int R, i
   }
 }
 
-template <int MODE>
-ST_DEV void tile_st(float (*S)[GB_M + 4], const float (&v)[8]) {
+// stores a loaded tile k-major into LDS: S[k * ld + r] (S may point at a column offset of a wider tile)
+template <int MODE, int ld>
+ST_DEV void tile_st(float* S, const float (&v)[8]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -98,15 +99,15 @@ ST_DEV void tile_st(float (*S)[GB_M + 4], const float (&v)[8]) {
     if (MODE == LD_KF) {
       const int r = i >> 3, k = 4 * (i & 7);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) S[k + t][r] = v[4 * j + t];
+      for (int t = 0; t < 4; ++t) S[(k + t) * ld + r] = v[4 * j + t];
     } else if (MODE == LD_RF) {
       const int kk = i >> 4, r = 4 * (i & 15);
-      *reinterpret_cast<float4*>(&S[kk][r]) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+      *reinterpret_cast<float4*>(&S[kk * ld + r]) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
     } else {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int q = i * 4 + t;
-        S[q >> 6][q & 63] = v[4 * j + t];
+        S[(q >> 6) * ld + (q & 63)] = v[4 * j + t];
       }
     }
   }
@@ -129,8 +130,8 @@ __global__ void __launch_bounds__(GB_T) f32b_gemm_kernel(GemmF32 g) {
   tile_ld<AM>(g.A, g.am, g.ak, m0, g.M, k_begin, k_end, va);
   tile_ld<BM>(g.B, g.bn, g.bk, n0, g.N, k_begin, k_end, vb);
   for (int k0 = k_begin; k0 < k_end; k0 += GB_K) {
-    tile_st<AM>(As, va);
-    tile_st<BM>(Bs, vb);
+    tile_st<AM, GB_M + 4>(&As[0][0], va);
+    tile_st<BM, GB_N + 4>(&Bs[0][0], vb);
     __syncthreads();
     if (k0 + GB_K < k_end) {   // the next k-tile in flight under this one's MFMAs
       tile_ld<AM>(g.A, g.am, g.ak, m0, g.M, k0 + GB_K, k_end, va);
@@ -209,18 +210,9 @@ __global__ void __launch_bounds__(GB_T) f32b_fwd2_kernel(Fwd2F32 p) {
   };
   load(0);
   for (int k0 = 0; k0 < p.K; k0 += GB_K) {
-    tile_st<LD_KF>(As, va);
+    tile_st<LD_KF, GB_M + 4>(&As[0][0], va);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      // column block q of Bs: the 64 x 32 loader's layout shifted by 64 q columns
-      const int tid2 = threadIdx.x;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int i = tid2 + GB_T * j, r = i >> 3, k = 4 * (i & 7);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) Bs[k + t][64 * q + r] = vb[q][4 * j + t];
-      }
-    }
+    for (int q = 0; q < 4; ++q) tile_st<LD_KF, F2_N + 4>(&Bs[0][64 * q], vb[q]);   // hidden units 64 q ..
     __syncthreads();
     if (k0 + GB_K < p.K) load(k0 + GB_K);
 #pragma unroll
