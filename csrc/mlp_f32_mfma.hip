@@ -30,8 +30,9 @@ namespace st {
 // C(m, n) = sum_k A(m, k) B(k, n), operands addressed by strides (either may be transposed in memory):
 // A(m, k) = A[m * am + k * ak], B(k, n) = B[k * bk + n * bn], C(m, n) = C[m * ldc + n].
 // Epilogues: EPI_STORE (+ bias[n], optional relu), EPI_MASK (C = acc * [aux(m, n) > 0], aux row stride
-// ldaux), EPI_ATOMIC (C += acc: split-K over gridDim.z, C zeroed beforehand).
-enum { F32B_STORE = 0, F32B_MASK = 1, F32B_ATOMIC = 2 };
+// ldaux), EPI_ATOMIC (C += acc: split-K over gridDim.z, C zeroed beforehand), EPI_PARTIAL (split z stores its
+// partial at C + z * zstride; st_f32b_splitsum adds the partials in split order: deterministic, no atomics).
+enum { F32B_STORE = 0, F32B_MASK = 1, F32B_ATOMIC = 2, F32B_PARTIAL = 3 };
 
 struct GemmF32 {
   const float* A;
@@ -42,6 +43,7 @@ struct GemmF32 {
   int M, N, K;
   long long am, ak, bk, bn, ldc, ldaux;
   int epi, relu, kchunk;   // kchunk: K per split (gridDim.z splits)
+  long long zstride;       // EPI_PARTIAL: elements between split z's partial tiles
 };
 
 constexpr int GB_M = 64, GB_N = 64, GB_K = 32, GB_T = 256;
@@ -165,7 +167,9 @@ __global__ void __launch_bounds__(GB_T) f32b_gemm_kernel(GemmF32 g) {
         if (m >= g.M) continue;
         float v = acc[r][c][i];
         float* dst = g.C + (long long)m * g.ldc + n;
-        if (g.epi == F32B_ATOMIC) {
+        if (g.epi == F32B_PARTIAL) {
+          dst[(long long)blockIdx.z * g.zstride] = v;
+        } else if (g.epi == F32B_ATOMIC) {
           atomicAdd(dst, v);
         } else if (g.epi == F32B_MASK) {
           *dst = g.aux[(long long)m * g.ldaux + n] > 0.f ? v : 0.f;
@@ -510,12 +514,27 @@ __global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long l
   atomicAdd(out + n, s);
 }
 
+// out[i] = sum over z of part[z * zstride + i] (split-K partials of EPI_PARTIAL, added in split order);
+// float4 per thread (n % 4 == 0, 16-byte aligned, checked on the host)
+__global__ void __launch_bounds__(256) f32b_splitsum_kernel(const float* part, int splits, long long zstride,
+                                                            float* out, long long n4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = reinterpret_cast<const float4*>(part)[i];
+  for (int z = 1; z < splits; ++z) {
+    const float4 b = reinterpret_cast<const float4*>(part + (long long)z * zstride)[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  reinterpret_cast<float4*>(out)[i] = a;
+}
+
 }  // namespace st
 
 extern "C" hipError_t st_f32b_gemm(const st::GemmF32* g, int splits, hipStream_t stream) {
   using namespace st;
   if (g->M <= 0 || g->N <= 0 || g->K <= 0 || splits < 1) return hipErrorInvalidValue;
-  if (splits > 1 && g->epi != F32B_ATOMIC) return hipErrorInvalidValue;
+  if (splits > 1 && g->epi != F32B_ATOMIC && g->epi != F32B_PARTIAL) return hipErrorInvalidValue;
+  if (g->epi == F32B_PARTIAL && g->zstride < (long long)g->M * g->ldc) return hipErrorInvalidValue;
   GemmF32 a = *g;
   a.kchunk = ((g->K + splits - 1) / splits + GB_K - 1) / GB_K * GB_K;
   const int z = (g->K + a.kchunk - 1) / a.kchunk;
@@ -537,6 +556,17 @@ extern "C" hipError_t st_f32b_fwd2(const st::Fwd2F32* p, hipStream_t stream) {
       ((reinterpret_cast<uintptr_t>(p->A) | reinterpret_cast<uintptr_t>(p->W1) | reinterpret_cast<uintptr_t>(p->Q)) & 15))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(f32b_fwd2_kernel, dim3((p->M + GB_M - 1) / GB_M), dim3(GB_T), 0, stream, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_f32b_splitsum(const float* part, int splits, long long zstride, float* out, long long n,
+                                       hipStream_t stream) {
+  if (splits < 1 || n <= 0 || n % 4 || zstride % 4 ||
+      ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15))
+    return hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(st::f32b_splitsum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, splits,
+                     zstride, out, n4);
   return hipGetLastError();
 }
 

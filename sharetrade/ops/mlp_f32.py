@@ -356,6 +356,7 @@ class GemmF32(C.Structure):
         ("am", C.c_longlong), ("ak", C.c_longlong), ("bk", C.c_longlong), ("bn", C.c_longlong),
         ("ldc", C.c_longlong), ("ldaux", C.c_longlong),
         ("epi", C.c_int), ("relu", C.c_int), ("kchunk", C.c_int),
+        ("zstride", C.c_longlong),
     ]
 
 
@@ -387,7 +388,7 @@ class Fwd2F32(C.Structure):
     ]
 
 
-F32B_STORE, F32B_MASK, F32B_ATOMIC = 0, 1, 2
+F32B_STORE, F32B_MASK, F32B_ATOMIC, F32B_PARTIAL = 0, 1, 2, 3
 
 
 def _bind_batched():
@@ -397,6 +398,8 @@ def _bind_batched():
         L.st_f32b_gemm.restype = C.c_int
         L.st_f32b_fwd2.argtypes = [C.POINTER(Fwd2F32), C.c_void_p]
         L.st_f32b_fwd2.restype = C.c_int
+        L.st_f32b_splitsum.argtypes = [C.c_void_p, C.c_int, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
+        L.st_f32b_splitsum.restype = C.c_int
         for n in ("st_f32b_gather", "st_f32b_env", "st_f32b_td"):
             getattr(L, n).argtypes = [C.POINTER(F32Batch), C.c_void_p]
             getattr(L, n).restype = C.c_int
@@ -446,6 +449,12 @@ class F32BatchedStep:
         # at least 256 envs per split.  One split per 256 envs on every product (the first form) put 4,096
         # workgroups and 16.7 M fp32 atomics on the 208 x 208 product: 164 us of a 750 us step at 65,536 envs
         self.splits = splits
+        # split-K partial tiles of the weight-gradient products (EPI_PARTIAL + st_f32b_splitsum);
+        # SHARETRADE_F32_SPLIT_ATOMIC=1: fp32 atomics into the gradient instead
+        need = max(self._splits(lay.pdims[l + 1], lay.pdims[l], E) * lay.pdims[l + 1] * lay.pdims[l]
+                   for l in range(lay.n_layers))
+        self.partials = (None if os.environ.get("SHARETRADE_F32_SPLIT_ATOMIC", "0") == "1"
+                         else torch.empty(need, dtype=torch.float32, device=eng.device))
         st, s = eng.state, self.s
         r = F32Batch()
         r.E, r.in_p, r.H, r.T, r.bias_col = E, lay.in_p, eng.H, eng.T, lay.bias_col
@@ -560,9 +569,24 @@ class F32BatchedStep:
             Kin, Nout = lay.pdims[l], lay.pdims[l + 1]
             dz = s.dz[l]
             # dW_l^T[out][in] += sum_e dZ_l[e][out] A_l[e][in]  (K = envs, split over workgroups)
-            g = self._gemm(dz.data_ptr(), s.A[l].data_ptr(), out.data_ptr() + 4 * net.off_w[l], Nout, Kin, E,
-                           1, Nout, Kin, 1, Kin, F32B_ATOMIC, splits=self._splits(Nout, Kin, E))
-            self._run([g], sh)
+            sp = self._splits(Nout, Kin, E)
+            dst = out.data_ptr() + 4 * net.off_w[l]
+            if sp > 1 and self.partials is not None and (Nout * Kin) % 4 == 0 and dst % 16 == 0:
+                # split-K partials into scratch, then one deterministic sum (the fp32 atomics of every
+                # split's tile were the cost of the 224 x 224 product at 65,536 envs)
+                zs = Nout * Kin
+                g = self._gemm(dz.data_ptr(), s.A[l].data_ptr(), self.partials.data_ptr(), Nout, Kin, E,
+                               1, Nout, Kin, 1, Kin, F32B_PARTIAL, splits=sp)
+                g[0].zstride = zs
+                self._run([g], sh)
+                # (the launcher's actual split count: K rounded to whole 32-wide k-tiles per split)
+                kchunk = -(-(-(-E // sp)) // 32) * 32
+                native.check(L.st_f32b_splitsum(self.partials.data_ptr(), -(-E // kchunk), zs, dst, zs, sh),
+                             "st_f32b_splitsum")
+            else:
+                g = self._gemm(dz.data_ptr(), s.A[l].data_ptr(), dst, Nout, Kin, E,
+                               1, Nout, Kin, 1, Kin, F32B_ATOMIC, splits=sp)
+                self._run([g], sh)
             if net.off_b[l] >= 0:
                 native.check(L.st_f32b_colsum(dz.data_ptr(), Nout, E, Nout, out.data_ptr() + 4 * net.off_b[l], sh),
                              "st_f32b_colsum")
