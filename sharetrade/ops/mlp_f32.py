@@ -449,12 +449,12 @@ class F32BatchedStep:
         # at least 256 envs per split.  One split per 256 envs on every product (the first form) put 4,096
         # workgroups and 16.7 M fp32 atomics on the 208 x 208 product: 164 us of a 750 us step at 65,536 envs
         self.splits = splits
-        # split-K partial tiles of the weight-gradient products (EPI_PARTIAL + st_f32b_splitsum);
-        # SHARETRADE_F32_SPLIT_ATOMIC=1: fp32 atomics into the gradient instead
+        # split-K partial tiles of the weight-gradient products (EPI_PARTIAL + st_f32b_splitsum, deterministic)
+        # with SHARETRADE_F32_SPLIT_PARTIAL=1; default: fp32 atomics into the gradient
         need = max(self._splits(lay.pdims[l + 1], lay.pdims[l], E) * lay.pdims[l + 1] * lay.pdims[l]
                    for l in range(lay.n_layers))
-        self.partials = (None if os.environ.get("SHARETRADE_F32_SPLIT_ATOMIC", "0") == "1"
-                         else torch.empty(need, dtype=torch.float32, device=eng.device))
+        self.partials = (torch.empty(need, dtype=torch.float32, device=eng.device)
+                         if os.environ.get("SHARETRADE_F32_SPLIT_PARTIAL", "0") == "1" else None)
         st, s = eng.state, self.s
         r = F32Batch()
         r.E, r.in_p, r.H, r.T, r.bias_col = E, lay.in_p, eng.H, eng.T, lay.bias_col
