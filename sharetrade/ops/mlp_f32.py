@@ -409,6 +409,13 @@ def _bind_batched():
     return L
 
 
+class _Fwd2Op:
+    """A fused two-layer forward launch (st_f32b_fwd2) in a batched step's launch list."""
+
+    def __init__(self, args: Fwd2F32):
+        self.args = args
+
+
 class _BatchedScratch:
     def __init__(self, layout: qn.QNetLayout, E: int, device):
         f = dict(dtype=torch.float32, device=device)
@@ -527,7 +534,7 @@ class F32BatchedStep:
             f.H, f.Q = acts[1].data_ptr(), q.data_ptr()
             f.M, f.K, f.N1, f.nout = E, lay.pdims[0], lay.pdims[1], lay.n_actions
             f.relu_out, f.lda = int(bool(net.output_relu)), lay.pdims[0]
-            return [("fwd2", f)]
+            return [_Fwd2Op(f)]
         out = []
         for l in range(lay.n_layers):
             K, N = lay.pdims[l], lay.pdims[l + 1]
@@ -546,11 +553,12 @@ class F32BatchedStep:
         tiles = -(-M // 64) * -(-N // 64)
         return max(1, min(-(-1024 // tiles), K // 256))
 
-    def _run(self, structs, sh):
-        for g, splits in structs:
-            if g == "fwd2":
-                native.check(self.L.st_f32b_fwd2(C.byref(splits), sh), "st_f32b_fwd2")
+    def _run(self, ops, sh):
+        for op in ops:
+            if isinstance(op, _Fwd2Op):
+                native.check(self.L.st_f32b_fwd2(C.byref(op.args), sh), "st_f32b_fwd2")
             else:
+                g, splits = op
                 native.check(self.L.st_f32b_gemm(C.byref(g), splits, sh), "st_f32b_gemm")
 
     def grad(self, out: torch.Tensor) -> torch.Tensor:
