@@ -320,6 +320,11 @@ struct F32Batch {
   float eps, inv_ramp, b0, inv_b0, gamma, coef, td_clip;
   uint32_t key0, key1;
   double* stat;        // optional [2]: += sum of rewards, += sum of squared TD errors (VectorEngine.stat_acc)
+  // learning experiments (sharetrade/env/trading.py engine_step_ref: target_params / double_dqn /
+  // reward_scale / ramp_pos): QT = Q(x') of a target copy of the parameters (null: none)
+  const float* QT;
+  float reward_scale;
+  int double_dqn, ramp_global;
 };
 
 ST_DEV float f32b_feat(float w, float inv, int mode) { return mode ? __fsub_rn(__fmul_rn(w, inv), 1.0f) : w; }
@@ -378,7 +383,8 @@ __global__ void __launch_bounds__(256) f32b_env_kernel(F32Batch r) {
            c3 = 0u;
   philox4x32(c0, c1, c2, c3, r.key0, r.key1);
   const float u1 = u24(c0), u2 = u24(c1);
-  const bool exploit = u1 < fminf(r.eps, __fmul_rn((float)ps, r.inv_ramp));
+  const float rpos = r.ramp_global ? (float)step : (float)ps;   // exploit ramp over the step count (global)
+  const bool exploit = u1 < fminf(r.eps, __fmul_rn(rpos, r.inv_ramp));
   int rnd = (int)(u2 * 3.0f);
   rnd = rnd > 2 ? 2 : rnd;
   const int a = exploit ? greedy : rnd;
@@ -421,7 +427,18 @@ __global__ void __launch_bounds__(1024) f32b_td_kernel(F32Batch r) {
   if (n2 > mx) { mx = n2; am = 2; }
   const int slot = r.target_compat ? am : r.s_act[e];
   const float rew = r.s_rew[e];
-  const float y = __fadd_rn(rew, __fmul_rn(r.gamma, mx));
+  // bootstrap value: max of Q(x') (online or target net); compat and Double DQN: the online argmax's value
+  float boot = mx;
+  if (r.QT != nullptr) {
+    const float* qt = r.QT + (size_t)e * 16;
+    if (r.target_compat || r.double_dqn) {
+      boot = qt[am];
+    } else {
+      boot = fmaxf(fmaxf(qt[0], qt[1]), qt[2]);
+    }
+  }
+  const float rs = r.reward_scale != 1.f ? __fmul_rn(rew, r.reward_scale) : rew;
+  const float y = __fadd_rn(rs, __fmul_rn(r.gamma, boot));
   const float qs = r.Q[(size_t)e * 16 + slot];
   const float diff = __fsub_rn(qs, y);
   float dq = r.coef * (r.td_clip > 0.f ? fminf(fmaxf(diff, -r.td_clip), r.td_clip) : diff);
@@ -528,6 +545,15 @@ __global__ void __launch_bounds__(256) f32b_splitsum_kernel(const float* part, i
   reinterpret_cast<float4*>(out)[i] = a;
 }
 
+// target network refresh inside the captured step: copy the parameters when the (already advanced) step
+// counter is a multiple of `every` (engine_step_ref: after the optimizer step of step s, if (s + 1) % every == 0)
+__global__ void __launch_bounds__(256) f32b_target_sync_kernel(const float* params, float* target, long long n,
+                                                               const unsigned long long* ctrl, long long every) {
+  if (ctrl[0] % (unsigned long long)every != 0ull) return;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) target[i] = params[i];
+}
+
 }  // namespace st
 
 extern "C" hipError_t st_f32b_gemm(const st::GemmF32* g, int splits, hipStream_t stream) {
@@ -567,6 +593,14 @@ extern "C" hipError_t st_f32b_splitsum(const float* part, int splits, long long 
   const long long n4 = n / 4;
   hipLaunchKernelGGL(st::f32b_splitsum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, splits,
                      zstride, out, n4);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_f32b_target_sync(const float* params, float* target, long long n,
+                                           const unsigned long long* ctrl, long long every, hipStream_t stream) {
+  if (n <= 0 || every <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::f32b_target_sync_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, params,
+                     target, n, ctrl, every);
   return hipGetLastError();
 }
 

@@ -376,6 +376,7 @@ class F32Batch(C.Structure):
         ("gamma", C.c_float), ("coef", C.c_float), ("td_clip", C.c_float),
         ("key0", C.c_uint32), ("key1", C.c_uint32),
         ("stat", C.c_void_p),
+        ("QT", C.c_void_p), ("reward_scale", C.c_float), ("double_dqn", C.c_int), ("ramp_global", C.c_int),
     ]
 
 
@@ -400,6 +401,8 @@ def _bind_batched():
         L.st_f32b_fwd2.restype = C.c_int
         L.st_f32b_splitsum.argtypes = [C.c_void_p, C.c_int, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
         L.st_f32b_splitsum.restype = C.c_int
+        L.st_f32b_target_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
+        L.st_f32b_target_sync.restype = C.c_int
         for n in ("st_f32b_gather", "st_f32b_env", "st_f32b_td"):
             getattr(L, n).argtypes = [C.POINTER(F32Batch), C.c_void_p]
             getattr(L, n).restype = C.c_int
@@ -492,6 +495,18 @@ class F32BatchedStep:
         # step statistics (reward sum, TD loss sum) accumulated by the TD kernel into stat_acc[0:2]
         r.stat = eng.stat_acc.data_ptr() if eng.stat_acc.dtype == torch.float64 and eng.stat_acc.is_cuda else None
         self.stats_in_kernel = r.stat is not None
+        # learning experiments (agent.target_every / double_dqn / reward_scale / ramp_mode; the torch oracle's
+        # engine_step_ref semantics): Q(x') of a target copy refreshed on the device every target_every steps
+        a = cfg.agent
+        r.reward_scale, r.double_dqn, r.ramp_global = float(a.reward_scale), int(a.double_dqn), int(a.ramp_mode == "global")
+        self.target_every = int(a.target_every)
+        self._fwd_t = None
+        if self.target_every:
+            eng.params_target = eng.params.detach().clone()
+            s.qt = torch.zeros(E, 16, dtype=torch.float32, device=eng.device)
+            r.QT = s.qt.data_ptr()
+        else:
+            r.QT = None
         self.rows = r          # (policy_overrides edits eps / inv_ramp here)
         a = cfg.agent
         o = F32Optim()
@@ -504,6 +519,8 @@ class F32BatchedStep:
         o.mode = 2
         self.optim = o
         self._fwd = [self._fwd_structs(s.A, s.q), self._fwd_structs(s.AN, s.qn)]
+        if self.target_every:   # target net on x' (its hidden activations reuse AN: the backward reads A only)
+            self._fwd_t = self._fwd_structs(s.AN, s.qt, params=eng.params_target)
 
     def _gemm(self, A, B, Cp, M, N, K, am, ak, bk, bn, ldc, epi, bias=None, relu=False, aux=None, ldaux=0, splits=1):
         g = GemmF32()
@@ -523,9 +540,9 @@ class F32BatchedStep:
                 and lay.pdims[2] == 16 and lay.n_actions <= 3 and lay.pdims[0] % 4 == 0
                 and self.net.off_w[0] % 4 == 0)
 
-    def _fwd_structs(self, acts, q):
+    def _fwd_structs(self, acts, q, params=None):
         lay, net, E = self.layout, self.net, self.eng.E
-        P = self.eng.params
+        P = self.eng.params if params is None else params
         if self._fwd2_ok():
             f = Fwd2F32()
             f.A, f.W1, f.W2 = acts[0].data_ptr(), P.data_ptr() + 4 * net.off_w[0], P.data_ptr() + 4 * net.off_w[1]
@@ -572,6 +589,8 @@ class F32BatchedStep:
         self._run(self._fwd[0], sh)
         native.check(L.st_f32b_env(C.byref(r), sh), "st_f32b_env")
         self._run(self._fwd[1], sh)
+        if self._fwd_t is not None:
+            self._run(self._fwd_t, sh)
         native.check(L.st_f32b_td(C.byref(r), sh), "st_f32b_td")
         for l in reversed(range(lay.n_layers)):
             Kin, Nout = lay.pdims[l], lay.pdims[l + 1]
@@ -615,3 +634,7 @@ class F32BatchedStep:
         self.optim.grad = g.data_ptr()
         native.check(self.L.st_f32_grad_optim(self.net, self.optim, sh), "st_f32_update(batched)")
         native.check(self.L.st_f32_advance(self.eng.ctrl.data_ptr(), sh), "st_f32_advance")
+        if self.target_every:
+            e = self.eng
+            native.check(self.L.st_f32b_target_sync(e.params.data_ptr(), e.params_target.data_ptr(), e.params.numel(),
+                                                    e.ctrl.data_ptr(), self.target_every, sh), "st_f32b_target_sync")

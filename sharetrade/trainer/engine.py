@@ -139,9 +139,11 @@ class VectorEngine:
             be = "native" if self.device.type == "cuda" else "torch"
         self.backend = be
         a = cfg.agent
-        if be != "torch" and (a.target_every or a.double_dqn or a.reward_scale != 1.0 or a.ramp_mode != "position"):
+        self._learn_knobs = bool(a.target_every or a.double_dqn or a.reward_scale != 1.0 or a.ramp_mode != "position")
+        if self._learn_knobs and not (be == "torch" or (be == "native" and cfg.engine.dtype == "fp32")):
             raise NotImplementedError("agent.target_every / double_dqn / reward_scale / ramp_mode are learning "
-                                      "experiments of the torch backend (engine.backend='torch')")
+                                      "experiments of the torch backend and the batched fp32 native step "
+                                      "(engine.backend='torch', or engine.dtype='fp32' with engine.f32_batched)")
         if a.ramp_mode not in ("position", "global"):
             raise ValueError(f"agent.ramp_mode: {a.ramp_mode!r}")
         if a.double_dqn and not a.target_every:
@@ -281,6 +283,9 @@ class VectorEngine:
             if fb not in ("auto", "on", "off"):
                 raise ValueError(f"engine.f32_batched: {fb!r}")
             self.f32_path = "batched" if (fb == "on" or (fb == "auto" and self.E >= 1024)) else "rows"
+            if self._learn_knobs and self.f32_path != "batched":
+                raise NotImplementedError("the learning-experiment knobs need the batched fp32 step "
+                                          "(engine.f32_batched='on', or 'auto' with >= 1,024 envs)")
             self._f32 = F32BatchedStep(self) if self.f32_path == "batched" else F32EngineStep(self)
             return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)

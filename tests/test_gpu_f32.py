@@ -285,3 +285,40 @@ def test_fp32_fused_forward_matches_two_gemm_forward(dev, preset, monkeypatch):
     assert _rel(qf, qg) < 1e-5, _rel(qf, qg)
     assert _rel(pf, pg) < 1e-5, _rel(pf, pg)
     assert torch.all(qf[:, 3:] == 0)
+
+
+@pytest.mark.parametrize("preset,knobs", [
+    ("intended", dict(target_every=2, double_dqn=True, reward_scale=10.0, ramp_mode="global")),
+    ("intended", dict(target_every=3)),
+    ("reference_compat", dict(target_every=2, reward_scale=4.0)),
+])
+def test_fp32_batched_learning_knobs_match_torch_engine(dev, preset, knobs):
+    """Target network (refreshed on the device every target_every steps), Double DQN, reward scale and the
+    exploit ramp over the step count on the batched fp32 step vs the torch oracle engine (engine_step_ref):
+    same transitions, parameters and target parameters within fp32 summation-order tolerance over 5 steps."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config(preset)
+    cfg.engine.dtype = "fp32"
+    cfg.agent.epsilon = 0.5
+    cfg.agent.ramp = 4.0
+    for k, v in knobs.items():
+        setattr(cfg.agent, k, v)
+    if preset == "intended":
+        cfg.agent.target_slot = "action"
+    E, T = 1024, 260
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 5, n_series=E).astype(np.float32))
+    g = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    c = VectorEngine(cfg, prices=prices, device=torch.device("cpu"), envs=E, backend="torch")
+    assert g.f32_path == "batched"
+    for _ in range(5):
+        g.step()
+        c.step()
+        torch.cuda.synchronize()
+        for k in ("budget", "shares", "pos"):
+            assert torch.equal(getattr(g.state, k).cpu(), getattr(c.state, k)), k
+        assert _rel(g.params.cpu(), c.params) < 1e-5, _rel(g.params.cpu(), c.params)
+        if knobs.get("target_every"):
+            assert _rel(g.params_target.cpu(), c.params_target) < 1e-5
