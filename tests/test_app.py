@@ -60,7 +60,7 @@ def test_full_length_compat_run_vector_engine():
     from sharetrade.app import run
 
     cfg = _cfg()
-    cfg.router.poll_interval_s = 0.25
+    cfg.router.poll_interval_s = 1.0     # 201 polls span 201 s: room for a loaded CPU (the run alone takes ~40 s)
     t0 = time.perf_counter()
     res = run(cfg, engine="vector", device="cpu", quiet=True)
     assert res["completed"] == 1.0, res
