@@ -9,13 +9,17 @@
 //
 //   f32b_gather   X, X' [E][in_p] from the HBM price bank + env state (features, layer-0 bias column)
 //   GEMM          A_{l+1} = relu(A_l . W_l^T + b_l)   for x; last layer -> Q [E][16]
+//                 (two-layer nets from 8,192 envs: f32b_fwd2, both layers in one launch)
 //   f32b_env      epsilon-greedy (Philox) + Buy/Sell/Hold step: budget / shares columns of X'
-//   GEMM          the same forward for x' -> Q'
-//   f32b_td       TD target, dQ (one-hot at the target slot), loss, env write-back
+//   GEMM          the same forward for x' -> Q' (and, with a target network, for x' on the target copy)
+//   f32b_td       TD target (online / target / Double-DQN bootstrap), dQ (one-hot at the target slot),
+//                 loss, env write-back, step statistics
 //   GEMM          dZ_{l-1} = (dZ_l . W_l) * [A_l > 0]                       (backward, data)
-//   GEMM          dW_l^T += dZ_l^T . A_l  (split-K over envs, fp32 atomics)  (weight gradient)
+//   GEMM          dW_l^T += dZ_l^T . A_l  (split-K over envs: fp32 atomics, or partial tiles +
+//                 f32b_splitsum)                                             (weight gradient)
 //   f32b_colsum   db_l += sum_e dZ_l
 //   f32_grad_optim (mode 2, csrc/mlp_f32.hip)  AdaGrad (TF ApplyAdagrad) / Adam / SGD
+//   f32b_target_sync  the target copy refreshed every target_every steps (device-side condition)
 //
 // Every product is v_mfma_f32_16x16x4_f32: fp32 operands and accumulation, each product exact in fp32
 // (gfx950's f32-input MFMA runs at the fp32 vector rate, so this is about data reuse, not precision);
