@@ -76,12 +76,6 @@ constexpr int WS_GXP = 2;       // paired slots: X fragment pairs read this many
 #ifndef WS_LDU_CAST
 #define WS_LDU_CAST 0
 #endif
-#ifndef WS_GATHER64
-#define WS_GATHER64 0     // 1: k-order permuted so each window load covers 64 contiguous bytes per env (csrc/ab/qstep_ws_gather64.hip)
-#endif
-#ifndef WS_PC_PERM
-#define WS_PC_PERM 0      // 1: x''s extra window values by ds_bpermute from the neighbour lane group (csrc/ab/qstep_ws_pcperm.hip)
-#endif
 #ifndef WS_NOWB
 #define WS_NOWB 0       // timing build csrc/ab/qstep_ws_nowb.hip: no env-state write-back (wrong results)
 #endif
@@ -138,16 +132,7 @@ static_assert(SLOT_BYTES % 16 == 0 && oSLOT % 16 == 0, "alignment");
 //   g4 = 0: 201 budget, 202 shares, 203 constant 1 (layer-0 bias column), 200 (the window's last price)
 //   g4 = 1: 192..195;  g4 = 2: 196..199;  g4 = 3: pads 204..207
 ST_DEV int slot_col(int s) {
-#if WS_GATHER64
-  // 32-wide k-steps: lane group g4 holds window columns 4 g4 .. + 3 and 16 + 4 g4 .. + 3 (one 64-byte run
-  // per env and load instruction)
-  if (s < 192) {
-    const int t = s & 31, g = t >> 3, j = t & 7;
-    return (s & ~31) + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
-  }
-#else
   if (s < 192) return s;
-#endif
   const int t = s - 192, g = t >> 2, j = t & 3;
   if (g == 0) return j < 3 ? 201 + j : 200;
   if (g == 1) return 192 + j;
@@ -437,19 +422,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
     const float* b_ = p.prices4 + (size_t)e_ * p.T4 + (size_t)pc_;  /* 4-B aligned dwordx4 reads */   \
     pl = ldu4(b_ + 200);  /* first: the back edge copies it (see below) */                         \
-    if (WS_GATHER64) {                                                                           \
-      _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                         \
-        pa[ks] = ldu4(b_ + 32 * ks + 4 * g4);                                                    \
-        pb[ks] = ldu4(b_ + 32 * ks + 16 + 4 * g4);                                               \
-      }                                                                                          \
-      pc[5] = b_[192];                                                                           \
-    } else {                                                                                     \
-      _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                         \
-        const float* q_ = b_ + 32 * ks + 8 * g4;                                                 \
-        pa[ks] = ldu4(q_);                                                                       \
-        pb[ks] = ldu4(q_ + 4);                                                                   \
-        if (!WS_PC_PERM || ks == 5) pc[ks] = q_[8];                                               \
-      }                                                                                          \
+    _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
+      const float* q_ = b_ + 32 * ks + 8 * g4;                                                   \
+      pa[ks] = ldu4(q_);                                                                         \
+      pb[ks] = ldu4(q_ + 4);                                                                     \
+      pc[ks] = q_[8];                                                                            \
     }                                                                                            \
     if (g4 == 1 || g4 == 2) {                                                                    \
       const float* r_ = b_ + 188 + 4 * g4;                                                       \
@@ -516,39 +493,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         return FEAT ? __fmaf_rn(w, invn, -1.0f) : w;
       };
       s8v X[6], Xn[6];
-#if WS_PC_PERM
-      // x' needs the window value after each lane group's 8: lane group g4 + 1's first value of the same
-      // k-step, or for g4 = 3 lane group 0's first value of the next k-step -- one ds_bpermute per k-step
-      // instead of a 4-byte HBM load (k-step 5's is still loaded: it is lane group 1's pd.x)
-#pragma unroll
-      for (int ks = 0; ks < 5; ++ks) {
-        const float src = g4 == 0 ? pa[ks + 1].x : pa[ks].x;
-        pc[ks] = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 16) & 63) << 2, __float_as_int(src)));
-      }
-#endif
-#if WS_GATHER64
-      // x' needs each run's next value: from the next lane group (lane + 16; lane group 3 wraps to 0,
-      // whose B run / next k-step's A run continues it); k-step 5's last one is the loaded p[192]
-#pragma unroll
-      for (int ks = 0; ks < 6; ++ks) {
-        const int srcA = __float_as_int(g4 == 0 ? pb[ks].x : pa[ks].x);
-        const float nA = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 16) & 63) << 2, srcA));
-        float nB = pc[5];
-        if (ks < 5) {
-          const int srcB = __float_as_int(g4 == 0 ? pa[ks + 1].x : pb[ks].x);
-          const float t = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 16) & 63) << 2, srcB));
-          nB = t;
-        } else {
-          const int srcB = __float_as_int(pb[ks].x);
-          const float t = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 16) & 63) << 2, srcB));
-          nB = g4 == 3 ? pc[5] : t;
-        }
-        X[ks] = cat8(pk4(fx(pa[ks].x), fx(pa[ks].y), fx(pa[ks].z), fx(pa[ks].w)),
-                     pk4(fx(pb[ks].x), fx(pb[ks].y), fx(pb[ks].z), fx(pb[ks].w)));
-        Xn[ks] = cat8(pk4(fxn(pa[ks].y), fxn(pa[ks].z), fxn(pa[ks].w), fxn(nA)),
-                      pk4(fxn(pb[ks].y), fxn(pb[ks].z), fxn(pb[ks].w), fxn(nB)));
-      }
-#else
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
         X[ks] = cat8(pk4(fx(pa[ks].x), fx(pa[ks].y), fx(pa[ks].z), fx(pa[ks].w)),
@@ -556,7 +500,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         Xn[ks] = cat8(pk4(fxn(pa[ks].y), fxn(pa[ks].z), fxn(pa[ks].w), fxn(pb[ks].x)),
                       pk4(fxn(pb[ks].y), fxn(pb[ks].z), fxn(pb[ks].w), fxn(pc[ks])));
       }
-#endif
       // last k-step (16 wide, slot order): g4 = 0 (budget, shares, 1, col 200); 1, 2 window columns; 3 pads
       s4v X6, Xn6;
       if (g4 == 0) {
