@@ -8,7 +8,8 @@ gradient).  Modes:
 * ``sync``    -- synchronous DP (bench.py's default at N > 1): step kernel, slab reduce, RCCL all-reduce,
                  Adam, all captured in the HIP graphs;
 * ``overlap`` -- ``--dp-overlap``: this step's all-reduce on RCCL's stream beside the next step's kernel
-                 (one-step-delayed gradient, eager launches, dynamic chunk schedule);
+                 (one-step-delayed gradient, eager launches; chunk schedule ``auto``: static for ws since
+                 profiles/r4_flagship_dp.md, the dynamic one when this ran first);
 * ``single_dyn`` / ``overlap_static`` -- the same with the other chunk schedule (separates the schedule's
                  cost from the overlapped path's).
 
