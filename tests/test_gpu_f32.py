@@ -322,3 +322,29 @@ def test_fp32_batched_learning_knobs_match_torch_engine(dev, preset, knobs):
         assert _rel(g.params.cpu(), c.params) < 1e-5, _rel(g.params.cpu(), c.params)
         if knobs.get("target_every"):
             assert _rel(g.params_target.cpu(), c.params_target) < 1e-5
+
+
+def test_fp32_batched_split_partials_match_atomics(dev, monkeypatch):
+    """Weight gradients of the batched step with split-K partial tiles + one ordered sum
+    (SHARETRADE_F32_SPLIT_PARTIAL=1, bit-reproducible) vs the default fp32 atomics: equal up to fp32
+    summation order, and two partial-sum runs bit-identical."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, T = 8192, 260
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 13, n_series=E).astype(np.float32))
+    grads, wsl = {}, []
+    for mode in ("partial", "partial2", "atomic"):
+        monkeypatch.setenv("SHARETRADE_F32_SPLIT_PARTIAL", "0" if mode == "atomic" else "1")
+        cfg = preset_config("intended")
+        cfg.engine.dtype = "fp32"
+        cfg.engine.f32_batched = "on"
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert (eng._f32.partials is None) == (mode == "atomic")
+        grads[mode] = eng.native_grad().detach().cpu().clone()
+        net, pd = eng._f32.net, eng.layout.pdims
+        wsl = [slice(net.off_w[l], net.off_w[l] + pd[l + 1] * pd[l]) for l in range(eng.layout.n_layers)]
+    for w in wsl:   # the weight gradients are bit-reproducible (the bias column sums still use atomics)
+        assert torch.equal(grads["partial"][w], grads["partial2"][w])
+    assert _rel(grads["partial"], grads["atomic"]) < 1e-5, _rel(grads["partial"], grads["atomic"])
