@@ -70,6 +70,9 @@ constexpr int WS_GXP = 2;       // paired slots: X fragment pairs read this many
                           // choice (production: 6x, the round-3 form; not unrolled is 0.8-0.9 % slower,
                           // profiles/r4_ws_ab.md; csrc/ab/qstep_ws_wunroll*.hip)
 #endif
+#ifndef WS_SLEEP
+#define WS_SLEEP 1        // s_sleep argument between ring-wait polls (0 / 2 / 4 A/B'd: profiles/r4_ws_ab.md)
+#endif
 #ifndef WS_ABORT_WORD
 #define WS_ABORT_WORD 1   // ring waits check the workgroup's sticky abort word (0: csrc/ab/qstep_ws_noabort.hip)
 #endif
@@ -274,7 +277,7 @@ ST_DEV void ring_wait(const QStepParams& p, int* ctl, const int* w, Pred pred) {
 #endif
   for (int spin = 0; !pred(lds_acq(w)); ++spin) {
     if (WS_ABORT_WORD && lds_acq(ctl + CTL_ABORT)) break;
-    __builtin_amdgcn_s_sleep(1);
+    if (WS_SLEEP > 0) __builtin_amdgcn_s_sleep(WS_SLEEP);
     if (spin > SPIN_LIMIT) { ws_fail(p, ctl); break; }   // never expected: report, do not hang the GPU
   }
 }
