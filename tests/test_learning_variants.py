@@ -1,5 +1,6 @@
-"""Learning-quality experiment knobs of the torch backend (agent.target_every / double_dqn / reward_scale /
-ramp_mode; tools/learning_eval.py --backend torch).  The reference bootstraps Q(x') from the online net with
+"""Learning-quality experiment knobs (agent.target_every / double_dqn / reward_scale / ramp_mode) on the torch
+backend (tools/learning_eval.py --backend torch; the native batched fp32 step is pinned to it by
+tests/test_gpu_f32.py::test_fp32_batched_learning_knobs_match_torch_engine).  The reference bootstraps Q(x') from the online net with
 the exploit ramp over the episode position (QDecisionPolicyActor.scala:58-71); these runs test whether a
 target network, Double DQN, a larger reward scale or a ramp annealed over training help the learned policy."""
 import numpy as np
@@ -60,7 +61,7 @@ def test_global_ramp_and_reward_scale():
     assert not torch.equal(a.params, ref.params) and not torch.equal(b.params, ref.params)
 
 
-def test_native_refuses_torch_only_knobs():
+def test_fused_bf16_native_refuses_the_knobs():
     cfg = preset_config("flagship")
     cfg.agent.target_every = 10
     with pytest.raises(NotImplementedError):
