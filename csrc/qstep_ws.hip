@@ -68,16 +68,13 @@ constexpr int WS_GXP = 2;       // paired slots: X fragment pairs read this many
 #ifndef WS_WAIT_UNROLL
 #define WS_WAIT_UNROLL -1 // ring-wait poll loops: 0 not unrolled, > 0 unrolled by this count, -1 the compiler's
                           // choice (production: 6x, the round-3 form; not unrolled is 0.8-0.9 % slower,
-                          // profiles/r4_ws_ab.md; csrc/ab/qstep_ws_wunroll*.hip)
+                          // profiles/r4_ws_ab.md; csrc/ab/qstep_ws_wunroll0.hip)
 #endif
 #ifndef WS_SLEEP
 #define WS_SLEEP 1        // s_sleep argument between ring-wait polls (0 / 2 / 4 A/B'd: profiles/r4_ws_ab.md)
 #endif
 #ifndef WS_ABORT_WORD
 #define WS_ABORT_WORD 1   // ring waits check the workgroup's sticky abort word (0: csrc/ab/qstep_ws_noabort.hip)
-#endif
-#ifndef WS_LDU_CAST
-#define WS_LDU_CAST 0
 #endif
 #ifndef WS_NOWB
 #define WS_NOWB 0       // timing build csrc/ab/qstep_ws_nowb.hip: no env-state write-back (wrong results)
@@ -285,13 +282,9 @@ ST_DEV void ring_wait(const QStepParams& p, int* ctl, const int* w, Pred pred) {
 // 16-byte loads from 4-byte-aligned addresses (the one padded bank copy is read at every shift): a memcpy
 // from a float pointer promises the compiler only 4-byte alignment; it is still one dwordx4 load
 ST_DEV float4 ldu4(const float* a) {
-#if WS_LDU_CAST
-  return *reinterpret_cast<const float4*>(a);   // A/B only (csrc/ab/qstep_ws_f4cast.hip): the round-3 form
-#else
   float4 v;
   __builtin_memcpy(&v, a, sizeof(v));
   return v;
-#endif
 }
 
 // env-state rows addressed as a uniform row base + a 32-bit byte offset, so the loads / stores use the
