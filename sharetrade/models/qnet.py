@@ -192,10 +192,13 @@ def _kernel_device(dev: torch.device):
     if dev.type == "cuda":
         return dev
     try:
-        from ..ops import native
+        # torch.cuda first: on a machine without a GPU, loading the HIP library (native.available()) starts
+        # runtime threads that slowed the CPU actor runtime ~3x
+        if torch.cuda.is_available():
+            from ..ops import native
 
-        if native.available() and torch.cuda.is_available():
-            return torch.device("cuda", torch.cuda.current_device())
+            if native.available():
+                return torch.device("cuda", torch.cuda.current_device())
     except Exception:  # noqa: BLE001 -- no usable GPU: host mirror
         pass
     return None

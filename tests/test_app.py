@@ -69,6 +69,7 @@ def test_full_length_compat_run_vector_engine():
 
 
 @pytest.mark.slow
+@pytest.mark.timeout(1200)
 def test_full_length_compat_run_actors_engine():
     """Message-level parity at full length: the `actors` engine runs the reference app exactly as
     `ShareTradeHelper.scala:20-48` wires it -- 10 TrainerChildActor FSMs, each asking ONE shared
@@ -78,12 +79,12 @@ def test_full_length_compat_run_actors_engine():
     from sharetrade.app import run
 
     cfg = _cfg()
-    cfg.router.poll_interval_s = 2.0     # the app's 201 polls then span 402 s
+    cfg.router.poll_interval_s = 5.0     # the reference's own poll (ShareTradeHelper.scala:33): 201 polls span 1,005 s
     t0 = time.perf_counter()
     res = run(cfg, engine="actors", device="cpu", quiet=True)
     assert res["completed"] == 1.0, res
     assert res["avg"] == 2400.0 and res["std"] == 0.0, res
-    assert time.perf_counter() - t0 < 900
+    assert time.perf_counter() - t0 < 1100
 
 
 def test_intended_semantics_trade():
