@@ -144,7 +144,8 @@ def philox_normal(rows: int, cols: int, std: float, seed: int, stream: int) -> t
     return torch.from_numpy((np.float32(std) * z.astype(np.float32)).reshape(rows, cols))
 
 
-def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0, device=None) -> torch.Tensor:
+def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0, device=None,
+                host_mirror: bool = False) -> torch.Tensor:
     """fp32 flat params; ``W ~ N(0, init_std)`` (tf.RandomNormalInitializer,
     QDecisionPolicyActor.scala:41,45) or He-normal; biases = ``bias_init``.
 
@@ -154,10 +155,11 @@ def init_params(layout: QNetLayout, m: ModelConfig, seed: int = 0, device=None) 
     (PolicyServer, serve_eval) and a device engine get bit-identical weights for one seed -- and by its
     NumPy mirror on a machine without a GPU (the same values up to libm ulps: logf / cosf vs NumPy).
     ``"torch"`` uses torch's CPU generator and reproduces the seeded runs of rounds 1-2.  The result
-    lives on ``device`` (CPU by default)."""
+    lives on ``device`` (CPU by default).  ``host_mirror``: always draw with the NumPy mirror (tests pin
+    the mirror against the kernel with it, since a GPU-less host relies on the mirror)."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
     flat = torch.zeros(layout.numel, dtype=torch.float32, device=dev)
-    kdev = _kernel_device(dev) if m.init_rng == "philox" else None
+    kdev = _kernel_device(dev) if (m.init_rng == "philox" and not host_mirror) else None
     use_kernel = kdev is not None
     if use_kernel:
         from ..ops import native

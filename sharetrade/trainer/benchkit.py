@@ -155,12 +155,14 @@ def evaluation_snapshot(eng):
     try:
         yield eng
     finally:
+        # no error-word check in here: it would replace an exception raised by the body
         eng.synchronize(check=False)
         eng.load_state_dict(snap)
         for t, c in zip([t for t in (getattr(eng, "stat_acc", None), getattr(eng, "stats", None))
                          if torch.is_tensor(t)], acc):
             t.copy_(c)
-        eng.synchronize()
+        eng.synchronize(check=False)
+    eng.check_kernel_err()   # reached only when the body succeeded
 
 
 def _episode_summary(eng, ep0: torch.Tensor, world: int, group, steps: int) -> Dict[str, float]:
@@ -224,11 +226,17 @@ def buy_and_hold_returns(eng, world: int = 1, group=None) -> Dict[str, float]:
     steps = T - H
     b = torch.full((P.shape[0],), float(c.budget), dtype=torch.float32, device=P.device)
     sh = torch.full((P.shape[0],), int(c.shares), dtype=torch.int32, device=P.device)
+    b0 = b.clone()
+    s0 = sh.clone()
     for pos in range(steps):
         v = P[:, pos + H]
-        buy = b >= v
-        b = torch.where(buy, b - v, b)
-        sh = sh + buy.to(torch.int32)
+        # the env's own Buy transition: with env.compat_decisions (TrainerChildActor.scala:120-122) the
+        # decision and its update start from the constructor budget / shares at every step, so Buy never
+        # accumulates -- the baseline is still "Buy at every step" of THAT env
+        bd, sd = (b0, s0) if c.compat_decisions else (b, sh)
+        buy = bd >= v
+        b = torch.where(buy, bd - v, bd)
+        sh = sd + buy.to(torch.int32)
     fin = (b + sh.to(torch.float32) * P[:, T - 1]).double() - float(c.budget)
     done = torch.ones_like(fin, dtype=torch.bool)
     return _reduce_returns(done, fin, P.shape[0], world, group, steps)

@@ -546,11 +546,19 @@ class VectorEngine:
                 o.lr = float(lr)
         elif self.backend == "native":
             q, o = self._qp, self._op
-            undo.append((q, "eps", q.eps)); undo.append((q, "inv_ramp", q.inv_ramp)); undo.append((o, "lr", o.lr))
+            # overlapped DP applies its updates through struct copies of self._op (``_ov['ops']``): a
+            # gradient still in flight is a TRAINING gradient -- applied now, at the training lr -- and the
+            # copies take the override too, so no evaluation step changes the weights
+            self.flush_pending()
+            ops = [o] + list(getattr(self, "_ov", {}).get("ops", []))
+            undo.append((q, "eps", q.eps)); undo.append((q, "inv_ramp", q.inv_ramp))
+            for oo in ops:
+                undo.append((oo, "lr", oo.lr))
             if epsilon is not None:
                 q.eps, q.inv_ramp = float(epsilon), inv
             if lr is not None:
-                o.lr = float(lr)
+                for oo in ops:
+                    oo.lr = float(lr)
         undo.append((a, "epsilon", a.epsilon)); undo.append((a, "lr", a.lr))
         if epsilon is not None:
             a.epsilon = float(epsilon)
@@ -559,6 +567,8 @@ class VectorEngine:
         try:
             yield self
         finally:
+            # the last overridden step's gradient (overlapped DP) is applied under the override
+            self.flush_pending()
             for obj, k, v in reversed(undo):
                 setattr(obj, k, v)
             self._graph, self._graph_k = saved_graphs
@@ -725,6 +735,12 @@ class VectorEngine:
             native.to_bf16(self.params, self.params_bf)
 
     def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
+        ov = getattr(self, "_ov", None)
+        if ov is not None and ov["pending"] is not None:
+            # a gradient in flight belongs to the replaced state: wait for its collective (every rank
+            # started it), then drop it instead of applying it to the restored parameters
+            ov["pending"][0]()
+            ov["pending"] = None
         self.params.copy_(d["params"].to(self.device))
         self.params.mul_(self._real)
         if self.params_ema is not None:
@@ -736,6 +752,10 @@ class VectorEngine:
         if "params_target" in d:
             self._target_params()
             self.params_target.copy_(d["params_target"].to(self.device))
+        elif self.params_target is not None:
+            # a checkpoint without a target net: bootstrap from the loaded parameters (as the torch
+            # backend's lazy first copy does), not from the construction-time weights
+            self.params_target.copy_(self.params)
         self.opt.t = int(d["opt_t"][0])
         self.step_count = int(d["step"][0])
         for k in self.state.as_dict():
@@ -751,7 +771,9 @@ class VectorEngine:
             return
         import torch.distributed as dist
 
-        for t in (self.params, self.opt.s1, self.opt.s2):
+        # the target net too (agent.target_every): a re-joined rank must bootstrap from rank 0's target
+        tgt = (self.params_target,) if self.params_target is not None else ()
+        for t in (self.params, self.opt.s1, self.opt.s2) + tgt:
             if t.numel():
                 dist.broadcast(t, src_rank, group=self.group)
         if self.backend == "native" and self.kernel == "bf16_fused":
@@ -775,5 +797,6 @@ class VectorEngine:
         if err is not None and err.device.type == "cuda":
             v = max(abs(int(x)) for x in err.cpu().tolist())
             if v:
+                err.zero_()   # reported once: the next launch starts from a clean word
                 raise RuntimeError(f"step kernel reported error word {v:#x} (ws ring protocol wait gave up; "
                                    f"gradients of the failing launch are invalid)")

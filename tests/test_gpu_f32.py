@@ -163,7 +163,7 @@ def test_init_normal_kernel_matches_host_mirror(native_built):
     for preset in ("reference_compat", "flagship"):
         cfg = preset_config(preset)
         L = qn.QNetLayout.from_config(cfg.model)
-        host = qn.init_params(L, cfg.model, seed=5)
+        host = qn.init_params(L, cfg.model, seed=5, host_mirror=True)   # the NumPy mirror, not the kernel
         dev = qn.init_params(L, cfg.model, seed=5, device="cuda:0").cpu()
         assert torch.equal(dev == 0, host == 0)                 # same padding pattern
         assert torch.allclose(dev, host, rtol=2e-5, atol=2e-6), float((dev - host).abs().max())
