@@ -129,6 +129,10 @@ def lib() -> C.CDLL:
     L.st_qstep_ws_launch.restype = C.c_int
     L.st_qstep_ws_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
     L.st_qstep_ws_lds_bytes.restype = C.c_int
+    L.st_qstep_pipe_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.st_qstep_pipe_launch.restype = C.c_int
+    L.st_qstep_pipe_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.st_qstep_pipe_lds_bytes.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
     L.st_reduce_optim.restype = C.c_int
     L.st_advance.argtypes = [C.c_void_p, C.c_void_p]
@@ -200,6 +204,14 @@ def qstep_ws_supported(inp: int, h1p: int, h2p: int) -> bool:
     if not available():
         return False
     return lib().st_qstep_ws_lds_bytes(inp, h1p, h2p) > 0
+
+
+def qstep_pipe_supported(inp: int, h1p: int, h2p: int) -> bool:
+    """Unit-sliced pipelined variant (csrc/qstep_pipe.hip: weight slices in VGPRs, activations through
+    LDS, five tiles' stages between two barriers)."""
+    if not available():
+        return False
+    return lib().st_qstep_pipe_lds_bytes(inp, h1p, h2p) > 0
 
 
 def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float, key0: int, key1: int) -> None:

@@ -168,14 +168,20 @@ class VectorEngine:
         self.chunk = 32
         self.step_kernel = "narrow"
         sk = cfg.engine.step_kernel
-        if sk not in ("auto", "wide", "narrow", "ws"):
+        if sk not in ("auto", "wide", "narrow", "ws", "pipe"):
             raise ValueError(f"engine.step_kernel: {sk!r}")
         if cfg.engine.step_variant:
             # timing / debug builds of the ws kernel only; refused unless SHARETRADE_AB_BUILDS=1
-            if sk not in ("auto", "ws"):
-                raise ValueError("engine.step_variant selects a build of the ws kernel (step_kernel 'ws')")
-            native.variant_launch(cfg.engine.step_variant)
-        if self.kernel == "bf16_fused" and (sk == "ws" or (sk == "auto" and int(cfg.engine.chunk) == 0
+            if sk not in ("auto", "ws", "pipe"):
+                raise ValueError("engine.step_variant selects a build of the ws or pipe kernel")
+            native.variant_launch(cfg.engine.step_variant,
+                                  "st_qstep_pipe_launch_" if sk == "pipe" else "st_qstep_ws_launch_")
+        if self.kernel == "bf16_fused" and sk == "pipe":
+            if not (self.ws_ok(cfg, L) and native.qstep_pipe_supported(L.pdims[0], L.pdims[1], L.pdims[2])):
+                raise NotImplementedError(f"engine.step_kernel='pipe' needs E % 64 == 0, history 201 and padded dims "
+                                          f"(224, 128, 128); got E={self.E}, H={self.H}, dims {L.pdims}")
+            self.chunk, self.step_kernel = 64, "pipe"
+        elif self.kernel == "bf16_fused" and (sk == "ws" or (sk == "auto" and int(cfg.engine.chunk) == 0
                                                             and cfg.engine.step_waves == 8 and self.ws_ok(cfg, L))):
             if not self.ws_ok(cfg, L):
                 raise NotImplementedError(f"engine.step_kernel='ws' needs E % 64 == 0, history 201, padded dims "
@@ -291,7 +297,7 @@ class VectorEngine:
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
         # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide
         # kernels; one padded copy for ws (4-B-aligned dwordx4 reads, as fast: profiles/r3_ws_ab.md)
-        self.prices4 = native.replicate4(self.prices, 1 if self.step_kernel == "ws" else 4)
+        self.prices4 = native.replicate4(self.prices, 1 if self.step_kernel in ("ws", "pipe") else 4)
         native.to_bf16(self.params, self.params_bf)
         props = torch.cuda.get_device_properties(dev)
         self.grid = max(1, min(self.cfg.engine.grid or props.multi_processor_count, self.E // self.chunk))
@@ -394,7 +400,11 @@ class VectorEngine:
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
 
     def _launch_qstep(self, L, sh) -> None:
-        if self.step_kernel == "ws":
+        if self.step_kernel == "pipe":
+            fn = L.st_qstep_pipe_launch
+            if self.cfg.engine.step_variant:   # timing builds (csrc/ab/qstep_pipe_<v>.hip), same contract
+                fn = native.variant_launch(self.cfg.engine.step_variant, "st_qstep_pipe_launch_")
+        elif self.step_kernel == "ws":
             fn = L.st_qstep_ws_launch
             if self._qp.stamps:   # tools/stamp_qstep.py: the debug stamps build (opt-in A/B library)
                 fn = native.variant_launch(self.cfg.engine.step_variant or "stamps")

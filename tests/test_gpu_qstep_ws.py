@@ -16,13 +16,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _cfg(compat=False):
+KERNELS = ["ws", "pipe"]   # csrc/qstep_ws.hip, csrc/qstep_pipe.hip: the same contract, the same checks
+
+
+def _cfg(compat=False, kernel="ws"):
     from sharetrade.config import preset_config
 
     cfg = preset_config("flagship")
-    cfg.engine.step_kernel = "ws"
-    # a tuning build of the same kernel (csrc/qstep_ws_<v>.hip) under the same checks, for A/B candidates
-    cfg.engine.step_variant = os.environ.get("SHARETRADE_WS_VARIANT", "")
+    cfg.engine.step_kernel = kernel
+    # a tuning build of the ws kernel (csrc/qstep_ws_<v>.hip) under the same checks, for A/B candidates
+    cfg.engine.step_variant = os.environ.get("SHARETRADE_WS_VARIANT", "") if kernel == "ws" else ""
     if compat:
         cfg.env.compat_decisions = True
         cfg.agent.target_slot = "compat"
@@ -51,18 +54,19 @@ def _oracle(cfg, prices, st0, params, layout, step, loss_coef, **kw):
         loss_coef=loss_coef, reward_mode=cfg.agent.reward_mode, td_clip=cfg.agent.td_clip, **kw)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("compat", [False, True])
 @pytest.mark.parametrize("E,grid", [(64, 0), (256, 0), (640, 2), (1024, 3), (4096, 0)])
-def test_ws_matches_oracle(native_built, compat, E, grid):
+def test_ws_matches_oracle(native_built, kernel, compat, E, grid):
     from sharetrade.trainer.engine import VectorEngine
 
-    cfg = _cfg(compat)
+    cfg = _cfg(compat, kernel)
     cfg.agent.epsilon = 0.5
     cfg.engine.grid = grid
     prices = _prices(E)
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
-    assert eng.step_kernel == "ws"
+    assert eng.step_kernel == kernel
     st0 = eng.state.clone()
     st0.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 3 % 190)
     st0.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
@@ -78,6 +82,7 @@ def test_ws_matches_oracle(native_built, compat, E, grid):
     rew = eng.rewards_out.cpu().clone()
     _, _, info0 = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=True)
     mism = (info0["actions"].cpu() != acts).float().mean().item()
+    print(f"[meas] oracle {kernel} compat={compat} E={E} grid={grid} action_mismatch={mism:.4f}")
     assert mism <= 0.05, f"action mismatch rate {mism}"
     ns, g_ref, info = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=True,
                               forced_actions=acts)
@@ -87,12 +92,15 @@ def test_ws_matches_oracle(native_built, compat, E, grid):
     L = eng.layout
     for l in range(L.n_layers):
         gw, rw = L.w(grad, l), L.w(g_ref, l)
+        print(f"[meas] oracle {kernel} compat={compat} E={E} layer={l} w_rel_bf16={_rel(gw, rw):.3e}"
+              + (f" b_rel_bf16={_rel(L.b(grad, l), L.b(g_ref, l)):.3e}" if l > 0 else ""))
         assert _rel(gw, rw) < 3e-2, (l, _rel(gw, rw))
         if l > 0:
             assert _rel(L.b(grad, l), L.b(g_ref, l)) < 3e-2, l
     # and vs the pure fp32 oracle (no bf16 emulation, same actions): the bound the wide kernel meets
     _, g32, _ = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=False,
                         forced_actions=acts)
+    print(f"[meas] oracle {kernel} compat={compat} E={E} grad_rel_fp32={_rel(grad, g32):.3e}")
     assert _rel(grad, g32) < 0.1, _rel(grad, g32)
     # statistics slab: reward sum and the number of explore draws
     st = eng.stat_slab.sum(0).cpu()
@@ -100,13 +108,14 @@ def test_ws_matches_oracle(native_built, compat, E, grid):
     assert int(round(float(st[2]))) == int((~info0["exploit"]).sum())
 
 
-def test_ws_episode_end_and_reset(native_built):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_ws_episode_end_and_reset(native_built, kernel):
     """Envs at the last position of their series finish the episode in this step: last_final, episode
     counter and the reset of budget / shares / position written by the data waves."""
     from sharetrade.trainer.engine import VectorEngine
 
     E, T = 256, 260
-    cfg = _cfg()
+    cfg = _cfg(kernel=kernel)
     prices = _prices(E, T=T, seed=9)
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
@@ -140,11 +149,8 @@ def test_ws_and_wide_agree_over_steps(native_built):
     prices = _prices(E, seed=4)
     dev = torch.device("cuda", 0)
     out = {}
-    for kern in ("wide", "ws"):
-        cfg = _cfg()
-        cfg.engine.step_kernel = kern
-        if kern != "ws":
-            cfg.engine.step_variant = ""
+    for kern in ("wide", "ws", "pipe"):
+        cfg = _cfg(kernel=kern)
         cfg.agent.epsilon = 0.0          # every action a uniform draw: identical trajectories
         eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
         assert eng.step_kernel == kern
@@ -155,16 +161,19 @@ def test_ws_and_wide_agree_over_steps(native_built):
         out[kern] = (eng.params.detach().cpu().clone(), {k: v.cpu().clone() for k, v in eng.state.as_dict().items()},
                      eng.stat_acc.cpu().clone())
     pw, sw, stw = out["wide"]
-    pv, sv, stv = out["ws"]
-    for k in ("budget", "shares", "pos", "value"):
-        assert torch.equal(sw[k], sv[k]), k
-    assert _rel(pv, pw) < 1e-2, _rel(pv, pw)
-    assert torch.allclose(stv[0], stw[0], rtol=1e-5, atol=1e-5)     # reward sums
-    assert torch.allclose(stv[1], stw[1], rtol=2e-2)                # TD loss sums
+    for kern in ("ws", "pipe"):
+        pv, sv, stv = out[kern]
+        for k in ("budget", "shares", "pos", "value"):
+            assert torch.equal(sw[k], sv[k]), (kern, k)
+        print(f"[agree] {kern} vs wide: params rel {_rel(pv, pw):.3e}")
+        assert _rel(pv, pw) < 1e-2, (kern, _rel(pv, pw))
+        assert torch.allclose(stv[0], stw[0], rtol=1e-5, atol=1e-5), kern     # reward sums
+        assert torch.allclose(stv[1], stw[1], rtol=2e-2), kern                # TD loss sums
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("compat", [False, True])
-def test_ws_trajectory_matches_torch_oracle(native_built, compat):
+def test_ws_trajectory_matches_torch_oracle(native_built, kernel, compat):
     """Ten eager ws steps against the plain-PyTorch oracle engine (engine_step_ref + optimizer_step_ref)
     driven with the kernel's actions: env transitions and rewards exact at every step, the learned
     parameter change within bf16 tolerance of the oracle's (bf16-emulating forward / backward) and
@@ -174,14 +183,14 @@ def test_ws_trajectory_matches_torch_oracle(native_built, compat):
     from sharetrade.trainer.engine import VectorEngine
 
     E = 1024
-    cfg = _cfg(compat)
+    cfg = _cfg(compat, kernel)
     cfg.agent.epsilon = 0.6
     cfg.agent.optimizer = "sgd"
     cfg.agent.lr = 0.01
     prices = _prices(E, T=320, seed=11)
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
-    assert eng.step_kernel == "ws"
+    assert eng.step_kernel == kernel
     eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 100)
     refs = {}
     for emulate in (True, False):
@@ -208,6 +217,7 @@ def test_ws_trajectory_matches_torch_oracle(native_built, compat):
     d = eng.params.detach().cpu() - p0
     for emulate, tol in ((True, 3e-2), (False, 0.1)):
         dr = refs[emulate].params - p0
+        print(f"[meas] trajectory {kernel} compat={compat} emulate_bf16={emulate} dparam_rel={_rel(d, dr):.3e}")
         assert _rel(d, dr) < tol, (emulate, _rel(d, dr))
 
 
