@@ -36,6 +36,11 @@ struct QStepParams {
   int reward_mode;          // 0: reward = change of portfolio value; 1: its one-step return (change / previous)
   float td_clip;            // > 0: the TD error fed back is clamped to [-td_clip, td_clip] (Huber loss)
   unsigned* err;            // csrc/qstep_ws.hip: bit 0 = a ring wait gave up (bounded spin), or null
+  // learning-quality knobs of the torch oracle (sharetrade/env/trading.py engine_step_ref), ws / pipe kernels:
+  float reward_scale;       // the reward in the TD target is multiplied by this (1: the reference)
+  int ramp_global;          // 1: the exploit ramp runs over the step count instead of the episode position
+  const float* qt;          // target net (csrc/qtarget.hip): [E][3][4] Q_target(x' after action a), or null
+  int double_dqn;           // with qt: the next action is the online net's argmax, valued by the target
 };
 
 // rows of QStepParams::env

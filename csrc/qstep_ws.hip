@@ -312,7 +312,9 @@ ST_DEV bool wait_full_or_end(const QStepParams& p, int* ctl, int sa, int q) {
 }
 
 // ---------------------------------------------------------------------------------- the kernel
-template <int FEAT, bool DYN>
+// KN: the learning-quality knobs (target net, double DQN, reward scale, global exploit ramp) -- a separate
+// instance, so the production build carries none of their code
+template <int FEAT, bool DYN, bool KN>
 __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* W0p = reinterpret_cast<bf16_t*>(smem + oW0);
@@ -635,7 +637,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         float best = q0;
         if (q1 > best) { best = q1; greedy = 1; }
         if (q2 > best) { best = q2; greedy = 2; }
-        const bool exploit = u1 < fminf(p.eps, __fmul_rn((float)pos, p.inv_ramp));
+        const bool exploit = u1 < fminf(p.eps, __fmul_rn((KN && p.ramp_global) ? (float)step : (float)pos, p.inv_ramp));
         int rnd = (int)(u2 * 3.0f);
         rnd = rnd > 2 ? 2 : rnd;
         act = exploit ? greedy : rnd;
@@ -695,6 +697,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       float dq = 0.f;
       int slot = 0;
       if (g4 == 0) {
+        // target net (csrc/qtarget.hip: Q_target of the next state after each action, this step's weights)
+        float4 tq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (KN && p.qt != nullptr) tq = *reinterpret_cast<const float4*>(p.qt + ((size_t)e * 3 + act) * 4);
         float n0 = qn[0] + b2v[0], n1 = qn[1] + b2v[1], n2 = qn[2] + b2v[2];
         if (p.output_relu) { n0 = fmaxf(n0, 0.f); n1 = fmaxf(n1, 0.f); n2 = fmaxf(n2, 0.f); }
         int am = 0;
@@ -702,7 +707,12 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         if (n1 > mx) { mx = n1; am = 1; }
         if (n2 > mx) { mx = n2; am = 2; }
         slot = p.target_compat ? am : act;
-        const float y = __fadd_rn(rew, __fmul_rn(p.gamma, mx));
+        float vnext = mx;   // the online net's max (QDecisionPolicyActor.scala:67-71)
+        if (KN && p.qt != nullptr)   // target value: of the online argmax (compat slot, double DQN) or its max
+          vnext = (p.target_compat || p.double_dqn) ? (am == 0 ? tq.x : (am == 1 ? tq.y : tq.z))
+                                                    : fmaxf(fmaxf(tq.x, tq.y), tq.z);
+        const float rsc = (KN && p.reward_scale != 1.0f) ? __fmul_rn(rew, p.reward_scale) : rew;
+        const float y = __fadd_rn(rsc, __fmul_rn(p.gamma, vnext));
         const float qs = slot == 0 ? q0 : (slot == 1 ? q1 : q2);
         const float diff = __fsub_rn(qs, y);
         dq = p.loss_coef * (p.td_clip > 0.f ? fminf(fmaxf(diff, -p.td_clip), p.td_clip) : diff);
@@ -992,16 +1002,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;   // 1-based update count for the optimizer
 }
 
-template <int FEAT, bool DYN>
+template <int FEAT, bool DYN, bool KN>
 static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)qstep_ws_kernel<FEAT, DYN>,
+    hipError_t e = hipFuncSetAttribute((const void*)qstep_ws_kernel<FEAT, DYN, KN>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((qstep_ws_kernel<FEAT, DYN>), dim3(grid), dim3(NT), LDS_BYTES, stream, p);
+  hipLaunchKernelGGL((qstep_ws_kernel<FEAT, DYN, KN>), dim3(grid), dim3(NT), LDS_BYTES, stream, p);
   return hipGetLastError();
 }
 
@@ -1025,7 +1035,12 @@ extern "C" hipError_t WS_API(st_qstep_ws_launch)(const st::QStepParams* p, int i
   if (p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->slab_bf16 && (p->slab_rows != grid || p->P % 32 != 0)) return hipErrorInvalidValue;
+  const bool kn = p->qt != nullptr || p->reward_scale != 1.0f || p->ramp_global || p->double_dqn;
+  if (kn) {   // learning-quality knobs: static schedule only
+    if (p->chunk_heads != nullptr || (p->double_dqn && p->qt == nullptr)) return hipErrorInvalidValue;
+    return p->feat_mode ? launch_f<1, false, true>(*p, grid, stream) : launch_f<0, false, true>(*p, grid, stream);
+  }
   if (p->chunk_heads != nullptr)
-    return p->feat_mode ? launch_f<1, true>(*p, grid, stream) : launch_f<0, true>(*p, grid, stream);
-  return p->feat_mode ? launch_f<1, false>(*p, grid, stream) : launch_f<0, false>(*p, grid, stream);
+    return p->feat_mode ? launch_f<1, true, false>(*p, grid, stream) : launch_f<0, true, false>(*p, grid, stream);
+  return p->feat_mode ? launch_f<1, false, false>(*p, grid, stream) : launch_f<0, false, false>(*p, grid, stream);
 }

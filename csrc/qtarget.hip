@@ -1,0 +1,211 @@
+// Target-network values of the three candidate next states of every env, for the flagship bf16 step kernels
+// (agent.target_every / agent.double_dqn on csrc/qstep_ws.hip; the learning-quality knobs of the torch oracle,
+// sharetrade/env/trading.py engine_step_ref: `qt = forward(target_params, x2)`).
+//
+// The next state x' of an env depends on the action the step kernel has not drawn yet, but only through its
+// last three features (budget, shares after Buy / Sell / Hold: TrainerChildActor.scala:118-146); the price
+// window of x' is fixed.  So this pass, run before the step kernel, evaluates the target net on all three
+// candidates: layer 1 of the shared window once, then for each candidate its 3-feature tail, layer 2 and the
+// output layer.  QT[e][a][0..2] = Q_target(x' after action a)[0..2] (output ReLU applied when the model has
+// it); the step kernel reads the row of the action it takes.
+//
+// MFMA layout (one 16-env tile per wave, 4 waves per workgroup, grid-stride over tiles): the target weights
+// are converted to bf16 into LDS once per workgroup (fp32 master copy of the target net: no second bf16
+// image to keep in sync); x' features are built in registers as B operands (the ws kernel's slot order: the
+// last 16-wide k-step carries budget, shares, 1, fxn(vnew) in lane group 0); hidden activations stay in
+// registers (layer-1 / layer-2 accumulator tiles re-packed as the next layer's B operand, the hidden-unit
+// permutation absorbed by the column order of the W1 / W2 images).  Numerics: bf16 operands, fp32
+// accumulation, the rounding points of the step kernel.
+#include "qstep.h"
+
+namespace st {
+namespace qtgt {
+
+constexpr int NW = 4, NT = 64 * NW;
+constexpr int INP = 224, HP = 128, KX = 208, HWIN = 201;
+
+constexpr int oW0 = 0;                         // W0 [128][208] bf16 (slot order)
+constexpr int oW1 = oW0 + HP * KX * 2;         // W1 [128][128] bf16, columns in pi order
+constexpr int oW2 = oW1 + HP * HP * 2;         // W2 [4][128] bf16, columns in pi order (row 3 zero)
+constexpr int oB1 = oW2 + 4 * HP * 2;          // b1 [128] f32
+constexpr int LDS_BYTES = oB1 + HP * 4;
+
+ST_DEV int slot_col(int s) {
+  if (s < 192) return s;
+  const int t = s - 192, g = t >> 2, j = t & 3;
+  if (g == 0) return j < 3 ? 201 + j : 200;
+  if (g == 1) return 192 + j;
+  if (g == 2) return 196 + j;
+  return 204 + j;
+}
+// position s of a B operand built from accumulator tiles 2 ks, 2 ks + 1 -> hidden unit (qstep_ws.hip's pi)
+ST_DEV int pi_unit(int s) {
+  const int ks = s >> 5, g = (s >> 3) & 3, j = s & 7;
+  return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
+}
+ST_DEV s8v cat8(s4v a, s4v b) {
+  s8v r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+ST_DEV s4v pk4(float a, float b, float c, float d) {
+  uint2 v;
+  v.x = pack_bf2(a, b);
+  v.y = pack_bf2(c, d);
+  return __builtin_bit_cast(s4v, v);
+}
+typedef short s2v __attribute__((ext_vector_type(2)));
+ST_DEV s4v relu_bf(f4v v) {
+  const s2v z = {0, 0};
+  const s2v a = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf2(v[0], v[1])), z);
+  const s2v b = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf2(v[2], v[3])), z);
+  s4v r = {a[0], a[1], b[0], b[1]};
+  return r;
+}
+ST_DEV float4 ldu4(const float* a) {
+  float4 v;
+  __builtin_memcpy(&v, a, sizeof(v));
+  return v;
+}
+
+struct QTargetParams {
+  const float* prices4;   // one padded copy of the bank [E][T4]
+  const int* env;         // env state rows (qstep.h EnvRow)
+  const float* wt;        // fp32 flat target params (engine layout)
+  float* qt;              // [E][3][4] out
+  int T, E, T4;
+  int off_w0, off_w1, off_b1, off_w2, off_b2;
+  float b0, inv_b0;
+  int s0, compat_env, output_relu, feat_mode;
+};
+
+template <int FEAT>
+__global__ void __launch_bounds__(NT, 1) qtarget_kernel(QTargetParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* W0 = reinterpret_cast<bf16_t*>(smem + oW0);
+  bf16_t* W1 = reinterpret_cast<bf16_t*>(smem + oW1);
+  bf16_t* W2 = reinterpret_cast<bf16_t*>(smem + oW2);
+  float* B1 = reinterpret_cast<float*>(smem + oB1);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int w = tid >> 6;
+  for (int i = tid; i < HP * KX; i += NT) {
+    const int r = i / KX, s = i % KX;
+    W0[i] = f2bf(p.wt[p.off_w0 + r * INP + slot_col(s)]);
+  }
+  for (int i = tid; i < HP * HP; i += NT) {
+    const int r = i / HP, s = i % HP;
+    W1[i] = f2bf(p.wt[p.off_w1 + r * HP + pi_unit(s)]);
+  }
+  for (int i = tid; i < 4 * HP; i += NT) {
+    const int a = i / HP, s = i % HP;
+    W2[i] = a < 3 ? f2bf(p.wt[p.off_w2 + a * HP + pi_unit(s)]) : (bf16_t)0;
+  }
+  for (int i = tid; i < HP; i += NT) B1[i] = p.wt[p.off_b1 + i];
+  __syncthreads();
+  const float b2v[3] = {p.wt[p.off_b2], p.wt[p.off_b2 + 1], p.wt[p.off_b2 + 2]};
+  const size_t E = (size_t)p.E;
+  const int ntiles = p.E / 16;
+  for (int t = blockIdx.x * NW + w; t < ntiles; t += gridDim.x * NW) {
+    const int e = 16 * t + l16;
+    const int pos = p.env[ER_POS * E + e];
+    const float bud = __int_as_float(p.env[ER_BUDGET * E + e]);
+    const int sh = p.env[ER_SHARES * E + e];
+    const int pc = min(max(pos, 0), p.T - HWIN - 1);
+    const float* b = p.prices4 + (size_t)e * p.T4 + (size_t)pc;
+    const float vnew = b[201];
+    const float invn = FEAT ? __fdiv_rn(1.0f, vnew) : 0.f;
+    auto fxn = [&](float v) { return FEAT ? __fmaf_rn(v, invn, -1.0f) : v; };
+    // x' window B operands: k-step ks, lane group g4: x'[32 ks + 8 g4 + j] = p[pos + 1 + 32 ks + 8 g4 + j]
+    s8v X[6];
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      const float4 u = ldu4(b + 1 + 32 * ks + 8 * g4), v = ldu4(b + 5 + 32 * ks + 8 * g4);
+      X[ks] = cat8(pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w)), pk4(fxn(v.x), fxn(v.y), fxn(v.z), fxn(v.w)));
+    }
+    // the last 16-wide k-step: lane groups 1, 2 window columns 192..199 of x' (p[pos + 193 ..]); group 0 the
+    // candidate's tail (below); group 3 pads
+    s4v Xw = {0, 0, 0, 0};
+    if (g4 == 1 || g4 == 2) {
+      const float4 u = ldu4(b + 193 + 4 * (g4 - 1));
+      Xw = pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w));
+    }
+    // layer 1 over the window (shared by the candidates)
+    f4v a1[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f4v acc = {0.f, 0.f, 0.f, 0.f};
+      const bf16_t* wr = W0 + (16 * i + l16) * KX + 8 * g4;
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) acc = mfma32(lds_ld8(wr + 32 * ks), X[ks], acc);
+      a1[i] = mfma16(lds_ld4(W0 + (16 * i + l16) * KX + 192 + 4 * g4), Xw, acc);
+    }
+    // the three candidates: Buy, Sell, Hold from (bd, sd) -- the env's own transition
+    const float bd = p.compat_env ? p.b0 : bud;
+    const int sd = p.compat_env ? p.s0 : sh;
+    const float fvn = FEAT ? __fmaf_rn(vnew, invn, -1.0f) : vnew;
+#pragma unroll 1
+    for (int a = 0; a < 3; ++a) {
+      const bool buy = a == 0 && bd >= vnew, sell = a == 1 && sd > 0;
+      const float b2 = buy ? __fsub_rn(bd, vnew) : (sell ? __fadd_rn(bd, vnew) : bd);
+      const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
+      const s4v tl = g4 == 0 ? pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fvn)
+                             : s4v{0, 0, 0, 0};
+      s8v H1[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f4v z0 = mfma16(lds_ld4(W0 + (16 * (2 * ks) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks]);
+        const f4v z1 = mfma16(lds_ld4(W0 + (16 * (2 * ks + 1) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks + 1]);
+        H1[ks] = cat8(relu_bf(z0), relu_bf(z1));
+      }
+      s8v H2[4];
+#pragma unroll
+      for (int ks2 = 0; ks2 < 4; ++ks2) {
+        f4v z[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * ks2 + h;
+          f4v acc = *reinterpret_cast<const f4v*>(B1 + 16 * i + 4 * g4);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) acc = mfma32(lds_ld8(W1 + (16 * i + l16) * HP + 32 * ks + 8 * g4), H1[ks], acc);
+          z[h] = acc;
+        }
+        H2[ks2] = cat8(relu_bf(z[0]), relu_bf(z[1]));
+      }
+      f4v q = {0.f, 0.f, 0.f, 0.f};
+      const bf16_t* w2r = W2 + min(l16, 3) * HP + 8 * g4;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) q = mfma32(lds_ld8(w2r + 32 * ks), H2[ks], q);
+      if (g4 == 0) {
+        float o[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          o[j] = q[j] + b2v[j];
+          if (p.output_relu) o[j] = fmaxf(o[j], 0.f);
+        }
+        *reinterpret_cast<float4*>(p.qt + ((size_t)e * 3 + a) * 4) = make_float4(o[0], o[1], o[2], 0.f);
+      }
+    }
+  }
+}
+
+}  // namespace qtgt
+}  // namespace st
+
+extern "C" hipError_t st_qtarget_launch(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
+  using namespace st::qtgt;
+  if (p->E % 16 != 0 || grid < 1 || p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;
+  static bool attr[2] = {false, false};
+  const int f = p->feat_mode ? 1 : 0;
+  const void* fn = f ? (const void*)qtarget_kernel<1> : (const void*)qtarget_kernel<0>;
+  if (!attr[f]) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr[f] = true;
+  }
+  if (f)
+    hipLaunchKernelGGL(qtarget_kernel<1>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+  else
+    hipLaunchKernelGGL(qtarget_kernel<0>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+  return hipGetLastError();
+}

@@ -44,6 +44,18 @@ class QStepParams(C.Structure):
         ("chunk_heads", C.c_void_p),
         ("reward_mode", C.c_int), ("td_clip", C.c_float),
         ("err", C.c_void_p),
+        ("reward_scale", C.c_float), ("ramp_global", C.c_int), ("qt", C.c_void_p), ("double_dqn", C.c_int),
+    ]
+
+
+class QTargetParams(C.Structure):
+    """csrc/qtarget.hip: target-net values of the three candidate next states of every env."""
+    _fields_ = [
+        ("prices4", C.c_void_p), ("env", C.c_void_p), ("wt", C.c_void_p), ("qt", C.c_void_p),
+        ("T", C.c_int), ("E", C.c_int), ("T4", C.c_int),
+        ("off_w0", C.c_int), ("off_w1", C.c_int), ("off_b1", C.c_int), ("off_w2", C.c_int), ("off_b2", C.c_int),
+        ("b0", C.c_float), ("inv_b0", C.c_float),
+        ("s0", C.c_int), ("compat_env", C.c_int), ("output_relu", C.c_int), ("feat_mode", C.c_int),
     ]
 
 
@@ -129,6 +141,10 @@ def lib() -> C.CDLL:
     L.st_qstep_ws_launch.restype = C.c_int
     L.st_qstep_ws_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
     L.st_qstep_ws_lds_bytes.restype = C.c_int
+    L.st_qtarget_launch.argtypes = [C.POINTER(QTargetParams), C.c_int, C.c_void_p]
+    L.st_qtarget_launch.restype = C.c_int
+    L.st_f32b_target_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
+    L.st_f32b_target_sync.restype = C.c_int
     L.st_qstep_pipe_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_qstep_pipe_launch.restype = C.c_int
     L.st_qstep_pipe_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]

@@ -140,10 +140,6 @@ class VectorEngine:
         self.backend = be
         a = cfg.agent
         self._learn_knobs = bool(a.target_every or a.double_dqn or a.reward_scale != 1.0 or a.ramp_mode != "position")
-        if self._learn_knobs and not (be == "torch" or (be == "native" and cfg.engine.dtype == "fp32")):
-            raise NotImplementedError("agent.target_every / double_dqn / reward_scale / ramp_mode are learning "
-                                      "experiments of the torch backend and the batched fp32 native step "
-                                      "(engine.backend='torch', or engine.dtype='fp32' with engine.f32_batched)")
         if a.ramp_mode not in ("position", "global"):
             raise ValueError(f"agent.ramp_mode: {a.ramp_mode!r}")
         if a.double_dqn and not a.target_every:
@@ -207,6 +203,11 @@ class VectorEngine:
                                           f"(224, 128, 128); got E={self.E}, dims {L.pdims}")
             self.chunk = 64 if (want in (0, 64) and wide_ok) else 32
             self.step_kernel = "wide" if self.chunk == 64 else "narrow"
+        if self._learn_knobs and self.kernel == "bf16_fused" and self.step_kernel != "ws":
+            # bf16: the ws kernel's knob build (csrc/qstep_ws.hip KN) + the target pass (csrc/qtarget.hip)
+            raise NotImplementedError("agent.target_every / double_dqn / reward_scale / ramp_mode on the bf16 "
+                                      "native step need the ws kernel (engine.step_kernel='ws' or 'auto'; "
+                                      f"this config selected {self.step_kernel!r})")
         # ------------------------------------------------------------ data
         if prices is not None:
             bank = padded_bank(prices.shape[0], prices.shape[1], self.device)
@@ -325,6 +326,13 @@ class VectorEngine:
         self.chunk_schedule = "dynamic" if (sched == "dynamic" and dyn_ok) else "static"
         self.chunk_heads = (torch.zeros(8 * 32, dtype=torch.int32, device=dev)
                             if self.chunk_schedule == "dynamic" else None)
+        # target network (agent.target_every): an fp32 copy of the parameters refreshed every target_every
+        # optimizer steps, and QT[e][a][0..3] = its Q values of the three candidate next states, written by
+        # csrc/qtarget.hip before each step kernel
+        self.qt_buf = None
+        if self.cfg.agent.target_every:
+            self.params_target = self.params.detach().clone()
+            self.qt_buf = torch.zeros(self.E * 12, dtype=torch.float32, device=dev)
         self._build_structs()
 
     def _build_structs(self):
@@ -358,7 +366,24 @@ class VectorEngine:
         q.td_clip = float(cfg.agent.td_clip)
         self.kernel_err = torch.zeros(4, dtype=torch.int32, device=self.device)
         q.err = native.ptr(self.kernel_err)
+        a = cfg.agent
+        q.reward_scale = float(a.reward_scale)
+        q.ramp_global = int(a.ramp_mode == "global")
+        q.double_dqn = int(a.double_dqn)
+        q.qt = native.ptr(self.qt_buf) if self.qt_buf is not None else None
         self._qp = q
+        self._qtp = None
+        if self.qt_buf is not None:
+            t = native.QTargetParams()
+            t.prices4, t.env, t.wt, t.qt = q.prices4, q.env, native.ptr(self.params_target), q.qt
+            t.T, t.E, t.T4 = q.T, q.E, q.T4
+            t.off_w0, t.off_w1, t.off_b1, t.off_w2, t.off_b2 = q.off_w0, q.off_w1, q.off_b1, q.off_w2, q.off_b2
+            t.b0, t.inv_b0, t.s0 = q.b0, q.inv_b0, q.s0
+            t.compat_env, t.output_relu, t.feat_mode = q.compat_env, q.output_relu, q.feat_mode
+            self._qtp = t
+            # one 16-env tile per wave, 4 waves per workgroup: >= 2 workgroups per CU when E allows it
+            self._qt_grid = max(1, min(2 * torch.cuda.get_device_properties(self.device).multi_processor_count,
+                                       self.E // 64))
         a = cfg.agent
         o = native.OptimParams()
         o.params, o.params_bf, o.mask = native.ptr(self.params), native.ptr(self.params_bf), native.ptr(self.mask)
@@ -398,8 +423,16 @@ class VectorEngine:
         else:
             self._op.mode = 0
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
+        if self._qtp is not None:
+            # after the counter advanced: copy when ctrl[0] % target_every == 0 (the torch engine's
+            # (step + 1) % target_every); under overlapped DP the copy follows the delayed update
+            native.check(L.st_f32b_target_sync(native.ptr(self.params), native.ptr(self.params_target),
+                                               self.params.numel(), native.ptr(self.ctrl),
+                                               int(self.cfg.agent.target_every), sh), "target_sync")
 
     def _launch_qstep(self, L, sh) -> None:
+        if self._qtp is not None:
+            native.check(L.st_qtarget_launch(self._qtp, self._qt_grid, sh), "qtarget")
         if self.step_kernel == "pipe":
             fn = L.st_qstep_pipe_launch
             if self.cfg.engine.step_variant:   # timing builds (csrc/ab/qstep_pipe_<v>.hip), same contract

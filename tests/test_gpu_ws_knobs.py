@@ -1,0 +1,204 @@
+"""Learning-quality knobs on the flagship bf16 step (csrc/qstep_ws.hip knob build + csrc/qtarget.hip) vs the
+plain-PyTorch oracle (sharetrade.env.trading.engine_step_ref):
+
+* agent.target_every -- TD target valued by an fp32 target copy of the parameters (csrc/qtarget.hip evaluates
+  it on the three candidate next states before the step kernel; the kernel reads the taken action's row),
+  refreshed every target_every optimizer steps (st_f32b_target_sync);
+* agent.double_dqn -- the max-Q(x') action of the online net valued by the target net;
+* agent.reward_scale -- reward multiplier inside the TD target;
+* agent.ramp_mode='global' -- the exploit ramp on the global step count instead of the episode position.
+
+The reference's agent has none of these (QDecisionPolicyActor.scala:58-71 is the online one-step DQN); they
+are the experiments of docs/LEARNING.md, here at the flagship kernel's speed.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_qstep_ws import _cfg, _oracle, _prices, _rel
+
+pytestmark = pytest.mark.gpu
+
+KNOBS = [
+    dict(target_every=3),
+    dict(target_every=3, double_dqn=True),
+    dict(reward_scale=0.5),
+    dict(ramp_mode="global"),
+    dict(target_every=2, double_dqn=True, reward_scale=2.0, ramp_mode="global"),
+]
+
+
+def _apply(cfg, knobs):
+    for k, v in knobs.items():
+        setattr(cfg.agent, k, v)
+    return cfg
+
+
+def _oracle_kw(eng, cfg, params_target, step):
+    a = cfg.agent
+    return dict(target_params=params_target, double_dqn=a.double_dqn, reward_scale=a.reward_scale,
+                ramp_pos=(torch.full((eng.E,), step, dtype=torch.int32) if a.ramp_mode == "global" else None))
+
+
+@pytest.mark.parametrize("compat", [False, True])
+def test_qtarget_values_match_forward(native_built, compat):
+    """QT[e][a] = Q_target(x' after action a) for the three candidate actions, vs the bf16-emulating forward of
+    the oracle on each forced action's next state."""
+    from sharetrade.models import qnet as qn
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 1024
+    cfg = _apply(_cfg(compat), dict(target_every=5))
+    prices = _prices(E, seed=21)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    assert eng.step_kernel == "ws" and eng.qt_buf is not None
+    eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 7 % 190)
+    eng.state.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 4)
+    eng.state.budget.copy_(torch.linspace(0.0, 3.0 * cfg.env.budget, E, device=dev))
+    # a target net that differs from the online one
+    g = torch.Generator().manual_seed(2)
+    eng.params_target.add_((torch.randn(eng.params.shape, generator=g) * 0.02).to(dev) * eng._real)
+    st0 = eng.state.clone().to("cpu")
+    pt = eng.params_target.detach().cpu().clone()
+    eng.native_grad()
+    torch.cuda.synchronize()
+    assert int(eng.kernel_err.sum()) == 0
+    qt = eng.qt_buf.view(E, 3, 4).cpu()
+    assert torch.all(qt[:, :, 3] == 0)
+    worst = 0.0
+    for act in range(3):
+        _, _, info = _oracle(cfg, prices, st0, eng.params.detach().cpu(), eng.layout, 0, eng.loss_coef,
+                             emulate_bf16=True, forced_actions=torch.full((E,), act, dtype=torch.int32))
+        ref, _, _ = qn.forward(pt, eng.layout, info["x_next"], cfg.model.output_relu, True)
+        r = _rel(qt[:, act, :3], ref[:, :3])
+        worst = max(worst, r)
+        assert r < 1e-2, (act, r)
+    print(f"[meas] qtarget compat={compat} worst_rel={worst:.3e}")
+
+
+@pytest.mark.parametrize("compat", [False, True])
+@pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()))
+def test_ws_knobs_one_step_matches_oracle(native_built, knobs, compat):
+    from sharetrade.trainer.engine import VectorEngine
+
+    if compat and knobs.get("double_dqn"):
+        pytest.skip("compat target slot already values the online argmax")
+    E = 2048
+    cfg = _apply(_cfg(compat), knobs)
+    cfg.agent.epsilon = 0.5
+    prices = _prices(E, seed=13)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    assert eng.step_kernel == "ws"
+    eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 3 % 190)
+    eng.state.shares.copy_(torch.arange(E, dtype=torch.int32, device=dev) % 3)
+    if eng.params_target is not None:
+        g = torch.Generator().manual_seed(4)
+        eng.params_target.add_((torch.randn(eng.params.shape, generator=g) * 0.02).to(dev) * eng._real)
+    step = 37
+    eng.ctrl.fill_(step)
+    st0 = eng.state.clone().to("cpu")
+    params = eng.params.detach().cpu().clone()
+    pt = eng.params_target.detach().cpu().clone() if eng.params_target is not None else None
+    grad = eng.native_grad().detach().cpu().clone()
+    torch.cuda.synchronize()
+    assert int(eng.kernel_err.sum()) == 0
+    acts = eng.actions_out.cpu().clone()
+    kw = _oracle_kw(eng, cfg, pt, step)
+    _, _, info0 = _oracle(cfg, prices, st0, params, eng.layout, step, eng.loss_coef, emulate_bf16=True, **kw)
+    mism = (info0["actions"] != acts).float().mean().item()
+    assert mism <= 0.05, mism
+    ns, g_ref, info = _oracle(cfg, prices, st0, params, eng.layout, step, eng.loss_coef, emulate_bf16=True,
+                              forced_actions=acts, **kw)
+    assert torch.equal(info["reward"], eng.rewards_out.cpu())
+    for k in ("budget", "shares", "value", "pos", "episodes"):
+        assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), k
+    r = _rel(grad, g_ref)
+    print(f"[meas] knobs {knobs} compat={compat} action_mismatch={mism:.4f} grad_rel_bf16={r:.3e}")
+    assert r < 3e-2, r
+    if knobs.get("ramp_mode") == "global":
+        # the ramp follows the step count: the exploit fraction differs from the per-position ramp's
+        _, _, info_pos = _oracle(cfg, prices, st0, params, eng.layout, step, eng.loss_coef, emulate_bf16=True,
+                                 **dict(kw, ramp_pos=None))
+        assert not torch.equal(info_pos["exploit"], info0["exploit"])
+
+
+def test_ws_target_trajectory_matches_oracle(native_built):
+    """Nine eager steps with target_every=3 and Double DQN: the target copy refreshes at steps 3, 6, 9 on the
+    device exactly as in the oracle engine, parameter change within bf16 tolerance of the oracle's."""
+    from sharetrade.models import qnet as qn
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 1024
+    cfg = _apply(_cfg(), dict(target_every=3, double_dqn=True, reward_scale=0.5))
+    cfg.agent.epsilon = 0.6
+    cfg.agent.optimizer = "sgd"
+    cfg.agent.lr = 0.01
+    prices = _prices(E, T=320, seed=17)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 100)
+    ref = VectorEngine(cfg, prices=prices, device=torch.device("cpu"), envs=E, backend="torch")
+    ref.params.copy_(eng.params.detach().cpu())
+    ref.params_target = ref.params.clone()
+    p0 = eng.params.detach().cpu().clone()
+    a = cfg.agent
+    for t in range(9):
+        st0 = eng.state.clone().to("cpu")
+        eng.step()
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        acts = eng.actions_out.cpu().clone()
+        ns, g, info = _oracle(cfg, prices, st0, ref.params, ref.layout, t, eng.loss_coef, emulate_bf16=True,
+                              forced_actions=acts, **_oracle_kw(eng, cfg, ref.params_target, t))
+        qn.optimizer_step_ref(ref.params, g, ref.opt, ref.mask, a.lr, a.adam_betas, a.adam_eps)
+        if (t + 1) % a.target_every == 0:
+            ref.params_target.copy_(ref.params)
+            assert torch.equal(eng.params_target.cpu(), eng.params.cpu()), t
+        else:
+            assert not torch.equal(eng.params_target.cpu(), eng.params.cpu()), t
+        assert torch.equal(info["reward"], eng.rewards_out.cpu()), t
+        for k in ("budget", "shares", "value", "pos", "episodes"):
+            assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (t, k)
+    d, dr = eng.params.detach().cpu() - p0, ref.params - p0
+    print(f"[meas] target trajectory dparam_rel={_rel(d, dr):.3e}")
+    assert _rel(d, dr) < 3e-2, _rel(d, dr)
+
+
+def test_ws_target_captured_graph(native_built):
+    """The target pass and the target copy inside a captured multi-step graph: the same trajectory as the
+    eager engine (uniform actions: identical env paths)."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 64 * 256
+    prices = _prices(E, seed=19)
+    dev = torch.device("cuda", 0)
+    res = {}
+    for graph in (False, True):
+        cfg = _apply(_cfg(), dict(target_every=4, double_dqn=True))
+        cfg.agent.epsilon = 0.0
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        if graph:
+            eng.capture_graph(warmup=1, graph_steps=4)
+            eng.run(11)
+        else:
+            eng.step()
+            for _ in range(11):
+                eng.step()
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        res[graph] = (eng.params.cpu().clone(), eng.params_target.cpu().clone(), eng.step_count)
+    (pe, te, ne), (pg, tg, ng) = res[False], res[True]
+    assert ne == ng == 12
+    assert _rel(pg, pe) < 1e-2, _rel(pg, pe)
+    assert _rel(tg, te) < 1e-2, _rel(tg, te)
+    assert torch.equal(tg, pg)   # 12 % 4 == 0: the target was just refreshed
+
+
+def test_other_bf16_kernels_refuse_the_knobs(native_built):
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = _apply(_cfg(kernel="wide"), dict(target_every=10))
+    with pytest.raises(NotImplementedError):
+        VectorEngine(cfg, prices=_prices(128), device=torch.device("cuda", 0), envs=128)

@@ -61,11 +61,8 @@ def test_global_ramp_and_reward_scale():
     assert not torch.equal(a.params, ref.params) and not torch.equal(b.params, ref.params)
 
 
-def test_fused_bf16_native_refuses_the_knobs():
-    cfg = preset_config("flagship")
-    cfg.agent.target_every = 10
-    with pytest.raises(NotImplementedError):
-        VectorEngine(cfg, device=torch.device("cpu"), envs=64, backend="native")
+def test_double_dqn_needs_a_target_net():
+    # (the bf16 native step takes the knobs on the ws kernel only: tests/test_gpu_ws_knobs.py)
     cfg = preset_config("flagship")
     cfg.agent.double_dqn = True
     with pytest.raises(ValueError):
