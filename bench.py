@@ -211,6 +211,13 @@ def main() -> int:
                 raise          # (a rank that stops mid-collective would hang its peers: fail the job)
             episode_error = f"{type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}"
             print(f"bench.py: episode evaluation failed: {episode_error}", file=sys.stderr)
+    # per-rank device-memory peak of this process's allocations (torch caching allocator: every engine buffer),
+    # gathered so a rank-0-only allocation that grows with the world size would show
+    peak = torch.tensor([torch.cuda.max_memory_allocated(dev) / 1e9], dtype=torch.float64, device=dev)
+    peaks = [peak]
+    if world > 1:
+        peaks = [torch.zeros_like(peak) for _ in range(world)]
+        torch.distributed.all_gather(peaks, peak)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -255,6 +262,7 @@ def main() -> int:
             free, total = torch.cuda.mem_get_info(eng.device)
             out["hbm_used_gb"] = round((total - free) / 1e9, 1)
             out["hbm_total_gb"] = round(total / 1e9, 1)
+            out["alloc_peak_gb_per_rank"] = [round(float(p_[0]), 2) for p_ in peaks]
         if allreduce_ms is not None:
             out["allreduce_ms_per_step"] = allreduce_ms
         if episode_error is not None:

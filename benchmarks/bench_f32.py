@@ -4,7 +4,7 @@ vector engine: env-steps/s of the per-env row kernels (csrc/mlp_f32.hip) vs the 
 (csrc/mlp_f32_mfma.hip) at several env counts, one MI355X, HIP graphs.  Preset ``intended`` (the
 reference's net and AdaGrad with its quirks fixed) unless ``--preset``.
 
-    python benchmarks/bench_f32.py [--envs 1024,16384,65536] [--steps 50] [--out profiles/x.md]
+    python benchmarks/bench_f32.py [--envs 1024,16384,65536] [--paths rows,batched,batched_det] [--out x.md]
 """
 import argparse
 import os
@@ -22,7 +22,9 @@ def _time(preset, path, E, steps, warm):
 
     cfg = preset_config(preset)
     cfg.engine.dtype = "fp32"
-    cfg.engine.f32_batched = "on" if path == "batched" else "off"
+    cfg.engine.f32_batched = "off" if path == "rows" else "on"
+    # batched: fp32 atomics; batched_det: ordered split-K / column-sum partials (bit-reproducible)
+    cfg.engine.f32_deterministic = "on" if path == "batched_det" else "off"
     cfg.data.source = "random_walk"
     eng = VectorEngine(cfg, device=torch.device("cuda", 0), envs=E)
     eng.capture_graph(warmup=1)
@@ -43,6 +45,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--preset", default="intended")
+    ap.add_argument("--paths", default="rows,batched,batched_det")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import build as B
@@ -52,8 +55,8 @@ def main():
              "batched MFMA step (`benchmarks/bench_f32.py`, 1x MI355X, HIP graphs)", "",
              "| envs | path | ms / step | env-steps/s |", "|---|---|---|---|"]
     for E in (int(x) for x in a.envs.split(",")):
-        for path in ("rows", "batched"):
-            steps = a.steps if path == "batched" or E <= 4096 else max(5, a.steps // 10)
+        for path in a.paths.split(","):
+            steps = a.steps if path != "rows" or E <= 4096 else max(5, a.steps // 10)
             ms = _time(a.preset, path, E, steps, a.warmup)
             lines.append(f"| {E} | {path} | {ms:.3f} | {E / ms * 1e3:.3e} |")
             print(lines[-1], flush=True)

@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(1024) f32b_td_kernel(F32Batch r) {
 // pass as float4 runs (N / 4 threads per row), sums `rows` rows (~E / 32), folds its row groups in LDS and
 // adds one atomic per column.  Other shapes: one thread per column and row group of 256.
 __global__ void __launch_bounds__(256) f32b_colsum4_kernel(const float* D, long long ld, int E, int N, int rows,
-                                                           float* out) {
+                                                           float* out, float* partials) {
   __shared__ float4 part[256];
   const int tr = N >> 2, rpi = 256 / tr;
   const int t = threadIdx.x, c4 = t % tr, rg = t / tr;
@@ -520,10 +520,14 @@ __global__ void __launch_bounds__(256) f32b_colsum4_kernel(const float* D, long 
       const float4 b = part[g * tr + t];
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
-    atomicAdd(out + 4 * t, a.x);
-    atomicAdd(out + 4 * t + 1, a.y);
-    atomicAdd(out + 4 * t + 2, a.z);
-    atomicAdd(out + 4 * t + 3, a.w);
+    if (partials) {   // deterministic mode: the block's column sums to its own row (st_f32b_splitsum adds them)
+      reinterpret_cast<float4*>(partials + (long long)blockIdx.x * N)[t] = a;
+    } else {
+      atomicAdd(out + 4 * t, a.x);
+      atomicAdd(out + 4 * t + 1, a.y);
+      atomicAdd(out + 4 * t + 2, a.z);
+      atomicAdd(out + 4 * t + 3, a.w);
+    }
   }
 }
 __global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long long ld, int E, int N, float* out) {
@@ -535,18 +539,43 @@ __global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long l
   atomicAdd(out + n, s);
 }
 
-// out[i] = sum over z of part[z * zstride + i] (split-K partials of EPI_PARTIAL, added in split order);
-// float4 per thread (n % 4 == 0, 16-byte aligned, checked on the host)
+// out[i] = sum over z of part[z * zstride + i] (split-K partials of EPI_PARTIAL, bias column-sum partials):
+// a fixed summation order, so bit-reproducible.  A block covers 16 float4 columns x 16 split groups: thread
+// (c, g) adds splits g, g + 16, ... (4 loads in flight), then the 16 group sums fold in LDS in group order.
+// (The first form -- one thread per float4 walking all splits -- put 49 blocks and a 64-deep dependent load
+// chain on the 224 x 224 product: most of the 0.412 -> 0.493 ms of the deterministic mode at 65,536 envs.)
 __global__ void __launch_bounds__(256) f32b_splitsum_kernel(const float* part, int splits, long long zstride,
                                                             float* out, long long n4) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  float4 a = reinterpret_cast<const float4*>(part)[i];
-  for (int z = 1; z < splits; ++z) {
-    const float4 b = reinterpret_cast<const float4*>(part + (long long)z * zstride)[i];
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  __shared__ float4 red[16][17];
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const long long i = (long long)blockIdx.x * 16 + c;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    const float4* p4 = reinterpret_cast<const float4*>(part) + i;
+    const long long zs4 = zstride >> 2;
+    int z = g;
+    for (; z + 48 < splits; z += 64) {
+      const float4 b0 = p4[z * zs4], b1 = p4[(z + 16) * zs4], b2 = p4[(z + 32) * zs4], b3 = p4[(z + 48) * zs4];
+      a.x += b0.x; a.y += b0.y; a.z += b0.z; a.w += b0.w;
+      a.x += b1.x; a.y += b1.y; a.z += b1.z; a.w += b1.w;
+      a.x += b2.x; a.y += b2.y; a.z += b2.z; a.w += b2.w;
+      a.x += b3.x; a.y += b3.y; a.z += b3.z; a.w += b3.w;
+    }
+    for (; z < splits; z += 16) {
+      const float4 b = p4[z * zs4];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
   }
-  reinterpret_cast<float4*>(out)[i] = a;
+  red[g][c] = a;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 s = red[0][c];
+    for (int k = 1; k < 16; ++k) {
+      const float4 b = red[k][c];
+      s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
 }
 
 // target network refresh inside the captured step: copy the parameters when the (already advanced) step
@@ -595,7 +624,7 @@ extern "C" hipError_t st_f32b_splitsum(const float* part, int splits, long long 
       ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15))
     return hipErrorInvalidValue;
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(st::f32b_splitsum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, splits,
+  hipLaunchKernelGGL(st::f32b_splitsum_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, stream, part, splits,
                      zstride, out, n4);
   return hipGetLastError();
 }
@@ -627,17 +656,35 @@ extern "C" hipError_t st_f32b_td(const st::F32Batch* r, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// part != nullptr (deterministic mode): N % 4 == 0, N <= 256 and 16-byte alignment required; the column sums
+// of the <= 32 blocks land in part[block][N] and one st_f32b_splitsum adds them into out (returns the block
+// count through *nparts)
+extern "C" hipError_t st_f32b_colsum_det(const float* D, long long ld, int E, int N, float* out, float* part,
+                                         int* nparts, hipStream_t stream);
 extern "C" hipError_t st_f32b_colsum(const float* D, long long ld, int E, int N, float* out, hipStream_t stream) {
+  return st_f32b_colsum_det(D, ld, E, N, out, nullptr, nullptr, stream);
+}
+extern "C" hipError_t st_f32b_colsum_det(const float* D, long long ld, int E, int N, float* out, float* part,
+                                         int* nparts, hipStream_t stream) {
   if (E <= 0 || N <= 0) return hipErrorInvalidValue;
-  if (N % 4 == 0 && N <= 256 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(D) & 15) == 0) {
+  const bool vec = N % 4 == 0 && N <= 256 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(D) & 15) == 0;
+  if (part && (!vec || (reinterpret_cast<uintptr_t>(part) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)))
+    return hipErrorInvalidValue;
+  if (vec) {
     // at most 32 blocks: every block adds one atomic per column, and same-address fp32 atomics serialise
     // (256 blocks on a 16-column output: 16 us at 65,536 rows, mostly the 256-deep atomic queue per column)
     const int rpi = 256 / (N / 4);
     int rows = (E + 31) / 32;
     rows = (rows + rpi - 1) / rpi * rpi;
     if (rows < 4 * rpi) rows = 4 * rpi;
-    hipLaunchKernelGGL(st::f32b_colsum4_kernel, dim3((E + rows - 1) / rows), dim3(256), 0, stream, D, ld, E, N, rows,
-                       out);
+    const int nb = (E + rows - 1) / rows;
+    hipLaunchKernelGGL(st::f32b_colsum4_kernel, dim3(nb), dim3(256), 0, stream, D, ld, E, N, rows, out, part);
+    if (part) {
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      if (nparts) *nparts = nb;
+      return st_f32b_splitsum(part, nb, N, out, N, stream);
+    }
     return hipGetLastError();
   }
   dim3 grid((N + 255) / 256, (E + 255) / 256);

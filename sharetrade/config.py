@@ -170,6 +170,9 @@ class EngineConfig:
     # fp32 engine (engine.dtype = "fp32": the reference geometry): "auto" = the batched MFMA step
     # (csrc/mlp_f32_mfma.hip) from 1,024 envs up, the per-env row kernels (csrc/mlp_f32.hip) below; "on" / "off"
     f32_batched: str = "auto"
+    # batched fp32 step: weight-gradient split-K partials + bias column sums added in a fixed order instead of
+    # fp32 atomics (bit-reproducible); "auto" = on for DP ranks and env.compat_decisions (reference_compat)
+    f32_deterministic: str = "auto"
     step_variant: str = ""          # timing / debug build of the ws kernel (csrc/ab/qstep_ws_<v>.hip); opt-in only
                                     # (SHARETRADE_AB_BUILDS=1, several compute wrong results); "" = production
     graph: bool = True              # capture the step in a HIP graph

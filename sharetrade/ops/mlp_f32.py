@@ -408,6 +408,9 @@ def _bind_batched():
             getattr(L, n).restype = C.c_int
         L.st_f32b_colsum.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.st_f32b_colsum.restype = C.c_int
+        L.st_f32b_colsum_det.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p]
+        L.st_f32b_colsum_det.restype = C.c_int
         L._f32b_bound = True
     return L
 
@@ -439,6 +442,21 @@ class _BatchedScratch:
         self.act = torch.zeros(E, dtype=torch.int32, device=device)
 
 
+def f32_deterministic(cfg, world_size: int) -> bool:
+    """engine.f32_deterministic: "on" / "off", or "auto" = on for DP ranks (world_size > 1) and for the
+    reference's decision semantics (env.compat_decisions: the reference_compat preset), where replays must be
+    bit-exact; SHARETRADE_F32_SPLIT_PARTIAL=0/1 overrides."""
+    env = os.environ.get("SHARETRADE_F32_SPLIT_PARTIAL")
+    if env in ("0", "1"):
+        return env == "1"
+    mode = cfg.engine.f32_deterministic
+    if mode not in ("auto", "on", "off"):
+        raise ValueError(f"engine.f32_deterministic: {mode!r}")
+    if mode == "auto":
+        return world_size > 1 or bool(cfg.env.compat_decisions)
+    return mode == "on"
+
+
 class F32BatchedStep:
     """Batched fp32 step of :class:`~sharetrade.trainer.engine.VectorEngine` on the matrix cores
     (csrc/mlp_f32_mfma.hip): the reference network's 203->200->3 geometry -- and any fp32 MLP of the
@@ -459,12 +477,16 @@ class F32BatchedStep:
         # at least 256 envs per split.  One split per 256 envs on every product (the first form) put 4,096
         # workgroups and 16.7 M fp32 atomics on the 208 x 208 product: 164 us of a 750 us step at 65,536 envs
         self.splits = splits
-        # split-K partial tiles of the weight-gradient products (EPI_PARTIAL + st_f32b_splitsum, deterministic)
-        # with SHARETRADE_F32_SPLIT_PARTIAL=1; default: fp32 atomics into the gradient
+        # deterministic mode (engine.f32_deterministic): split-K partial tiles of the weight-gradient products
+        # (EPI_PARTIAL) and per-block bias column sums, each added in a fixed order by st_f32b_splitsum -- no
+        # fp32 atomics, so the step is bit-reproducible (DP ranks replaying a dead rank's steps agree bit for
+        # bit).  Otherwise fp32 atomics into the gradient.  SHARETRADE_F32_SPLIT_PARTIAL=0/1 overrides.
+        self.deterministic = f32_deterministic(cfg, eng.world_size)
         need = max(self._splits(lay.pdims[l + 1], lay.pdims[l], E) * lay.pdims[l + 1] * lay.pdims[l]
                    for l in range(lay.n_layers))
-        self.partials = (torch.empty(need, dtype=torch.float32, device=eng.device)
-                         if os.environ.get("SHARETRADE_F32_SPLIT_PARTIAL", "0") == "1" else None)
+        self.partials = torch.empty(need, dtype=torch.float32, device=eng.device) if self.deterministic else None
+        self.colsum_part = (torch.empty(32 * 256 + 64, dtype=torch.float32, device=eng.device)
+                            if self.deterministic else None)
         st, s = eng.state, self.s
         r = F32Batch()
         r.E, r.in_p, r.H, r.T, r.bias_col = E, lay.in_p, eng.H, eng.T, lay.bias_col
@@ -598,7 +620,9 @@ class F32BatchedStep:
             # dW_l^T[out][in] += sum_e dZ_l[e][out] A_l[e][in]  (K = envs, split over workgroups)
             sp = self._splits(Nout, Kin, E)
             dst = out.data_ptr() + 4 * net.off_w[l]
-            if sp > 1 and self.partials is not None and (Nout * Kin) % 4 == 0 and dst % 16 == 0:
+            if sp > 1 and self.partials is not None:
+                if (Nout * Kin) % 4 or dst % 16:
+                    raise RuntimeError(f"deterministic fp32 step: layer {l} weight gradient not float4-aligned")
                 # split-K partials into scratch, then one deterministic sum (the fp32 atomics of every
                 # split's tile were the cost of the 224 x 224 product at 65,536 envs)
                 zs = Nout * Kin
@@ -614,7 +638,10 @@ class F32BatchedStep:
                 g = self._gemm(dz.data_ptr(), s.A[l].data_ptr(), dst, Nout, Kin, E,
                                1, Nout, Kin, 1, Kin, F32B_ATOMIC, splits=sp)
                 self._run([g], sh)
-            if net.off_b[l] >= 0:
+            if net.off_b[l] >= 0 and self.colsum_part is not None:
+                native.check(L.st_f32b_colsum_det(dz.data_ptr(), Nout, E, Nout, out.data_ptr() + 4 * net.off_b[l],
+                                                  self.colsum_part.data_ptr(), None, sh), "st_f32b_colsum_det")
+            elif net.off_b[l] >= 0:
                 native.check(L.st_f32b_colsum(dz.data_ptr(), Nout, E, Nout, out.data_ptr() + 4 * net.off_b[l], sh),
                              "st_f32b_colsum")
             if l > 0:

@@ -122,6 +122,18 @@ def tr_random_walk(E: int, T: int, start: float, vol: float, seed: int) -> np.nd
     return random_walk(T, start, vol, seed, n_series=E).astype(np.float32)
 
 
+class _SplitStepGraph:
+    """One synchronous-DP step as two captured graphs around an eager host-side all-reduce (gloo)."""
+
+    def __init__(self, pre, post, all_reduce, grad):
+        self.pre, self.post, self.all_reduce, self.grad = pre, post, all_reduce, grad
+
+    def replay(self) -> None:
+        self.pre.replay()
+        self.all_reduce(self.grad)
+        self.post.replay()
+
+
 class VectorEngine:
     """E envs + learner on one device; optionally one rank of a DP group."""
 
@@ -411,18 +423,35 @@ class VectorEngine:
             return
         L = native.lib()
         sh = native.stream_handle()
-        self._launch_qstep(L, sh)
         if self.world_size > 1 and self.cfg.engine.dp_overlap:
+            self._launch_qstep(L, sh)
             self._overlap_step(L, sh)
+            self._target_sync(L, sh)
         elif self.world_size > 1:
-            self._op.mode = 1
-            native.check(L.st_reduce_optim(self._op, sh), "reduce")
+            self._dp_pre()
             self._sync.all_reduce(self.grad)
-            self._op.mode = 2
-            native.check(L.st_reduce_optim(self._op, sh), "update")
+            self._dp_post()
         else:
+            self._launch_qstep(L, sh)
             self._op.mode = 0
             native.check(L.st_reduce_optim(self._op, sh), "reduce_optim")
+            self._target_sync(L, sh)
+
+    def _dp_pre(self) -> None:
+        """Synchronous DP, the part before the gradient all-reduce: step kernel + slab reduction."""
+        L, sh = native.lib(), native.stream_handle()
+        self._launch_qstep(L, sh)
+        self._op.mode = 1
+        native.check(L.st_reduce_optim(self._op, sh), "reduce")
+
+    def _dp_post(self) -> None:
+        """Synchronous DP, the part after the all-reduce: optimizer on the reduced gradient (+ target copy)."""
+        L, sh = native.lib(), native.stream_handle()
+        self._op.mode = 2
+        native.check(L.st_reduce_optim(self._op, sh), "update")
+        self._target_sync(L, sh)
+
+    def _target_sync(self, L, sh) -> None:
         if self._qtp is not None:
             # after the counter advanced: copy when ctrl[0] % target_every == 0 (the torch engine's
             # (step + 1) % target_every); under overlapped DP the copy follows the delayed update
@@ -662,8 +691,9 @@ class VectorEngine:
         if self.world_size > 1:
             import torch.distributed as dist
 
-            if dist.get_backend(self.group) != "nccl":   # gloo collectives run on the host: not capturable
-                return False
+            if dist.get_backend(self.group) != "nccl":
+                # gloo collectives run on the host and cannot be captured: two graphs around the all-reduce
+                return self._capture_split(warmup)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -688,6 +718,29 @@ class VectorEngine:
             self.step_count += 1
             if self._graph_k is not None:
                 self.prime_graph(prime_reps)
+        return True
+
+    def _capture_split(self, warmup: int) -> bool:
+        """Synchronous DP over a host-side collective (gloo rehearsal groups): the step as two HIP graphs --
+        step kernel + slab reduction, then optimizer (+ target copy) -- with the eager all-reduce of the flat
+        gradient between the replays.  ``step`` replays the pair; no multi-step graph (every step holds a
+        collective).  Every rank captures the same two graphs, so the collective sequence is unchanged."""
+        if self.kernel != "bf16_fused":
+            return False
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._native_step()
+                self.step_count += 1
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        pre, post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(pre, capture_error_mode=_CAPTURE_MODE):
+            self._dp_pre()
+        with torch.cuda.graph(post, capture_error_mode=_CAPTURE_MODE):
+            self._dp_post()
+        self._graph = _SplitStepGraph(pre, post, self._sync.all_reduce, self.grad)
+        self._graph_k = None
         return True
 
     def prime_graph(self, min_reps: int = 1, max_reps: int = 40, tol: float = 0.015) -> int:

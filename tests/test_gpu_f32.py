@@ -345,6 +345,8 @@ def test_fp32_batched_split_partials_match_atomics(dev, monkeypatch):
         grads[mode] = eng.native_grad().detach().cpu().clone()
         net, pd = eng._f32.net, eng.layout.pdims
         wsl = [slice(net.off_w[l], net.off_w[l] + pd[l + 1] * pd[l]) for l in range(eng.layout.n_layers)]
-    for w in wsl:   # the weight gradients are bit-reproducible (the bias column sums still use atomics)
+    for w in wsl:
         assert torch.equal(grads["partial"][w], grads["partial2"][w])
+    # and the bias column sums (per-block partials + ordered sum): the whole gradient is bit-reproducible
+    assert torch.equal(grads["partial"], grads["partial2"])
     assert _rel(grads["partial"], grads["atomic"]) < 1e-5, _rel(grads["partial"], grads["atomic"])

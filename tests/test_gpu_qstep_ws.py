@@ -83,7 +83,10 @@ def test_ws_matches_oracle(native_built, kernel, compat, E, grid):
     _, _, info0 = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=True)
     mism = (info0["actions"].cpu() != acts).float().mean().item()
     print(f"[meas] oracle {kernel} compat={compat} E={E} grid={grid} action_mismatch={mism:.4f}")
-    assert mism <= 0.05, f"action mismatch rate {mism}"
+    # bounds ~2x the largest measured value over these cases (profiles/r5_ws_numerics.md): relative errors
+    # <= 1.7e-3 vs the bf16-emulating oracle, <= 1.65e-2 vs pure fp32; actions: 0 mismatches measured, 1 %
+    # left for near-ties of Q (the fp32 summation order inside the MFMAs differs)
+    assert mism <= 0.01, f"action mismatch rate {mism}"
     ns, g_ref, info = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=True,
                               forced_actions=acts)
     assert torch.equal(info["reward"], rew)
@@ -94,14 +97,14 @@ def test_ws_matches_oracle(native_built, kernel, compat, E, grid):
         gw, rw = L.w(grad, l), L.w(g_ref, l)
         print(f"[meas] oracle {kernel} compat={compat} E={E} layer={l} w_rel_bf16={_rel(gw, rw):.3e}"
               + (f" b_rel_bf16={_rel(L.b(grad, l), L.b(g_ref, l)):.3e}" if l > 0 else ""))
-        assert _rel(gw, rw) < 3e-2, (l, _rel(gw, rw))
+        assert _rel(gw, rw) < 5e-3, (l, _rel(gw, rw))
         if l > 0:
-            assert _rel(L.b(grad, l), L.b(g_ref, l)) < 3e-2, l
+            assert _rel(L.b(grad, l), L.b(g_ref, l)) < 5e-3, l
     # and vs the pure fp32 oracle (no bf16 emulation, same actions): the bound the wide kernel meets
     _, g32, _ = _oracle(cfg, prices, st0, params, eng.layout, 5, eng.loss_coef, emulate_bf16=False,
                         forced_actions=acts)
     print(f"[meas] oracle {kernel} compat={compat} E={E} grad_rel_fp32={_rel(grad, g32):.3e}")
-    assert _rel(grad, g32) < 0.1, _rel(grad, g32)
+    assert _rel(grad, g32) < 3.5e-2, _rel(grad, g32)
     # statistics slab: reward sum and the number of explore draws
     st = eng.stat_slab.sum(0).cpu()
     assert abs(float(st[0]) - float(info["reward"].sum())) < 1e-3 + 1e-4 * float(info["reward"].abs().sum())
@@ -215,10 +218,53 @@ def test_ws_trajectory_matches_torch_oracle(native_built, kernel, compat):
                 for k in ("budget", "shares", "value", "pos", "episodes"):
                     assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (t, k)
     d = eng.params.detach().cpu() - p0
-    for emulate, tol in ((True, 3e-2), (False, 0.1)):
+    for emulate, tol in ((True, 5e-4), (False, 5e-3)):   # measured 2.0e-4 / 2.2e-3
         dr = refs[emulate].params - p0
         print(f"[meas] trajectory {kernel} compat={compat} emulate_bf16={emulate} dparam_rel={_rel(d, dr):.3e}")
         assert _rel(d, dr) < tol, (emulate, _rel(d, dr))
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_ws_adam_trajectory_matches_torch_oracle(native_built, kernel):
+    """Three eager steps with the flagship's Adam against the oracle engine driven with the kernel's actions.
+    Adam's first steps move each parameter by ~lr * sign(m): elements whose accumulated gradient is near zero
+    can flip, so the check is on the optimizer moments (linear / quadratic in the gradients) and on the
+    parameter change of the elements with a clear gradient (|m| above its median)."""
+    from sharetrade.models import qnet as qn
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 2048
+    cfg = _cfg(False, kernel)
+    cfg.agent.epsilon = 0.6
+    assert cfg.agent.optimizer == "adam"
+    prices = _prices(E, T=320, seed=23)
+    dev = torch.device("cuda", 0)
+    eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+    eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 5 % 100)
+    ref = VectorEngine(cfg, prices=prices, device=torch.device("cpu"), envs=E, backend="torch")
+    ref.params.copy_(eng.params.detach().cpu())
+    p0 = eng.params.detach().cpu().clone()
+    a = cfg.agent
+    for t in range(3):
+        st0 = eng.state.clone().to("cpu")
+        eng.step()
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        acts = eng.actions_out.cpu().clone()
+        ns, g, info = _oracle(cfg, prices, st0, ref.params, ref.layout, t, eng.loss_coef, emulate_bf16=True,
+                              forced_actions=acts)
+        qn.optimizer_step_ref(ref.params, g, ref.opt, ref.mask, a.lr, a.adam_betas, a.adam_eps)
+        assert torch.equal(info["reward"], eng.rewards_out.cpu()), t
+        for k in ("budget", "shares", "value", "pos"):
+            assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (t, k)
+    m, v = eng.opt.s1.cpu(), eng.opt.s2.cpu()
+    mr, vr = ref.opt.s1, ref.opt.s2
+    clear = mr.abs() > mr.abs()[ref.mask.bool()].median()
+    d, dr = (eng.params.detach().cpu() - p0)[clear], (ref.params - p0)[clear]
+    print(f"[meas] adam trajectory {kernel} m_rel={_rel(m, mr):.3e} v_rel={_rel(v, vr):.3e} "
+          f"dparam_rel(clear)={_rel(d, dr):.3e} sign_flips={(torch.sign(d) != torch.sign(dr)).float().mean():.4f}")
+    assert _rel(m, mr) < 5e-3 and _rel(v, vr) < 1e-2, (_rel(m, mr), _rel(v, vr))
+    assert _rel(d, dr) < 5e-2, _rel(d, dr)
 
 
 @pytest.mark.parametrize("E,grid", [(64 * 48, 16), (64 * 100, 8), (64 * 13, 8), (64 * 1000, 16), (64 * 2048, 256)])

@@ -67,3 +67,23 @@ def test_double_dqn_needs_a_target_net():
     cfg.agent.double_dqn = True
     with pytest.raises(ValueError):
         VectorEngine(cfg, device=torch.device("cpu"), envs=64, backend="torch")
+
+
+def test_f32_deterministic_auto_policy(monkeypatch):
+    """engine.f32_deterministic='auto': ordered partial sums (bit-reproducible) for DP ranks and for the
+    reference's decision semantics; fp32 atomics for a single 'intended' process; the env override wins."""
+    from sharetrade.ops.mlp_f32 import f32_deterministic
+
+    monkeypatch.delenv("SHARETRADE_F32_SPLIT_PARTIAL", raising=False)
+    ref, intended = preset_config("reference_compat"), preset_config("intended")
+    assert f32_deterministic(ref, 1) and f32_deterministic(intended, 2) and not f32_deterministic(intended, 1)
+    intended.engine.f32_deterministic = "on"
+    assert f32_deterministic(intended, 1)
+    ref.engine.f32_deterministic = "off"
+    assert not f32_deterministic(ref, 4)
+    monkeypatch.setenv("SHARETRADE_F32_SPLIT_PARTIAL", "1")
+    assert f32_deterministic(ref, 4)
+    intended.engine.f32_deterministic = "sometimes"
+    monkeypatch.delenv("SHARETRADE_F32_SPLIT_PARTIAL")
+    with pytest.raises(ValueError):
+        f32_deterministic(intended, 1)
