@@ -78,7 +78,7 @@ constexpr int C = 64;            // envs per chunk
 constexpr int INP = 224, HP = 128, KX = 208, HWIN = 201;
 constexpr int XS = 216;          // row stride (bf16) of the X / X' images
 constexpr int HS = 136;          // row stride (bf16) of the 128-wide images (H1, H1', dZ2, W1^T)
-constexpr int NXB = 6, NH1 = 4, NDZ = 2;
+constexpr int NXB = 6, NH1 = 5, NDZ = 3;
 constexpr int NJOB = TE * 26;    // feature jobs per tile: (env, group of 8 input slots)
 constexpr int DRAIN = 4;         // iterations past the last tile (the second half of its pair)
 
@@ -413,51 +413,23 @@ __global__ void __launch_bounds__(NT, 1) qstep_pipe_kernel(QStepParams p) {
       }
       // ------------------------------------------------ layer 2 + output share of Q(x), tile it - 1
       f4v qp, qpp;
-      layer2(oH1 + ((it - 1 + 4 * NH1) % NH1) * H_BYTES, h2N, qp);
+      layer2(oH1 + ((it + NH1 - 1) % NH1) * H_BYTES, h2N, qp);
       // ------------------------------------------------ layer 2 + output share of Q(x'), tile it - 2
       s4v h2n;
       layer2(oH1P, h2n, qpp);
       // ------------------------------------------------ dZ1 = (dZ2 W1) * [H1 > 0] of this wave's units, tile it - 3
       {
-        const bf16_t* dr = bf(oDZ + ((it - 3 + 4 * NDZ) % NDZ) * H_BYTES) + l16 * HS + 8 * g4;
+        const bf16_t* dr = bf(oDZ + ((it + NDZ - 3) % NDZ) * H_BYTES) + l16 * HS + 8 * g4;
         const int wrow = 16 * w + l16;
         f4v c = zero4();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
           c = mfma32(lds_ld8(dr + 32 * ks), lds_ld8(bf(oW1T) + w1t_off(wrow, 32 * ks + 8 * g4)), c);
         // c: lane (unit l16, g4)[j] = dZ1[16 w + l16][env 4 g4 + j]; the mask: H1 of the same (env, unit)
-        const s4v hm = lds_tr4(bf(oH1 + ((it - 3 + 4 * NH1) % NH1) * H_BYTES) + (4 * g4 + (l16 >> 2)) * HS +
+        const s4v hm = lds_tr4(bf(oH1 + ((it + 2 * NH1 - 3) % NH1) * H_BYTES) + (4 * g4 + (l16 >> 2)) * HS +
                                16 * w + 4 * (l16 & 3));
         dzN = mask_pk(c, hm);
       }
-      // ------------------------------------------------ weight gradients of the pair (tb - 1, tb): first half
-      // with the dZ1 of tb (this phase), second half one iteration later
-    {
-      const int tb1 = it - 3, tb2 = it - 4;
-      if ((tb1 & 1) && tb1 >= 1 && tb1 < ntile) {
-        // first half (dZ1 of tb is this iteration's): dW1 = dZ2^T H1 of this wave's u2 rows, dW0 slot groups 0..2
-        const int ta = tb1 - 1, tb = tb1;
-        const s8v a0 = cat8(dza, dzN);
-        const s8v a1 = trp(oDZ + (ta % NDZ) * H_BYTES, oDZ + (tb % NDZ) * H_BYTES, HS, 16 * w);
-        const int ha = oH1 + (ta % NH1) * H_BYTES, hb = oH1 + (tb % NH1) * H_BYTES;
-#pragma unroll
-        for (int n = 0; n < 8; ++n) gW1[n] = mfma32(a1, trp(ha, hb, HS, 16 * n), gW1[n]);
-        const int xa = oXB + (ta % NXB) * X_BYTES, xb = oXB + (tb % NXB) * X_BYTES;
-#pragma unroll
-        for (int n = 0; n < 3; ++n) gW0[n] = mfma32(a0, trp(xa, xb, XS, 16 * n), gW0[n]);
-        dzb = dzN;
-      } else if ((tb2 & 1) && tb2 >= 1 && tb2 < ntile) {
-        // second half: dW0 slot groups 3..12
-        const int ta = tb2 - 1, tb = tb2;
-        const s8v a0 = cat8(dza, dzb);
-        const int xa = oXB + (ta % NXB) * X_BYTES, xb = oXB + (tb % NXB) * X_BYTES;
-#pragma unroll
-        for (int n = 3; n < 13; ++n) gW0[n] = mfma32(a0, trp(xa, xb, XS, 16 * n), gW0[n]);
-        dza = dzN;   // (this iteration's dZ1 is tile tb2 + 1: the next pair's first)
-      } else {
-        dza = dzN;   // pipeline edges: the first tile's dZ1
-      }
-    }
       // stores: lane group 0 holds the partial output sums; feature lanes their slot groups
       *reinterpret_cast<f4v*>(g4 == 0 ? smem + oQP + (w * TE + l16) * 16 : sink + l16 * 16) = qp;
       *reinterpret_cast<f4v*>(g4 == 0 ? smem + oQPP + (w * TE + l16) * 16 : sink + l16 * 16) = qpp;
@@ -618,6 +590,33 @@ __global__ void __launch_bounds__(NT, 1) qstep_pipe_kernel(QStepParams p) {
     jcur = jn1;
     jn1 = jn2;
     if (jvalid && it + 3 < ntile) jn2 = load_pos(it + 3);
+    // ------------------------------------------------ weight gradients of the pair (tb - 1, tb)
+    {
+      const int tb1 = it - 3, tb2 = it - 4;
+      if ((tb1 & 1) && tb1 >= 1 && tb1 < ntile) {
+        // first half (dZ1 of tb is this iteration's): dW1 = dZ2^T H1 of this wave's u2 rows, dW0 slot groups 0..2
+        const int ta = tb1 - 1, tb = tb1;
+        const s8v a0 = cat8(dza, dzN);
+        const s8v a1 = trp(oDZ + (ta % NDZ) * H_BYTES, oDZ + (tb % NDZ) * H_BYTES, HS, 16 * w);
+        const int ha = oH1 + (ta % NH1) * H_BYTES, hb = oH1 + (tb % NH1) * H_BYTES;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) gW1[n] = mfma32(a1, trp(ha, hb, HS, 16 * n), gW1[n]);
+        const int xa = oXB + (ta % NXB) * X_BYTES, xb = oXB + (tb % NXB) * X_BYTES;
+#pragma unroll
+        for (int n = 0; n < 3; ++n) gW0[n] = mfma32(a0, trp(xa, xb, XS, 16 * n), gW0[n]);
+        dzb = dzN;
+      } else if ((tb2 & 1) && tb2 >= 1 && tb2 < ntile) {
+        // second half: dW0 slot groups 3..12
+        const int ta = tb2 - 1, tb = tb2;
+        const s8v a0 = cat8(dza, dzb);
+        const int xa = oXB + (ta % NXB) * X_BYTES, xb = oXB + (tb % NXB) * X_BYTES;
+#pragma unroll
+        for (int n = 3; n < 13; ++n) gW0[n] = mfma32(a0, trp(xa, xb, XS, 16 * n), gW0[n]);
+        dza = dzN;   // (this iteration's dZ1 is tile tb2 + 1: the next pair's first)
+      } else {
+        dza = dzN;   // pipeline edges: the first tile's dZ1
+      }
+    }
     PIPE_STAMP(5);
     // ------------------------------------------------ the partner's result; Q(x') layer-1 tail of it - 1; dZ2 of it - 2
     if (producer) {
@@ -633,7 +632,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_pipe_kernel(QStepParams p) {
       const s4v w2t = lds_ld4(g4 == 0 ? bf(oW2T) + (16 * w + l16) * 4 : bf(oZERO));
       const f4v zt = mfma16(w2t, dqf, zero4());   // lane (env l16, g4)[j]: unit 16 w + 4 g4 + j (exact products)
       const s4v dz = mask_pk(zt, h2A);
-      *reinterpret_cast<s4v*>(bf(oDZ + ((it - 2 + 4 * NDZ) % NDZ) * H_BYTES) + l16 * HS + 16 * w + 4 * g4) = dz;
+      *reinterpret_cast<s4v*>(bf(oDZ + ((it + NDZ - 2) % NDZ) * H_BYTES) + l16 * HS + 16 * w + 4 * g4) = dz;
 #pragma unroll
       for (int j = 0; j < 4; ++j) gB1[j] += bf2f((bf16_t)dz[j]);
       // dW2[a][u2] += dQ[a][env] H2[u2][env]: both operands transposed through this wave's scratch

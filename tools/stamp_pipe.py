@@ -13,14 +13,10 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-# (start stamp, end stamp, name); stamp 8 = the next iteration's stamp 0
-SEGMENTS = [(0, 2, "P0: features, layer 2 of Q(x) and Q(x'), dZ1, pair weight gradients"),
-            (2, 3, "P0 barrier"),
-            (3, 4, "P1: env step (waves 0-3) / TD (waves 4-7) beside layer 1"),
-            (4, 5, "P1: TD record, env write-back, statistics, next-tile DMA issue"),
-            (5, 6, "P1: partner wait, Q(x') layer-1 tail, dZ2 + dW2"),
-            (6, 7, "P1: counted s_waitcnt vmcnt (previous DMA landed)"),
-            (7, 8, "P1 barrier")]
+SEGMENTS = ["P0: features (staged window -> X, X', env record)", "P0: layer 2 Q(x), layer 2 Q(x'), dZ1",
+            "P0 barrier", "P1: env step + TD (waves 0-3)", "P1: stage DMA, layer 1, pair weight gradients",
+            "P1: partner waits, Q(x') layer-1 tail, dZ2 + dW2", "P1: s_waitcnt vmcnt(0) (DMA + stores landed)",
+            "P1 barrier"]
 
 
 def main():
@@ -60,12 +56,17 @@ def main():
     lines = [f"# pipe step kernel: workgroup 0 ({a.envs} envs, grid {eng.grid}, {4 * nmy} tiles; s_memtime ticks per "
              f"iteration, steady-state iterations {lo}..{hi - 1}; stamped step {ev[0].elapsed_time(ev[1]):.3f} ms)\n",
              "| segment | wave 0 (producer) | wave 4 (partner) |", "|---|---|---|"]
-    for a0, a1, name in SEGMENTS:
+    for wv, base in ((0, 0), (4, 8)):
+        pass
+    for i, name in enumerate(SEGMENTS):
         vals = []
         for base in (0, 8):
             b = s[lo:hi, base:base + 8]
-            end = s[lo + 1:hi + 1, base] if a1 == 8 else b[:, a1]
-            vals.append(float((end - b[:, a0]).mean()))
+            if i < 7:
+                d = b[:, i + 1] - b[:, i]
+            else:
+                d = s[lo + 1:hi + 1, base] - b[:, 7]
+            vals.append(float(d.mean()))
         lines.append(f"| {name} | {vals[0]:.0f} | {vals[1]:.0f} |")
     it = float((s[lo + 1:hi + 1, 0] - s[lo:hi, 0]).mean())
     lines.append(f"| iteration (stamp 0 -> stamp 0) | {it:.0f} | |")
