@@ -63,6 +63,15 @@ ST_DEV s4v relu_bf(f4v v) {
   s4v r = {a[0], a[1], b[0], b[1]};
   return r;
 }
+// a 16-wide k-step as a 16x16x32 MFMA with the upper halves of both operands zero (same cost on gfx950).  Not
+// v_mfma_f32_16x16x16_bf16: reading a 16x16x32 result as its accumulator needs >= 4 wait states on MI355X
+// (tools/ubench/mfma_raw_gen.py), hipcc (ROCm 7.2) emitted that pair with 1 here and the 16x16x16 MFMA saw the
+// accumulator without the last 16x16x32 k-step (2 % error in QT; tools/debug/qt_colprobe.py,
+// tools/mfma_hazard_scan.py)
+ST_DEV f4v mfma32z(s4v a, s4v b, f4v c) {
+  const s4v z = {0, 0, 0, 0};
+  return mfma32(cat8(a, z), cat8(b, z), c);
+}
 ST_DEV float4 ldu4(const float* a) {
   float4 v;
   __builtin_memcpy(&v, a, sizeof(v));
@@ -138,7 +147,7 @@ __global__ void __launch_bounds__(NT, 1) qtarget_kernel(QTargetParams p) {
       const bf16_t* wr = W0 + (16 * i + l16) * KX + 8 * g4;
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) acc = mfma32(lds_ld8(wr + 32 * ks), X[ks], acc);
-      a1[i] = mfma16(lds_ld4(W0 + (16 * i + l16) * KX + 192 + 4 * g4), Xw, acc);
+      a1[i] = mfma32z(lds_ld4(W0 + (16 * i + l16) * KX + 192 + 4 * g4), Xw, acc);
     }
     // the three candidates: Buy, Sell, Hold from (bd, sd) -- the env's own transition
     const float bd = p.compat_env ? p.b0 : bud;
@@ -154,8 +163,8 @@ __global__ void __launch_bounds__(NT, 1) qtarget_kernel(QTargetParams p) {
       s8v H1[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const f4v z0 = mfma16(lds_ld4(W0 + (16 * (2 * ks) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks]);
-        const f4v z1 = mfma16(lds_ld4(W0 + (16 * (2 * ks + 1) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks + 1]);
+        const f4v z0 = mfma32z(lds_ld4(W0 + (16 * (2 * ks) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks]);
+        const f4v z1 = mfma32z(lds_ld4(W0 + (16 * (2 * ks + 1) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks + 1]);
         H1[ks] = cat8(relu_bf(z0), relu_bf(z1));
       }
       s8v H2[4];

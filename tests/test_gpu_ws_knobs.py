@@ -73,7 +73,7 @@ def test_qtarget_values_match_forward(native_built, compat):
         ref, _, _ = qn.forward(pt, eng.layout, info["x_next"], cfg.model.output_relu, True)
         r = _rel(qt[:, act, :3], ref[:, :3])
         worst = max(worst, r)
-        assert r < 1e-2, (act, r)
+        assert r < 3e-4, (act, r)          # measured <= 1.4e-4 (profiles/r5_ws_numerics.md)
     print(f"[meas] qtarget compat={compat} worst_rel={worst:.3e}")
 
 
@@ -108,7 +108,7 @@ def test_ws_knobs_one_step_matches_oracle(native_built, knobs, compat):
     kw = _oracle_kw(eng, cfg, pt, step)
     _, _, info0 = _oracle(cfg, prices, st0, params, eng.layout, step, eng.loss_coef, emulate_bf16=True, **kw)
     mism = (info0["actions"] != acts).float().mean().item()
-    assert mism <= 0.05, mism
+    assert mism <= 0.01, mism            # measured 0 in every case
     ns, g_ref, info = _oracle(cfg, prices, st0, params, eng.layout, step, eng.loss_coef, emulate_bf16=True,
                               forced_actions=acts, **kw)
     assert torch.equal(info["reward"], eng.rewards_out.cpu())
@@ -116,7 +116,7 @@ def test_ws_knobs_one_step_matches_oracle(native_built, knobs, compat):
         assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), k
     r = _rel(grad, g_ref)
     print(f"[meas] knobs {knobs} compat={compat} action_mismatch={mism:.4f} grad_rel_bf16={r:.3e}")
-    assert r < 3e-2, r
+    assert r < 7e-4, r                   # measured <= 3.3e-4
     if knobs.get("ramp_mode") == "global":
         # the ramp follows the step count: the exploit fraction differs from the per-position ramp's
         _, _, info_pos = _oracle(cfg, prices, st0, params, eng.layout, step, eng.loss_coef, emulate_bf16=True,
@@ -163,7 +163,7 @@ def test_ws_target_trajectory_matches_oracle(native_built):
             assert torch.equal(getattr(ns, k), getattr(eng.state, k).cpu()), (t, k)
     d, dr = eng.params.detach().cpu() - p0, ref.params - p0
     print(f"[meas] target trajectory dparam_rel={_rel(d, dr):.3e}")
-    assert _rel(d, dr) < 3e-2, _rel(d, dr)
+    assert _rel(d, dr) < 5e-4, _rel(d, dr)   # measured 1.9e-4
 
 
 def test_ws_target_captured_graph(native_built):
