@@ -73,6 +73,11 @@ def main() -> int:
     ap.add_argument("--no-episode", action="store_true",
                     help="skip the untimed full-episode returns after the timed window (greedy learned policy, "
                          "greedy random-init policy, buy-and-hold, online learned episode, random policy)")
+    ap.add_argument("--target-every", type=int, default=0,
+                    help="learning knob: target network refreshed every N steps (csrc/qtarget.hip pass per step)")
+    ap.add_argument("--double-dqn", action="store_true", help="learning knob: Double DQN (needs --target-every)")
+    ap.add_argument("--reward-scale", type=float, default=1.0, help="learning knob: reward multiplier in the TD target")
+    ap.add_argument("--ramp-mode", default="position", help="learning knob: exploit ramp over 'position' | 'global'")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -121,6 +126,8 @@ def main() -> int:
     cfg.engine.chunk_schedule = args.chunk_schedule
     if args.graph_steps:
         cfg.engine.graph_steps = args.graph_steps
+    cfg.agent.target_every, cfg.agent.double_dqn = args.target_every, bool(args.double_dqn)
+    cfg.agent.reward_scale, cfg.agent.ramp_mode = args.reward_scale, args.ramp_mode
     eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
     eng.sync_params_from(0)
     init_params = None if args.no_episode else eng.params.detach().clone()   # the frozen-init baseline
@@ -246,6 +253,8 @@ def main() -> int:
                 "kernel_chunk": eng.chunk,
                 "step_kernel": getattr(eng, "step_kernel", None),
                 "chunk_schedule": getattr(eng, "chunk_schedule", "static"),
+                "learning_knobs": {"target_every": cfg.agent.target_every, "double_dqn": cfg.agent.double_dqn,
+                                   "reward_scale": cfg.agent.reward_scale, "ramp_mode": cfg.agent.ramp_mode},
             },
             "graph_prime_steps": prime_steps,
             "world_size": world,

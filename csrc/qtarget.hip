@@ -9,7 +9,7 @@
 // output layer.  QT[e][a][0..2] = Q_target(x' after action a)[0..2] (output ReLU applied when the model has
 // it); the step kernel reads the row of the action it takes.
 //
-// MFMA layout (one 16-env tile per wave, 4 waves per workgroup, grid-stride over tiles): the target weights
+// MFMA layout (TPW 16-env tiles per wave, NWV waves per workgroup, grid-stride): the target weights
 // are converted to bf16 into LDS once per workgroup (fp32 master copy of the target net: no second bf16
 // image to keep in sync); x' features are built in registers as B operands (the ws kernel's slot order: the
 // last 16-wide k-step carries budget, shares, 1, fxn(vnew) in lane group 0); hidden activations stay in
@@ -21,7 +21,7 @@
 namespace st {
 namespace qtgt {
 
-constexpr int NW = 4, NT = 64 * NW;
+
 constexpr int INP = 224, HP = 128, KX = 208, HWIN = 201;
 
 constexpr int oW0 = 0;                         // W0 [128][208] bf16 (slot order)
@@ -89,8 +89,11 @@ struct QTargetParams {
   int s0, compat_env, output_relu, feat_mode;
 };
 
-template <int FEAT>
-__global__ void __launch_bounds__(NT, 1) qtarget_kernel(QTargetParams p) {
+// TPW 16-env tiles per wave (each weight fragment read from LDS feeds TPW MFMAs), NWV waves per workgroup (one
+// workgroup per CU: the weight images take 87.5 KB of LDS)
+template <int FEAT, int TPW, int NWV>
+__global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
+  constexpr int NW = NWV, NT = 64 * NWV;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* W0 = reinterpret_cast<bf16_t*>(smem + oW0);
   bf16_t* W1 = reinterpret_cast<bf16_t*>(smem + oW1);
@@ -115,84 +118,128 @@ __global__ void __launch_bounds__(NT, 1) qtarget_kernel(QTargetParams p) {
   const float b2v[3] = {p.wt[p.off_b2], p.wt[p.off_b2 + 1], p.wt[p.off_b2 + 2]};
   const size_t E = (size_t)p.E;
   const int ntiles = p.E / 16;
-  for (int t = blockIdx.x * NW + w; t < ntiles; t += gridDim.x * NW) {
-    const int e = 16 * t + l16;
-    const int pos = p.env[ER_POS * E + e];
-    const float bud = __int_as_float(p.env[ER_BUDGET * E + e]);
-    const int sh = p.env[ER_SHARES * E + e];
-    const int pc = min(max(pos, 0), p.T - HWIN - 1);
-    const float* b = p.prices4 + (size_t)e * p.T4 + (size_t)pc;
-    const float vnew = b[201];
-    const float invn = FEAT ? __fdiv_rn(1.0f, vnew) : 0.f;
-    auto fxn = [&](float v) { return FEAT ? __fmaf_rn(v, invn, -1.0f) : v; };
-    // x' window B operands: k-step ks, lane group g4: x'[32 ks + 8 g4 + j] = p[pos + 1 + 32 ks + 8 g4 + j]
-    s8v X[6];
+  // the tail A fragments (input slots 192..207 of every unit tile): read once
+  s4v w0t[8];
 #pragma unroll
-    for (int ks = 0; ks < 6; ++ks) {
-      const float4 u = ldu4(b + 1 + 32 * ks + 8 * g4), v = ldu4(b + 5 + 32 * ks + 8 * g4);
-      X[ks] = cat8(pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w)), pk4(fxn(v.x), fxn(v.y), fxn(v.z), fxn(v.w)));
+  for (int i = 0; i < 8; ++i) w0t[i] = lds_ld4(W0 + (16 * i + l16) * KX + 192 + 4 * g4);
+  for (int t0 = (blockIdx.x * NW + w) * TPW; t0 < ntiles; t0 += gridDim.x * NW * TPW) {
+    // an opaque zero offset per iteration: the weight-fragment LDS reads are loop-invariant, and hoisted out of
+    // the loops they would pin ~400 registers (W0 / W1 / W2 fragments) and spill
+    int zo = 0;
+    asm volatile("" : "+s"(zo));
+    const bf16_t* W0i = W0 + zo;
+    // ---------------------------------------------------------------- x' features of the wave's TPW env tiles
+    float vnew[TPW], invn[TPW], bd[TPW];
+    int sd[TPW];
+    s8v X[TPW][6];
+    s4v Xw[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+      const int e = 16 * (t0 + q) + l16;
+      const int pos = p.env[ER_POS * E + e];
+      const float bud = __int_as_float(p.env[ER_BUDGET * E + e]);
+      const int sh = p.env[ER_SHARES * E + e];
+      const int pc = min(max(pos, 0), p.T - HWIN - 1);
+      const float* b = p.prices4 + (size_t)e * p.T4 + (size_t)pc;
+      vnew[q] = b[201];
+      invn[q] = FEAT ? __fdiv_rn(1.0f, vnew[q]) : 0.f;
+      const float iv = invn[q];
+      auto fxn = [&](float v) { return FEAT ? __fmaf_rn(v, iv, -1.0f) : v; };
+      // x' window B operands: k-step ks, lane group g4: x'[32 ks + 8 g4 + j] = p[pos + 1 + 32 ks + 8 g4 + j]
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const float4 u = ldu4(b + 1 + 32 * ks + 8 * g4), v = ldu4(b + 5 + 32 * ks + 8 * g4);
+        X[q][ks] = cat8(pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w)), pk4(fxn(v.x), fxn(v.y), fxn(v.z), fxn(v.w)));
+      }
+      // the last 16-wide k-step: lane groups 1, 2 window columns 192..199 of x' (p[pos + 193 ..]); group 0 the
+      // candidate's tail (below); group 3 pads
+      Xw[q] = s4v{0, 0, 0, 0};
+      if (g4 == 1 || g4 == 2) {
+        const float4 u = ldu4(b + 193 + 4 * (g4 - 1));
+        Xw[q] = pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w));
+      }
+      // the three candidates: Buy, Sell, Hold from (bd, sd) -- the env's own transition
+      bd[q] = p.compat_env ? p.b0 : bud;
+      sd[q] = p.compat_env ? p.s0 : sh;
     }
-    // the last 16-wide k-step: lane groups 1, 2 window columns 192..199 of x' (p[pos + 193 ..]); group 0 the
-    // candidate's tail (below); group 3 pads
-    s4v Xw = {0, 0, 0, 0};
-    if (g4 == 1 || g4 == 2) {
-      const float4 u = ldu4(b + 193 + 4 * (g4 - 1));
-      Xw = pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w));
-    }
-    // layer 1 over the window (shared by the candidates)
-    f4v a1[8];
+    // ---------------------------------------------------------------- layer 1 over the window (shared by the
+    // candidates): one W0 fragment read per (unit tile, k-step) feeds the TPW env tiles' MFMAs
+    f4v a1[TPW][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      f4v acc = {0.f, 0.f, 0.f, 0.f};
-      const bf16_t* wr = W0 + (16 * i + l16) * KX + 8 * g4;
 #pragma unroll
-      for (int ks = 0; ks < 6; ++ks) acc = mfma32(lds_ld8(wr + 32 * ks), X[ks], acc);
-      a1[i] = mfma32z(lds_ld4(W0 + (16 * i + l16) * KX + 192 + 4 * g4), Xw, acc);
+      for (int q = 0; q < TPW; ++q) a1[q][i] = f4v{0.f, 0.f, 0.f, 0.f};
+      const bf16_t* wr = W0i + (16 * i + l16) * KX + 8 * g4;
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const s8v A = lds_ld8(wr + 32 * ks);
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) a1[q][i] = mfma32(A, X[q][ks], a1[q][i]);
+      }
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) a1[q][i] = mfma32z(w0t[i], Xw[q], a1[q][i]);
     }
-    // the three candidates: Buy, Sell, Hold from (bd, sd) -- the env's own transition
-    const float bd = p.compat_env ? p.b0 : bud;
-    const int sd = p.compat_env ? p.s0 : sh;
-    const float fvn = FEAT ? __fmaf_rn(vnew, invn, -1.0f) : vnew;
 #pragma unroll 1
     for (int a = 0; a < 3; ++a) {
-      const bool buy = a == 0 && bd >= vnew, sell = a == 1 && sd > 0;
-      const float b2 = buy ? __fsub_rn(bd, vnew) : (sell ? __fadd_rn(bd, vnew) : bd);
-      const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
-      const s4v tl = g4 == 0 ? pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fvn)
-                             : s4v{0, 0, 0, 0};
-      s8v H1[4];
+      int za = 0;
+      asm volatile("" : "+s"(za));
+      const bf16_t* W1a = W1 + za;
+      const bf16_t* W2a = W2 + za;
+      s8v H1[TPW][4];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const f4v z0 = mfma32z(lds_ld4(W0 + (16 * (2 * ks) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks]);
-        const f4v z1 = mfma32z(lds_ld4(W0 + (16 * (2 * ks + 1) + l16) * KX + 192 + 4 * g4), tl, a1[2 * ks + 1]);
-        H1[ks] = cat8(relu_bf(z0), relu_bf(z1));
+      for (int q = 0; q < TPW; ++q) {
+        const bool buy = a == 0 && bd[q] >= vnew[q], sell = a == 1 && sd[q] > 0;
+        const float b2 = buy ? __fsub_rn(bd[q], vnew[q]) : (sell ? __fadd_rn(bd[q], vnew[q]) : bd[q]);
+        const int s2 = buy ? sd[q] + 1 : (sell ? sd[q] - 1 : sd[q]);
+        const float fvn = FEAT ? __fmaf_rn(vnew[q], invn[q], -1.0f) : vnew[q];
+        const s4v tl = g4 == 0 ? pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew[q], p.inv_b0, FEAT),
+                                     1.0f, fvn)
+                               : s4v{0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const f4v z0 = mfma32z(w0t[2 * ks], tl, a1[q][2 * ks]);
+          const f4v z1 = mfma32z(w0t[2 * ks + 1], tl, a1[q][2 * ks + 1]);
+          H1[q][ks] = cat8(relu_bf(z0), relu_bf(z1));
+        }
       }
-      s8v H2[4];
+      // layer 2: one W1 fragment read per (unit tile, k-step) for the TPW env tiles; each pair of unit tiles
+      // (one k-step of the output layer) goes into the output MFMA as soon as it is done
+      f4v qo[TPW];
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) qo[q] = f4v{0.f, 0.f, 0.f, 0.f};
+      const bf16_t* w2r = W2a + min(l16, 3) * HP + 8 * g4;
 #pragma unroll
       for (int ks2 = 0; ks2 < 4; ++ks2) {
-        f4v z[2];
+        f4v z[TPW][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int i = 2 * ks2 + h;
-          f4v acc = *reinterpret_cast<const f4v*>(B1 + 16 * i + 4 * g4);
+          const f4v bias = *reinterpret_cast<const f4v*>(B1 + 16 * i + 4 * g4);
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) acc = mfma32(lds_ld8(W1 + (16 * i + l16) * HP + 32 * ks + 8 * g4), H1[ks], acc);
-          z[h] = acc;
+          for (int q = 0; q < TPW; ++q) z[q][h] = bias;
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const s8v A = lds_ld8(W1a + (16 * i + l16) * HP + 32 * ks + 8 * g4);
+#pragma unroll
+            for (int q = 0; q < TPW; ++q) z[q][h] = mfma32(A, H1[q][ks], z[q][h]);
+          }
         }
-        H2[ks2] = cat8(relu_bf(z[0]), relu_bf(z[1]));
+        const s8v A2 = lds_ld8(w2r + 32 * ks2);
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) qo[q] = mfma32(A2, cat8(relu_bf(z[q][0]), relu_bf(z[q][1])), qo[q]);
       }
-      f4v q = {0.f, 0.f, 0.f, 0.f};
-      const bf16_t* w2r = W2 + min(l16, 3) * HP + 8 * g4;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) q = mfma32(lds_ld8(w2r + 32 * ks), H2[ks], q);
       if (g4 == 0) {
-        float o[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          o[j] = q[j] + b2v[j];
-          if (p.output_relu) o[j] = fmaxf(o[j], 0.f);
+        for (int q = 0; q < TPW; ++q) {
+          float o[3];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            o[j] = qo[q][j] + b2v[j];
+            if (p.output_relu) o[j] = fmaxf(o[j], 0.f);
+          }
+          const int e = 16 * (t0 + q) + l16;
+          *reinterpret_cast<float4*>(p.qt + ((size_t)e * 3 + a) * 4) = make_float4(o[0], o[1], o[2], 0.f);
         }
-        *reinterpret_cast<float4*>(p.qt + ((size_t)e * 3 + a) * 4) = make_float4(o[0], o[1], o[2], 0.f);
       }
     }
   }
@@ -201,20 +248,42 @@ __global__ void __launch_bounds__(NT, 1) qtarget_kernel(QTargetParams p) {
 }  // namespace qtgt
 }  // namespace st
 
-extern "C" hipError_t st_qtarget_launch(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
+namespace {
+template <int TPW, int NWV>
+hipError_t launch_qt(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
   using namespace st::qtgt;
-  if (p->E % 16 != 0 || grid < 1 || p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;
+  if (p->E % (16 * TPW) != 0) return hipErrorInvalidValue;
   static bool attr[2] = {false, false};
   const int f = p->feat_mode ? 1 : 0;
-  const void* fn = f ? (const void*)qtarget_kernel<1> : (const void*)qtarget_kernel<0>;
+  const void* fn = f ? (const void*)qtarget_kernel<1, TPW, NWV> : (const void*)qtarget_kernel<0, TPW, NWV>;
   if (!attr[f]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
     attr[f] = true;
   }
   if (f)
-    hipLaunchKernelGGL(qtarget_kernel<1>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+    hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
   else
-    hipLaunchKernelGGL(qtarget_kernel<0>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
+    hipLaunchKernelGGL((qtarget_kernel<0, TPW, NWV>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
   return hipGetLastError();
+}
+}  // namespace
+
+// variant (tiles per wave, waves per workgroup): 0 = (4, 4), 1 = (2, 8), 2 = (1, 8), 3 = (1, 16).  At 1.835 M
+// envs (tools/bench_qtarget.py, profiles/r5_ws_knobs_cost.md): 658 / 489 / 779 / 703 us -- the pass streams
+// every env's 202-price x' window from HBM (1.47 GB), and variant 1 keeps the most bytes in flight (two waves
+// per SIMD) while each weight fragment still feeds two MFMAs; the engine uses it
+extern "C" hipError_t st_qtarget_launch_v(const st::qtgt::QTargetParams* p, int grid, int variant, hipStream_t stream) {
+  using namespace st::qtgt;
+  if (grid < 1 || p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;
+  switch (variant) {
+    case 0: return launch_qt<4, 4>(p, grid, stream);
+    case 1: return launch_qt<2, 8>(p, grid, stream);
+    case 2: return launch_qt<1, 8>(p, grid, stream);
+    case 3: return launch_qt<1, 16>(p, grid, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+extern "C" hipError_t st_qtarget_launch(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
+  return st_qtarget_launch_v(p, grid, 1, stream);
 }

@@ -48,6 +48,10 @@ class QStepParams(C.Structure):
     ]
 
 
+# csrc/qtarget.hip launch variants: (16-env tiles per wave, waves per workgroup)
+QTARGET_VARIANTS = {0: (4, 4), 1: (2, 8), 2: (1, 8), 3: (1, 16)}
+
+
 class QTargetParams(C.Structure):
     """csrc/qtarget.hip: target-net values of the three candidate next states of every env."""
     _fields_ = [
@@ -143,6 +147,8 @@ def lib() -> C.CDLL:
     L.st_qstep_ws_lds_bytes.restype = C.c_int
     L.st_qtarget_launch.argtypes = [C.POINTER(QTargetParams), C.c_int, C.c_void_p]
     L.st_qtarget_launch.restype = C.c_int
+    L.st_qtarget_launch_v.argtypes = [C.POINTER(QTargetParams), C.c_int, C.c_int, C.c_void_p]
+    L.st_qtarget_launch_v.restype = C.c_int
     L.st_f32b_target_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
     L.st_f32b_target_sync.restype = C.c_int
     L.st_qstep_pipe_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]

@@ -25,6 +25,7 @@ from __future__ import annotations
 import contextlib
 
 import math
+import os
 import time
 from typing import Dict, Optional
 
@@ -393,9 +394,13 @@ class VectorEngine:
             t.b0, t.inv_b0, t.s0 = q.b0, q.inv_b0, q.s0
             t.compat_env, t.output_relu, t.feat_mode = q.compat_env, q.output_relu, q.feat_mode
             self._qtp = t
-            # one 16-env tile per wave, 4 waves per workgroup: >= 2 workgroups per CU when E allows it
-            self._qt_grid = max(1, min(2 * torch.cuda.get_device_properties(self.device).multi_processor_count,
-                                       self.E // 64))
+            # one workgroup per CU (the weight images take 87.5 KB of LDS), grid-stride over 16-env tiles
+            self._qt_variant = int(os.environ.get("SHARETRADE_QT_VARIANT", "1"))
+            tpw, nw = native.QTARGET_VARIANTS[self._qt_variant]
+            if self.E % (16 * tpw):
+                raise NotImplementedError(f"target pass: E % {16 * tpw} != 0")
+            self._qt_grid = max(1, min(torch.cuda.get_device_properties(self.device).multi_processor_count,
+                                       self.E // (16 * tpw * nw)))
         a = cfg.agent
         o = native.OptimParams()
         o.params, o.params_bf, o.mask = native.ptr(self.params), native.ptr(self.params_bf), native.ptr(self.mask)
@@ -461,7 +466,7 @@ class VectorEngine:
 
     def _launch_qstep(self, L, sh) -> None:
         if self._qtp is not None:
-            native.check(L.st_qtarget_launch(self._qtp, self._qt_grid, sh), "qtarget")
+            native.check(L.st_qtarget_launch_v(self._qtp, self._qt_grid, self._qt_variant, sh), "qtarget")
         if self.step_kernel == "pipe":
             fn = L.st_qstep_pipe_launch
             if self.cfg.engine.step_variant:   # timing builds (csrc/ab/qstep_pipe_<v>.hip), same contract

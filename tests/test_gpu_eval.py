@@ -130,6 +130,38 @@ def test_greedy_learned_beats_random(native_built):
     assert g["median"] > r["median"] + 50.0, (g, r)
 
 
+def test_greedy_learned_beats_random_ar1_with_target_net(native_built):
+    """The AR(1) bank (mean-reverting log returns) on the flagship bf16 ws step with the stabilisers: target
+    network refreshed every 1,000 steps, Double DQN, reward scale 100, the exploit ramp over training steps,
+    gamma 0.99.  After two online episodes the frozen greedy policy's median beats the uniform-random
+    policy's by a wide margin and its mean beats random's (profiles/r5_learning_ws_knobs.md, run ar1_all:
+    greedy medians 186-707 over 20 episodes vs random 18; without the knobs the greedy median swings from
+    -142 to 451 and the round-4 version of this test failed on AR(1))."""
+    from sharetrade.config import preset_config
+    from sharetrade.trainer import benchkit
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship")
+    cfg.data.source = "ar1"
+    cfg.data.length = 1601
+    a = cfg.agent
+    a.target_every, a.double_dqn, a.reward_scale, a.ramp_mode, a.ramp, a.gamma = 1000, True, 100.0, "global", 3000.0, 0.99
+    eng = VectorEngine(cfg, device=torch.device("cuda", 0), envs=262144)
+    assert eng.step_kernel == "ws" and eng.qt_buf is not None
+    eng.capture_graph(warmup=0)
+    for _ in range(2):
+        benchkit.reset_episodes(eng)
+        eng.run(eng.T - eng.H)
+    eng.synchronize()
+    g = benchkit.greedy_episode_returns(eng)
+    r = benchkit.full_episode_returns(eng, random_policy=True)
+    print(f"[meas] ar1 knobs greedy mean {g['mean']:.0f} median {g['median']:.0f}; "
+          f"random mean {r['mean']:.0f} median {r['median']:.0f}")
+    assert g["complete_frac"] == 1.0 and r["complete_frac"] == 1.0
+    assert g["median"] > r["median"] + 100.0, (g, r)
+    assert g["mean"] > r["mean"], (g, r)
+
+
 def test_train_falls_back_to_eager_when_capture_fails(native_built, monkeypatch):
     """SHARETRADE_FAIL_CAPTURE on this rank: train() drops the graphs (sticky HIP error cleared) and
     runs eager steps to the same result as the captured run."""
