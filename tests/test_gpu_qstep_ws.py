@@ -263,8 +263,9 @@ def test_ws_adam_trajectory_matches_torch_oracle(native_built, kernel):
     d, dr = (eng.params.detach().cpu() - p0)[clear], (ref.params - p0)[clear]
     print(f"[meas] adam trajectory {kernel} m_rel={_rel(m, mr):.3e} v_rel={_rel(v, vr):.3e} "
           f"dparam_rel(clear)={_rel(d, dr):.3e} sign_flips={(torch.sign(d) != torch.sign(dr)).float().mean():.4f}")
-    assert _rel(m, mr) < 5e-3 and _rel(v, vr) < 1e-2, (_rel(m, mr), _rel(v, vr))
-    assert _rel(d, dr) < 5e-2, _rel(d, dr)
+    # measured 3.1e-4 / 3.1e-4 / 1.7e-4, no sign flips (profiles/r5_ws_numerics.md)
+    assert _rel(m, mr) < 7e-4 and _rel(v, vr) < 7e-4, (_rel(m, mr), _rel(v, vr))
+    assert _rel(d, dr) < 4e-4, _rel(d, dr)
 
 
 @pytest.mark.parametrize("E,grid", [(64 * 48, 16), (64 * 100, 8), (64 * 13, 8), (64 * 1000, 16), (64 * 2048, 256)])
