@@ -37,10 +37,11 @@ def _bank(n, T=400):
     return torch.from_numpy(random_walk(T, 50.0, 0.02, 3, n_series=n).astype(np.float32))
 
 
-def _worker(rank, world, port, E, steps, kernel, out, overlap=False):
+def _worker(rank, world, port, E, steps, kernel, out, overlap=False, evaluate=False, graph=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
+    from sharetrade.trainer import benchkit
     from sharetrade.trainer.engine import VectorEngine
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -51,10 +52,23 @@ def _worker(rank, world, port, E, steps, kernel, out, overlap=False):
                        world_size=world, group=dist.group.WORLD, envs=E)
     assert eng.backend == "native"
     eng.sync_params_from(0)
+    res = {}
+    if graph:
+        # gloo: the sync-DP step as two captured graphs around the host-side all-reduce
+        res["captured"] = eng.capture_graph(warmup=0)
     eng.run(steps)
+    if evaluate:
+        # a frozen-weight greedy episode in the middle of (overlapped) training: the parameters and the
+        # pending gradient of the last training step survive it (greedy_episode_returns raises if the
+        # evaluation moved the weights)
+        before = eng.params.detach().clone()
+        res["greedy"] = benchkit.greedy_episode_returns(eng, world, dist.group.WORLD)["mean"]
+        assert torch.equal(eng.params, before)
+        eng.run(2)
     eng.flush_pending()
     torch.cuda.synchronize()
-    torch.save({"params": eng.params.cpu(), "budget": eng.state.budget.cpu()}, os.path.join(out, f"r{rank}.pt"))
+    res.update({"params": eng.params.cpu(), "budget": eng.state.budget.cpu()})
+    torch.save(res, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
@@ -92,6 +106,34 @@ def test_overlapped_dp_is_rank_consistent_and_one_step_delayed(native_built):
     p_sync = out[False][0]["params"]
     rel = float((a["params"] - p_sync).norm() / p_sync.norm())
     assert 0.0 < rel < 5e-2, rel
+
+
+def test_overlapped_dp_greedy_evaluation_keeps_weights_frozen(native_built):
+    """the greedy evaluation under overlapped DP ran with the training lr on the delayed-
+    update structs and moved the weights; now both ranks evaluate with frozen weights and continue training."""
+    E, steps, world = 64, 5, 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _port(), E, steps, "bf16", d, True, True), nprocs=world,
+                           join=True, start_method="spawn")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert torch.equal(res[0]["params"], res[1]["params"]) and torch.isfinite(res[0]["params"]).all()
+    assert res[0]["greedy"] == res[1]["greedy"]
+
+
+def test_gloo_dp_split_graphs_match_eager(native_built):
+    """gloo groups: capture_graph builds the two graphs around the host-side all-reduce (_capture_split);
+    replaying them gives the eager trajectory bit for bit on both ranks."""
+    E, steps, world = 64, 6, 2
+    out = {}
+    for graph in (False, True):
+        with tempfile.TemporaryDirectory() as d:
+            mp.start_processes(_worker, args=(world, _port(), E, steps, "bf16", d, False, False, graph),
+                               nprocs=world, join=True, start_method="spawn")
+            out[graph] = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert all(r["captured"] for r in out[True])
+    for r in range(world):
+        assert torch.equal(out[True][r]["params"], out[False][r]["params"])
+        assert torch.equal(out[True][r]["budget"], out[False][r]["budget"])
 
 
 def _rccl_capture_worker(_rank, port, out):
