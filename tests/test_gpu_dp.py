@@ -61,6 +61,7 @@ def _worker(rank, world, port, E, steps, kernel, out, overlap=False, evaluate=Fa
         # a frozen-weight greedy episode in the middle of (overlapped) training: the parameters and the
         # pending gradient of the last training step survive it (greedy_episode_returns raises if the
         # evaluation moved the weights)
+        eng.flush_pending()          # (the last training step's delayed update, applied before the snapshot)
         before = eng.params.detach().clone()
         res["greedy"] = benchkit.greedy_episode_returns(eng, world, dist.group.WORLD)["mean"]
         assert torch.equal(eng.params, before)
