@@ -24,8 +24,11 @@ namespace qtgt {
 
 constexpr int INP = 224, HP = 128, KX = 208, HWIN = 201;
 
-constexpr int oW0 = 0;                         // W0 [128][208] bf16 (slot order)
-constexpr int oW1 = oW0 + HP * KX * 2;         // W1 [128][128] bf16, columns in pi order
+constexpr int KS = 216;                        // W0 image row stride (bf16): 432 B rows, so the 16 rows of a
+                                               // fragment read start 16 distinct 4-bank groups (208: 2-way)
+constexpr int oW0 = 0;                         // W0 [128][KS] bf16 (slot order)
+constexpr int oW1 = oW0 + HP * KS * 2;         // W1 [128][128] bf16, columns in pi order, 16-B chunks
+                                               // XOR-swizzled by the row (w1_off): conflict-free fragments
 constexpr int oW2 = oW1 + HP * HP * 2;         // W2 [4][128] bf16, columns in pi order (row 3 zero)
 constexpr int oB1 = oW2 + 4 * HP * 2;          // b1 [128] f32
 constexpr int LDS_BYTES = oB1 + HP * 4;
@@ -43,6 +46,10 @@ ST_DEV int pi_unit(int s) {
   const int ks = s >> 5, g = (s >> 3) & 3, j = s & 7;
   return 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
 }
+// W1 image: 16-byte chunk c / 8 of row r stored at chunk (c / 8) ^ (r & 15).  The fragment read of unit tile
+// i, k-step ks (lane (l16, g4): row 16 i + l16, chunk 4 ks + g4) then hits 16 different chunks per lane group
+// instead of one bank group 16 times (256-byte rows)
+ST_DEV int w1_off(int r, int c) { return r * HP + ((((c >> 3) ^ (r & 15))) << 3) + (c & 7); }
 ST_DEV s8v cat8(s4v a, s4v b) {
   s8v r;
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
@@ -103,11 +110,11 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
   const int w = tid >> 6;
   for (int i = tid; i < HP * KX; i += NT) {
     const int r = i / KX, s = i % KX;
-    W0[i] = f2bf(p.wt[p.off_w0 + r * INP + slot_col(s)]);
+    W0[r * KS + s] = f2bf(p.wt[p.off_w0 + r * INP + slot_col(s)]);
   }
   for (int i = tid; i < HP * HP; i += NT) {
     const int r = i / HP, s = i % HP;
-    W1[i] = f2bf(p.wt[p.off_w1 + r * HP + pi_unit(s)]);
+    W1[w1_off(r, s)] = f2bf(p.wt[p.off_w1 + r * HP + pi_unit(s)]);
   }
   for (int i = tid; i < 4 * HP; i += NT) {
     const int a = i / HP, s = i % HP;
@@ -121,7 +128,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
   // the tail A fragments (input slots 192..207 of every unit tile): read once
   s4v w0t[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) w0t[i] = lds_ld4(W0 + (16 * i + l16) * KX + 192 + 4 * g4);
+  for (int i = 0; i < 8; ++i) w0t[i] = lds_ld4(W0 + (16 * i + l16) * KS + 192 + 4 * g4);
   for (int t0 = (blockIdx.x * NW + w) * TPW; t0 < ntiles; t0 += gridDim.x * NW * TPW) {
     // an opaque zero offset per iteration: the weight-fragment LDS reads are loop-invariant, and hoisted out of
     // the loops they would pin ~400 registers (W0 / W1 / W2 fragments) and spill
@@ -169,7 +176,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int q = 0; q < TPW; ++q) a1[q][i] = f4v{0.f, 0.f, 0.f, 0.f};
-      const bf16_t* wr = W0i + (16 * i + l16) * KX + 8 * g4;
+      const bf16_t* wr = W0i + (16 * i + l16) * KS + 8 * g4;
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
         const s8v A = lds_ld8(wr + 32 * ks);
@@ -219,7 +226,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
           for (int q = 0; q < TPW; ++q) z[q][h] = bias;
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
-            const s8v A = lds_ld8(W1a + (16 * i + l16) * HP + 32 * ks + 8 * g4);
+            const s8v A = lds_ld8(W1a + w1_off(16 * i + l16, 32 * ks + 8 * g4));
 #pragma unroll
             for (int q = 0; q < TPW; ++q) z[q][h] = mfma32(A, H1[q][ks], z[q][h]);
           }
@@ -270,9 +277,10 @@ hipError_t launch_qt(const st::qtgt::QTargetParams* p, int grid, hipStream_t str
 }  // namespace
 
 // variant (tiles per wave, waves per workgroup): 0 = (4, 4), 1 = (2, 8), 2 = (1, 8), 3 = (1, 16).  At 1.835 M
-// envs (tools/bench_qtarget.py, profiles/r5_ws_knobs_cost.md): 658 / 489 / 779 / 703 us -- the pass streams
-// every env's 202-price x' window from HBM (1.47 GB), and variant 1 keeps the most bytes in flight (two waves
-// per SIMD) while each weight fragment still feeds two MFMAs; the engine uses it
+// envs (tools/bench_qtarget.py, profiles/r5_ws_knobs_cost.md): 629 / 447 / 568 / 442 us with the conflict-free
+// weight images (658 / 489 / 779 / 703 before: the 256-byte W1 rows put every fragment read 16-way on one bank
+// group).  The pass streams every env's 202-price x' window from HBM (1.47 GB, 300 us alone at ~5 TB/s);
+// variant 1 keeps two waves per SIMD and feeds each weight fragment to two MFMAs; the engine uses it
 extern "C" hipError_t st_qtarget_launch_v(const st::qtgt::QTargetParams* p, int grid, int variant, hipStream_t stream) {
   using namespace st::qtgt;
   if (grid < 1 || p->T < HWIN + 2 || p->T4 < p->T + 4) return hipErrorInvalidValue;
