@@ -24,8 +24,9 @@ namespace qtgt {
 
 constexpr int INP = 224, HP = 128, KX = 208, HWIN = 201;
 
-constexpr int KS = 216;                        // W0 image row stride (bf16): 432 B rows, so the 16 rows of a
-                                               // fragment read start 16 distinct 4-bank groups (208: 2-way)
+constexpr int KS = 208;                        // W0 image row stride (bf16): 416-byte rows are conflict-free
+                                               // for the 16-row b128 fragment reads (tools/lds_bank_sim.py;
+                                               // 216 would be 2-way)
 constexpr int oW0 = 0;                         // W0 [128][KS] bf16 (slot order)
 constexpr int oW1 = oW0 + HP * KS * 2;         // W1 [128][128] bf16, columns in pi order, 16-B chunks
                                                // XOR-swizzled by the row (w1_off): conflict-free fragments
@@ -279,7 +280,7 @@ hipError_t launch_qt(const st::qtgt::QTargetParams* p, int grid, hipStream_t str
 // variant (tiles per wave, waves per workgroup): 0 = (4, 4), 1 = (2, 8), 2 = (1, 8), 3 = (1, 16).  At 1.835 M
 // envs (tools/bench_qtarget.py, profiles/r5_ws_knobs_cost.md): 629 / 447 / 568 / 442 us with the conflict-free
 // weight images (658 / 489 / 779 / 703 before: the 256-byte W1 rows put every fragment read 16-way on one bank
-// group).  The pass streams every env's 202-price x' window from HBM (1.47 GB, 300 us alone at ~5 TB/s);
+// group; W0 rows at 216 bf16 were measured too, 2-way per the bank model and no faster).  The pass streams every env's 202-price x' window from HBM (1.47 GB, 300 us alone at ~5 TB/s);
 // variant 1 keeps two waves per SIMD and feeds each weight fragment to two MFMAs; the engine uses it
 extern "C" hipError_t st_qtarget_launch_v(const st::qtgt::QTargetParams* p, int grid, int variant, hipStream_t stream) {
   using namespace st::qtgt;
