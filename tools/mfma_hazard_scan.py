@@ -113,10 +113,17 @@ def main():
     defs = [f"-D{d}" for d in a.defines.split(",") if d]
     total = 0
     with tempfile.TemporaryDirectory() as d:
-        for src in srcs:
+        def compile_one(src):
             out = os.path.join(d, os.path.basename(src) + ".s")
             cmd = [build.HIPCC] + build.HIP_FLAGS + defs + ["--cuda-device-only", "-S", src, "-o", out]
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            return out
+
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+            outs = list(ex.map(compile_one, srcs))
+        for src, out in zip(srcs, outs):
             hits = scan(open(out).read())
             total += len(hits)
             print(f"{os.path.relpath(src, ROOT)}: {len(hits)} under-padded MFMA result reads")
