@@ -28,6 +28,8 @@ def _cfg(kernel):
     cfg.agent.lr = 1e-2
     if kernel == "fp32":
         cfg.engine.dtype = "fp32"
+    if kernel == "bf16_knobs":   # the ws knob build + target pass (agent.target_every / double_dqn)
+        cfg.agent.target_every, cfg.agent.double_dqn, cfg.agent.reward_scale = 2, True, 2.0
     return cfg
 
 
@@ -73,7 +75,7 @@ def _worker(rank, world, port, E, steps, kernel, out, overlap=False, evaluate=Fa
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kernel", ["bf16", "fp32"])
+@pytest.mark.parametrize("kernel", ["bf16", "fp32", "bf16_knobs"])
 def test_native_dp_two_ranks_match_single_process(native_built, kernel):
     from sharetrade.trainer.engine import VectorEngine
 
