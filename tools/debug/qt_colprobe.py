@@ -1,11 +1,13 @@
 """Column probe of csrc/qtarget.hip: a target net that passes input column c straight to Q[0]
 (W0 rows 0 / 1 = +e_c / -e_c, W1 rows 0 / 1 = e_0 / e_1, W2 row 0 = (1, -1)), so QT[e][a][0] = x'_a[e][c]."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, "/root/repo")
-sys.path.insert(0, "/root/repo/tests")
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, ROOT + "/tests")
 from test_gpu_qstep_ws import _cfg, _oracle, _prices  # noqa: E402
 
 from sharetrade.ops import native  # noqa: E402

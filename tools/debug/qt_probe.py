@@ -1,10 +1,12 @@
 """Where does csrc/qtarget.hip differ from the oracle's target forward?  Per action, per env group."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, "/root/repo")
-sys.path.insert(0, "/root/repo/tests")
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, ROOT + "/tests")
 from test_gpu_qstep_ws import _cfg, _oracle, _prices, _rel  # noqa: E402
 
 from sharetrade.models import qnet as qn  # noqa: E402

@@ -1,11 +1,13 @@
 """Hidden-unit probe of csrc/qtarget.hip: h1[u] = (u + 1) / 128 (through the constant input column), layer 2 a
 permutation sigma, the output row 0 = e_v: QT[.][.][0] must be h1[sigma^-1(v)] (and with W0 = 0, relu(b1[v]))."""
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, "/root/repo")
-sys.path.insert(0, "/root/repo/tests")
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, ROOT + "/tests")
 from test_gpu_qstep_ws import _cfg, _prices  # noqa: E402
 
 from sharetrade.ops import native  # noqa: E402
