@@ -11,7 +11,7 @@ Commands
             engine checkpoint or random init).
 ``config``  print the resolved configuration (JSON).
 
-Common flags: ``--preset {reference_compat,intended,flagship,test}``,
+Common flags: ``--preset {reference_compat,intended,flagship,flagship_stable,test}``,
 ``--config file.{json,toml}``, ``--set section.key=value`` (repeatable).
 """
 from __future__ import annotations

@@ -290,6 +290,10 @@ def preset_config(name: str = "reference_compat") -> Config:
     * ``intended`` — same network but with the quirks fixed (default semantics).
     * ``flagship`` — BASELINE.json config 2/3: 2x128 MLP, bf16 fused step,
       normalised features, correct env/TD semantics, Adam.
+    * ``flagship_stable`` — ``flagship`` plus the learning stabilisers that make its greedy policy beat
+      buy-and-hold's median on the AR(1) and trend banks (profiles/r5_learning_ws_knobs*.md): a target
+      network refreshed every 1,000 steps, Double DQN, reward scale 100, the exploit ramp over 3,000
+      training steps, gamma 0.99.  Same fused bf16 step (its knob build + csrc/qtarget.hip), ~1.7x its time.
     * ``test`` — the test profile (src/test/resources/application.conf): in-memory
       journal, DEBUG log level, test event listener.
     """
@@ -320,6 +324,12 @@ def preset_config(name: str = "reference_compat") -> Config:
         cfg.data.source = "random_walk"
         cfg.engine.dtype = "bf16"
         cfg.engine.envs_per_rank = 65536
+        return cfg
+    if name == "flagship_stable":
+        cfg = preset_config("flagship")
+        a = cfg.agent
+        a.target_every, a.double_dqn, a.reward_scale = 1000, True, 100.0
+        a.ramp_mode, a.ramp, a.gamma = "global", 3000.0, 0.99
         return cfg
     if name == "recurrent":
         # BASELINE config 5: GRU(256) Q-net on minute bars (sharetrade/trainer/recurrent.py)

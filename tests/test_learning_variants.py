@@ -87,3 +87,16 @@ def test_f32_deterministic_auto_policy(monkeypatch):
     monkeypatch.delenv("SHARETRADE_F32_SPLIT_PARTIAL")
     with pytest.raises(ValueError):
         f32_deterministic(intended, 1)
+
+
+def test_flagship_stable_preset_runs_the_knobs():
+    """preset flagship_stable = flagship + target net / Double DQN / reward scale / global ramp; the torch
+    engine steps it (the native ws path is pinned on the GPU: tests/test_gpu_ws_knobs.py)."""
+    cfg = preset_config("flagship_stable")
+    a = cfg.agent
+    assert (a.target_every, a.double_dqn, a.reward_scale, a.ramp_mode, a.gamma) == (1000, True, 100.0, "global", 0.99)
+    assert cfg.model.hidden == preset_config("flagship").model.hidden
+    e = VectorEngine(cfg, device=torch.device("cpu"), envs=8, backend="torch")
+    for _ in range(2):
+        e.step()
+    assert e.params_target is not None and torch.isfinite(e.params).all()
