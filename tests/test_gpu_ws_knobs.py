@@ -202,3 +202,33 @@ def test_other_bf16_kernels_refuse_the_knobs(native_built):
     cfg = _apply(_cfg(kernel="wide"), dict(target_every=10))
     with pytest.raises(NotImplementedError):
         VectorEngine(cfg, prices=_prices(128), device=torch.device("cuda", 0), envs=128)
+
+
+def test_ws_target_state_dict_resume_is_bit_exact(native_built):
+    """Checkpoint / resume with the target network on the flagship path: state_dict after 5 steps (target
+    copy included), a fresh engine loads it and runs 6 more steps -- bit-identical parameters, target copy and
+    env state to the uninterrupted 11-step run (the refresh at step 8 happens in both)."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 64 * 64
+    prices = _prices(E, seed=29)
+    dev = torch.device("cuda", 0)
+
+    def make():
+        cfg = _apply(_cfg(), dict(target_every=4, double_dqn=True, reward_scale=2.0))
+        return VectorEngine(cfg, prices=prices, device=dev, envs=E)
+
+    ref = make()
+    ref.run(11)
+    a = make()
+    a.run(5)
+    sd = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in a.state_dict().items()}
+    b = make()
+    b.load_state_dict(sd)
+    b.run(6)
+    torch.cuda.synchronize()
+    assert b.step_count == ref.step_count == 11
+    assert torch.equal(b.params, ref.params)
+    assert torch.equal(b.params_target, ref.params_target)
+    for k in ("budget", "shares", "pos", "value"):
+        assert torch.equal(getattr(b.state, k), getattr(ref.state, k)), k
