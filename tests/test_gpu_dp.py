@@ -111,6 +111,17 @@ def test_overlapped_dp_is_rank_consistent_and_one_step_delayed(native_built):
     assert 0.0 < rel < 5e-2, rel
 
 
+def test_overlapped_dp_with_target_net_is_rank_consistent(native_built):
+    """dp_overlap + the target net / Double DQN on the ws kernel: the target copy follows the delayed update
+    on every rank, so both ranks end with identical parameters."""
+    E, steps, world = 64, 7, 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _port(), E, steps, "bf16_knobs", d, True), nprocs=world,
+                           join=True, start_method="spawn")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert torch.equal(res[0]["params"], res[1]["params"]) and torch.isfinite(res[0]["params"]).all()
+
+
 def test_overlapped_dp_greedy_evaluation_keeps_weights_frozen(native_built):
     """the greedy evaluation under overlapped DP ran with the training lr on the delayed-
     update structs and moved the weights; now both ranks evaluate with frozen weights and continue training."""
