@@ -9,7 +9,8 @@
 // output layer.  QT[e][a][0..2] = Q_target(x' after action a)[0..2] (output ReLU applied when the model has
 // it); the step kernel reads the row of the action it takes.
 //
-// MFMA layout (TPW 16-env tiles per wave, NWV waves per workgroup, grid-stride): the target weights
+// MFMA layout (TPW 16-env tiles per wave, NWV waves per workgroup, one workgroup per CU, grid-stride; each
+// weight fragment read from LDS feeds the TPW tiles' MFMAs): the target weights
 // are converted to bf16 into LDS once per workgroup (fp32 master copy of the target net: no second bf16
 // image to keep in sync); x' features are built in registers as B operands (the ws kernel's slot order: the
 // last 16-wide k-step carries budget, shares, 1, fxn(vnew) in lane group 0); hidden activations stay in
@@ -20,7 +21,6 @@
 
 namespace st {
 namespace qtgt {
-
 
 constexpr int INP = 224, HP = 128, KX = 208, HWIN = 201;
 
