@@ -82,8 +82,9 @@ class AgentConfig:
     # envs whose prices drift apart (bf16 engine kernels and the torch oracle)
     reward_mode: str = "absolute"
     td_clip: float = 0.0            # > 0: clamp the TD error fed back (Huber loss); 0 = squared error
-    # learning-quality experiments (tools/learning_eval.py): the torch backend and the native batched fp32
-    # step implement them; the fused bf16 kernels refuse non-default values:
+    # learning-quality experiments (tools/learning_eval.py, preset flagship_stable): the torch backend, the
+    # native batched fp32 step and the flagship bf16 ws step implement them (the wide / narrow bf16 kernels
+    # refuse non-default values):
     target_every: int = 0           # > 0: Q(x') from a target copy of the params, refreshed every N steps
     double_dqn: bool = False        # with target_every: max-Q(x') action by the online net, valued by the target
     reward_scale: float = 1.0       # multiplies the reward in the TD target
