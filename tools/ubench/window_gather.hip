@@ -4,7 +4,13 @@
 //   A  operand pattern (the kernels today): a wave owns a 16-env tile; lane (env l16, group g4) loads the
 //      float4 pairs of its MFMA B operand -- per instruction 16 rows x 4 scattered 16-byte pieces;
 //   B  row pattern: one instruction per env row, lane i loads floats 4i .. 4i + 3 (51 lanes cover the
-//      202 floats): every instruction reads one contiguous 816-byte run.
+//      202 floats): every instruction reads one contiguous 816-byte run;
+//   C  pattern A over a 16-bit copy of the bank (u16 ticks of a per-env power-of-two grid): per lane and
+//      k-step one 16-byte load of 8 ticks (2-byte aligned) + one 2-byte load, converted to fp32;
+//   D  time-major bank (bank[t][env]): lane (env l16, group g4) loads its 9 times per k-step one value per
+//      instruction, so each instruction reads 4 time rows x 16 consecutive envs (4 x 64 B);
+//   E  as D over u16 ticks (4 x 32 B per instruction).
+// argv[2] = "same": every env at the same window position (the engine's lock-step envs), else random.
 //
 // Each wave folds what it loaded into one value per lane (so nothing is dead) and writes it out.  Reports
 // useful bytes / kernel time.  One bank row per env, T4 floats apart (as the engine's padded copy), random
@@ -67,6 +73,63 @@ __global__ void __launch_bounds__(512) gather_rows(const float* bank, const int*
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+// C: the operand pattern over u16 ticks (half the bytes; one cvt per value)
+__device__ __forceinline__ uint4 ldu4h(const unsigned short* a) {
+  uint4 v;
+  __builtin_memcpy(&v, a, sizeof(v));
+  return v;
+}
+__device__ __forceinline__ float lo16(unsigned x) { return (float)(x & 0xFFFFu); }
+__device__ __forceinline__ float hi16(unsigned x) { return (float)(x >> 16); }
+__global__ void __launch_bounds__(512) gather_u16(const unsigned short* bank, const int* pos, float* out, int E) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+  float acc = 0.f;
+  for (int t = wave; t < E / 16; t += nwaves) {
+    const int e = 16 * t + l16;
+    const unsigned short* b = bank + (size_t)e * T4 + pos[e];
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      const uint4 u = ldu4h(b + 1 + 32 * ks + 8 * g4);
+      acc += lo16(u.x) + hi16(u.x) + lo16(u.y) + hi16(u.y) + lo16(u.z) + hi16(u.z) + lo16(u.w) + hi16(u.w);
+      acc += (float)b[9 + 32 * ks + 8 * g4];
+    }
+    if (g4 == 1 || g4 == 2) {
+      uint2 u;
+      __builtin_memcpy(&u, b + 193 + 4 * (g4 - 1), sizeof(u));
+      acc += lo16(u.x) + hi16(u.x) + lo16(u.y) + hi16(u.y);
+    }
+    acc += (float)b[201];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+// D / E: time-major layouts (row t holds every env's price at time t; row stride ET elements)
+template <typename TT>
+__global__ void __launch_bounds__(512) gather_tm(const TT* bank, size_t ET, const int* pos, float* out, int E) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+  float acc = 0.f;
+  for (int t = wave; t < E / 16; t += nwaves) {
+    const int e = 16 * t + l16;
+    const TT* b = bank + (size_t)pos[e] * ET + e;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      float v[9];
+#pragma unroll
+      for (int j = 0; j < 9; ++j) v[j] = (float)b[(size_t)(1 + 32 * ks + 8 * g4 + j) * ET];
+#pragma unroll
+      for (int j = 0; j < 9; ++j) acc += v[j];
+    }
+    if (g4 == 1 || g4 == 2) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) acc += (float)b[(size_t)(193 + 4 * (g4 - 1) + j) * ET];
+    }
+    acc += (float)b[(size_t)201 * ET];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 int main(int argc, char** argv) {
   const int E = argc > 1 ? atoi(argv[1]) : 1835008;
   float* bank;
@@ -77,16 +140,21 @@ int main(int argc, char** argv) {
   if (hipMemset(bank, 0, nb * sizeof(float)) != hipSuccess) return 1;
   std::vector<int> hp(E);
   srand(7);
-  for (int i = 0; i < E; ++i) hp[i] = rand() % (T - H - 2);
+  const bool same = argc > 2 && argv[2][0] == 's';
+  for (int i = 0; i < E; ++i) hp[i] = same ? 1234 : rand() % (T - H - 2);
   if (hipMalloc(&pos, E * sizeof(int)) != hipSuccess) return 1;
   if (hipMemcpy(pos, hp.data(), E * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) return 1;
   if (hipMalloc(&out, 1 << 24) != hipSuccess) return 1;
+  unsigned short* bank16;
+  if (hipMalloc(&bank16, nb * sizeof(unsigned short)) != hipSuccess) return 1;
+  if (hipMemset(bank16, 0, nb * sizeof(unsigned short)) != hipSuccess) return 1;
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  const double useful = (double)E * 202 * 4;
+  const double useful = (double)E * 202 * 4;   // (fp32-equivalent bytes for C too)
+  printf("positions: %s\n\n", same ? "same for every env" : "random per env");
   printf("| pattern | waves / CU | grid | us | useful GB/s |\n|---|---|---|---|---|\n");
-  for (int pat = 0; pat < 2; ++pat)
+  for (int pat = 0; pat < 5; ++pat)
     for (int wpc : {8, 16, 32}) {
       const int threads = 512, blocks = 256 * wpc / 8;
       for (int rep = 0; rep < 2; ++rep) {   // (first rep warms up)
@@ -94,6 +162,12 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 5; ++i) {
           if (pat == 0)
             hipLaunchKernelGGL(gather_operand, dim3(blocks), dim3(threads), 0, 0, bank, pos, out, E);
+          else if (pat == 3)
+            hipLaunchKernelGGL(gather_tm<float>, dim3(blocks), dim3(threads), 0, 0, bank, (size_t)E, pos, out, E);
+          else if (pat == 4)
+            hipLaunchKernelGGL(gather_tm<unsigned short>, dim3(blocks), dim3(threads), 0, 0, bank16, (size_t)E, pos, out, E);
+          else if (pat == 2)
+            hipLaunchKernelGGL(gather_u16, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
           else
             hipLaunchKernelGGL(gather_rows, dim3(blocks), dim3(threads), 0, 0, bank, pos, out, E);
         }
@@ -102,9 +176,10 @@ int main(int argc, char** argv) {
         float ms;
         (void)hipEventElapsedTime(&ms, a, b);
         if (rep == 1)
-          printf("| %s | %d | %d | %.1f | %.0f |\n", pat == 0 ? "A operand (today)" : "B row per instruction", wpc,
+          printf("| %s | %d | %d | %.1f | %.0f |\n", pat == 0 ? "A operand (today)" : (pat == 1 ? "B row per instruction" : (pat == 2 ? "C operand, u16 ticks" : (pat == 3 ? "D time-major fp32" : "E time-major u16"))), wpc,
                  blocks, ms / 5 * 1e3, useful / (ms / 5 * 1e-3) / 1e9);
       }
     }
+  (void)hipFree(bank16);
   return hipFree(bank) == hipSuccess ? 0 : 2;
 }
