@@ -9,7 +9,8 @@
 //      k-step one 16-byte load of 8 ticks (2-byte aligned) + one 2-byte load, converted to fp32;
 //   D  time-major bank (bank[t][env]): lane (env l16, group g4) loads its 9 times per k-step one value per
 //      instruction, so each instruction reads 4 time rows x 16 consecutive envs (4 x 64 B);
-//   E  as D over u16 ticks (4 x 32 B per instruction).
+//   E  as D over u16 ticks (4 x 32 B per instruction);
+//   C' as C with the 9th tick of each k-step read by a 4-byte load instead of a 2-byte one.
 // argv[2] = "same": every env at the same window position (the engine's lock-step envs), else random.
 //
 // Each wave folds what it loaded into one value per lane (so nothing is dead) and writes it out.  Reports
@@ -81,6 +82,7 @@ __device__ __forceinline__ uint4 ldu4h(const unsigned short* a) {
 }
 __device__ __forceinline__ float lo16(unsigned x) { return (float)(x & 0xFFFFu); }
 __device__ __forceinline__ float hi16(unsigned x) { return (float)(x >> 16); }
+template <bool WIDE9>
 __global__ void __launch_bounds__(512) gather_u16(const unsigned short* bank, const int* pos, float* out, int E) {
   const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -92,7 +94,13 @@ __global__ void __launch_bounds__(512) gather_u16(const unsigned short* bank, co
     for (int ks = 0; ks < 6; ++ks) {
       const uint4 u = ldu4h(b + 1 + 32 * ks + 8 * g4);
       acc += lo16(u.x) + hi16(u.x) + lo16(u.y) + hi16(u.y) + lo16(u.z) + hi16(u.z) + lo16(u.w) + hi16(u.w);
-      acc += (float)b[9 + 32 * ks + 8 * g4];
+      if (WIDE9) {   // the 9th tick through a 4-byte load (2-byte aligned) instead of a 2-byte load
+        unsigned w;
+        __builtin_memcpy(&w, b + 9 + 32 * ks + 8 * g4, sizeof(w));
+        acc += lo16(w);
+      } else {
+        acc += (float)b[9 + 32 * ks + 8 * g4];
+      }
     }
     if (g4 == 1 || g4 == 2) {
       uint2 u;
@@ -154,7 +162,7 @@ int main(int argc, char** argv) {
   const double useful = (double)E * 202 * 4;   // (fp32-equivalent bytes for C too)
   printf("positions: %s\n\n", same ? "same for every env" : "random per env");
   printf("| pattern | waves / CU | grid | us | useful GB/s |\n|---|---|---|---|---|\n");
-  for (int pat = 0; pat < 5; ++pat)
+  for (int pat = 0; pat < 6; ++pat)
     for (int wpc : {8, 16, 32}) {
       const int threads = 512, blocks = 256 * wpc / 8;
       for (int rep = 0; rep < 2; ++rep) {   // (first rep warms up)
@@ -167,7 +175,9 @@ int main(int argc, char** argv) {
           else if (pat == 4)
             hipLaunchKernelGGL(gather_tm<unsigned short>, dim3(blocks), dim3(threads), 0, 0, bank16, (size_t)E, pos, out, E);
           else if (pat == 2)
-            hipLaunchKernelGGL(gather_u16, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
+            hipLaunchKernelGGL(gather_u16<false>, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
+          else if (pat == 5)
+            hipLaunchKernelGGL(gather_u16<true>, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
           else
             hipLaunchKernelGGL(gather_rows, dim3(blocks), dim3(threads), 0, 0, bank, pos, out, E);
         }
@@ -176,7 +186,7 @@ int main(int argc, char** argv) {
         float ms;
         (void)hipEventElapsedTime(&ms, a, b);
         if (rep == 1)
-          printf("| %s | %d | %d | %.1f | %.0f |\n", pat == 0 ? "A operand (today)" : (pat == 1 ? "B row per instruction" : (pat == 2 ? "C operand, u16 ticks" : (pat == 3 ? "D time-major fp32" : "E time-major u16"))), wpc,
+          printf("| %s | %d | %d | %.1f | %.0f |\n", pat == 0 ? "A operand (today)" : (pat == 1 ? "B row per instruction" : (pat == 2 ? "C operand, u16 ticks" : (pat == 3 ? "D time-major fp32" : (pat == 4 ? "E time-major u16" : "C' as C, 9th tick by a 4-byte load")))), wpc,
                  blocks, ms / 5 * 1e3, useful / (ms / 5 * 1e-3) / 1e9);
       }
     }
