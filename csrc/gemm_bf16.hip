@@ -55,11 +55,9 @@ struct GemmBatch {
   int n;
 };
 
-// BK: K tile (64, or 32 for the deeper-ring variants: the same LDS bytes buy twice the stages, so more
-// K-tiles are in flight per block at two blocks per CU)
-template <int BM, int BN, int S = 2, int BK = GBK>
+template <int BM, int BN, int S = 2>
 struct GemmGeo {
-  static constexpr int A_EL = BM * BK, B_EL = BN * BK;
+  static constexpr int A_EL = BM * GBK, B_EL = BN * GBK;
   static constexpr int BUF_EL = A_EL + B_EL;
   static constexpr int KLOOP_BYTES = S * BUF_EL * 2;   // S-stage LDS ring
   // 256 x 256 tiles stage only C for the epilogue (C and C^T would need 270 KB): no transposed output
@@ -71,31 +69,25 @@ struct GemmGeo {
   // (one block per CU, 256 accumulator registers per lane: half the LDS fragment bytes per MFMA of
   // the 64 x 64 wave tiles)
   static constexpr int NWM = (BM >= 256 && BN < 256) ? 4 : 2, NWN = 2, NT = 64 * NWM * NWN;
-  static constexpr int MINB = (NT > 256 || BM * BN >= 256 * 256 || 2 * LDS_BYTES > 163840) ? 1 : 2;
+  static constexpr int MINB = (NT > 256 || S > 2 || BM * BN >= 256 * 256) ? 1 : 2;
   // LDS-DMA instructions per wave per K-tile (vmcnt budget of the S-stage ring)
-  static constexpr int LPT = (BM * BK / 512 + NT / 64 - 1) / (NT / 64) + (BN * BK / 512 + NT / 64 - 1) / (NT / 64);
+  static constexpr int LPT = (BM / 8 + NT / 64 - 1) / (NT / 64) + (BN / 8 + NT / 64 - 1) / (NT / 64);
   static constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
   static constexpr int TM = WM / 16, TN = WN / 16;  // 16x16 MFMA tiles per wave
-  static_assert(BM % 32 == 0 && BN % 32 == 0 && (BK == 64 || BK == 32), "tile");
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
   static_assert(LDS_BYTES * MINB <= 163840, "LDS per CU");
 };
 
-// 16-B chunk swizzle of a staged row: BK = 64 (128-B rows) XOR (r & 7); BK = 32 (64-B rows) XOR ((r >> 1) & 3)
-// -- both conflict-free for the 16x16x32 fragment reads (tools/lds_bank_sim.py model)
-template <int BK>
-ST_DEV int chunk_swz(int r) { return BK == 64 ? (r & 7) : ((r >> 1) & 3); }
-
-// stage one operand tile (ROWS x BK bf16) of K-tile k0 into a linear LDS image with the
-// chunk swizzle moved to the source address.  ROWS*BK/8 16-B pieces, 64 per wave-instruction.
-template <int ROWS, int NWAVE = GT / 64, int BK = GBK>
+// stage one operand tile (ROWS x 64 bf16) of K-tile k0 into a linear LDS image with the
+// chunk swizzle moved to the source address.  ROWS*8 16-B pieces, 64 per wave-instruction.
+template <int ROWS, int NWAVE = GT / 64>
 ST_DEV void stage_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, bf16_t* lds, int wave, int lane) {
-  constexpr int CPR = BK / 8;              // 16-B chunks per row
-  constexpr int INSTR = ROWS * CPR / 64;   // wave-instructions per tile
+  constexpr int INSTR = ROWS / 8;        // wave-instructions per tile
 #pragma unroll
   for (int j = wave; j < INSTR; j += NWAVE) {
-    const int r = j * (64 / CPR) + lane / CPR;
-    const int c = lane % CPR;
-    const int g = c ^ chunk_swz<BK>(r);
+    const int r = j * 8 + (lane >> 3);
+    const int c = lane & 7;
+    const int g = c ^ (r & 7);
     const bf16_t* src = G + (size_t)(row0 + r) * ld + k0 + g * 8;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(lds + j * 512), 16, 0, 0);
@@ -103,13 +95,14 @@ ST_DEV void stage_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, b
 }
 
 // fragment (8 bf16) of row r, global chunk g of a staged tile
-template <int BK = GBK>
 ST_DEV s8v frag_sw(const bf16_t* lds, int r, int g) {
-  return lds_ld8(lds + r * BK + ((g ^ chunk_swz<BK>(r)) << 3));
+  return lds_ld8(lds + r * GBK + ((g ^ (r & 7)) << 3));
 }
 
 template <int BM, int BN> constexpr int gemm_threads() { return (BM >= 256 && BN < 256) ? 512 : 256; }
-template <int BM, int BN, int S, int BK = GBK> constexpr int gemm_min_blocks() { return GemmGeo<BM, BN, S, BK>::MINB; }
+template <int BM, int BN, int S> constexpr int gemm_min_blocks() {
+  return ((BM >= 256 && BN < 256) || S > 2 || BM * BN >= 256 * 256) ? 1 : 2;
+}
 
 // s_waitcnt immediate: vmcnt = N (gfx9 split field), expcnt / lgkmcnt not waited on
 template <int N>
@@ -129,9 +122,9 @@ ST_DEV int xcd_remap(int bid, int all) {   // neighbouring ids on one XCD's L2 (
 }
 
 // one workgroup's tile (and K split) of product p; bid = its index within p's blocks
-template <int BM, int BN, int EPI, int S, int BK = GBK>
+template <int BM, int BN, int EPI, int S>
 ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
-  using G = GemmGeo<BM, BN, S, BK>;
+  using G = GemmGeo<BM, BN, S>;
   constexpr int NW = G::NT / 64;
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
@@ -149,16 +142,16 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) acc[i][j] = zero4();
 
-  const int nk = p.K / BK / nsplit;
-  const int kb = ks * nk * BK;
+  const int nk = p.K / GBK / nsplit;
+  const int kb = ks * nk * GBK;
   if constexpr (S > 2) {
     // S-stage ring: tiles t+1 .. t+S-2 stay in flight while tile t is multiplied; one barrier per
     // K-tile (it also retires every wave's reads of tile t-1, whose buffer the next load refills)
 #pragma unroll
     for (int s0 = 0; s0 < S - 1; ++s0)
       if (s0 < nk) {
-        stage_tile<BM, NW, BK>(p.A, p.lda, m0, kb + s0 * BK, buf + s0 * G::BUF_EL, wave, lane);
-        stage_tile<BN, NW, BK>(p.B, p.ldb, n0, kb + s0 * BK, buf + s0 * G::BUF_EL + G::A_EL, wave, lane);
+        stage_tile<BM, NW>(p.A, p.lda, m0, kb + s0 * GBK, buf + s0 * G::BUF_EL, wave, lane);
+        stage_tile<BN, NW>(p.B, p.ldb, n0, kb + s0 * GBK, buf + s0 * G::BUF_EL + G::A_EL, wave, lane);
       }
     int slot = 0;
     for (int t = 0; t < nk; ++t) {
@@ -167,18 +160,18 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
       __syncthreads();
       if (t + S - 1 < nk) {
         const int ls = slot == 0 ? S - 1 : slot - 1;        // (t + S - 1) % S: tile t-1's buffer
-        stage_tile<BM, NW, BK>(p.A, p.lda, m0, kb + (t + S - 1) * BK, buf + ls * G::BUF_EL, wave, lane);
-        stage_tile<BN, NW, BK>(p.B, p.ldb, n0, kb + (t + S - 1) * BK, buf + ls * G::BUF_EL + G::A_EL, wave, lane);
+        stage_tile<BM, NW>(p.A, p.lda, m0, kb + (t + S - 1) * GBK, buf + ls * G::BUF_EL, wave, lane);
+        stage_tile<BN, NW>(p.B, p.ldb, n0, kb + (t + S - 1) * GBK, buf + ls * G::BUF_EL + G::A_EL, wave, lane);
       }
       const bf16_t* cA = buf + slot * G::BUF_EL;
       const bf16_t* cB = cA + G::A_EL;
 #pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
+      for (int kk = 0; kk < GBK / 32; ++kk) {
         s8v a[G::TM], b[G::TN];
 #pragma unroll
-        for (int i = 0; i < G::TM; ++i) a[i] = frag_sw<BK>(cA, wm * G::WM + 16 * i + l16, kk * 4 + g4);
+        for (int i = 0; i < G::TM; ++i) a[i] = frag_sw(cA, wm * G::WM + 16 * i + l16, kk * 4 + g4);
 #pragma unroll
-        for (int j = 0; j < G::TN; ++j) b[j] = frag_sw<BK>(cB, wn * G::WN + 16 * j + l16, kk * 4 + g4);
+        for (int j = 0; j < G::TN; ++j) b[j] = frag_sw(cB, wn * G::WN + 16 * j + l16, kk * 4 + g4);
 #pragma unroll
         for (int i = 0; i < G::TM; ++i)
 #pragma unroll
@@ -188,26 +181,26 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
     }
     __syncthreads();   // every wave's last reads retired before the epilogue reuses the ring
   } else {
-  stage_tile<BM, NW, BK>(p.A, p.lda, m0, kb, buf, wave, lane);
-  stage_tile<BN, NW, BK>(p.B, p.ldb, n0, kb, buf + G::A_EL, wave, lane);
+  stage_tile<BM, NW>(p.A, p.lda, m0, kb, buf, wave, lane);
+  stage_tile<BN, NW>(p.B, p.ldb, n0, kb, buf + G::A_EL, wave, lane);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     bf16_t* cur = buf + (t & 1) * G::BUF_EL;
     if (t + 1 < nk) {
       bf16_t* nxt = buf + ((t + 1) & 1) * G::BUF_EL;
-      stage_tile<BM, NW, BK>(p.A, p.lda, m0, kb + (t + 1) * BK, nxt, wave, lane);
-      stage_tile<BN, NW, BK>(p.B, p.ldb, n0, kb + (t + 1) * BK, nxt + G::A_EL, wave, lane);
+      stage_tile<BM, NW>(p.A, p.lda, m0, kb + (t + 1) * GBK, nxt, wave, lane);
+      stage_tile<BN, NW>(p.B, p.ldb, n0, kb + (t + 1) * GBK, nxt + G::A_EL, wave, lane);
     }
     const bf16_t* cA = cur;
     const bf16_t* cB = cur + G::A_EL;
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+    for (int kk = 0; kk < GBK / 32; ++kk) {
       s8v a[G::TM], b[G::TN];
 #pragma unroll
-      for (int i = 0; i < G::TM; ++i) a[i] = frag_sw<BK>(cA, wm * G::WM + 16 * i + l16, kk * 4 + g4);
+      for (int i = 0; i < G::TM; ++i) a[i] = frag_sw(cA, wm * G::WM + 16 * i + l16, kk * 4 + g4);
 #pragma unroll
-      for (int j = 0; j < G::TN; ++j) b[j] = frag_sw<BK>(cB, wn * G::WN + 16 * j + l16, kk * 4 + g4);
+      for (int j = 0; j < G::TN; ++j) b[j] = frag_sw(cB, wn * G::WN + 16 * j + l16, kk * 4 + g4);
 #pragma unroll
       for (int i = 0; i < G::TM; ++i)
 #pragma unroll
@@ -289,10 +282,10 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
 }
 
 // a batch of same-shape products (one problem per range of workgroups)
-template <int BM, int BN, int EPI, int S = 2, int BK = GBK>
-__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S, BK>())) gemm_nt_kernel(GemmBatch batch) {
-  using G = GemmGeo<BM, BN, S, BK>;
-  static_assert(G::NT == gemm_threads<BM, BN>(), "launch bounds");
+template <int BM, int BN, int EPI, int S = 2>
+__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_nt_kernel(GemmBatch batch) {
+  using G = GemmGeo<BM, BN, S>;
+  static_assert(G::NT == gemm_threads<BM, BN>() && G::MINB == gemm_min_blocks<BM, BN, S>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   // problems may differ in shape (grouped GEMM): workgroup ranges in problem order
   int all = 0;
@@ -304,50 +297,50 @@ __global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM,
     bid -= nb;
   }
   pi = __builtin_amdgcn_readfirstlane(pi);
-  gemm_body<BM, BN, EPI, S, BK>(batch.a[pi], bid, gsm);
+  gemm_body<BM, BN, EPI, S>(batch.a[pi], bid, gsm);
 }
 
 // two products of any shapes and epilogues in one grid (e.g. a layer's data gradient beside the
 // next layer's split-K weight gradient): no fork / join of streams between them
-template <int BM, int BN, int EPI0, int EPI1, int S = 2, int BK = GBK>
-__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S, BK>())) gemm_dual_kernel(GemmArgs a0,
-                                                                                                              GemmArgs a1) {
+template <int BM, int BN, int EPI0, int EPI1, int S = 2>
+__global__ void __launch_bounds__((gemm_threads<BM, BN>()), (gemm_min_blocks<BM, BN, S>())) gemm_dual_kernel(GemmArgs a0,
+                                                                                                          GemmArgs a1) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int n0 = gemm_blocks<BM, BN>(a0), n1 = gemm_blocks<BM, BN>(a1);
   const int bid = xcd_remap(blockIdx.x, n0 + n1);
-  if (bid < n0) gemm_body<BM, BN, EPI0, S, BK>(a0, bid, gsm);
-  else gemm_body<BM, BN, EPI1, S, BK>(a1, bid - n0, gsm);
+  if (bid < n0) gemm_body<BM, BN, EPI0, S>(a0, bid, gsm);
+  else gemm_body<BM, BN, EPI1, S>(a1, bid - n0, gsm);
 }
 
-template <int EPI0, int EPI1, int S = 2, int BK = GBK>
+template <int EPI0, int EPI1>
 static hipError_t launch_dual(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
-  using G = GemmGeo<128, 128, S, BK>;
+  using G = GemmGeo<128, 128, 2>;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_dual_kernel<128, 128, EPI0, EPI1, S, BK>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_dual_kernel<128, 128, EPI0, EPI1, 2>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int nwg = (a0.M / 128) * (a0.N / 128) * (a0.splitk > 1 ? a0.splitk : 1) +
                   (a1.M / 128) * (a1.N / 128) * (a1.splitk > 1 ? a1.splitk : 1);
-  hipLaunchKernelGGL((gemm_dual_kernel<128, 128, EPI0, EPI1, S, BK>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, a0, a1);
+  hipLaunchKernelGGL((gemm_dual_kernel<128, 128, EPI0, EPI1, 2>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, a0, a1);
   return hipGetLastError();
 }
 
-template <int BM, int BN, int EPI, int S = 2, int BK = GBK>
+template <int BM, int BN, int EPI, int S = 2>
 static hipError_t launch_gemm(const GemmBatch& p, hipStream_t s) {
-  using G = GemmGeo<BM, BN, S, BK>;
+  using G = GemmGeo<BM, BN, S>;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, EPI, S, BK>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, EPI, S>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
   int nwg = 0;
   for (int i = 0; i < p.n; ++i) nwg += (p.a[i].M / BM) * (p.a[i].N / BN) * (p.a[i].splitk > 1 ? p.a[i].splitk : 1);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI, S, BK>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, EPI, S>), dim3(nwg), dim3(G::NT), G::LDS_BYTES, s, p);
   return hipGetLastError();
 }
 
@@ -730,8 +723,7 @@ static hipError_t launch_gemm_w4(const GemmArgs& p, hipStream_t s) {
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
 //       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU),
-//       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output),
-//       10 / 11 = 128x128 with BK = 32 and a 4- / 3-stage LDS ring (two blocks per CU)
+//       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output)
 // shape / stride / epilogue checks of one product for a BM x BN tile (the kernel assumes whole tiles)
 static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool has_t) {
   if (!has_t && p->outT) return false;
@@ -745,8 +737,8 @@ static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool ha
 
 // n products (any shapes; same tile and epilogue) in one launch; st_gemm_nt = n 1
 extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi, int tile, hipStream_t stream) {
-  if (tile < 0 || (tile > 6 && tile != 10 && tile != 11) || n < 1 || n > st::GEMM_MAXB) return hipErrorInvalidValue;
-  const int bm = (tile == 3 || tile == 6) ? 256 : (tile == 1 ? 64 : 128);   // (10, 11: 128x128)
+  if (tile < 0 || tile > 6 || n < 1 || n > st::GEMM_MAXB) return hipErrorInvalidValue;
+  const int bm = (tile == 3 || tile == 6) ? 256 : (tile == 1 ? 64 : 128);
   const int bn = (tile == 1 || tile == 2) ? 64 : (tile == 6 ? 256 : 128);
   st::GemmBatch b;
   b.n = n;
@@ -755,11 +747,11 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
     if (!gemm_args_ok(p, epi, bm, bn, tile != 6)) return hipErrorInvalidValue;
     b.a[i] = *p;
   }
-#define ST_G(BM_, BN_, S_, ...)                                                          \
+#define ST_G(BM_, BN_, S_)                                                               \
   switch (epi) {                                                                         \
-    case 0: return st::launch_gemm<BM_, BN_, 0, S_, ##__VA_ARGS__>(b, stream);           \
-    case 1: return st::launch_gemm<BM_, BN_, 1, S_, ##__VA_ARGS__>(b, stream);           \
-    case 2: return st::launch_gemm<BM_, BN_, 2, S_, ##__VA_ARGS__>(b, stream);           \
+    case 0: return st::launch_gemm<BM_, BN_, 0, S_>(b, stream);                          \
+    case 1: return st::launch_gemm<BM_, BN_, 1, S_>(b, stream);                          \
+    case 2: return st::launch_gemm<BM_, BN_, 2, S_>(b, stream);                          \
     default: return hipErrorInvalidValue;                                                \
   }
   if (tile == 0) { ST_G(128, 128, 2) }
@@ -769,32 +761,18 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
   if (tile == 4) { ST_G(128, 128, 3) }
   if (tile == 5) { ST_G(128, 128, 4) }
   if (tile == 6) { ST_G(256, 256, 2) }
-  if (tile == 10) { ST_G(128, 128, 4, 32) }
-  if (tile == 11) { ST_G(128, 128, 3, 32) }
 #undef ST_G
   return hipErrorInvalidValue;
 }
 
 // two products of any shapes / epilogues on 128x128 tiles in one launch (epi pairs: relu-grad + f32,
 // f32 + f32, bf16 + f32)
-// kvar: 0 = BK 64, 2-stage ring; 1 = BK 32, 4 stages; 2 = BK 32, 3 stages (tiles 0 / 10 / 11)
-extern "C" hipError_t st_gemm_dual_v(const st::GemmArgs* a0, int epi0, const st::GemmArgs* a1, int epi1, int kvar,
-                                     hipStream_t stream) {
-  if (!gemm_args_ok(a0, epi0, 128, 128, true) || !gemm_args_ok(a1, epi1, 128, 128, true)) return hipErrorInvalidValue;
-#define ST_D(S_, BK_)                                                                                      \
-  if (epi0 == st::EPI_RELU_GRAD && epi1 == st::EPI_F32) return st::launch_dual<1, 2, S_, BK_>(*a0, *a1, stream); \
-  if (epi0 == st::EPI_F32 && epi1 == st::EPI_F32) return st::launch_dual<2, 2, S_, BK_>(*a0, *a1, stream);       \
-  if (epi0 == st::EPI_BF16 && epi1 == st::EPI_F32) return st::launch_dual<0, 2, S_, BK_>(*a0, *a1, stream);      \
-  return hipErrorInvalidValue;
-  if (kvar == 0) { ST_D(2, 64) }
-  if (kvar == 1) { ST_D(4, 32) }
-  if (kvar == 2) { ST_D(3, 32) }
-#undef ST_D
-  return hipErrorInvalidValue;
-}
-
 extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::GemmArgs* a1, int epi1, hipStream_t stream) {
-  return st_gemm_dual_v(a0, epi0, a1, epi1, 0, stream);
+  if (!gemm_args_ok(a0, epi0, 128, 128, true) || !gemm_args_ok(a1, epi1, 128, 128, true)) return hipErrorInvalidValue;
+  if (epi0 == st::EPI_RELU_GRAD && epi1 == st::EPI_F32) return st::launch_dual<1, 2>(*a0, *a1, stream);
+  if (epi0 == st::EPI_F32 && epi1 == st::EPI_F32) return st::launch_dual<2, 2>(*a0, *a1, stream);
+  if (epi0 == st::EPI_BF16 && epi1 == st::EPI_F32) return st::launch_dual<0, 2>(*a0, *a1, stream);
+  return hipErrorInvalidValue;
 }
 
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {

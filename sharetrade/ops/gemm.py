@@ -4,7 +4,6 @@ assumes whole tiles)."""
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import Optional
 
 import torch
@@ -14,14 +13,9 @@ from . import native
 EPI_BF16, EPI_RELU_GRAD, EPI_F32 = 0, 1, 2
 # (BM, BN) or (BM, BN, LDS stages) -> st_gemm_nt tile id (csrc/gemm_bf16.hip)
 TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2, (256, 128): 3, (128, 128, 3): 4, (128, 128, 4): 5,
-         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8, (256, 256, "w4"): 9,
-         (128, 128, "k32"): 10, (128, 128, "k32s3"): 11}
+         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8, (256, 256, "w4"): 9}
 # 7: 8-wave ping-pong, 8: the same with s_setprio on the MFMA segments, 9: 4 waves of 128x128 with
-# fragment double buffering; 7-9 are gemm_nt only (no batch / C^T / split-K).  10 / 11: 128x128 with a
-# 32-wide K tile and a 4- / 3-stage LDS ring at two blocks per CU (3 / 2 K-tiles in flight per block)
-_K32 = {"": None, "0": None, "s4": "k32", "s3": "k32s3"}
-# A/B knob: SHARETRADE_GEMM_BK32=s4|s3 puts every auto-picked 128x128 product and gemm_dual on those rings
-K32 = _K32[os.environ.get("SHARETRADE_GEMM_BK32", "")]
+# fragment double buffering; 7-9 are gemm_nt only (no batch / C^T / split-K)
 
 
 class GemmArgs(C.Structure):
@@ -42,8 +36,6 @@ def _bind():
         L.st_gemm_nt_batched.restype = C.c_int
         L.st_gemm_dual.argtypes = [C.POINTER(GemmArgs), C.c_int, C.POINTER(GemmArgs), C.c_int, C.c_void_p]
         L.st_gemm_dual.restype = C.c_int
-        L.st_gemm_dual_v.argtypes = [C.POINTER(GemmArgs), C.c_int, C.POINTER(GemmArgs), C.c_int, C.c_int, C.c_void_p]
-        L.st_gemm_dual_v.restype = C.c_int
         L._gemm_bound = True
     return L
 
@@ -51,7 +43,7 @@ def _bind():
 def pick_tile(M: int, N: int) -> tuple:
     """128x128 when that still gives >= ~256 workgroups, else smaller tiles."""
     if M % 128 == 0 and N % 128 == 0 and (M // 128) * (N // 128) >= 200:
-        return (128, 128, K32) if K32 else (128, 128)
+        return (128, 128)
     if M % 128 == 0 and N % 64 == 0 and (M // 128) * (N // 64) >= 200:
         return (128, 64)
     return (64, 64)
@@ -167,7 +159,7 @@ def gemm_nt_batched(problems, epi: int = EPI_BF16, tile=None) -> None:
                  "st_gemm_nt_batched")
 
 
-def gemm_dual(first, epi0: int, second, epi1: int, kvar: Optional[int] = None) -> None:
+def gemm_dual(first, epi0: int, second, epi1: int) -> None:
     """Two products of any shapes / epilogues on 128x128 tiles in ONE launch (``first`` / ``second``
     = ``(A, B, out, kwargs)``; epilogue pairs relu-grad + f32, f32 + f32, bf16 + f32): e.g. a layer's
     data gradient beside the next layer's split-K weight gradient, with no stream fork / join."""
@@ -184,7 +176,4 @@ def gemm_dual(first, epi0: int, second, epi1: int, kvar: Optional[int] = None) -
         if g.M % 128 or g.N % 128 or g.K % 64:
             raise ValueError(f"gemm_dual: shape {g.M}x{g.N}x{g.K} not a multiple of 128x128 / BK 64")
         args.append(g)
-    if kvar is None:   # 0: BK 64, 2 stages; 1 / 2: BK 32, 4 / 3 stages (tiles 10 / 11)
-        kvar = {None: 0, "k32": 1, "k32s3": 2}[K32]
-    native.check(_bind().st_gemm_dual_v(args[0], epi0, args[1], epi1, int(kvar), native.stream_handle()),
-                 "st_gemm_dual")
+    native.check(_bind().st_gemm_dual(args[0], epi0, args[1], epi1, native.stream_handle()), "st_gemm_dual")

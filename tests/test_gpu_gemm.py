@@ -14,9 +14,7 @@ def _bf(shape, seed, scale=1.0):
                                         (128, 192, 64, (64, 64)), (4096, 64, 1024, (128, 64)),
                                         (1024, 1024, 4096, (64, 64)), (512, 256, 256, (256, 128)),
                                         (256, 256, 128, (128, 128, 4)), (512, 1024, 1024, (128, 128, 3)),
-                                        (256, 512, 64, (128, 128, 3)), (512, 256, 1024, (128, 128, 4)),
-                                        (512, 1024, 1024, (128, 128, "k32")), (256, 256, 64, (128, 128, "k32")),
-                                        (256, 512, 128, (128, 128, "k32s3")), (512, 256, 1024, (128, 128, "k32s3"))])
+                                        (256, 512, 64, (128, 128, 3)), (512, 256, 1024, (128, 128, 4))])
 def test_gemm_f32_epilogue(native_built, M, N, K, tile):
     from sharetrade.ops.gemm import EPI_F32, gemm_nt
 
@@ -32,8 +30,7 @@ def test_gemm_f32_epilogue(native_built, M, N, K, tile):
     assert torch.allclose(out, 2 * ref, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("tile", [(128, 128), (64, 64), (256, 128), (128, 128, 3), (128, 128, 4), (128, 128, "k32"),
-                                  (128, 128, "k32s3")])
+@pytest.mark.parametrize("tile", [(128, 128), (64, 64), (256, 128), (128, 128, 3), (128, 128, 4)])
 def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     from sharetrade.ops.gemm import EPI_BF16, gemm_nt
 
@@ -49,7 +46,7 @@ def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     assert torch.equal(outT, out.t().contiguous())
 
 
-@pytest.mark.parametrize("tile", [(64, 64), (256, 128), (128, 128, 4), (128, 128, "k32")])
+@pytest.mark.parametrize("tile", [(64, 64), (256, 128), (128, 128, 4)])
 def test_gemm_relu_grad_epilogue(native_built, tile):
     from sharetrade.ops.gemm import EPI_RELU_GRAD, gemm_nt
 
@@ -238,42 +235,3 @@ def test_gemm_dual_equals_two_launches(native_built, sk):
         assert torch.equal(o1, r1)
     else:
         assert torch.allclose(o1, r1, rtol=1e-5, atol=1e-4)
-
-
-@pytest.mark.parametrize("tile,kvar", [((128, 128, "k32"), 1), ((128, 128, "k32s3"), 2)])
-def test_gemm_bk32_rings_bit_identical(native_built, tile, kvar):
-    """The 32-wide K tile rings run the same MFMA sequence in the same k order as the 64-wide 2-stage
-    kernel: batched (C + C^T) and dual (relu-grad + split-K f32) results are bit-identical."""
-    from sharetrade.ops.gemm import EPI_BF16, EPI_F32, EPI_RELU_GRAD, gemm_dual, gemm_nt, gemm_nt_batched
-
-    M, N, K = 1024, 512, 1024
-    A, B, A2 = _bf((M, K), 51), _bf((N, K), 52), _bf((M, K), 53)
-    bias = torch.randn(N, device="cuda")
-    outs = {}
-    for t in ((128, 128), tile):
-        o1 = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-        o1T = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
-        o2 = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-        gemm_nt_batched([(A, B, o1, dict(outT=o1T, bias=bias, relu=True)), (A2, B, o2, dict(bias=bias, relu=True))],
-                        EPI_BF16, tile=t)
-        outs[t] = (o1, o1T, o2)
-    torch.cuda.synchronize()
-    for a, b in zip(outs[(128, 128)], outs[tile]):
-        assert torch.equal(a, b)
-    # dual: G = (G_l . W) * mask with C^T beside dW = G_l^T . X (split-K 4)
-    M1, N1, K1 = 256, 384, 1024
-    A1, B1 = _bf((M1, K1), 54), _bf((N1, K1), 55)
-    aux = torch.relu(torch.randn(N, M, device="cuda")).to(torch.bfloat16)
-    res = []
-    for kv in (0, kvar):
-        g, gT = torch.empty(M, N, dtype=torch.bfloat16, device="cuda"), torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
-        d1 = torch.empty(M1, N1, device="cuda")
-        gemm_dual((A, B, g, dict(outT=gT, auxT=aux)), EPI_RELU_GRAD, (A1, B1, d1, dict(splitk=1)), EPI_F32, kvar=kv)
-        res.append((g, gT, d1))
-    torch.cuda.synchronize()
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
-    ref = A1.float() @ B1.float().t()
-    assert float((res[1][2] - ref).abs().max() / ref.abs().max()) < 1e-5
-    with pytest.raises(ValueError):   # split-K must divide the 64-wide K-tiles (host check)
-        gemm_nt(A, B, torch.empty(M, N, device="cuda"), EPI_F32, tile=tile, splitk=3)
