@@ -78,22 +78,16 @@ struct GemmGeo {
   static_assert(LDS_BYTES * MINB <= 163840, "LDS per CU");
 };
 
-// 16-B chunk swizzle of a staged row: BK = 64 (128-B rows) XOR (r & 7); BK = 32 (64-B rows) XOR ((r >> 1) & 3)
-// -- both conflict-free for the 16x16x32 fragment reads (tools/lds_bank_sim.py model)
-template <int BK>
-ST_DEV int chunk_swz(int r) { return BK == 64 ? (r & 7) : ((r >> 1) & 3); }
-
-// stage one operand tile (ROWS x BK bf16) of K-tile k0 into a linear LDS image with the
-// chunk swizzle moved to the source address.  ROWS*BK/8 16-B pieces, 64 per wave-instruction.
-template <int ROWS, int NWAVE = GT / 64, int BK = GBK>
+// stage one operand tile (ROWS x 64 bf16) of K-tile k0 into a linear LDS image with the
+// chunk swizzle moved to the source address.  ROWS*8 16-B pieces, 64 per wave-instruction.
+template <int ROWS, int NWAVE = GT / 64>
 ST_DEV void stage_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, bf16_t* lds, int wave, int lane) {
-  constexpr int CPR = BK / 8;              // 16-B chunks per row
-  constexpr int INSTR = ROWS * CPR / 64;   // wave-instructions per tile
+  constexpr int INSTR = ROWS / 8;        // wave-instructions per tile
 #pragma unroll
   for (int j = wave; j < INSTR; j += NWAVE) {
-    const int r = j * (64 / CPR) + lane / CPR;
-    const int c = lane % CPR;
-    const int g = c ^ chunk_swz<BK>(r);
+    const int r = j * 8 + (lane >> 3);
+    const int c = lane & 7;
+    const int g = c ^ (r & 7);
     const bf16_t* src = G + (size_t)(row0 + r) * ld + k0 + g * 8;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(lds + j * 512), 16, 0, 0);
@@ -101,9 +95,8 @@ ST_DEV void stage_tile(const bf16_t* __restrict__ G, int ld, int row0, int k0, b
 }
 
 // fragment (8 bf16) of row r, global chunk g of a staged tile
-template <int BK = GBK>
 ST_DEV s8v frag_sw(const bf16_t* lds, int r, int g) {
-  return lds_ld8(lds + r * BK + ((g ^ chunk_swz<BK>(r)) << 3));
+  return lds_ld8(lds + r * GBK + ((g ^ (r & 7)) << 3));
 }
 
 template <int BM, int BN> constexpr int gemm_threads() { return (BM >= 256 && BN < 256) ? 512 : 256; }
@@ -726,174 +719,11 @@ static hipError_t launch_gemm_w4(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-
-// ---------------------------------------------------------------- 256x256, 4 waves of 128x128, deep LDS ring
-// The w4 structure (one wave per SIMD, a 128x128 AGPR accumulator block, 4 MFMAs per fragment read) with
-// 32-wide K-tiles in a W4K_S-stage ring of 32 KB stages (5 x 32 KB = the whole LDS).  Phase t multiplies
-// K-tile t from registers (64 MFMAs) while it reads K-tile t+1's fragments into the other register set;
-// the barrier that opens phase t also retires every wave's reads of K-tile t, so its buffer is restaged
-// at once with K-tile t + S.  A K-tile is therefore issued S - 1 phases before the wait that needs it
-// (w4: 2 phases, one 64-wide K-tile), with S - 1 tiles of LDS-DMA in flight per wave.
-namespace w4k {
-constexpr int NT = 256, BK = 32, S = 5;
-constexpr int TILE = 256 * BK;                          // one operand of one K-tile (elements)
-constexpr int BUF = 2 * TILE;                           // A + B
-constexpr int KLOOP_BYTES = S * BUF * 2;                // 160 KB
-constexpr int LPT = 2 * (256 * BK / 512) / 4;           // LDS-DMA instructions per wave per K-tile (8)
-constexpr int SC = 256 + 8;
-constexpr int EPI_BYTES = 256 * SC * 2;
-constexpr int LDS_BYTES = KLOOP_BYTES > EPI_BYTES ? KLOOP_BYTES : EPI_BYTES;
-static_assert(LDS_BYTES <= 163840, "LDS");
-static_assert((S - 1) * LPT < 64, "vmcnt");
-}  // namespace w4k
-
-template <int EPI>
-__global__ void __launch_bounds__(256, 1) gemm_w4k_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char gsm[];
-  bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
-  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntn = p.N / 256, ntm = p.M / 256;
-  const int bid = xcd_remap(blockIdx.x, ntn * ntm);
-  const int m0 = (bid / ntn) * 256, n0 = (bid % ntn) * 256;
-  const int nk = p.K / w4k::BK;
-  constexpr int S = w4k::S;
-
-  auto stage = [&](int kt) {   // both operands of K-tile kt into ring slot kt % S (8 global_load_lds per thread)
-    if (kt < nk) {
-      bf16_t* b = buf + (kt % S) * w4k::BUF;
-      stage_tile<256, 4, 32>(p.A, p.lda, m0, kt * w4k::BK, b, wave, lane);
-      stage_tile<256, 4, 32>(p.B, p.ldb, n0, kt * w4k::BK, b + w4k::TILE, wave, lane);
-    }
-  };
-  s8v Fa[8], Fb[8], Ga[8], Gb[8];
-  auto read = [&](s8v (&fa)[8], s8v (&fb)[8], int kt) {
-    const bf16_t* bA = buf + (kt % S) * w4k::BUF;
-    const bf16_t* bB = bA + w4k::TILE;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = frag_sw<32>(bA, wr * 128 + 16 * i + l16, g4);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fb[j] = frag_sw<32>(bB, wc * 128 + 16 * j + l16, g4);
-  };
-  f4v acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = zero4();
-  auto mma = [&](const s8v (&fa)[8], const s8v (&fb)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[j]));
-  };
-  // open phase t: K-tile t+1 landed (this wave's part; the newer tiles t+2 .. t+S-1 may still fly), this
-  // wave's fragment reads of K-tile t retired, then every wave past the barrier
-  auto open = [&](int t) {
-    if (t + S - 1 < nk) pp::wait_vm_lgkm0<(S - 2) * w4k::LPT>(); else pp::wait_vm_lgkm0<0>();
-    pp::barrier();
-  };
-
-  // prologue: K-tiles 0 .. S-1 in flight, K-tile 0 landed and visible, its fragments read
-#pragma unroll
-  for (int kt = 0; kt < S; ++kt) stage(kt);
-  if (nk >= S) pp::wait_vm_lgkm0<(S - 1) * w4k::LPT>(); else pp::wait_vm_lgkm0<0>();
-  pp::barrier();
-  read(Fa, Fb, 0);
-  // two phases per trip (the register sets alternate; nk is even: the host requires K % 64 == 0).  One
-  // uniform loop body and no peeled tail: a tail made the allocator re-home the accumulators with
-  // v_accvgpr_mov right behind the asm MFMAs, whose result hazards it does not see.  The last trip re-reads
-  // K-tile nk-1 (still resident: never restaged) instead of a conditional read.
-  for (int t = 0; t < nk; t += 2) {
-    open(t);
-    stage(t + S);
-    read(Ga, Gb, t + 1);
-    mma(Fa, Fb);
-    open(t + 1);
-    stage(t + 1 + S);
-    read(Fa, Fb, min(t + 2, nk - 1));
-    mma(Ga, Gb);
-  }
-  // the hazard recognizer does not see through the asm MFMAs: cover the last MFMAs' result latency.  The
-  // accumulators the last eight MFMAs wrote are operands of the nop block, so no accvgpr read of them can be
-  // scheduled above it (a plain volatile asm did not stop that: the loop exit read a254 two instructions
-  // after the last MFMA); every other accumulator was written >= 8 MFMAs earlier
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7"
-               : "+a"(acc[7][7]), "+a"(acc[7][6]), "+a"(acc[7][5]), "+a"(acc[7][4]), "+a"(acc[7][3]),
-                 "+a"(acc[7][2]), "+a"(acc[7][1]), "+a"(acc[7][0])::"memory");
-  pp::wait_vm_lgkm0<0>();
-  pp::barrier();   // every wave is done with the ring
-
-  // ------------------------------------------------------------------ epilogues (as gemm_w4_kernel)
-  const int wm0 = wr * 128, wn0 = wc * 128;
-  float bj[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bj[j] = 0.f;
-  if (p.bias) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bj[j] = p.bias[n0 + wn0 + 16 * j + l16];
-  }
-  if constexpr (EPI == EPI_F32) {
-    float* out = reinterpret_cast<float*>(p.out);
-    auto store = [&](auto accumulate) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int n = n0 + wn0 + 16 * j + l16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm0 + 16 * i + 4 * g4 + r;
-            float* o = out + (size_t)m * p.ldo + n;
-            const float v = p.alpha * acc[i][j][r] + bj[j];
-            if constexpr (decltype(accumulate)::value) *o += v; else *o = v;
-          }
-        }
-    };
-    if (p.accumulate) store(std::true_type{}); else store(std::false_type{});
-  } else {
-    bf16_t* sC = buf;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int nl = wn0 + 16 * j + l16, ml = wm0 + 16 * i + 4 * g4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = p.alpha * acc[i][j][r] + bj[j];
-          sC[(ml + r) * w4k::SC + nl] = f2bf(p.relu ? fmaxf(x, 0.f) : x);
-        }
-      }
-    __syncthreads();
-    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-    for (int c = tid; c < 256 * 32; c += w4k::NT) {
-      const int r = c >> 5, k = (c & 31) * 8;
-      *reinterpret_cast<uint4*>(out + (size_t)(m0 + r) * p.ldo + n0 + k) = *reinterpret_cast<const uint4*>(sC + r * w4k::SC + k);
-    }
-  }
-}
-
-template <int EPI>
-static hipError_t launch_gemm_w4k(const GemmArgs& p, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_w4k_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       w4k::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL((gemm_w4k_kernel<EPI>), dim3((p.M / 256) * (p.N / 256)), dim3(w4k::NT), w4k::LDS_BYTES, s, p);
-  return hipGetLastError();
-}
-
 }  // namespace st
 
 // tile: 0 = 128x128, 1 = 64x64, 2 = 128x64, 3 = 256x128 (BM x BN; 3 runs 8 waves),
 //       4 / 5 = 128x128 with a 3- / 4-stage LDS ring (one block per CU),
-//       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output);
-// st_gemm_nt only: 7 / 8 = 256x256 ping-pong (8: s_setprio), 9 = 4 waves of 128x128 (w4), 10 = w4 with a
-// 5-stage ring of 32-wide K-tiles (w4k)
+//       6 = 256x256 (4 waves of 128x128, one block per CU; no transposed output)
 // shape / stride / epilogue checks of one product for a BM x BN tile (the kernel assumes whole tiles)
 static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool has_t) {
   if (!has_t && p->outT) return false;
@@ -946,14 +776,6 @@ extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::G
 }
 
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
-  if (tile == 10) {   // 256x256, 4 waves of 128x128, 5-stage ring of 32-wide K-tiles (as tile 9's limits)
-    if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
-    if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)
-      return hipErrorInvalidValue;
-    if (epi == st::EPI_BF16) return st::launch_gemm_w4k<st::EPI_BF16>(*p, stream);
-    if (epi == st::EPI_F32) return st::launch_gemm_w4k<st::EPI_F32>(*p, stream);
-    return hipErrorInvalidValue;
-  }
   if (tile == 9) {   // 256x256, 4 waves of 128x128 (bf16 / fp32 epilogues, no C^T, no split-K)
     if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
     if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)

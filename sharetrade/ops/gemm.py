@@ -4,7 +4,6 @@ assumes whole tiles)."""
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import Optional
 
 import torch
@@ -14,11 +13,9 @@ from . import native
 EPI_BF16, EPI_RELU_GRAD, EPI_F32 = 0, 1, 2
 # (BM, BN) or (BM, BN, LDS stages) -> st_gemm_nt tile id (csrc/gemm_bf16.hip)
 TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2, (256, 128): 3, (128, 128, 3): 4, (128, 128, 4): 5,
-         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8, (256, 256, "w4"): 9, (256, 256, "w4k"): 10}
+         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8, (256, 256, "w4"): 9}
 # 7: 8-wave ping-pong, 8: the same with s_setprio on the MFMA segments, 9: 4 waves of 128x128 with
-# fragment double buffering, 10: the same with a 5-stage ring of 32-wide K-tiles; 7-10 are gemm_nt only
-# (no batch / C^T / split-K)
-_BIG = ("pp", "ppp", "w4", "w4k")
+# fragment double buffering; 7-9 are gemm_nt only (no batch / C^T / split-K)
 
 
 class GemmArgs(C.Structure):
@@ -104,8 +101,6 @@ def pick_splitk(M: int, N: int, K: int, tile) -> int:
 
 
 PINGPONG = True   # auto_tile may pick the ping-pong kernel (benchmarks/bench_deep.py --no-pingpong turns it off)
-# the 256x256 kernel auto_tile picks (A/B knob SHARETRADE_GEMM_BIG=w4k)
-BIG_TILE = (256, 256, os.environ.get("SHARETRADE_GEMM_BIG", "pp"))
 
 
 def auto_tile(M: int, N: int, epi: int, kw: dict) -> tuple:
@@ -114,7 +109,7 @@ def auto_tile(M: int, N: int, epi: int, kw: dict) -> tuple:
     pick_tile."""
     if (PINGPONG and epi != EPI_RELU_GRAD and kw.get("outT") is None and kw.get("splitk", 1) in (1, "auto") and
             M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= 256):
-        return BIG_TILE
+        return (256, 256, "pp")
     return pick_tile(M, N)
 
 
@@ -122,7 +117,7 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_
     """``out = A . B^T`` (+ epilogue).  ``splitk="auto"`` (fp32 epilogue only) splits long-K,
     few-tile products (weight gradients) over extra workgroups with atomic accumulation."""
     t = tile or auto_tile(A.shape[0], B.shape[0], epi, kw)
-    if len(t) == 3 and t[2] in _BIG and kw.get("splitk", 1) == "auto":
+    if len(t) == 3 and t[2] in ("pp", "ppp", "w4") and kw.get("splitk", 1) == "auto":
         kw = dict(kw, splitk=1)
     sk = kw.pop("splitk", 1)
     prezeroed = kw.pop("prezeroed", False)   # split-K output already zeroed by an earlier kernel

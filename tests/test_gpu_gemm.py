@@ -176,7 +176,7 @@ def test_gemm_grouped_mixed_shapes(native_built):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 1024),
-                                   (2048, 1024, 512), (512, 512, 320)])
+                                   (2048, 1024, 512)])
 def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     """256x256 ping-pong kernel (8 waves, two groups one barrier interval apart, LDS-DMA staging with
     counted waits): bit-identical to the 128x128 kernel (same k order per output), both epilogues;
@@ -189,7 +189,7 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     ref = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     gemm_nt(A, B, ref, EPI_BF16, tile=(128, 128), bias=bias, relu=True)
     out = torch.empty_like(ref)
-    for t in ((256, 256, "pp"), (256, 256, "w4"), (256, 256, "w4k")):
+    for t in ((256, 256, "pp"), (256, 256, "w4")):
         for _ in range(3):
             out.fill_(7)
             gemm_nt(A, B, out, EPI_BF16, tile=t, bias=bias, relu=True)
@@ -201,10 +201,8 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     o32 = torch.full((M, N), float("nan"), device="cuda")
     gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), bias=bias, alpha=0.5)
     gemm_nt(A, B, o32w, EPI_F32, tile=(256, 256, "w4"), bias=bias, alpha=0.5)
-    o32k = torch.full((M, N), float("nan"), device="cuda")
-    gemm_nt(A, B, o32k, EPI_F32, tile=(256, 256, "w4k"), bias=bias, alpha=0.5)
     torch.cuda.synchronize()
-    assert torch.equal(o32, r32) and torch.equal(o32w, r32) and torch.equal(o32k, r32)
+    assert torch.equal(o32, r32) and torch.equal(o32w, r32)
     gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), alpha=0.5, accumulate=True)
     full = 0.5 * (A.float() @ B.float().t())
     torch.cuda.synchronize()

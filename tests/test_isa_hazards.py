@@ -31,3 +31,20 @@ def test_scanner_flags_the_qtarget_pattern():
     ok = bad.replace("\tv_cvt_pk_bf16_f32", "\ts_nop 3\n\tv_cvt_pk_bf16_f32")
     chain = bad.replace("16x16x16_bf16 a[56:59], v[150:151]", "16x16x32_bf16 a[56:59], v[150:153]")
     assert len(scan(bad)) == 1 and scan(ok) == [] and scan(chain) == []
+
+
+def test_scanner_follows_the_loop_exit_fall_through():
+    """The w4k GEMM's first form: the loop exit read an accumulator two instructions after the loop's last
+    (inline-asm) MFMA, behind a conditional branch."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from mfma_hazard_scan import scan
+
+    bad = """k:
+\tv_mfma_f32_16x16x32_bf16 a[252:255], v[66:69], v[70:73], a[252:255]
+\ts_cbranch_scc1 .LBB24_74
+\tv_accvgpr_read_b32 v1, a254
+"""
+    ok = bad.replace("\tv_accvgpr_read_b32", "\ts_nop 7\n\tv_accvgpr_read_b32")
+    jump = bad.replace("s_cbranch_scc1", "s_branch")
+    mov = bad.replace("v_accvgpr_read_b32 v1, a254", "v_accvgpr_mov_b32 a0, a254")
+    assert len(scan(bad)) == 1 and scan(ok) == [] and scan(jump) == [] and len(scan(mov)) == 1

@@ -82,15 +82,20 @@ def scan(text):
             n = int(ops[0], 0) + 1 if ops else 1
             live = [(p, o, d, ws + n) for p, o, d, ws in live]
             continue
-        if op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_endpgm")):
+        # an unconditional transfer ends the straight-line path; a conditional branch does not (its
+        # fall-through continues: a loop exit that reads an accumulator right after the loop's last MFMA
+        # is such a path)
+        if op.startswith(("s_branch", "s_setpc", "s_endpgm")):
             live = []
+            continue
+        if op.startswith("s_cbranch"):
             continue
         if op.startswith("v_mfma") and len(ops) >= 4:
             srcc = regs(ops[3])
             for p, o, d, ws in live:
                 if op.startswith(SRCC_CONSUMERS) and srcc & d and ws < need(o, "srcc"):
                     hits.append((fn, "SrcC", ws, need(o, "srcc"), p, line))
-        elif op == "v_accvgpr_read_b32" and len(ops) >= 2:
+        elif op in ("v_accvgpr_read_b32", "v_accvgpr_mov_b32") and len(ops) >= 2:   # (mov: AGPR source, unmeasured; same rule)
             src = regs(ops[1])
             for p, o, d, ws in live:
                 if src & d and ws < need(o, "acc"):
