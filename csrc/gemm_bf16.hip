@@ -650,9 +650,13 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p) {
   mma(F0a, F0b);
   mma(F1a, F1b);
 #if ST_W4_ASM
-  // the hazard recognizer does not see through the asm MFMAs: cover the last MFMA's result latency
-  // before the epilogue's accumulator reads
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  // the hazard recognizer does not see through the asm MFMAs: cover the last MFMAs' result latency before
+  // the epilogue's accumulator reads.  The accumulators the last eight MFMAs wrote are operands of the nop
+  // block, so the compiler cannot schedule a read of them above it (a plain volatile asm does not order
+  // register reads; profiles/r5_gemm_w4k.md)
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7"
+               : "+a"(acc[7][7]), "+a"(acc[7][6]), "+a"(acc[7][5]), "+a"(acc[7][4]), "+a"(acc[7][3]),
+                 "+a"(acc[7][2]), "+a"(acc[7][1]), "+a"(acc[7][0])::"memory");
 #endif
   pp::wait_vm_lgkm0<0>();
   pp::barrier();   // every wave is done with the K-loop buffers
