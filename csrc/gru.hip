@@ -651,14 +651,24 @@ __global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
     v.slot = w[15 * 64];
     return v;
   };
-  auto env_st = [&](auto sl, const ActEnv& v) {
+  // (next = false: the next step's cB / rB / fB are not stored -- the env phase DMAs them in)
+  auto env_st = [&](auto sl, const ActEnv& v, bool next = true) {
     unsigned* w = reinterpret_cast<unsigned*>(base(sl) + Act2Lds::ENV) + lane;
     w[0 * 64] = (unsigned)v.t; w[1 * 64] = (unsigned)v.es; w[2 * 64] = (unsigned)v.pz; w[3 * 64] = (unsigned)v.eps;
     w[4 * 64] = __float_as_uint(v.en); w[5 * 64] = __float_as_uint(v.er); w[6 * 64] = __float_as_uint(v.lr);
-    w[7 * 64] = __float_as_uint(v.cA); w[8 * 64] = __float_as_uint(v.cB);
-    w[9 * 64] = __float_as_uint(v.rA); w[10 * 64] = __float_as_uint(v.rB);
-    w[11 * 64] = v.fB.x; w[12 * 64] = v.fB.y; w[13 * 64] = v.fB.z; w[14 * 64] = v.fB.w;
+    w[7 * 64] = __float_as_uint(v.cA);
+    w[9 * 64] = __float_as_uint(v.rA);
+    if (next) {
+      w[8 * 64] = __float_as_uint(v.cB);
+      w[10 * 64] = __float_as_uint(v.rB);
+      w[11 * 64] = v.fB.x; w[12 * 64] = v.fB.y; w[13 * 64] = v.fB.z; w[14 * 64] = v.fB.w;
+    }
     w[15 * 64] = v.slot;
+  };
+  // one dword per lane from global memory into LDS at base + 4 * lane (LDS-DMA; base wave-uniform)
+  auto dma4 = [&](const void* src, unsigned* base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)base, 4, 0, 0);
   };
 
   // load a chunk into a slot: h (fp32 registers + fp8 LDS tile 0), env state (wave 0), x_0, Philox draws
@@ -796,6 +806,9 @@ __global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
     int* sDone = reinterpret_cast<int*>(sb + Act2Lds::DN);
     const int me = e0_[K] + (lane & (RN - 1));
     const bool valid = valid_[K];
+    // this slot's LDS-DMA of cB / rB / fB (issued by this wave in its previous env phase, two barrier
+    // intervals ago) has landed: vmcnt(0) (a workgroup barrier does not wait for a wave's own loads)
+    __builtin_amdgcn_s_waitcnt(0xF70);
     ActEnv v = env_ld(sl);
     float q[3];
 #pragma unroll
@@ -877,10 +890,17 @@ __global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
     v.cA = cx;
     v.rA = rx;
     const size_t o1 = (size_t)me * p.T + min(v.t + 1, p.T - 1);
-    v.cB = p.close[o1];
-    v.rB = p.ret[o1];
-    v.fB = *reinterpret_cast<const uint4*>(p.feat + o1 * RMF);
-    env_st(sl, v);
+    // the next step's close / return / bar features go straight from HBM into the parked env state by
+    // LDS-DMA (one dword per lane and field, the parking layout): nothing in this env phase waits for them
+    // -- they land behind the other slot's MFMA phase, and the barrier closing it retires them (a register
+    // load stored with the rest of the state held the env phase for a whole HBM round trip)
+    env_st(sl, v, false);
+    unsigned* w = reinterpret_cast<unsigned*>(base(sl) + Act2Lds::ENV);
+    dma4(p.close + o1, w + 8 * 64);             // cB
+    dma4(p.ret + o1, w + 10 * 64);             // rB
+    const unsigned* f = reinterpret_cast<const unsigned*>(p.feat + o1 * RMF);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma4(f + j, w + (11 + j) * 64);   // fB
   };
 
   // h of envs whose episode ended restarts from 0 (after the env phase's barrier)
