@@ -203,6 +203,8 @@ struct GruAct {
   float* stats;                // [4] reward sum, explore count, episodes done, finished-episode return sum
   float* q_out;                // optional [E][4]: Q of the last step (tests)
   unsigned long long* stamps;  // optional debug: s_memtime of workgroup 0, waves 0 and 1: [step][2][8]
+  unsigned* done_ctr;          // optional (pair actor): workgroups finished; the last one advances rctrl /
+                               // ctrl itself and re-zeroes it (else a separate advance launch follows)
 };
 
 struct ActLds {
@@ -986,6 +988,20 @@ __global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
       atomicAdd(p.stats + 3, st_fin);
     }
   }
+  // the launch's counters advance in its last workgroup (every workgroup read them at its start, and the
+  // last one to finish runs after all of those reads): no separate one-thread launch on the iteration's
+  // critical path
+  if (p.done_ctr != nullptr && tid == 0) {
+    __threadfence();
+    if (atomicAdd(p.done_ctr, 1u) == gridDim.x - 1) {
+      const unsigned long long w = p.rctrl[0] + (unsigned long long)p.E;
+      p.rctrl[0] = w;
+      p.rctrl[1] = w < (unsigned long long)p.cap ? w : (unsigned long long)p.cap;
+      p.ctrl[0] = p.ctrl[0] + 1;
+      *p.done_ctr = 0u;
+      __threadfence();
+    }
+  }
 }
 
 __global__ void gru_advance_kernel(unsigned long long* rctrl, unsigned long long* ctrl, int E, int cap) {
@@ -1054,7 +1070,8 @@ extern "C" hipError_t st_gru_act_pair(const st::GruAct* p, int grid, hipStream_t
   const int npairs = (p->E / st::RN + 1) / 2;
   hipLaunchKernelGGL(st::gru_act_pair_kernel, dim3(grid < npairs ? grid : npairs), dim3(st::RT), st::Act2Lds::BYTES,
                      s, *p);
-  hipLaunchKernelGGL(st::gru_advance_kernel, dim3(1), dim3(1), 0, s, p->rctrl, p->ctrl, p->E, p->cap);
+  if (p->done_ctr == nullptr)   // (else the kernel's last workgroup advanced the counters)
+    hipLaunchKernelGGL(st::gru_advance_kernel, dim3(1), dim3(1), 0, s, p->rctrl, p->ctrl, p->E, p->cap);
   return hipGetLastError();
 }
 

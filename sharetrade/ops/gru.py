@@ -53,7 +53,8 @@ class ActArgs(C.Structure):
                 ("entry", C.c_void_p), ("ep_ret", C.c_void_p), ("episodes", C.c_void_p), ("last_ret", C.c_void_p),
                 ("rx", C.c_void_p), ("ra", C.c_void_p), ("rr", C.c_void_p), ("rd", C.c_void_p), ("rh0", C.c_void_p),
                 ("rctrl", C.c_void_p), ("cap", C.c_int), ("key0", C.c_uint32), ("key1", C.c_uint32),
-                ("ctrl", C.c_void_p), ("stats", C.c_void_p), ("q_out", C.c_void_p), ("stamps", C.c_void_p)]
+                ("ctrl", C.c_void_p), ("stats", C.c_void_p), ("q_out", C.c_void_p), ("stamps", C.c_void_p),
+                ("done_ctr", C.c_void_p)]
 
 
 class GatherArgs(C.Structure):

@@ -170,6 +170,9 @@ class RecurrentDQN:
         self.rh0 = torch.zeros(self.cap, HID, dtype=b16, device=dev)
         self.rctrl = torch.zeros(2, dtype=torch.int64, device=dev)
         self.ctrl = torch.zeros(1, dtype=torch.int64, device=dev)
+        # the pair actor's finished-workgroup count (its last workgroup advances rctrl / ctrl; always 0
+        # between launches)
+        self._act_done = torch.zeros(1, dtype=torch.int32, device=dev)
         self.stats = torch.zeros(4, device=dev)
         self.loss = torch.zeros(1, device=dev)
         # ---------------------------------------------------------------- learner buffers (time-major rows t*B + b)
@@ -238,6 +241,7 @@ class RecurrentDQN:
             a.rctrl, a.cap = self.rctrl.data_ptr(), self.cap
             a.key0, a.key1 = (int(x) for x in rng.key_for(self.seed, 5))
             a.ctrl, a.stats, a.q_out = self.ctrl.data_ptr(), self.stats.data_ptr(), None
+            a.done_ctr = self._act_done.data_ptr()   # (used by the pair actor only)
             self._acts.append(a)
         self._packs = {}
         for net, src in (("on0", self.P), ("on1", self.P), ("tg", self.T_P)):
