@@ -168,7 +168,7 @@ struct DeepEnv {
   const float* q;             // [E, ldq] fp32 Q(x)
   int ldq;
   uint32_t key0, key1;
-  unsigned long long* ctrl;   // [0] = env step counter
+  unsigned long long* ctrl;   // [0] = env step counter, [1] = finished blocks of the running env step
   Replay rp;
   float* stats;               // [4]: reward sum, explore count, episodes done, final sum (atomics)
 };
@@ -242,13 +242,22 @@ __global__ void __launch_bounds__(256) deep_env_step_kernel(DeepEnv p) {
     atomicAdd(p.stats + 0, r_);
     atomicAdd(p.stats + 1, x_);
   }
-}
-
-// ring cursor advance after an env step (one thread): cursor += E, size = min(cursor, cap); step += 1
-__global__ void deep_advance_kernel(unsigned long long* rctrl, unsigned long long* ectrl, int E, int cap) {
-  rctrl[0] += (unsigned long long)E;
-  rctrl[1] = rctrl[0] < (unsigned long long)cap ? rctrl[0] : (unsigned long long)cap;
-  ectrl[0] += 1;
+  // the ring cursor / step counter advance in the launch's last block (every thread read them above, and
+  // the last block to finish runs after all of those reads): no one-thread launch behind the env step.
+  // ctrl[1] counts finished blocks (0 between launches).
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    unsigned* done_blocks = reinterpret_cast<unsigned*>(p.ctrl + 1);
+    if (atomicAdd(done_blocks, 1u) == gridDim.x - 1) {
+      const unsigned long long w = p.rp.ctrl[0] + (unsigned long long)p.E;
+      p.rp.ctrl[0] = w;
+      p.rp.ctrl[1] = w < (unsigned long long)p.rp.cap ? w : (unsigned long long)p.rp.cap;
+      p.ctrl[0] = step + 1;
+      *done_blocks = 0u;
+      __threadfence();
+    }
+  }
 }
 
 struct DeepTD {
@@ -578,8 +587,7 @@ extern "C" hipError_t st_deep_gather(const st::DeepGather* g, hipStream_t s) {
 }
 
 extern "C" hipError_t st_deep_env_step(const st::DeepEnv* p, hipStream_t s) {
-  hipLaunchKernelGGL(st::deep_env_step_kernel, dim3((p->E + 255) / 256), dim3(256), 0, s, *p);
-  hipLaunchKernelGGL(st::deep_advance_kernel, dim3(1), dim3(1), 0, s, p->rp.ctrl, p->ctrl, p->E, p->rp.cap);
+  hipLaunchKernelGGL(st::deep_env_step_kernel, dim3((p->E + 255) / 256), dim3(256), 0, s, *p);   // (advances too)
   return hipGetLastError();
 }
 
