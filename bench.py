@@ -139,8 +139,10 @@ def main() -> int:
     torch.cuda.synchronize()
     # capture -> vote (all ranks agree on graphs vs eager) -> prime with the same step counts on every
     # rank (each step holds the DP all-reduce); untimed, reported as "graph_prime_steps"
+    # a fixed 16 multi-step replays (256 steps; the clock settles within ~13 on every box measured): the
+    # policy evaluated after the window has trained the same number of steps on every run
     use_graph, _ = benchkit.prepare_steps(eng, not args.no_graph and not cfg.engine.dp_overlap, rank, world,
-                                          group, prime_reps=8)
+                                          group, prime_reps=8 if world > 1 else 16, fixed_prime=True)
     prime_steps = eng.step_count
     eng.run(args.warmup)
     eng.synchronize()

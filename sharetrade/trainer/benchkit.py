@@ -52,14 +52,17 @@ def _fail_capture_here(rank: int) -> bool:
 
 
 def prepare_steps(eng, want_graph: bool, rank: int, world: int, group=None, prime_reps: int = 4,
-                  eager_prime: int = 64, log=None) -> Tuple[bool, int]:
+                  eager_prime: int = 64, log=None, fixed_prime: bool = False) -> Tuple[bool, int]:
     """Capture the step graphs (``want_graph``), agree across ranks, then prime.
 
     Returns ``(use_graph, prime_steps)``.  The 2 eager warm-up steps (each holds an all-reduce) run
     on every rank BEFORE the capture; the capture itself issues no collective (a captured RCCL call
     runs at replay), so a rank whose capture fails has issued exactly the collectives its peers
     have.  The vote follows, then every rank either replays the graphs a fixed number of times or
-    runs ``eager_prime`` eager steps: identical collective counts everywhere."""
+    runs ``eager_prime`` eager steps: identical collective counts everywhere.  ``fixed_prime``: exactly
+    ``prime_reps`` multi-step replays on one rank too (instead of replaying until the clock settles), so
+    the number of training steps before the timed window -- and the learned policy the bench evaluates --
+    is the same on every run."""
     log = log or (lambda m: print(m, file=sys.stderr))
     start = eng.step_count
     ok = False
@@ -88,7 +91,7 @@ def prepare_steps(eng, want_graph: bool, rank: int, world: int, group=None, prim
                     gk[0].replay()
                     eng.step_count += gk[1]
         else:
-            eng.prime_graph(prime_reps)
+            eng.prime_graph(prime_reps, max_reps=prime_reps if fixed_prime else 40)
     else:
         eng.run(eager_prime)
     return use_graph, eng.step_count - start
