@@ -408,3 +408,6 @@ def test_graph_priming_is_rank_uniform(native_built):
     s1 = eng.step_count
     assert eng.prime_graph(5) == 5 and eng.step_count == s1 + 20
     eng.world_size = 1
+    # bench.py's fixed priming (max_reps = min_reps): exactly that many replays on one process too
+    s2 = eng.step_count
+    assert eng.prime_graph(6, max_reps=6) == 6 and eng.step_count == s2 + 24
