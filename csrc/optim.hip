@@ -35,7 +35,18 @@ struct OptimParams {
                            // re-zeroed by the slab pass (it runs after the step kernel, before the next)
   float* ema;              // [P] Polyak average of the parameters (the weights to serve) or null
   float ema_decay;         // ema <- ema + (1 - decay) (w - ema) after every update
+  // the ws step kernel's weight images (csrc/qstep_ws.hip QStepParams::wimg) kept current: img_map[i] = bf16
+  // element of img (>= 0), -(fp32 word) - 2, or -1 (not in it); both null = no image
+  const int* img_map;
+  unsigned char* img;
 };
+
+// write parameter i (fp32 value w) into the ws weight image
+ST_DEV void img_put(unsigned char* img, const int* map, int i, float w) {
+  const int d = map[i];
+  if (d >= 0) reinterpret_cast<bf16_t*>(img)[d] = f2bf(w);
+  else if (d <= -2) reinterpret_cast<float*>(img)[-d - 2] = w;
+}
 
 constexpr int CW = 16;    // 16-byte slab columns per workgroup (256 B of every slab row)
 constexpr int SLAB_BLK = 128;   // bf16 slabs: parameters per reduce workgroup (= CW x 8) = 4 column blocks
@@ -162,6 +173,7 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
   }
   p.params[pidx] = w;
   if (p.params_bf) p.params_bf[pidx] = f2bf(w);
+  if (p.img) img_put(p.img, p.img_map, pidx, w);
   if (p.ema) p.ema[pidx] = ema + (1.f - p.ema_decay) * (w - ema);
 }
 
@@ -169,6 +181,12 @@ __global__ void __launch_bounds__(RT) reduce_optim_kernel(OptimParams p) {
 __global__ void advance_kernel(unsigned long long* ctrl) { ctrl[1] = ctrl[0] + 1; }
 // ctrl[0] = ctrl[1] : commit the step index without an optimizer update (first overlapped-DP step)
 __global__ void commit_kernel(unsigned long long* ctrl) { ctrl[0] = ctrl[1]; }
+
+// the whole ws weight image from the fp32 parameters (after parameters change outside the optimizer pass)
+__global__ void img_pack_kernel(const float* __restrict__ params, const int* __restrict__ map, unsigned char* img, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) img_put(img, map, i, params[i]);
+}
 
 __global__ void to_bf16_kernel(const float* __restrict__ in, bf16_t* __restrict__ out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -199,6 +217,12 @@ extern "C" hipError_t st_advance(unsigned long long* ctrl, hipStream_t stream) {
 
 extern "C" hipError_t st_commit_step(unsigned long long* ctrl, hipStream_t stream) {
   hipLaunchKernelGGL(st::commit_kernel, dim3(1), dim3(1), 0, stream, ctrl);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_img_pack(const float* params, const int* map, unsigned char* img, int n, hipStream_t stream) {
+  if (n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::img_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, params, map, img, n);
   return hipGetLastError();
 }
 

@@ -41,6 +41,9 @@ struct QStepParams {
   int ramp_global;          // 1: the exploit ramp runs over the step count instead of the episode position
   const float* qt;          // target net (csrc/qtarget.hip): [E][3][4] Q_target(x' after action a), or null
   int double_dqn;           // with qt: the next action is the online net's argmax, valued by the target
+  // csrc/qstep_ws.hip: the workgroup's weight images in LDS byte order (kept current by the optimizer pass,
+  // csrc/optim.hip img / img_map), copied into LDS by DMA in the prologue; null = gather them from wq / wf
+  const unsigned char* wimg;
 };
 
 // rows of QStepParams::env

@@ -344,7 +344,25 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   };
 
   // ------------------------------------------------------------------ prologue: weight images, ring state
+#if defined(WS_PROLOGUE_REPS) && WS_PROLOGUE_REPS > 1   // timing build csrc/ab/qstep_ws_pro2.hip: images built twice
+  for (int rep_ = 0; rep_ < WS_PROLOGUE_REPS; ++rep_) {
+    __syncthreads();
+#else
   {
+#endif
+   if (p.wimg != nullptr) {
+    // the images as one 87,872-byte run (oW0 .. oSLOT, built by the optimizer pass): 16 bytes per lane and
+    // LDS-DMA instruction, 11 per wave, all in flight at once (the gather below takes ~10 us per launch:
+    // profiles/r5_ws_prologue.md)
+    constexpr int NCH = (oSLOT - oW0) / 16;
+    for (int j = wave; j * 64 < NCH; j += NT / 64) {
+      const int c = j * 64 + lane;
+      if (c < NCH)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.wimg + 16 * c),
+                                         (__attribute__((address_space(3))) void*)(smem + oW0 + 1024 * j), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's copies landed (the barrier below joins the waves)
+   } else {
     const bf16_t* w0 = p.wq + p.off_w0;
     for (int i = tid; i < HP * KX; i += NT) {          // W0p[r][s] = W0^T[r][slot_col(s)]
       const int r = i / KX, s = i % KX;
@@ -362,6 +380,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     }
     for (int i = tid; i < HP; i += NT) sB1[i] = p.wf[p.off_b1 + i];
     if (tid < 16) sB2[tid] = tid < 4 ? p.wf[p.off_b2 + tid] : 0.f;
+   }
     if (tid < 16) ctl[tid] = 0;
     if (DYN && tid == 0) {
       int r = 0;
@@ -1015,8 +1034,32 @@ static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// the prologue's image entries, inverted: map[parameter] = bf16 element of the image (>= 0), -(fp32 word) - 2
+// (biases), or -1 (not in the image; the host fills -1 first).  Same index math as the prologue's gather, so
+// the optimizer pass's scatter (csrc/optim.hip) rebuilds exactly the bytes the gather would.
+__global__ void __launch_bounds__(256) ws_img_map_kernel(int* map, int off_w0, int off_w1, int off_w2, int off_b1,
+                                                         int off_b2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < HP * KX) map[off_w0 + (i / KX) * INP + slot_col(i % KX)] = oW0 / 2 + i;
+  if (i < HP * HP) map[off_w1 + (i >> 7) * HP + pi_unit(i & 127)] = oW1 / 2 + w1_off(i >> 7, i & 127);
+  if (i < 5 * HP) map[off_w2 + (i >> 7) * HP + pi_unit(i & 127)] = oW2 / 2 + i;
+  if (i < HP) map[off_b1 + i] = -(oB1 / 4 + i) - 2;
+  if (i < 4) map[off_b2 + i] = -(oB2 / 4 + i) - 2;
+}
+
 }  // namespace WS_NS
 }  // namespace st
+
+extern "C" int WS_API(st_qstep_ws_img_bytes)() { return st::WS_NS::oSLOT - st::WS_NS::oW0; }
+
+extern "C" hipError_t WS_API(st_qstep_ws_img_map)(int* map, int off_w0, int off_w1, int off_w2, int off_b1, int off_b2,
+                                                  hipStream_t stream) {
+  using namespace st::WS_NS;
+  static_assert(oW0 == 0 && (oSLOT - oW0) % 16 == 0, "image run");
+  hipLaunchKernelGGL(ws_img_map_kernel, dim3((HP * KX + 255) / 256), dim3(256), 0, stream, map, off_w0, off_w1, off_w2,
+                     off_b1, off_b2);
+  return hipGetLastError();
+}
 
 extern "C" int WS_API(st_qstep_ws_lds_bytes)(int inp, int h1p, int h2p) {
   if (inp == st::WS_NS::INP && h1p == st::WS_NS::HP && h2p == st::WS_NS::HP) return st::WS_NS::LDS_BYTES;

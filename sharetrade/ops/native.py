@@ -45,6 +45,7 @@ class QStepParams(C.Structure):
         ("reward_mode", C.c_int), ("td_clip", C.c_float),
         ("err", C.c_void_p),
         ("reward_scale", C.c_float), ("ramp_global", C.c_int), ("qt", C.c_void_p), ("double_dqn", C.c_int),
+        ("wimg", C.c_void_p),
     ]
 
 
@@ -73,6 +74,7 @@ class OptimParams(C.Structure):
         ("tdelay", C.c_int), ("slab_bf16", C.c_int),
         ("chunk_heads", C.c_void_p),
         ("ema", C.c_void_p), ("ema_decay", C.c_float),
+        ("img_map", C.c_void_p), ("img", C.c_void_p),
     ]
 
 
@@ -163,6 +165,12 @@ def lib() -> C.CDLL:
     L.st_commit_step.restype = C.c_int
     L.st_to_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.st_to_bf16.restype = C.c_int
+    L.st_img_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.st_img_pack.restype = C.c_int
+    L.st_qstep_ws_img_bytes.argtypes = []
+    L.st_qstep_ws_img_bytes.restype = C.c_int
+    L.st_qstep_ws_img_map.argtypes = [C.c_void_p] + [C.c_int] * 5 + [C.c_void_p]
+    L.st_qstep_ws_img_map.restype = C.c_int
     L.st_random_walk.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_uint32,
                                  C.c_uint32, C.c_void_p]
     L.st_random_walk.restype = C.c_int
@@ -267,6 +275,22 @@ def init_normal(block: torch.Tensor, rows: int, cols: int, std: float, key0: int
         raise ValueError("init_normal: block too small")
     check(lib().st_init_normal(ptr(block), rows, cols, block.stride(0), std, key0 & 0xFFFFFFFF, key1 & 0xFFFFFFFF,
                                stream, stream_handle()), "st_init_normal")
+
+
+def ws_weight_image(params: torch.Tensor, seg) -> tuple:
+    """The ws step kernel's weight images in LDS byte order (``QStepParams::wimg``) and the parameter ->
+    image map the optimizer pass keeps it current with (``OptimParams::img`` / ``img_map``)."""
+    L = lib()
+    img = torch.zeros(L.st_qstep_ws_img_bytes(), dtype=torch.uint8, device=params.device)
+    m = torch.full((params.numel(),), -1, dtype=torch.int32, device=params.device)
+    check(L.st_qstep_ws_img_map(ptr(m), seg["W0"].offset, seg["W1"].offset, seg["W2"].offset, seg["b1"].offset,
+                                seg["b2"].offset, stream_handle()), "st_qstep_ws_img_map")
+    img_pack(params, m, img)
+    return img, m
+
+
+def img_pack(params: torch.Tensor, m: torch.Tensor, img: torch.Tensor) -> None:
+    check(lib().st_img_pack(ptr(params), ptr(m), ptr(img), params.numel(), stream_handle()), "st_img_pack")
 
 
 def to_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:

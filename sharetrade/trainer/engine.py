@@ -312,7 +312,12 @@ class VectorEngine:
         # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide
         # kernels; one padded copy for ws (4-B-aligned dwordx4 reads, as fast: profiles/r3_ws_ab.md)
         self.prices4 = native.replicate4(self.prices, 1 if self.step_kernel in ("ws", "pipe") else 4)
-        native.to_bf16(self.params, self.params_bf)
+        # ws: the weight images in LDS byte order, kept current by the optimizer pass and copied by DMA in the
+        # kernel's prologue (the per-launch gather of them cost ~10 us: profiles/r5_ws_prologue.md)
+        self._wimg = self._wimg_map = None
+        if self.step_kernel == "ws" and os.environ.get("SHARETRADE_WS_WIMG", "1") != "0":
+            self._wimg, self._wimg_map = native.ws_weight_image(self.params, self.layout.segments)
+        self._bf16_refresh()
         props = torch.cuda.get_device_properties(dev)
         self.grid = max(1, min(self.cfg.engine.grid or props.multi_processor_count, self.E // self.chunk))
         # per-workgroup gradient partials: bf16 rows for the 64-env-chunk kernel by default (the slab
@@ -355,6 +360,7 @@ class VectorEngine:
         q.prices4, q.T4 = native.ptr(self.prices4), int(self.prices4.shape[2])
         q.prices, q.env = native.ptr(self.prices), native.ptr(self.env_soa)
         q.wq, q.wf = native.ptr(self.params_bf), native.ptr(self.params)
+        q.wimg = native.ptr(self._wimg) if self._wimg is not None else None
         q.slab, q.stats = native.ptr(self.slab), native.ptr(self.stat_slab)
         q.slab_bf16, q.slab_rows = int(self.slab_bf16), self.grid
         q.ctrl = native.ptr(self.ctrl)
@@ -404,6 +410,8 @@ class VectorEngine:
         a = cfg.agent
         o = native.OptimParams()
         o.params, o.params_bf, o.mask = native.ptr(self.params), native.ptr(self.params_bf), native.ptr(self.mask)
+        if self._wimg is not None:
+            o.img, o.img_map = native.ptr(self._wimg), native.ptr(self._wimg_map)
         o.s1 = native.ptr(self.opt.s1) if self.opt.s1.numel() else None
         o.s2 = native.ptr(self.opt.s2) if self.opt.s2.numel() else None
         o.slab, o.grad, o.ctrl = native.ptr(self.slab), native.ptr(self.grad), native.ptr(self.ctrl)
@@ -828,12 +836,19 @@ class VectorEngine:
             return self.step_count
         return self.opt.t
 
+    def _bf16_refresh(self) -> None:
+        """The bf16 image of the parameters (and the ws weight images) after they changed outside the
+        optimizer pass."""
+        native.to_bf16(self.params, self.params_bf)
+        if getattr(self, "_wimg", None) is not None:
+            native.img_pack(self.params, self._wimg_map, self._wimg)
+
     def set_params(self, params: torch.Tensor) -> None:
         """Overwrite the live parameters (fp32 master copy and, for the bf16 kernels, its bf16 image)."""
         self.params.copy_(params.to(self.device))
         self.params.mul_(self._real)
         if self.backend == "native" and self.kernel == "bf16_fused":
-            native.to_bf16(self.params, self.params_bf)
+            self._bf16_refresh()
 
     def load_state_dict(self, d: Dict[str, torch.Tensor]) -> None:
         ov = getattr(self, "_ov", None)
@@ -863,7 +878,7 @@ class VectorEngine:
             getattr(self.state, k).copy_(d["env_" + k].to(self.device))
         if self.backend == "native":
             if self.kernel == "bf16_fused":
-                native.to_bf16(self.params, self.params_bf)
+                self._bf16_refresh()
             self.ctrl.fill_(self.step_count)
 
     def sync_params_from(self, src_rank: int = 0) -> None:
@@ -878,7 +893,7 @@ class VectorEngine:
             if t.numel():
                 dist.broadcast(t, src_rank, group=self.group)
         if self.backend == "native" and self.kernel == "bf16_fused":
-            native.to_bf16(self.params, self.params_bf)
+            self._bf16_refresh()
 
     def synchronize(self, check: bool = True) -> None:
         """Wait for the device; then (``check``) raise if a step kernel reported a protocol error."""
