@@ -95,6 +95,7 @@ struct QTargetParams {
   int off_w0, off_w1, off_b1, off_w2, off_b2;
   float b0, inv_b0;
   int s0, compat_env, output_relu, feat_mode;
+  const unsigned char* wimg;   // the weight images in LDS byte order (refreshed with the target copy), or null
 };
 
 // TPW 16-env tiles per wave (each weight fragment read from LDS feeds TPW MFMAs), NWV waves per workgroup (one
@@ -109,6 +110,20 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
   float* B1 = reinterpret_cast<float*>(smem + oB1);
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, g4 = lane >> 4;
   const int w = tid >> 6;
+  if (p.wimg != nullptr) {
+    // the images as one run (packed from the target net right before the pass): 16 bytes per lane and LDS-DMA
+    // instruction (the element-wise gather + conversion below cost ~10 us per launch in the step kernel's
+    // equivalent, profiles/r5_ws_prologue.md)
+    constexpr int NCH = LDS_BYTES / 16;
+    const int lane_ = tid & 63;
+    for (int j = tid >> 6; j * 64 < NCH; j += NW) {
+      const int c = j * 64 + lane_;
+      if (c < NCH)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.wimg + 16 * c),
+                                         (__attribute__((address_space(3))) void*)(smem + 1024 * j), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0)
+  } else {
   for (int i = tid; i < HP * KX; i += NT) {
     const int r = i / KX, s = i % KX;
     W0[r * KS + s] = f2bf(p.wt[p.off_w0 + r * INP + slot_col(s)]);
@@ -122,6 +137,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
     W2[i] = a < 3 ? f2bf(p.wt[p.off_w2 + a * HP + pi_unit(s)]) : (bf16_t)0;
   }
   for (int i = tid; i < HP; i += NT) B1[i] = p.wt[p.off_b1 + i];
+  }
   __syncthreads();
   const float b2v[3] = {p.wt[p.off_b2], p.wt[p.off_b2 + 1], p.wt[p.off_b2 + 2]};
   const size_t E = (size_t)p.E;
@@ -253,8 +269,29 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
   }
 }
 
+// the prologue's image entries, inverted (map[parameter] = bf16 element (>= 0), -(fp32 word) - 2, or -1 (host
+// fill)): the same index math as the gather above
+__global__ void __launch_bounds__(256) qt_img_map_kernel(int* map, int off_w0, int off_w1, int off_w2, int off_b1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < HP * KX) map[off_w0 + (i / KX) * INP + slot_col(i % KX)] = oW0 / 2 + (i / KX) * KS + i % KX;
+  if (i < HP * HP) map[off_w1 + (i / HP) * HP + pi_unit(i % HP)] = oW1 / 2 + w1_off(i / HP, i % HP);
+  if (i < 3 * HP) map[off_w2 + (i / HP) * HP + pi_unit(i % HP)] = oW2 / 2 + i;
+  if (i < HP) map[off_b1 + i] = -(oB1 / 4 + i) - 2;
+}
+
 }  // namespace qtgt
 }  // namespace st
+
+extern "C" int st_qtarget_img_bytes() { return st::qtgt::LDS_BYTES; }
+
+extern "C" hipError_t st_qtarget_img_map(int* map, int off_w0, int off_w1, int off_w2, int off_b1, hipStream_t stream) {
+  using namespace st::qtgt;
+  static_assert(LDS_BYTES % 16 == 0 && oW0 == 0, "image run");
+  hipLaunchKernelGGL(qt_img_map_kernel, dim3((HP * KX + 255) / 256), dim3(256), 0, stream, map, off_w0, off_w1, off_w2,
+                     off_b1);
+  return hipGetLastError();
+}
+
 
 namespace {
 template <int TPW, int NWV>

@@ -61,6 +61,7 @@ class QTargetParams(C.Structure):
         ("off_w0", C.c_int), ("off_w1", C.c_int), ("off_b1", C.c_int), ("off_w2", C.c_int), ("off_b2", C.c_int),
         ("b0", C.c_float), ("inv_b0", C.c_float),
         ("s0", C.c_int), ("compat_env", C.c_int), ("output_relu", C.c_int), ("feat_mode", C.c_int),
+        ("wimg", C.c_void_p),
     ]
 
 
@@ -151,6 +152,10 @@ def lib() -> C.CDLL:
     L.st_qtarget_launch.restype = C.c_int
     L.st_qtarget_launch_v.argtypes = [C.POINTER(QTargetParams), C.c_int, C.c_int, C.c_void_p]
     L.st_qtarget_launch_v.restype = C.c_int
+    L.st_qtarget_img_bytes.argtypes = []
+    L.st_qtarget_img_bytes.restype = C.c_int
+    L.st_qtarget_img_map.argtypes = [C.c_void_p] + [C.c_int] * 4 + [C.c_void_p]
+    L.st_qtarget_img_map.restype = C.c_int
     L.st_f32b_target_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
     L.st_f32b_target_sync.restype = C.c_int
     L.st_qstep_pipe_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -286,6 +291,17 @@ def ws_weight_image(params: torch.Tensor, seg) -> tuple:
     check(L.st_qstep_ws_img_map(ptr(m), seg["W0"].offset, seg["W1"].offset, seg["W2"].offset, seg["b1"].offset,
                                 seg["b2"].offset, stream_handle()), "st_qstep_ws_img_map")
     img_pack(params, m, img)
+    return img, m
+
+
+def qtarget_weight_image(target: torch.Tensor, seg) -> tuple:
+    """The target pass's weight images in LDS byte order (``QTargetParams::wimg``) and its parameter map."""
+    L = lib()
+    img = torch.zeros(L.st_qtarget_img_bytes(), dtype=torch.uint8, device=target.device)
+    m = torch.full((target.numel(),), -1, dtype=torch.int32, device=target.device)
+    check(L.st_qtarget_img_map(ptr(m), seg["W0"].offset, seg["W1"].offset, seg["W2"].offset, seg["b1"].offset,
+                               stream_handle()), "st_qtarget_img_map")
+    img_pack(target, m, img)
     return img, m
 
 

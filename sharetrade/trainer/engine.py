@@ -399,6 +399,11 @@ class VectorEngine:
             t.off_w0, t.off_w1, t.off_b1, t.off_w2, t.off_b2 = q.off_w0, q.off_w1, q.off_b1, q.off_w2, q.off_b2
             t.b0, t.inv_b0, t.s0 = q.b0, q.inv_b0, q.s0
             t.compat_env, t.output_relu, t.feat_mode = q.compat_env, q.output_relu, q.feat_mode
+            # the target net's weight images in LDS byte order, refreshed with every target copy (the pass
+            # DMA-copies them instead of gathering and converting per launch)
+            if os.environ.get("SHARETRADE_WS_WIMG", "1") != "0":
+                self._qt_img, self._qt_map = native.qtarget_weight_image(self.params_target, seg)
+                t.wimg = native.ptr(self._qt_img)
             self._qtp = t
             # one workgroup per CU (the weight images take 87.5 KB of LDS), grid-stride over 16-env tiles
             self._qt_variant = int(os.environ.get("SHARETRADE_QT_VARIANT", "1"))
@@ -472,8 +477,15 @@ class VectorEngine:
                                                self.params.numel(), native.ptr(self.ctrl),
                                                int(self.cfg.agent.target_every), sh), "target_sync")
 
+    def _target_img_refresh(self) -> None:
+        """The target pass's weight images from the current target net (every step, right before the pass:
+        the target may also be written directly, as the fp32 copy the pass used to gather from)."""
+        if getattr(self, "_qt_img", None) is not None:
+            native.img_pack(self.params_target, self._qt_map, self._qt_img)
+
     def _launch_qstep(self, L, sh) -> None:
         if self._qtp is not None:
+            self._target_img_refresh()
             native.check(L.st_qtarget_launch_v(self._qtp, self._qt_grid, self._qt_variant, sh), "qtarget")
         if self.step_kernel == "pipe":
             fn = L.st_qstep_pipe_launch
