@@ -89,7 +89,14 @@ def build_hip(force: bool = False, jobs: int = 8, ab: bool = False) -> str:
     lib_path = AB_LIB if ab else HIP_LIB
     srcs = sorted(glob.glob(os.path.join(CSRC, "ab" if ab else "", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "*.h")))
-    if not force and not _newer(lib_path, srcs + hdrs + ([os.path.join(CSRC, "qstep_ws.hip")] if ab else [])):
+    manifest = lib_path + ".srcs"   # the sources linked last time: a removed / moved source forces a relink
+    listing = "\n".join(os.path.relpath(s, ROOT) for s in srcs) + "\n"
+    try:
+        with open(manifest) as f:
+            same_srcs = f.read() == listing
+    except OSError:
+        same_srcs = True   # no record (first build or an older tree): the mtime rule alone decides
+    if not force and same_srcs and not _newer(lib_path, srcs + hdrs + ([os.path.join(CSRC, "qstep_ws.hip")] if ab else [])):
         return lib_path   # library newer than every source: nothing to do (the object dir need not exist)
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(OUT, exist_ok=True)
@@ -102,8 +109,10 @@ def build_hip(force: bool = False, jobs: int = 8, ab: bool = False) -> str:
             todo.append((s, o))
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(lambda so: _run([HIPCC] + HIP_FLAGS + ["-c", so[0], "-o", so[1]]), todo))
-    if force or todo or _newer(lib_path, objs):
+    if force or todo or not same_srcs or _newer(lib_path, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path] + objs)
+    with open(manifest, "w") as f:
+        f.write(listing)
     return lib_path
 
 

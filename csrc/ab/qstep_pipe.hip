@@ -42,7 +42,7 @@
 //
 // Specialised to the flagship geometry: window H = 201, padded dims 224-128-128-16 (input slots 208),
 // 64-env chunks (4 tiles of 16 envs), static chunk schedule.
-#include "qstep.h"
+#include "../qstep.h"
 
 #ifndef PIPE_STAMPS
 #define PIPE_STAMPS 0   // debug builds (csrc/ab/qstep_pipe_stamps.hip): s_memtime at 8 points per iteration of

@@ -2,4 +2,4 @@
 #define PIPE_STAMPS 1
 #define PIPE_NS pipe_stamps
 #define PIPE_API(name) name##_stamps
-#include "../qstep_pipe.hip"
+#include "qstep_pipe.hip"

@@ -530,13 +530,29 @@ __global__ void __launch_bounds__(256) f32b_colsum4_kernel(const float* D, long 
     }
   }
 }
-__global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long long ld, int E, int N, float* out) {
+__global__ void __launch_bounds__(256) f32b_colsum_kernel(const float* D, long long ld, int E, int N, float* out,
+                                                          float* partials) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
   const int e0 = blockIdx.y * 256, e1 = min(E, e0 + 256);
   float s = 0.f;
   for (int e = e0; e < e1; ++e) s += D[(long long)e * ld + n];
-  atomicAdd(out + n, s);
+  if (partials)   // deterministic mode: row group y's column sums to its own row (added in order below)
+    partials[(long long)blockIdx.y * N + n] = s;
+  else
+    atomicAdd(out + n, s);
+}
+
+// out[i] = sum over z of part[z * zstride + i] in split order, one thread per element: the deterministic sum
+// for shapes the float4 form (f32b_splitsum_kernel) does not take -- widths not a multiple of 4, offsets not
+// 16-byte aligned (any fp32 MLP of the flat layout, engine.f32_deterministic)
+__global__ void __launch_bounds__(256) f32b_splitsum1_kernel(const float* part, int splits, long long zstride,
+                                                             float* out, long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a = 0.f;
+  for (int z = 0; z < splits; ++z) a += part[z * zstride + i];
+  out[i] = a;
 }
 
 // out[i] = sum over z of part[z * zstride + i] (split-K partials of EPI_PARTIAL, bias column-sum partials):
@@ -620,9 +636,13 @@ extern "C" hipError_t st_f32b_fwd2(const st::Fwd2F32* p, hipStream_t stream) {
 
 extern "C" hipError_t st_f32b_splitsum(const float* part, int splits, long long zstride, float* out, long long n,
                                        hipStream_t stream) {
-  if (splits < 1 || n <= 0 || n % 4 || zstride % 4 ||
-      ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15))
-    return hipErrorInvalidValue;
+  if (splits < 1 || n <= 0 || zstride < n) return hipErrorInvalidValue;
+  if (n % 4 || zstride % 4 || ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15)) {
+    // unaligned shapes: the same fixed order, one element per thread
+    hipLaunchKernelGGL(st::f32b_splitsum1_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part,
+                       splits, zstride, out, n);
+    return hipGetLastError();
+  }
   const long long n4 = n / 4;
   hipLaunchKernelGGL(st::f32b_splitsum_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, stream, part, splits,
                      zstride, out, n4);
@@ -656,9 +676,10 @@ extern "C" hipError_t st_f32b_td(const st::F32Batch* r, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// part != nullptr (deterministic mode): N % 4 == 0, N <= 256 and 16-byte alignment required; the column sums
-// of the <= 32 blocks land in part[block][N] and one st_f32b_splitsum adds them into out (returns the block
-// count through *nparts)
+// part != nullptr (deterministic mode): the column sums of the blocks land in part[block][N] and one
+// st_f32b_splitsum adds them into out in block order (returns the block count through *nparts).  N % 4 == 0,
+// N <= 256 and 16-byte alignment: <= 32 blocks of the float4 form, part needs 32 * N floats; other shapes:
+// one block row per 256 envs, part needs ceil(E / 256) * N floats (st_f32b_colsum_part_floats)
 extern "C" hipError_t st_f32b_colsum_det(const float* D, long long ld, int E, int N, float* out, float* part,
                                          int* nparts, hipStream_t stream);
 extern "C" hipError_t st_f32b_colsum(const float* D, long long ld, int E, int N, float* out, hipStream_t stream) {
@@ -667,9 +688,8 @@ extern "C" hipError_t st_f32b_colsum(const float* D, long long ld, int E, int N,
 extern "C" hipError_t st_f32b_colsum_det(const float* D, long long ld, int E, int N, float* out, float* part,
                                          int* nparts, hipStream_t stream) {
   if (E <= 0 || N <= 0) return hipErrorInvalidValue;
-  const bool vec = N % 4 == 0 && N <= 256 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(D) & 15) == 0;
-  if (part && (!vec || (reinterpret_cast<uintptr_t>(part) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)))
-    return hipErrorInvalidValue;
+  const bool vec = N % 4 == 0 && N <= 256 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(D) & 15) == 0 &&
+                   (!part || ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15) == 0);
   if (vec) {
     // at most 32 blocks: every block adds one atomic per column, and same-address fp32 atomics serialise
     // (256 blocks on a 16-column output: 16 us at 65,536 rows, mostly the 256-deep atomic queue per column)
@@ -689,6 +709,18 @@ extern "C" hipError_t st_f32b_colsum_det(const float* D, long long ld, int E, in
   }
   dim3 grid((N + 255) / 256, (E + 255) / 256);
   if (grid.y > 65535) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(st::f32b_colsum_kernel, grid, dim3(256), 0, stream, D, ld, E, N, out);
+  hipLaunchKernelGGL(st::f32b_colsum_kernel, grid, dim3(256), 0, stream, D, ld, E, N, out, part);
+  if (part) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (nparts) *nparts = (int)grid.y;
+    return st_f32b_splitsum(part, (int)grid.y, N, out, N, stream);
+  }
   return hipGetLastError();
+}
+
+// scratch (floats) st_f32b_colsum_det needs for an [E][N] column sum in deterministic mode
+extern "C" long long st_f32b_colsum_part_floats(int E, int N) {
+  const bool vec = N % 4 == 0 && N <= 256;
+  return vec ? 32ll * 256 : (long long)((E + 255) / 256) * N;
 }

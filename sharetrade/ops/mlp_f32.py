@@ -485,7 +485,10 @@ class F32BatchedStep:
         need = max(self._splits(lay.pdims[l + 1], lay.pdims[l], E) * lay.pdims[l + 1] * lay.pdims[l]
                    for l in range(lay.n_layers))
         self.partials = torch.empty(need, dtype=torch.float32, device=eng.device) if self.deterministic else None
-        self.colsum_part = (torch.empty(32 * 256 + 64, dtype=torch.float32, device=eng.device)
+        # per-block bias column sums: 32 x 256 floats for the float4 form (widths <= 256), else one row of
+        # partial sums per 256 envs at the widest biased layer (csrc/mlp_f32_mfma.hip st_f32b_colsum_det)
+        cs = max([32 * 256] + [-(-E // 256) * lay.pdims[l + 1] for l in range(lay.n_layers)])
+        self.colsum_part = (torch.empty(cs + 64, dtype=torch.float32, device=eng.device)
                             if self.deterministic else None)
         st, s = eng.state, self.s
         r = F32Batch()
@@ -621,8 +624,8 @@ class F32BatchedStep:
             sp = self._splits(Nout, Kin, E)
             dst = out.data_ptr() + 4 * net.off_w[l]
             if sp > 1 and self.partials is not None:
-                if (Nout * Kin) % 4 or dst % 16:
-                    raise RuntimeError(f"deterministic fp32 step: layer {l} weight gradient not float4-aligned")
+                # (widths not a multiple of 4 / unaligned offsets: st_f32b_splitsum's one-element-per-thread
+                # form, the same fixed order)
                 # split-K partials into scratch, then one deterministic sum (the fp32 atomics of every
                 # split's tile were the cost of the 224 x 224 product at 65,536 envs)
                 zs = Nout * Kin

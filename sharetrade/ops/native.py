@@ -158,10 +158,6 @@ def lib() -> C.CDLL:
     L.st_qtarget_img_map.restype = C.c_int
     L.st_f32b_target_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_longlong, C.c_void_p]
     L.st_f32b_target_sync.restype = C.c_int
-    L.st_qstep_pipe_launch.argtypes = [C.POINTER(QStepParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
-    L.st_qstep_pipe_launch.restype = C.c_int
-    L.st_qstep_pipe_lds_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
-    L.st_qstep_pipe_lds_bytes.restype = C.c_int
     L.st_reduce_optim.argtypes = [C.POINTER(OptimParams), C.c_void_p]
     L.st_reduce_optim.restype = C.c_int
     L.st_advance.argtypes = [C.c_void_p, C.c_void_p]
@@ -242,11 +238,15 @@ def qstep_ws_supported(inp: int, h1p: int, h2p: int) -> bool:
 
 
 def qstep_pipe_supported(inp: int, h1p: int, h2p: int) -> bool:
-    """Unit-sliced pipelined variant (csrc/qstep_pipe.hip: weight slices in VGPRs, activations through
-    LDS, five tiles' stages between two barriers)."""
+    """Unit-sliced pipelined variant (csrc/ab/qstep_pipe.hip: weight slices in VGPRs, activations through
+    LDS, five tiles' stages between two barriers).  Measured 2.6x slower than ws (profiles/r5_pipe_kernel.md),
+    so it lives in the opt-in A/B library: needs SHARETRADE_AB_BUILDS=1."""
     if not available():
         return False
-    return lib().st_qstep_pipe_lds_bytes(inp, h1p, h2p) > 0
+    fn = ab_lib().st_qstep_pipe_lds_bytes
+    fn.argtypes = [C.c_int, C.c_int, C.c_int]
+    fn.restype = C.c_int
+    return fn(inp, h1p, h2p) > 0
 
 
 def random_walk(out: torch.Tensor, start_price: float, vol: float, drift: float, key0: int, key1: int) -> None:

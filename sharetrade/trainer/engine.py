@@ -186,6 +186,9 @@ class VectorEngine:
             native.variant_launch(cfg.engine.step_variant,
                                   "st_qstep_pipe_launch_" if sk == "pipe" else "st_qstep_ws_launch_")
         if self.kernel == "bf16_fused" and sk == "pipe":
+            if not native.ab_builds_enabled():
+                raise RuntimeError("engine.step_kernel='pipe' (csrc/ab/qstep_pipe.hip: 2.6x slower than ws, kept "
+                                   "as a measured record) is in the opt-in A/B library: set SHARETRADE_AB_BUILDS=1")
             if not (self.ws_ok(cfg, L) and native.qstep_pipe_supported(L.pdims[0], L.pdims[1], L.pdims[2])):
                 raise NotImplementedError(f"engine.step_kernel='pipe' needs E % 64 == 0, history 201 and padded dims "
                                           f"(224, 128, 128); got E={self.E}, H={self.H}, dims {L.pdims}")
@@ -337,6 +340,12 @@ class VectorEngine:
                      else "static")
         if sched not in ("static", "dynamic"):
             raise ValueError(f"engine.chunk_schedule: {sched!r}")
+        if sched == "dynamic" and self.step_kernel == "ws" and self._learn_knobs:
+            # the ws knob build (target net, double DQN, reward scale, global ramp) has the static schedule only
+            # (csrc/qstep_ws.hip returns InvalidValue for it): refuse here, not at the first launch
+            raise ValueError("engine.chunk_schedule='dynamic' is not available with the learning knobs "
+                             "(agent.target_every / double_dqn / reward_scale / ramp_mode) on the ws kernel; "
+                             "use 'static' or 'auto'")
         # dynamic: 8 per-XCD claim heads, one per 128-byte line (csrc/qstep_wide.hip, csrc/qstep_ws.hip);
         # needs grid % 8 == 0 (the wide kernel also (E / 64) % 8 == 0), else the static schedule is used
         dyn_ok = ((self.step_kernel == "wide" and self.grid % 8 == 0 and (self.E // 64) % 8 == 0)
@@ -488,9 +497,10 @@ class VectorEngine:
             self._target_img_refresh()
             native.check(L.st_qtarget_launch_v(self._qtp, self._qt_grid, self._qt_variant, sh), "qtarget")
         if self.step_kernel == "pipe":
-            fn = L.st_qstep_pipe_launch
-            if self.cfg.engine.step_variant:   # timing builds (csrc/ab/qstep_pipe_<v>.hip), same contract
-                fn = native.variant_launch(self.cfg.engine.step_variant, "st_qstep_pipe_launch_")
+            # the measured-and-retired unit-sliced kernel (csrc/ab/qstep_pipe.hip, opt-in A/B library) and
+            # its timing builds (csrc/ab/qstep_pipe_<v>.hip), same contract
+            fn = native.variant_launch(self.cfg.engine.step_variant, "st_qstep_pipe_launch_") \
+                if self.cfg.engine.step_variant else native.variant_launch("", "st_qstep_pipe_launch")
         elif self.step_kernel == "ws":
             fn = L.st_qstep_ws_launch
             if self._qp.stamps:   # tools/stamp_qstep.py: the debug stamps build (opt-in A/B library)
@@ -546,9 +556,15 @@ class VectorEngine:
         wait_prev()
         upd = ov["ops"][j]
         upd.mode, upd.tdelay = 2, 0          # the last step's own update count
-        native.check(native.lib().st_reduce_optim(upd, native.stream_handle()), "update")
+        L, sh = native.lib(), native.stream_handle()
+        native.check(L.st_reduce_optim(upd, sh), "update")
         upd.tdelay = 1
         ov["pending"] = None
+        # the target copy of a boundary step (ctrl[0] % target_every == 0) followed the delayed update; with the
+        # last update applied, copy again, so a checkpoint / evaluation taken here sees the target net that
+        # synchronous training has at this step.  The counter does not move: continued overlapped
+        # training then starts from synchronous state (its next step only commits the counter).
+        self._target_sync(L, sh)
 
     def _f32_stats(self) -> None:
         if getattr(self._f32, "stats_in_kernel", False):   # the batched path's TD kernel accumulates them

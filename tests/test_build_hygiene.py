@@ -17,6 +17,7 @@ def test_production_sources_exclude_ab_builds():
     prod = sorted(os.path.basename(p) for p in glob.glob(os.path.join(ROOT, "csrc", "*.hip")))
     assert not any(p.startswith("qstep_ws_") for p in prod), prod
     assert "qstep_pair.hip" not in prod
+    assert "qstep_pipe.hip" not in prod   # measured 2.6x slower than ws: retired to the opt-in A/B library
     ab = sorted(os.path.basename(p) for p in glob.glob(os.path.join(ROOT, "csrc", "ab", "*.hip")))
     assert "qstep_ws_stamps.hip" in ab and "qstep_ws_gskip.hip" in ab
 
@@ -42,5 +43,6 @@ def test_production_library_has_no_timing_builds():
     syms = [ln.split()[-1] for ln in out.splitlines() if ln.strip()]
     step = [s for s in syms if s.startswith("st_qstep")]
     assert "st_qstep_ws_launch" in step
-    bad = [s for s in step if s.startswith("st_qstep_ws_launch_") or "pair" in s]
+    bad = [s for s in step if s.startswith("st_qstep_ws_launch_") or "pair" in s or "pipe" in s]
     assert not bad, bad
+    assert not [s for s in syms if "qstep_pipe" in s], "csrc/ab/qstep_pipe.hip leaked into the production library"

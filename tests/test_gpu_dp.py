@@ -71,6 +71,8 @@ def _worker(rank, world, port, E, steps, kernel, out, overlap=False, evaluate=Fa
     eng.flush_pending()
     torch.cuda.synchronize()
     res.update({"params": eng.params.cpu(), "budget": eng.state.budget.cpu()})
+    if eng.params_target is not None:
+        res["target"] = eng.params_target.cpu()
     torch.save(res, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
 
@@ -114,12 +116,20 @@ def test_overlapped_dp_is_rank_consistent_and_one_step_delayed(native_built):
 def test_overlapped_dp_with_target_net_is_rank_consistent(native_built):
     """dp_overlap + the target net / Double DQN on the ws kernel: the target copy follows the delayed update
     on every rank, so both ranks end with identical parameters."""
-    E, steps, world = 64, 7, 2
-    with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _port(), E, steps, "bf16_knobs", d, True), nprocs=world,
-                           join=True, start_method="spawn")
-        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
-    assert torch.equal(res[0]["params"], res[1]["params"]) and torch.isfinite(res[0]["params"]).all()
+    E, world = 64, 2
+    for steps in (7, 6):
+        with tempfile.TemporaryDirectory() as d:
+            mp.start_processes(_worker, args=(world, _port(), E, steps, "bf16_knobs", d, True), nprocs=world,
+                               join=True, start_method="spawn")
+            res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+        assert torch.equal(res[0]["params"], res[1]["params"]) and torch.isfinite(res[0]["params"]).all()
+        assert torch.equal(res[0]["target"], res[1]["target"])
+        if steps % 2 == 0:
+            # the last step is a target boundary (target_every = 2): after flush_pending the target holds the
+            # fully updated parameters, as in synchronous training (ADVICE r5)
+            assert torch.equal(res[0]["target"], res[0]["params"])
+        else:
+            assert not torch.equal(res[0]["target"], res[0]["params"])
 
 
 def test_overlapped_dp_greedy_evaluation_keeps_weights_frozen(native_built):

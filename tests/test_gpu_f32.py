@@ -350,3 +350,34 @@ def test_fp32_batched_split_partials_match_atomics(dev, monkeypatch):
     # and the bias column sums (per-block partials + ordered sum): the whole gradient is bit-reproducible
     assert torch.equal(grads["partial"], grads["partial2"])
     assert _rel(grads["partial"], grads["atomic"]) < 1e-5, _rel(grads["partial"], grads["atomic"])
+
+
+@pytest.mark.parametrize("hidden", [[512], [520, 300]])
+def test_fp32_batched_deterministic_wide_layers(dev, monkeypatch, hidden):
+    """Deterministic mode (engine.f32_deterministic: on for every DP rank and for reference_compat) on layers
+    wider than the 256-column float4 bias sum, with biases trained: the ordered fallback sums (one partial row
+    per 256 envs, st_f32b_splitsum's one-element form) instead of an error on the first step.  Two runs are
+    bit-identical and agree with the fp32-atomic mode up to summation order."""
+    from sharetrade.config import preset_config
+    from sharetrade.data.prices import random_walk
+    from sharetrade.trainer.engine import VectorEngine
+
+    E, T = 4096, 260
+    prices = torch.from_numpy(random_walk(T, 50.0, 0.02, 17, n_series=E).astype(np.float32))
+    grads = {}
+    for mode in ("det", "det2", "atomic"):
+        monkeypatch.delenv("SHARETRADE_F32_SPLIT_PARTIAL", raising=False)
+        cfg = preset_config("intended")
+        cfg.model.hidden = list(hidden)
+        cfg.model.train_bias = True
+        cfg.engine.dtype = "fp32"
+        cfg.engine.f32_batched = "on"
+        cfg.engine.f32_deterministic = "off" if mode == "atomic" else "on"
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert (eng._f32.partials is None) == (mode == "atomic")
+        grads[mode] = eng.native_grad().detach().cpu().clone()
+        eng.step()   # and a whole step (gradient -> optimizer) runs
+        torch.cuda.synchronize()
+        assert torch.isfinite(eng.params).all()
+    assert torch.equal(grads["det"], grads["det2"])
+    assert _rel(grads["det"], grads["atomic"]) < 1e-5, _rel(grads["det"], grads["atomic"])

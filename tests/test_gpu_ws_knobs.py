@@ -202,6 +202,13 @@ def test_other_bf16_kernels_refuse_the_knobs(native_built):
     cfg = _apply(_cfg(kernel="wide"), dict(target_every=10))
     with pytest.raises(NotImplementedError):
         VectorEngine(cfg, prices=_prices(128), device=torch.device("cuda", 0), envs=128)
+    # the ws knob build has the static chunk schedule only: an explicit dynamic schedule is a config error at
+    # construction, not an opaque launch failure
+    cfg = _apply(_cfg(), dict(target_every=10))
+    cfg.engine.chunk_schedule = "dynamic"
+    cfg.engine.grid = 8
+    with pytest.raises(ValueError, match="dynamic"):
+        VectorEngine(cfg, prices=_prices(1024), device=torch.device("cuda", 0), envs=1024)
 
 
 def test_ws_target_state_dict_resume_is_bit_exact(native_built):

@@ -112,6 +112,44 @@ __global__ void __launch_bounds__(512) gather_u16(const unsigned short* bank, co
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+// F: the operand pattern over u16 ticks with 4-byte-aligned loads only: per lane and k-step one dwordx4 + one
+//    dword from the 4-byte boundary at or below the lane's first tick (20 bytes = 10 ticks cover its 9), the
+//    odd-position shift undone by v_alignbyte (per lane: the kernel's envs may sit at different positions);
+//    the tail (ticks 193..201) through one dwordx4 + one dword in lanes g4 = 1, 2 -- 14 loads per lane per tile
+//    at half the bytes of A, none of them 2-byte
+__device__ __forceinline__ unsigned shr16(unsigned lo, unsigned hi, unsigned sh) {   // ({hi, lo} >> sh)[31:0]
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__global__ void __launch_bounds__(512) gather_u16a(const unsigned short* bank, const int* pos, float* out, int E) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+  float acc = 0.f;
+  for (int t = wave; t < E / 16; t += nwaves) {
+    const int e = 16 * t + l16;
+    const int p0 = pos[e] + 1;
+    const unsigned sh = (p0 & 1) * 2;   // bytes
+    const unsigned* b = reinterpret_cast<const unsigned*>(bank + (size_t)e * T4) + (p0 >> 1);
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      uint4 u;
+      __builtin_memcpy(&u, b + 16 * ks + 4 * g4, sizeof(u));
+      const unsigned w = b[16 * ks + 4 * g4 + 4];
+      const unsigned x0 = shr16(u.x, u.y, sh), x1 = shr16(u.y, u.z, sh), x2 = shr16(u.z, u.w, sh),
+                     x3 = shr16(u.w, w, sh), x4 = shr16(w, 0u, sh);
+      acc += lo16(x0) + hi16(x0) + lo16(x1) + hi16(x1) + lo16(x2) + hi16(x2) + lo16(x3) + hi16(x3) + lo16(x4);
+    }
+    if (g4 == 1 || g4 == 2) {
+      uint2 u;
+      __builtin_memcpy(&u, b + 96 + 2 * (g4 - 1), sizeof(u));
+      const unsigned w = b[98 + 2 * (g4 - 1)];
+      const unsigned x0 = shr16(u.x, u.y, sh), x1 = shr16(u.y, w, sh);
+      acc += lo16(x0) + hi16(x0) + lo16(x1) + hi16(x1);
+    }
+    acc += (float)(shr16(b[100], b[101], sh) & 0xFFFFu);
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 // D / E: time-major layouts (row t holds every env's price at time t; row stride ET elements)
 template <typename TT>
 __global__ void __launch_bounds__(512) gather_tm(const TT* bank, size_t ET, const int* pos, float* out, int E) {
@@ -162,7 +200,8 @@ int main(int argc, char** argv) {
   const double useful = (double)E * 202 * 4;   // (fp32-equivalent bytes for C too)
   printf("positions: %s\n\n", same ? "same for every env" : "random per env");
   printf("| pattern | waves / CU | grid | us | useful GB/s |\n|---|---|---|---|---|\n");
-  for (int pat = 0; pat < 6; ++pat)
+  const int pat0 = argc > 3 ? atoi(argv[3]) : 0;
+  for (int pat = pat0; pat < 7; ++pat)
     for (int wpc : {8, 16, 32}) {
       const int threads = 512, blocks = 256 * wpc / 8;
       for (int rep = 0; rep < 2; ++rep) {   // (first rep warms up)
@@ -178,6 +217,8 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL(gather_u16<false>, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
           else if (pat == 5)
             hipLaunchKernelGGL(gather_u16<true>, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
+          else if (pat == 6)
+            hipLaunchKernelGGL(gather_u16a, dim3(blocks), dim3(threads), 0, 0, bank16, pos, out, E);
           else
             hipLaunchKernelGGL(gather_rows, dim3(blocks), dim3(threads), 0, 0, bank, pos, out, E);
         }
@@ -186,7 +227,7 @@ int main(int argc, char** argv) {
         float ms;
         (void)hipEventElapsedTime(&ms, a, b);
         if (rep == 1)
-          printf("| %s | %d | %d | %.1f | %.0f |\n", pat == 0 ? "A operand (today)" : (pat == 1 ? "B row per instruction" : (pat == 2 ? "C operand, u16 ticks" : (pat == 3 ? "D time-major fp32" : (pat == 4 ? "E time-major u16" : "C' as C, 9th tick by a 4-byte load")))), wpc,
+          printf("| %s | %d | %d | %.1f | %.0f |\n", pat == 0 ? "A operand (today)" : (pat == 1 ? "B row per instruction" : (pat == 2 ? "C operand, u16 ticks" : (pat == 3 ? "D time-major fp32" : (pat == 4 ? "E time-major u16" : (pat == 5 ? "C' as C, 9th tick by a 4-byte load" : "F u16 ticks, 4-B-aligned dwordx4 + dword, alignbyte"))))), wpc,
                  blocks, ms / 5 * 1e3, useful / (ms / 5 * 1e-3) / 1e9);
       }
     }
