@@ -478,6 +478,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_pipe_kernel(QStepParams p) {
         rew = __fsub_rn(nw, cur);
         const float rrel = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
         rew = p.reward_mode ? rrel : rew;
+        if (p.reward_mode == 2) rew = __fsub_rn(rew, __fmul_rn(__fmul_rn(rew, 0.5f), rew));   // growth
         const float invn = FEAT ? __fdiv_rn(1.0f, vnew_e) : 0.f;
         const float fvn = FEAT ? __fmaf_rn(vnew_e, invn, -1.0f) : vnew_e;
         const s4v tl = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew_e, p.inv_b0, FEAT), 1.0f, fvn);

@@ -222,6 +222,7 @@ __global__ void __launch_bounds__(F_NT) f32_rows_kernel(F32Net net, F32Rows r) {
       const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
       float rew = __fsub_rn(nw, cur);
       if (r.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
+        if (r.reward_mode == 2) rew = __fsub_rn(rew, __fmul_rn(__fmul_rn(rew, 0.5f), rew));   // growth: log1p to 2nd order
       s_env[3] = b2;
       s_env[4] = rew;
       s_envi[1] = s2;

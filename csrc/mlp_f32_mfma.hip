@@ -406,6 +406,7 @@ __global__ void __launch_bounds__(256) f32b_env_kernel(F32Batch r) {
   const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
   float rew = __fsub_rn(nw, cur);
   if (r.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
+        if (r.reward_mode == 2) rew = __fsub_rn(rew, __fmul_rn(__fmul_rn(rew, 0.5f), rew));   // growth: log1p to 2nd order
   r.s_b2[e] = b2;
   r.s_s2[e] = s2;
   r.s_rew[e] = rew;

@@ -44,6 +44,11 @@ struct QStepParams {
   // csrc/qstep_ws.hip: the workgroup's weight images in LDS byte order (kept current by the optimizer pass,
   // csrc/optim.hip img / img_map), copied into LDS by DMA in the prologue; null = gather them from wq / wf
   const unsigned char* wimg;
+  // csrc/qstep_ws.hip / csrc/qtarget.hip: the bank as 16-bit ticks (csrc/series.hip tick16: [E][T16], price =
+  // tick * tscale[e], a power of two per env) -- read instead of prices4 when non-null (relative features only)
+  const unsigned short* ticks;
+  const float* tscale;
+  int T16;
 };
 
 // rows of QStepParams::env

@@ -464,6 +464,7 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
       const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
       float rew = __fsub_rn(nw, cur);
       if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
+        if (p.reward_mode == 2) rew = __fsub_rn(rew, __fmul_rn(__fmul_rn(rew, 0.5f), rew));   // growth: log1p to 2nd order
       sEnv[r * 8 + 3] = b2;
       sEnv[r * 8 + 4] = rew;
       sEnvI[r * 4 + 1] = s2;

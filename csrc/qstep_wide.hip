@@ -682,6 +682,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_wide_kernel(QStepParams p) {
         const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
         float rew = __fsub_rn(nw, cur);
         if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
+        if (p.reward_mode == 2) rew = __fsub_rn(rew, __fmul_rn(__fmul_rn(rew, 0.5f), rew));   // growth: log1p to 2nd order
         sEnv[r * ENVF + 3] = b2;
         sEnv[r * ENVF + 4] = rew;
         sEnvI[r * 4 + 1] = s2;

@@ -314,8 +314,11 @@ ST_DEV bool wait_full_or_end(const QStepParams& p, int* ctl, int sa, int q) {
 // ---------------------------------------------------------------------------------- the kernel
 // KN: the learning-quality knobs (target net, double DQN, reward scale, global exploit ramp) -- a separate
 // instance, so the production build carries none of their code
-template <int FEAT, bool DYN, bool KN>
+// U16: the windows come from the 16-bit tick bank (p.ticks, csrc/series.hip tick16; FEAT only): half the bytes,
+// 15 instead of 21 loads per lane and tile, 35 instead of 63 prefetch VGPRs, the same features bit for bit
+template <int FEAT, bool DYN, bool KN, bool U16 = false>
 __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
+  static_assert(!U16 || FEAT, "the tick bank serves the relative features (w / last - 1) only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* W0p = reinterpret_cast<bf16_t*>(smem + oW0);
   bf16_t* W1p = reinterpret_cast<bf16_t*>(smem + oW1);
@@ -420,11 +423,13 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     };
     int e_pos, e_sh, e_ep, n_pos, n_sh, n_ep;
     float e_b, e_val, e_rs, n_b, n_val, n_rs;
-#define WS_LOAD_ENV(K, REL, POS, B, SH, VAL, RS, EP)                                              \
+    float e_sc = 1.f, n_sc = 1.f;   // U16: the env's tick size (price = tick * sc)
+#define WS_LOAD_ENV(K, REL, POS, B, SH, VAL, RS, EP, SC)                                          \
   {                                                                                              \
     const int e_ = env_of(K, REL);                                                               \
     POS = ENV_I(ER_POS, e_); B = ENV_F(ER_BUDGET, e_); SH = ENV_I(ER_SHARES, e_);                \
     VAL = ENV_F(ER_VALUE, e_); RS = ENV_F(ER_RET_SUM, e_); EP = ENV_I(ER_EPISODES, e_);          \
+    if (U16) SC = p.tscale[e_];                                                                  \
   }
     // raw prices of a tile: per 32-wide k-step 9 floats (x uses 8, x' the 8 shifted by one); for the last
     // 16-wide k-step 5 (lanes g4 = 1, 2); the window's last and next price p[pos + 200], p[pos + 201]
@@ -433,8 +438,29 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
     float4 pd = make_float4(0.f, 0.f, 0.f, 0.f);
     float pe = 0.f;
     float4 pl;
+    // U16 (ticks as u16 pairs): per 32-wide k-step a dwordx4 + a dword from the 4-byte boundary at or below the
+    // lane's first tick (10 ticks cover its 9); the last k-step's window columns (lanes g4 = 1, 2) 3 dwords; the
+    // window's last and next tick 2 dwords.  An odd position is undone at the features (v_alignbyte).
+    uint4 ta[6];
+    unsigned tb[6];
+    uint2 td = make_uint2(0u, 0u);
+    unsigned te = 0u;
+    uint2 tl;
 #define WS_LOAD_PRICES(K, REL, POS)                                                               \
-  {                                                                                              \
+  if (U16) {                                                                                     \
+    const int e_ = env_of(K, REL);                                                               \
+    const int pc_ = min(max((POS), 0), p.T - HWIN - 1);                                          \
+    const unsigned* b_ = reinterpret_cast<const unsigned*>(p.ticks + (size_t)e_ * p.T16) + (pc_ >> 1); \
+    __builtin_memcpy(&tl, b_ + 100, sizeof(tl));                                                 \
+    _Pragma("unroll") for (int ks = 0; ks < 6; ++ks) {                                           \
+      __builtin_memcpy(&ta[ks], b_ + 16 * ks + 4 * g4, sizeof(uint4));                           \
+      tb[ks] = b_[16 * ks + 4 * g4 + 4];                                                         \
+    }                                                                                            \
+    if (g4 == 1 || g4 == 2) {                                                                    \
+      __builtin_memcpy(&td, b_ + 94 + 2 * g4, sizeof(td));                                       \
+      te = b_[96 + 2 * g4];                                                                      \
+    }                                                                                            \
+  } else {                                                                                       \
     const int e_ = env_of(K, REL);                                                               \
     const int pc_ = min(max((POS), 0), p.T - HWIN - 1);   /* address clamp: never read past the bank */ \
     const float* b_ = p.prices4 + (size_t)e_ * p.T4 + (size_t)pc_;  /* 4-B aligned dwordx4 reads */   \
@@ -451,9 +477,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       pe = r_[4];                                                                                \
     }                                                                                            \
   }
-    WS_LOAD_ENV(0, 0, e_pos, e_b, e_sh, e_val, e_rs, e_ep)
+    WS_LOAD_ENV(0, 0, e_pos, e_b, e_sh, e_val, e_rs, e_ep, e_sc)
     WS_LOAD_PRICES(0, 0, e_pos)
-    WS_LOAD_ENV(1, 1, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+    WS_LOAD_ENV(1, 1, n_pos, n_b, n_sh, n_val, n_rs, n_ep, n_sc)
 
     unsigned long long* stamps = ((WS_STAMPS & 1) && p.stamps != nullptr && blockIdx.x == 0 && d == 0 && lane == 0)
                                      ? p.stamps : nullptr;
@@ -497,11 +523,25 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       if (DYN && k >= 1) ck2 = __builtin_amdgcn_readfirstlane(ring_chunk(k + 2));   // for the env prefetch below
       const int e = chunk * C + 16 * d + l16;
       // ---------------------------------------------------------------- features -> X / X' B operands
-      const float last = pl.x, vnew = pl.y;
+      // lastw / vnew_w: the window's last and next value in the window's own units (fp32 prices, or U16 ticks:
+      // w / last - 1 is the same number either way); last / vnew: prices (U16: tick * the env's tick size, exact)
+      float lastw, vnew_w, last, vnew;
+      unsigned shb = 0u;   // U16: 2 when the tile's window starts at an odd tick (bytes to drop)
+      if (U16) {
+        shb = (unsigned)(min(max(e_pos, 0), p.T - HWIN - 1) & 1) * 2u;
+        const unsigned t01 = __builtin_amdgcn_alignbyte(tl.y, tl.x, shb);
+        lastw = (float)(t01 & 0xFFFFu);
+        vnew_w = (float)(t01 >> 16);
+        last = __fmul_rn(lastw, e_sc);
+        vnew = __fmul_rn(vnew_w, e_sc);
+      } else {
+        lastw = last = pl.x;
+        vnew_w = vnew = pl.y;
+      }
       float inv = 0.f, invn = 0.f;
       if (FEAT) {
-        inv = __fdiv_rn(1.0f, last);
-        invn = __fdiv_rn(1.0f, vnew);
+        inv = __fdiv_rn(1.0f, lastw);
+        invn = __fdiv_rn(1.0f, vnew_w);
       }
       auto fx = [&](float w) {
         return FEAT ? __fmaf_rn(w, inv, -1.0f) : w;
@@ -509,22 +549,44 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto fxn = [&](float w) {
         return FEAT ? __fmaf_rn(w, invn, -1.0f) : w;
       };
+      auto lo16f = [](unsigned v) { return (float)(v & 0xFFFFu); };
+      auto hi16f = [](unsigned v) { return (float)(v >> 16); };
       s8v X[6], Xn[6];
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
-        X[ks] = cat8(pk4(fx(pa[ks].x), fx(pa[ks].y), fx(pa[ks].z), fx(pa[ks].w)),
-                     pk4(fx(pb[ks].x), fx(pb[ks].y), fx(pb[ks].z), fx(pb[ks].w)));
-        Xn[ks] = cat8(pk4(fxn(pa[ks].y), fxn(pa[ks].z), fxn(pa[ks].w), fxn(pb[ks].x)),
-                      pk4(fxn(pb[ks].y), fxn(pb[ks].z), fxn(pb[ks].w), fxn(pc[ks])));
+        if (U16) {
+          const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
+                         w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),
+                         w2 = __builtin_amdgcn_alignbyte(ta[ks].w, ta[ks].z, shb),
+                         w3 = __builtin_amdgcn_alignbyte(tb[ks], ta[ks].w, shb),
+                         w4 = __builtin_amdgcn_alignbyte(0u, tb[ks], shb);
+          const float f0 = lo16f(w0), f1 = hi16f(w0), f2 = lo16f(w1), f3 = hi16f(w1), f4 = lo16f(w2),
+                      f5 = hi16f(w2), f6 = lo16f(w3), f7 = hi16f(w3), f8 = lo16f(w4);
+          X[ks] = cat8(pk4(fx(f0), fx(f1), fx(f2), fx(f3)), pk4(fx(f4), fx(f5), fx(f6), fx(f7)));
+          Xn[ks] = cat8(pk4(fxn(f1), fxn(f2), fxn(f3), fxn(f4)), pk4(fxn(f5), fxn(f6), fxn(f7), fxn(f8)));
+        } else {
+          X[ks] = cat8(pk4(fx(pa[ks].x), fx(pa[ks].y), fx(pa[ks].z), fx(pa[ks].w)),
+                       pk4(fx(pb[ks].x), fx(pb[ks].y), fx(pb[ks].z), fx(pb[ks].w)));
+          Xn[ks] = cat8(pk4(fxn(pa[ks].y), fxn(pa[ks].z), fxn(pa[ks].w), fxn(pb[ks].x)),
+                        pk4(fxn(pb[ks].y), fxn(pb[ks].z), fxn(pb[ks].w), fxn(pc[ks])));
+        }
       }
       // last k-step (16 wide, slot order): g4 = 0 (budget, shares, 1, col 200); 1, 2 window columns; 3 pads
       s4v X6, Xn6;
       if (g4 == 0) {
-        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, fx(last));
+        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, fx(lastw));
         Xn6 = zero_s4();   // completed after the env step
       } else if (g4 < 3) {
-        X6 = pk4(fx(pd.x), fx(pd.y), fx(pd.z), fx(pd.w));
-        Xn6 = pk4(fxn(pd.y), fxn(pd.z), fxn(pd.w), fxn(pe));
+        if (U16) {
+          const unsigned v0 = __builtin_amdgcn_alignbyte(td.y, td.x, shb), v1 = __builtin_amdgcn_alignbyte(te, td.y, shb),
+                         v2 = __builtin_amdgcn_alignbyte(0u, te, shb);
+          const float f0 = lo16f(v0), f1 = hi16f(v0), f2 = lo16f(v1), f3 = hi16f(v1), f4 = lo16f(v2);
+          X6 = pk4(fx(f0), fx(f1), fx(f2), fx(f3));
+          Xn6 = pk4(fxn(f1), fxn(f2), fxn(f3), fxn(f4));
+        } else {
+          X6 = pk4(fx(pd.x), fx(pd.y), fx(pd.z), fx(pd.w));
+          Xn6 = pk4(fxn(pd.y), fxn(pd.z), fxn(pd.w), fxn(pe));
+        }
       } else {
         X6 = zero_s4();
         Xn6 = zero_s4();
@@ -532,13 +594,13 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       const int pos = e_pos, sh0 = e_sh, ep0 = e_ep;
       const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
       // rotate the prefetched env state; load the one after next
-      e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep;
+      e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep; e_sc = n_sc;
       WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
       WS_SB();
       WS_STAMP(1);
       // (after the features: a store or load issued before them would hold their window wait)
       WS_WRITE_BACK()
-      WS_LOAD_ENV(k + 2, 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep)
+      WS_LOAD_ENV(k + 2, 2, n_pos, n_b, n_sh, n_val, n_rs, n_ep, n_sc)
       if (DYN && d == 0 && !ended) {   // the chunk of round k + 3 (used from tile k + 1 on); flags wave-uniform
         if (lane == 0) claim_v = atomicAdd(head, 1u);
         claim_out = true;
@@ -670,7 +732,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         const float nw = __fadd_rn(b2, __fmul_rn((float)s2, vnew));
         rew = __fsub_rn(nw, cur);
         if (p.reward_mode) rew = cur > 0.f ? __fdiv_rn(rew, cur) : 0.f;
-        Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fxn(vnew));
+        if (p.reward_mode == 2) rew = __fsub_rn(rew, __fmul_rn(__fmul_rn(rew, 0.5f), rew));   // growth: log1p to 2nd order
+        Xn6 = pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew, p.inv_b0, FEAT), 1.0f, fxn(vnew_w));
         st_explore += exploit ? 0.f : 1.f;
       }
       WS_WB_SET()
@@ -1021,16 +1084,16 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   if (blockIdx.x == 0 && tid == 0) p.ctrl[1] = step + 1;   // 1-based update count for the optimizer
 }
 
-template <int FEAT, bool DYN, bool KN>
+template <int FEAT, bool DYN, bool KN, bool U16 = false>
 static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)qstep_ws_kernel<FEAT, DYN, KN>,
+    hipError_t e = hipFuncSetAttribute((const void*)qstep_ws_kernel<FEAT, DYN, KN, U16>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((qstep_ws_kernel<FEAT, DYN, KN>), dim3(grid), dim3(NT), LDS_BYTES, stream, p);
+  hipLaunchKernelGGL((qstep_ws_kernel<FEAT, DYN, KN, U16>), dim3(grid), dim3(NT), LDS_BYTES, stream, p);
   return hipGetLastError();
 }
 
@@ -1079,6 +1142,15 @@ extern "C" hipError_t WS_API(st_qstep_ws_launch)(const st::QStepParams* p, int i
   if ((p->off_w0 | p->off_w1 | p->off_w2) & 7) return hipErrorInvalidValue;
   if (p->slab_bf16 && (p->slab_rows != grid || p->P % 32 != 0)) return hipErrorInvalidValue;
   const bool kn = p->qt != nullptr || p->reward_scale != 1.0f || p->ramp_global || p->double_dqn;
+  if (p->ticks != nullptr) {   // the 16-bit tick bank (relative features only)
+    if (!p->feat_mode || p->tscale == nullptr || p->T16 < p->T + 8 || p->T16 % 8) return hipErrorInvalidValue;
+    if (kn) {
+      if (p->chunk_heads != nullptr || (p->double_dqn && p->qt == nullptr)) return hipErrorInvalidValue;
+      return launch_f<1, false, true, true>(*p, grid, stream);
+    }
+    if (p->chunk_heads != nullptr) return launch_f<1, true, false, true>(*p, grid, stream);
+    return launch_f<1, false, false, true>(*p, grid, stream);
+  }
   if (kn) {   // learning-quality knobs: static schedule only
     if (p->chunk_heads != nullptr || (p->double_dqn && p->qt == nullptr)) return hipErrorInvalidValue;
     return p->feat_mode ? launch_f<1, false, true>(*p, grid, stream) : launch_f<0, false, true>(*p, grid, stream);

@@ -96,12 +96,16 @@ struct QTargetParams {
   float b0, inv_b0;
   int s0, compat_env, output_relu, feat_mode;
   const unsigned char* wimg;   // the weight images in LDS byte order (refreshed with the target copy), or null
+  const unsigned short* ticks; // the 16-bit tick bank [E][T16] (csrc/series.hip tick16) read instead of prices4
+  const float* tscale;         // when non-null (relative features only): price = tick * tscale[e]
+  int T16;
 };
 
 // TPW 16-env tiles per wave (each weight fragment read from LDS feeds TPW MFMAs), NWV waves per workgroup (one
 // workgroup per CU: the weight images take 87.5 KB of LDS)
-template <int FEAT, int TPW, int NWV>
+template <int FEAT, int TPW, int NWV, bool U16 = false>
 __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
+  static_assert(!U16 || FEAT, "the tick bank serves the relative features only");
   constexpr int NW = NWV, NT = 64 * NWV;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* W0 = reinterpret_cast<bf16_t*>(smem + oW0);
@@ -153,7 +157,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
     asm volatile("" : "+s"(zo));
     const bf16_t* W0i = W0 + zo;
     // ---------------------------------------------------------------- x' features of the wave's TPW env tiles
-    float vnew[TPW], invn[TPW], bd[TPW];
+    float vnew[TPW], invn[TPW], bd[TPW], vnw[TPW];   // vnw: vnew in the window's units (U16: the tick)
     int sd[TPW];
     s8v X[TPW][6];
     s4v Xw[TPW];
@@ -164,8 +168,42 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
       const float bud = __int_as_float(p.env[ER_BUDGET * E + e]);
       const int sh = p.env[ER_SHARES * E + e];
       const int pc = min(max(pos, 0), p.T - HWIN - 1);
+      if (U16) {
+        // x' starts at tick pc + 1: per k-step a dwordx4 + a dword from the 4-byte boundary at or below the lane's
+        // first tick, the odd start dropped by v_alignbyte; features from ticks are the fp32 prices' bit for bit
+        const unsigned* b = reinterpret_cast<const unsigned*>(p.ticks + (size_t)e * p.T16) + ((pc + 1) >> 1);
+        const unsigned shb = (unsigned)((pc + 1) & 1) * 2u;
+        const unsigned tv = __builtin_amdgcn_alignbyte(0u, b[100], shb);   // tick pc + 201
+        const float vw = (float)(tv & 0xFFFFu);
+        vnew[q] = __fmul_rn(vw, p.tscale[e]);
+        invn[q] = __fdiv_rn(1.0f, vw);
+        vnw[q] = vw;
+        const float iv = invn[q];
+        auto fxn = [&](float v) { return __fmaf_rn(v, iv, -1.0f); };
+        auto lo16f = [](unsigned v) { return (float)(v & 0xFFFFu); };
+        auto hi16f = [](unsigned v) { return (float)(v >> 16); };
+#pragma unroll
+        for (int ks = 0; ks < 6; ++ks) {
+          uint4 u;
+          __builtin_memcpy(&u, b + 16 * ks + 4 * g4, sizeof(u));
+          const unsigned t4 = b[16 * ks + 4 * g4 + 4];
+          const unsigned w0 = __builtin_amdgcn_alignbyte(u.y, u.x, shb), w1 = __builtin_amdgcn_alignbyte(u.z, u.y, shb),
+                         w2 = __builtin_amdgcn_alignbyte(u.w, u.z, shb), w3 = __builtin_amdgcn_alignbyte(t4, u.w, shb);
+          X[q][ks] = cat8(pk4(fxn(lo16f(w0)), fxn(hi16f(w0)), fxn(lo16f(w1)), fxn(hi16f(w1))),
+                          pk4(fxn(lo16f(w2)), fxn(hi16f(w2)), fxn(lo16f(w3)), fxn(hi16f(w3))));
+        }
+        Xw[q] = s4v{0, 0, 0, 0};
+        if (g4 == 1 || g4 == 2) {
+          uint2 u;
+          __builtin_memcpy(&u, b + 96 + 2 * (g4 - 1), sizeof(u));
+          const unsigned t2 = b[98 + 2 * (g4 - 1)];
+          const unsigned w0 = __builtin_amdgcn_alignbyte(u.y, u.x, shb), w1 = __builtin_amdgcn_alignbyte(t2, u.y, shb);
+          Xw[q] = pk4(fxn(lo16f(w0)), fxn(hi16f(w0)), fxn(lo16f(w1)), fxn(hi16f(w1)));
+        }
+      } else {
       const float* b = p.prices4 + (size_t)e * p.T4 + (size_t)pc;
       vnew[q] = b[201];
+      vnw[q] = vnew[q];
       invn[q] = FEAT ? __fdiv_rn(1.0f, vnew[q]) : 0.f;
       const float iv = invn[q];
       auto fxn = [&](float v) { return FEAT ? __fmaf_rn(v, iv, -1.0f) : v; };
@@ -181,6 +219,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
       if (g4 == 1 || g4 == 2) {
         const float4 u = ldu4(b + 193 + 4 * (g4 - 1));
         Xw[q] = pk4(fxn(u.x), fxn(u.y), fxn(u.z), fxn(u.w));
+      }
       }
       // the three candidates: Buy, Sell, Hold from (bd, sd) -- the env's own transition
       bd[q] = p.compat_env ? p.b0 : bud;
@@ -215,7 +254,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
         const bool buy = a == 0 && bd[q] >= vnew[q], sell = a == 1 && sd[q] > 0;
         const float b2 = buy ? __fsub_rn(bd[q], vnew[q]) : (sell ? __fadd_rn(bd[q], vnew[q]) : bd[q]);
         const int s2 = buy ? sd[q] + 1 : (sell ? sd[q] - 1 : sd[q]);
-        const float fvn = FEAT ? __fmaf_rn(vnew[q], invn[q], -1.0f) : vnew[q];
+        const float fvn = FEAT ? __fmaf_rn(vnw[q], invn[q], -1.0f) : vnew[q];
         const s4v tl = g4 == 0 ? pk4(feat_budget(b2, p.inv_b0, FEAT), feat_shares(s2, vnew[q], p.inv_b0, FEAT),
                                      1.0f, fvn)
                                : s4v{0, 0, 0, 0};
@@ -298,15 +337,20 @@ template <int TPW, int NWV>
 hipError_t launch_qt(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
   using namespace st::qtgt;
   if (p->E % (16 * TPW) != 0) return hipErrorInvalidValue;
-  static bool attr[2] = {false, false};
-  const int f = p->feat_mode ? 1 : 0;
-  const void* fn = f ? (const void*)qtarget_kernel<1, TPW, NWV> : (const void*)qtarget_kernel<0, TPW, NWV>;
+  static bool attr[3] = {false, false, false};
+  const bool u16 = p->ticks != nullptr;
+  if (u16 && (!p->feat_mode || p->tscale == nullptr || p->T16 < p->T + 8 || p->T16 % 8)) return hipErrorInvalidValue;
+  const int f = u16 ? 2 : (p->feat_mode ? 1 : 0);
+  const void* fn = f == 2 ? (const void*)qtarget_kernel<1, TPW, NWV, true>
+                          : (f ? (const void*)qtarget_kernel<1, TPW, NWV> : (const void*)qtarget_kernel<0, TPW, NWV>);
   if (!attr[f]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
     attr[f] = true;
   }
-  if (f)
+  if (f == 2)
+    hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV, true>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
+  else if (f)
     hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
   else
     hipLaunchKernelGGL((qtarget_kernel<0, TPW, NWV>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);

@@ -51,6 +51,56 @@ __global__ void __launch_bounds__(256) replicate4_kernel(const float* __restrict
   }
 }
 
+// 16-bit tick banks.  Every env's series on its own power-of-two grid: price = tick * 2^x_e with 0 < tick <=
+// 65535, x_e the smallest exponent that fits the series' largest price.  The flagship step reads windows as u16
+// ticks (half the bytes of fp32, 4-byte-aligned dwordx4 loads: profiles/r6_window_gather_ubench.md) and gets
+// bit-identical features: w / last - 1 = fma(tick_w, rn(1 / tick_last), -1) exactly (the powers of two cancel),
+// and prices for the env step as tick * 2^x_e (exact in fp32).
+//   mode 0 (quantize): bank[e][t] := tick * 2^x_e in place (synthetic banks are generated on the grid);
+//   mode 1 (check):    the bank is left alone; bad[0] |= 1 where a value is not exactly tick * 2^x_e with a
+//                      tick in [1, 65535] (the engine then keeps its fp32 window path).
+// Both write ticks[e][0 .. T16) (zero past T) and scale[e] = 2^x_e (mode 0: either may be null).  One wave per env.
+__global__ void __launch_bounds__(256) tick16_kernel(float* __restrict__ bank, int E, int T, unsigned short* __restrict__ ticks,
+                                                     int T16, float* __restrict__ scale, int mode, unsigned* bad) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= E) return;
+  float* row = bank + (size_t)wave * T;
+  float m = 0.f;
+  bool ok = true;
+  for (int t = lane; t < T; t += 64) {
+    const float v = row[t];
+    ok = ok && (v > 0.f) && (v <= 3.0e38f);
+    m = fmaxf(m, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  // smallest x with m * 2^-x <= 65535 (ldexpf is exact away from the subnormal range)
+  int x;
+  (void)frexpf(m, &x);   // m = f 2^x, f in [0.5, 1)
+  x -= 16;
+  while (x > -126 && ldexpf(m, -(x - 1)) <= 65535.f) --x;
+  while (ldexpf(m, -x) > 65535.f) ++x;
+  const float sc = ldexpf(1.0f, x);
+  unsigned short* trow = ticks ? ticks + (size_t)wave * T16 : nullptr;
+  for (int t = lane; t < T16; t += 64) {
+    unsigned tk = 0u;
+    if (t < T) {
+      const float v = row[t];
+      const float q = rintf(ldexpf(v, -x));
+      tk = (unsigned)fminf(fmaxf(q, 1.0f), 65535.0f);
+      const float back = ldexpf((float)tk, x);
+      if (mode == 0)
+        row[t] = back;
+      else if (back != v)
+        ok = false;
+    }
+    if (trow) trow[t] = (unsigned short)tk;
+  }
+  if (lane == 0 && scale) scale[wave] = sc;
+  if (mode == 1 && __any(!ok) && lane == 0) atomicOr(bad, 1u);
+}
+
 // Weight initialisation on the device (tf.RandomNormalInitializer, QDecisionPolicyActor.scala:41,45,
 // 80-81): W[r][c] = std * N(0,1) for r < rows, c < cols of a row-major [.., ld] block, one Philox4x32-10
 // counter per element -- (c0, c1, c2, c3) = (r * cols + c, 0, stream, 0x1417) -- and one Box-Muller
@@ -98,5 +148,18 @@ extern "C" hipError_t st_random_walk(float* out, int E, int T, float start_price
   const int grid = (int)((waves * 64 + threads - 1) / threads);
   hipLaunchKernelGGL(st::random_walk_kernel, dim3(grid), dim3(threads), 0, stream, out, E, T, start_price, vol,
                      drift, key0, key1);
+  return hipGetLastError();
+}
+
+// 16-bit tick bank of an [E][T] fp32 bank (tick16_kernel): ticks [E][T16] (T16 >= T + 8, a multiple of 8),
+// scale [E]; mode 0 quantizes the bank in place, mode 1 only checks it (*bad set when not on a tick grid)
+extern "C" hipError_t st_tick16(float* bank, int E, int T, unsigned short* ticks, int T16, float* scale, int mode,
+                                unsigned* bad, hipStream_t stream) {
+  if (E <= 0 || T <= 0 || (mode != 0 && mode != 1) || (mode == 1 && (bad == nullptr || ticks == nullptr)))
+    return hipErrorInvalidValue;
+  if (ticks != nullptr && (T16 < T + 8 || T16 % 8)) return hipErrorInvalidValue;
+  const long waves = E;
+  const int grid = (int)((waves * 64 + 255) / 256);
+  hipLaunchKernelGGL(st::tick16_kernel, dim3(grid), dim3(256), 0, stream, bank, E, T, ticks, T16, scale, mode, bad);
   return hipGetLastError();
 }

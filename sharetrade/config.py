@@ -79,7 +79,9 @@ class AgentConfig:
     loss_reduction: str = "sum"     # "sum" over the batch (reference, B=1) | "mean"
     # "absolute": reward = change of portfolio value in $ (TrainerChildActor.scala:142-143);
     # "relative": the portfolio's one-step return (change / previous value) -- scale-free across
-    # envs whose prices drift apart (bf16 engine kernels and the torch oracle)
+    # envs whose prices drift apart (bf16 engine kernels and the torch oracle); "growth": that return minus
+    # half its square, the portfolio's log growth to second order (Kelly: its expectation peaks at a position
+    # of mu / sigma^2 of wealth instead of at the largest one)
     reward_mode: str = "absolute"
     td_clip: float = 0.0            # > 0: clamp the TD error fed back (Huber loss); 0 = squared error
     # learning-quality experiments (tools/learning_eval.py, preset flagship_stable): the torch backend, the
@@ -121,6 +123,10 @@ class DataConfig:
     # trend source: log-return = mu_t + volatility * eps_t with a persistent, zero-mean drift
     # mu_t = rho mu_{t-1} + trend_sd sqrt(1 - rho^2) eta_t (regimes lasting ~1 / (1 - rho) days): a signal
     # that a policy moving one share per step can follow, unlike ar1's one-day momentum
+    # synthetic banks (random_walk, ar1, trend) generated on a 16-bit tick grid per series (price = tick * 2^x,
+    # tick <= 65535: a tick is <= 2^-16 of the series' largest price): the flagship kernel then streams its
+    # windows as u16 ticks with bit-identical features (data.prices.tick16_quantize, csrc/series.hip tick16)
+    tick16: bool = True
     trend_rho: float = 0.995
     trend_sd: float = 0.002
     seed: int = 7
@@ -193,6 +199,9 @@ class EngineConfig:
     # (dynamic for the wide kernel under overlapped DP with world_size > 1, else static: the ws kernel's
     # dynamic build is 14 % slower, profiles/r4_flagship_dp.md)
     chunk_schedule: str = "auto"
+    # ws step kernel + relative features: read the price windows from a 16-bit tick copy of the bank when every
+    # series is exactly on a tick grid (data.tick16, or user data that is): "auto" | "off" (the fp32 windows)
+    bank16: str = "auto"
     grid: int = 0                   # step-kernel workgroups: 0 = one per CU (capped at the chunk count)
     # > 0: keep a Polyak (exponential moving) average of the parameters, updated by the optimizer pass
     # after every step: ema <- ema + (1 - ema_decay) (w - ema).  The averaged weights are the ones to

@@ -111,6 +111,27 @@ def ar1_walk(length: int, start_price: float = 50.0, volatility: float = 0.02, p
     return start_price * np.exp(logp)
 
 
+def tick16_quantize(prices: np.ndarray) -> np.ndarray:
+    """Every row on its own 16-bit power-of-two tick grid: ``tick * 2**x`` with ``0 < tick <= 65535`` and ``x``
+    the smallest exponent that fits the row's largest price (the host mirror of csrc/series.hip tick16_kernel,
+    mode 0; float32 in and out).  On such a bank the flagship kernel reads windows as u16 ticks and computes
+    bit-identical relative features (w / last - 1 = tick_w / tick_last - 1 exactly); a tick is at most 2**-16
+    of the row's largest price -- far below the bf16 resolution of the features (2**-8 relative)."""
+    p = np.ascontiguousarray(prices, dtype=np.float32)
+    if p.ndim == 1:
+        return tick16_quantize(p[None])[0]
+    m = p.max(axis=1)
+    x = np.frexp(m)[1].astype(np.int64) - 16
+    for _ in range(40):   # smallest x with m * 2**-x <= 65535
+        dn = (x > -126) & (np.ldexp(m, -(x - 1)).astype(np.float32) <= 65535.0)
+        up = np.ldexp(m, -x).astype(np.float32) > 65535.0
+        if not dn.any() and not up.any():
+            break
+        x = np.where(dn, x - 1, np.where(up, x + 1, x))
+    t = np.clip(np.rint(np.ldexp(p, -x[:, None]).astype(np.float32)), 1.0, 65535.0).astype(np.float32)
+    return np.ldexp(t, x[:, None]).astype(np.float32)
+
+
 def random_walk_dates(length: int, start: Date = _dt.date(2000, 1, 3)) -> List[Date]:
     return [start + _dt.timedelta(days=i) for i in range(length)]
 

@@ -96,9 +96,14 @@ def gather_windows(prices: torch.Tensor, pos: torch.Tensor, H: int, shift: int =
 
 
 def env_transition(a: torch.Tensor, b: torch.Tensor, s: torch.Tensor, v_prev: torch.Tensor,
-                   v_new: torch.Tensor, compat: bool, b0: float, s0: int, relative: bool = False):
+                   v_new: torch.Tensor, compat: bool, b0: float, s0: int, relative: bool = False,
+                   growth: bool = False):
     """Apply actions; returns (b', s', reward).  fp32 arithmetic, no FMA contraction.
-    ``relative``: reward = change / previous portfolio value (0 where that value is not positive)."""
+    ``relative``: reward = change / previous portfolio value (0 where that value is not positive).
+    ``growth`` (with ``relative``): reward = rel - rel^2 / 2, the portfolio's log growth log1p(rel) to second
+    order -- its expectation is maximised by the Kelly fraction of wealth in the stock (mu / sigma^2: one half
+    on a zero-log-drift geometric walk) instead of by the largest position (profiles/r6_policy_breakdown.md);
+    the same three roundings as the kernels (rel * 0.5 exact, * rel, subtract)."""
     if compat:
         bd = torch.full_like(b, float(b0))
         sd = torch.full_like(s, int(s0))
@@ -111,8 +116,10 @@ def env_transition(a: torch.Tensor, b: torch.Tensor, s: torch.Tensor, v_prev: to
     cur = b + s.float() * v_prev
     new = b2 + s2.float() * v_new
     r = new - cur
-    if relative:
+    if relative or growth:
         r = torch.where(cur > 0, r / torch.where(cur > 0, cur, torch.ones_like(cur)), torch.zeros_like(r))
+    if growth:
+        r = r - (r * 0.5) * r
     return b2, s2, r
 
 
@@ -163,7 +170,7 @@ def engine_step_ref(prices: torch.Tensor, st: EnvState, params: torch.Tensor, la
     if forced_actions is not None:
         a = forced_actions.to(torch.int32)
     b2, s2, r = env_transition(a, st.budget, st.shares, st.value, v_new, compat_env, budget0, shares0,
-                               relative=(reward_mode == "relative"))
+                               relative=(reward_mode in ("relative", "growth")), growth=(reward_mode == "growth"))
     win2 = gather_windows(prices, pos, H, shift=1)
     x2 = features(win2, b2, s2, feature_mode, budget0)
     q2, _, _ = qn.forward(params, layout, x2, output_relu, emulate_bf16)

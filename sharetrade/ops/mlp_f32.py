@@ -24,6 +24,9 @@ F_MAXL = 6
 OPT_KIND = {"sgd": 0, "adagrad": 1, "adam": 2}
 
 
+# agent.reward_mode -> the kernels' code (csrc/mlp_f32*.hip, csrc/qstep_*.hip)
+REWARD_MODES = {"absolute": 0, "relative": 1, "growth": 2}
+
 class F32Net(C.Structure):
     _fields_ = [
         ("L", C.c_int), ("pd", C.c_int * (F_MAXL + 1)), ("dims", C.c_int * (F_MAXL + 1)),
@@ -289,7 +292,7 @@ class F32EngineStep:
         r.q_out, r.qn_out, r.acts, r.dz, r.loss = (self.s.q.data_ptr(), None, self.s.acts.data_ptr(),
                                                    self.s.dz.data_ptr(), self.s.loss.data_ptr())
         r.B, r.mode, r.gamma, r.coef = E, 2, float(cfg.agent.gamma), float(eng.loss_coef)
-        r.reward_mode = int(cfg.agent.reward_mode == "relative")
+        r.reward_mode = REWARD_MODES[cfg.agent.reward_mode]
         r.td_clip = float(cfg.agent.td_clip)
         r.prices = eng.prices.data_ptr()
         r.budget, r.shares, r.value, r.pos = (st.budget.data_ptr(), st.shares.data_ptr(), st.value.data_ptr(),
@@ -510,7 +513,7 @@ class F32BatchedStep:
         r.target_compat = int(cfg.agent.target_slot == "compat")
         r.output_relu = int(cfg.model.output_relu)
         r.s0, r.env_offset = int(cfg.env.shares), int(eng.env_offset)
-        r.reward_mode = int(cfg.agent.reward_mode == "relative")
+        r.reward_mode = REWARD_MODES[cfg.agent.reward_mode]
         r.eps = float(cfg.agent.epsilon)
         r.inv_ramp = float(np.float32(1.0 / cfg.agent.ramp))
         r.b0 = float(cfg.env.budget)

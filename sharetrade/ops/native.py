@@ -46,6 +46,7 @@ class QStepParams(C.Structure):
         ("err", C.c_void_p),
         ("reward_scale", C.c_float), ("ramp_global", C.c_int), ("qt", C.c_void_p), ("double_dqn", C.c_int),
         ("wimg", C.c_void_p),
+        ("ticks", C.c_void_p), ("tscale", C.c_void_p), ("T16", C.c_int),
     ]
 
 
@@ -62,6 +63,7 @@ class QTargetParams(C.Structure):
         ("b0", C.c_float), ("inv_b0", C.c_float),
         ("s0", C.c_int), ("compat_env", C.c_int), ("output_relu", C.c_int), ("feat_mode", C.c_int),
         ("wimg", C.c_void_p),
+        ("ticks", C.c_void_p), ("tscale", C.c_void_p), ("T16", C.c_int),
     ]
 
 
@@ -177,6 +179,9 @@ def lib() -> C.CDLL:
     L.st_random_walk.restype = C.c_int
     L.st_replicate4.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
     L.st_replicate4.restype = C.c_int
+    L.st_tick16.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                            C.c_void_p]
+    L.st_tick16.restype = C.c_int
     L.st_init_normal.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_uint32, C.c_uint32,
                                  C.c_uint32, C.c_void_p]
     L.st_init_normal.restype = C.c_int
@@ -269,6 +274,41 @@ def replicate4(src: torch.Tensor, reps: int = 4) -> torch.Tensor:
     out = flat[: reps * E * T4].view(reps, E, T4)
     check(lib().st_replicate4(ptr(src), ptr(out), E, T, T4, int(reps), stream_handle()), "st_replicate4")
     return out
+
+
+def tick16_stride(T: int) -> int:
+    """Row stride (u16 elements) of the tick bank: >= T + 8 (the window loads reach 2 ticks past the series'
+    end), a multiple of 8 (16-byte rows)."""
+    return (T + 8 + 7) // 8 * 8
+
+
+def tick16(bank: torch.Tensor, quantize: bool):
+    """The 16-bit tick copy of an [E, T] fp32 bank (csrc/series.hip tick16): ``(ticks [E, T16] int16 holding
+    u16, scale [E] fp32)``, or ``None`` when ``quantize`` is off and some value is not on its row's tick grid.
+    ``quantize=True`` first moves every value onto the grid IN PLACE (synthetic banks)."""
+    E, T = bank.shape
+    if not bank.is_contiguous():
+        raise ValueError("tick16: contiguous [E, T] bank expected")
+    T16 = tick16_stride(T)
+    flat = torch.zeros(E * T16 + 64, dtype=torch.int16, device=bank.device)   # +64: the last row's loads
+    ticks = flat[: E * T16].view(E, T16)
+    scale = torch.empty(E, dtype=torch.float32, device=bank.device)
+    bad = torch.zeros(1, dtype=torch.int32, device=bank.device)
+    check(lib().st_tick16(ptr(bank), E, T, ptr(ticks), T16, ptr(scale), 0 if quantize else 1, ptr(bad),
+                          stream_handle()), "st_tick16")
+    if not quantize and int(bad.item()) != 0:
+        return None
+    return ticks, scale
+
+
+def tick16_quantize_(bank: torch.Tensor) -> torch.Tensor:
+    """Move every value of an [E, T] fp32 device bank onto its row's 16-bit tick grid, in place (csrc/series.hip
+    tick16 mode 0; host mirror: data.prices.tick16_quantize)."""
+    E, T = bank.shape
+    if not bank.is_contiguous():
+        raise ValueError("tick16: contiguous [E, T] bank expected")
+    check(lib().st_tick16(ptr(bank), E, T, None, 0, None, 0, None, stream_handle()), "st_tick16")
+    return bank
 
 
 def init_normal(block: torch.Tensor, rows: int, cols: int, std: float, key0: int, key1: int, stream: int) -> None:

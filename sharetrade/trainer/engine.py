@@ -66,7 +66,20 @@ def padded_bank(E: int, T: int, device: torch.device) -> torch.Tensor:
 
 
 def make_price_bank(cfg: Config, E: int, device: torch.device, seed: int = 0) -> torch.Tensor:
-    """[E, T] fp32 price bank resident on ``device`` (tail-padded, see BANK_TAIL)."""
+    """[E, T] fp32 price bank resident on ``device`` (tail-padded, see BANK_TAIL).  Synthetic sources are put on
+    a 16-bit tick grid per series when ``data.tick16`` (the flagship kernel's u16 window path)."""
+    bank = _make_price_bank(cfg, E, device, seed)
+    if cfg.data.tick16 and cfg.data.source in ("random_walk", "ar1", "trend"):
+        if bank.device.type == "cuda":
+            native.tick16_quantize_(bank)
+        else:
+            from ..data.prices import tick16_quantize
+
+            bank.copy_(torch.from_numpy(tick16_quantize(bank.numpy())))
+    return bank
+
+
+def _make_price_bank(cfg: Config, E: int, device: torch.device, seed: int = 0) -> torch.Tensor:
     d = cfg.data
     if d.source == "random_walk":
         if device.type == "cuda":
@@ -312,9 +325,23 @@ class VectorEngine:
             self._f32 = F32BatchedStep(self) if self.f32_path == "batched" else F32EngineStep(self)
             return
         self.params_bf = torch.empty(L.numel, dtype=torch.bfloat16, device=dev)
-        # window-gather copies of the bank: 4 shifted replicas for the 16-B-aligned gathers of the wide
-        # kernels; one padded copy for ws (4-B-aligned dwordx4 reads, as fast: profiles/r3_ws_ab.md)
-        self.prices4 = native.replicate4(self.prices, 1 if self.step_kernel in ("ws", "pipe") else 4)
+        # ws + relative features: the windows as 16-bit ticks when every series is exactly on a tick grid (synthetic
+        # banks are generated on one, data.tick16): half the bytes of the fp32 windows, bit-identical features
+        # (csrc/series.hip tick16, profiles/r6_window_gather_ubench.md)
+        self.ticks = self.tscale = None
+        b16 = self.cfg.engine.bank16
+        if b16 not in ("auto", "off"):
+            raise ValueError(f"engine.bank16: {b16!r}")
+        if (b16 == "auto" and self.step_kernel == "ws" and self.cfg.env.features == "relative"
+                and self.prices.is_contiguous()):
+            t16 = native.tick16(self.prices, quantize=False)
+            if t16 is not None:
+                self.ticks, self.tscale = t16
+        # window-gather copies of the fp32 bank: 4 shifted replicas for the 16-B-aligned gathers of the wide
+        # kernels; one padded copy for ws (4-B-aligned dwordx4 reads, as fast: profiles/r3_ws_ab.md) -- none when
+        # the ws windows come from the tick bank
+        self.prices4 = (None if self.ticks is not None else
+                        native.replicate4(self.prices, 1 if self.step_kernel in ("ws", "pipe") else 4))
         # ws: the weight images in LDS byte order, kept current by the optimizer pass and copied by DMA in the
         # kernel's prologue (the per-launch gather of them cost ~10 us: profiles/r5_ws_prologue.md)
         self._wimg = self._wimg_map = None
@@ -366,7 +393,12 @@ class VectorEngine:
         cfg, L, st = self.cfg, self.layout, self.state
         seg = L.segments
         q = native.QStepParams()
-        q.prices4, q.T4 = native.ptr(self.prices4), int(self.prices4.shape[2])
+        if self.prices4 is not None:
+            q.prices4, q.T4 = native.ptr(self.prices4), int(self.prices4.shape[2])
+        else:
+            q.prices4, q.T4 = None, native.replica_stride(self.T)
+        if self.ticks is not None:
+            q.ticks, q.tscale, q.T16 = native.ptr(self.ticks), native.ptr(self.tscale), int(self.ticks.shape[1])
         q.prices, q.env = native.ptr(self.prices), native.ptr(self.env_soa)
         q.wq, q.wf = native.ptr(self.params_bf), native.ptr(self.params)
         q.wimg = native.ptr(self._wimg) if self._wimg is not None else None
@@ -390,7 +422,7 @@ class VectorEngine:
         q.key0, q.key1 = int(self.key0), int(self.key1)
         q.env_offset = self.env_offset
         q.chunk_heads = native.ptr(self.chunk_heads) if self.chunk_heads is not None else None
-        q.reward_mode = {"absolute": 0, "relative": 1}[cfg.agent.reward_mode]
+        q.reward_mode = {"absolute": 0, "relative": 1, "growth": 2}[cfg.agent.reward_mode]
         q.td_clip = float(cfg.agent.td_clip)
         self.kernel_err = torch.zeros(4, dtype=torch.int32, device=self.device)
         q.err = native.ptr(self.kernel_err)
@@ -405,6 +437,7 @@ class VectorEngine:
             t = native.QTargetParams()
             t.prices4, t.env, t.wt, t.qt = q.prices4, q.env, native.ptr(self.params_target), q.qt
             t.T, t.E, t.T4 = q.T, q.E, q.T4
+            t.ticks, t.tscale, t.T16 = q.ticks, q.tscale, q.T16
             t.off_w0, t.off_w1, t.off_b1, t.off_w2, t.off_b2 = q.off_w0, q.off_w1, q.off_b1, q.off_w2, q.off_b2
             t.b0, t.inv_b0, t.s0 = q.b0, q.inv_b0, q.s0
             t.compat_env, t.output_relu, t.feat_mode = q.compat_env, q.output_relu, q.feat_mode

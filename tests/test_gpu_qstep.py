@@ -344,8 +344,8 @@ def test_reward_modes_and_td_clip_match_oracle(native_built, chunk):
         assert _rel(grad, g_ref) < 3e-2, (mode, clip, _rel(grad, g_ref))
 
 
-@pytest.mark.parametrize("kernel,E", [("wide", 131072), ("ws", 393216)])
-def test_large_bank_gather_matches_oracle(native_built, kernel, E):
+@pytest.mark.parametrize("kernel,E,bank16", [("wide", 131072, "auto"), ("ws", 393216, "off"), ("ws", 786432, "auto")])
+def test_large_bank_gather_matches_oracle(native_built, kernel, E, bank16):
     """x 6,047 days: the wide kernel's 4 aligned replicas of 131,072 envs hold 3.2e9 floats, the ws
     kernel's single padded copy of 393,216 envs 2.4e9, so the window offsets of the upper envs pass
     2^31 elements (the bench runs 1,835,008 envs per GPU).  The last 512 envs (windows spread over the
@@ -358,11 +358,17 @@ def test_large_bank_gather_matches_oracle(native_built, kernel, E):
     cfg.agent.epsilon, cfg.agent.ramp = 1.0, 1.0   # exploit whenever pos >= 1: actions = argmax Q(x)
     cfg.data.source, cfg.data.length = "random_walk", 6047
     cfg.engine.step_kernel = kernel
+    cfg.engine.bank16 = bank16
     S = 512
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=E)
-    assert eng.chunk == 64 and eng.step_kernel == kernel and eng.prices4.numel() > 2 ** 31
-    assert eng.prices4.shape[0] == (1 if kernel == "ws" else 4)
+    assert eng.chunk == 64 and eng.step_kernel == kernel
+    if kernel == "ws" and bank16 == "auto":
+        # the synthetic bank is on a tick grid: the ws windows come from the 16-bit tick copy (4.8e9 ticks)
+        assert eng.prices4 is None and eng.ticks.numel() > 2 ** 32
+    else:
+        assert eng.ticks is None and eng.prices4.numel() > 2 ** 31
+        assert eng.prices4.shape[0] == (1 if kernel == "ws" else 4)
     idx = torch.arange(E, dtype=torch.int32, device=dev)
     eng.state.pos.copy_(1 + idx * 37 % (eng.T - cfg.model.history - 3))
     eng.state.shares.copy_(idx % 3)

@@ -34,10 +34,14 @@ def _cfg(compat=False, kernel="ws"):
     return cfg
 
 
-def _prices(E, T=400, seed=3):
-    from sharetrade.data.prices import random_walk
+def _prices(E, T=400, seed=3, tick16=True):
+    """Random-walk banks on the 16-bit tick grid (data.tick16, as the engine's synthetic banks): the ws kernel then
+    reads its windows as u16 ticks (the production path); ``tick16=False`` keeps arbitrary fp32 prices (its fp32
+    window path)."""
+    from sharetrade.data.prices import random_walk, tick16_quantize
 
-    return torch.from_numpy(random_walk(T, 50.0, 0.02, seed, n_series=E).astype(np.float32))
+    p = random_walk(T, 50.0, 0.02, seed, n_series=E).astype(np.float32)
+    return torch.from_numpy(tick16_quantize(p) if tick16 else p)
 
 
 def _rel(a, b):
@@ -269,6 +273,71 @@ def test_ws_adam_trajectory_matches_torch_oracle(native_built, kernel):
     assert _rel(d, dr) < 4e-4, _rel(d, dr)
 
 
+def test_tick16_kernel_matches_host_mirror(native_built):
+    """csrc/series.hip tick16 (mode 0: quantize in place) equals data.prices.tick16_quantize bit for bit; its
+    ticks times the row scale give the quantized prices back; mode 1 accepts a bank on the grid and rejects one
+    off it; the engine's synthetic random-walk bank is on the grid."""
+    from sharetrade.data.prices import random_walk, tick16_quantize
+    from sharetrade.ops import native
+    from sharetrade.trainer.engine import make_price_bank
+
+    p = random_walk(517, 50.0, 0.03, 3, n_series=300).astype(np.float32)
+    p[7] *= 1e-3
+    p[8] *= 1e5
+    dev = torch.device("cuda", 0)
+    g = torch.from_numpy(p).to(dev)
+    assert native.tick16(g.clone(), quantize=False) is None              # off the grid
+    native.tick16_quantize_(g)
+    q = tick16_quantize(p)
+    assert torch.equal(g.cpu(), torch.from_numpy(q))
+    ticks, scale = native.tick16(g, quantize=False)                       # on the grid now
+    t = ticks.cpu().numpy().view(np.uint16).astype(np.float32)
+    assert np.array_equal(t[:, :517] * scale.cpu().numpy()[:, None], q)
+    assert not t[:, 517:].any()
+    cfg = _cfg()
+    cfg.data.length = 700
+    bank = make_price_bank(cfg, 128, dev, seed=1)
+    assert native.tick16(bank, quantize=False) is not None
+
+
+@pytest.mark.parametrize("knobs", [False, True])
+def test_ws_tick_bank_bit_identical_to_fp32_windows(native_built, knobs):
+    """The 16-bit tick windows (engine.bank16='auto' on a bank on the tick grid) against the fp32 windows of the
+    same bank (bank16='off'): features are the same numbers (w / last - 1 = tick_w / tick_last - 1 exactly), so
+    6 captured steps give bit-identical parameters, optimizer state, env state and statistics -- with the
+    learning knobs, the target pass (csrc/qtarget.hip) on ticks too.  Positions spread so both odd and even
+    window starts occur in every tile.  And a bank off the grid keeps the fp32 path."""
+    from sharetrade.trainer.engine import VectorEngine
+
+    E = 2048
+    prices = _prices(E, T=330, seed=31)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for b16 in ("auto", "off"):
+        cfg = _cfg()
+        cfg.engine.bank16 = b16
+        cfg.agent.epsilon = 0.7
+        if knobs:
+            cfg.agent.target_every, cfg.agent.double_dqn, cfg.agent.reward_scale = 2, True, 3.0
+        eng = VectorEngine(cfg, prices=prices, device=dev, envs=E)
+        assert (eng.ticks is not None) == (b16 == "auto")
+        eng.state.pos.copy_(torch.arange(E, dtype=torch.int32, device=dev) * 13 % 120)
+        eng.capture_graph(warmup=1)
+        eng.run(6)
+        torch.cuda.synchronize()
+        assert int(eng.kernel_err.sum()) == 0
+        out[b16] = [eng.params.detach().cpu().clone(), eng.opt.s1.cpu().clone(), eng.opt.s2.cpu().clone(),
+                    eng.stat_acc.cpu().clone()] + [v.cpu().clone() for v in eng.state.as_dict().values()]
+    for x, y in zip(out["auto"], out["off"]):
+        if x.is_floating_point():
+            x, y = x.view(torch.int32) if x.dtype == torch.float32 else x.view(torch.int64), \
+                   y.view(torch.int32) if y.dtype == torch.float32 else y.view(torch.int64)
+        assert torch.equal(x, y)
+    cfg = _cfg()
+    eng = VectorEngine(cfg, prices=_prices(256, T=330, seed=31, tick16=False), device=dev, envs=256)
+    assert eng.ticks is None and eng.prices4 is not None
+
+
 def test_ws_weight_image_stays_equal_to_fresh_pack(native_built, monkeypatch):
     """The ws prologue DMA-copies a weight image that the optimizer keeps current by scatter writes (img_map).
     After several Adam steps it equals a fresh pack of the parameters byte for byte, and a run with the image
@@ -299,8 +368,11 @@ def test_ws_weight_image_stays_equal_to_fresh_pack(native_built, monkeypatch):
     a, b = out["1"], out["0"]
     for x, y in zip(a[:3], b[:3]):
         assert torch.equal(x, y)
-    for k in a[3]:
-        assert torch.equal(a[3][k], b[3][k]), k
+    for k in a[3]:   # (bit patterns: last_final holds NaN until an episode completes)
+        x, y = a[3][k], b[3][k]
+        if x.is_floating_point():
+            x, y = x.view(torch.int32), y.view(torch.int32)
+        assert torch.equal(x, y), k
 
 
 @pytest.mark.parametrize("E,grid", [(64 * 48, 16), (64 * 100, 8), (64 * 13, 8), (64 * 1000, 16), (64 * 2048, 256)])
