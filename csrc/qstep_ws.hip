@@ -747,6 +747,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) H1n[ks] = cat8(relu_bf(a1n[2 * ks]), relu_bf(a1n[2 * ks + 1]));
       // the next tile's price windows issued here
+      // (issued earlier -- right after the features or after layer 1 -- the u16 windows (35 VGPRs) still spill
+      // the data wave: 76-192 B of scratch, round 6)
       WS_LOAD_PRICES(k + 1, 1, e_pos)
 #pragma unroll
       for (int i = 0; i < 8; ++i) a2[i] = *reinterpret_cast<const f4v*>(sB1 + 16 * i + 4 * g4);

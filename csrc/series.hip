@@ -83,7 +83,8 @@ __global__ void __launch_bounds__(256) tick16_kernel(float* __restrict__ bank, i
   while (ldexpf(m, -x) > 65535.f) ++x;
   const float sc = ldexpf(1.0f, x);
   unsigned short* trow = ticks ? ticks + (size_t)wave * T16 : nullptr;
-  for (int t = lane; t < T16; t += 64) {
+  const int tend = trow ? T16 : T;
+  for (int t = lane; t < tend; t += 64) {
     unsigned tk = 0u;
     if (t < T) {
       const float v = row[t];
