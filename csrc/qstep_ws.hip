@@ -48,6 +48,13 @@
 #ifndef WS_PD1
 #define WS_PD1 8        // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs (10: 0.5 % slower, 12: 1 %)
 #endif
+#ifndef WS_FIL
+#define WS_FIL 0        // U16: window features of k-steps 1..5 and the tail built inside layer 1 (VALU slots between
+                        // its MFMAs) instead of before it
+#endif
+#ifndef WS_FILV
+#define WS_FILV 4       // WS_FIL: VALU instructions the schedule places between two MFMA pairs of layer 1
+#endif
 #ifndef WS_NOPHIL
 #define WS_NOPHIL 0     // timing build csrc/ab/qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
 #endif
@@ -552,8 +559,20 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto lo16f = [](unsigned v) { return (float)(v & 0xFFFFu); };
       auto hi16f = [](unsigned v) { return (float)(v >> 16); };
       s8v X[6], Xn[6];
+      constexpr bool FIL = U16 && WS_FIL;
+      auto feat_ks = [&](int ks) {   // U16: the k-step's B operands of x and x' from its 5 raw dwords
+          const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
+                         w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),
+                         w2 = __builtin_amdgcn_alignbyte(ta[ks].w, ta[ks].z, shb),
+                         w3 = __builtin_amdgcn_alignbyte(tb[ks], ta[ks].w, shb),
+                         w4 = __builtin_amdgcn_alignbyte(0u, tb[ks], shb);
+          const float f0 = lo16f(w0), f1 = hi16f(w0), f2 = lo16f(w1), f3 = hi16f(w1), f4 = lo16f(w2),
+                      f5 = hi16f(w2), f6 = lo16f(w3), f7 = hi16f(w3), f8 = lo16f(w4);
+          X[ks] = cat8(pk4(fx(f0), fx(f1), fx(f2), fx(f3)), pk4(fx(f4), fx(f5), fx(f6), fx(f7)));
+          Xn[ks] = cat8(pk4(fxn(f1), fxn(f2), fxn(f3), fxn(f4)), pk4(fxn(f5), fxn(f6), fxn(f7), fxn(f8)));
+      };
 #pragma unroll
-      for (int ks = 0; ks < 6; ++ks) {
+      for (int ks = 0; ks < (FIL ? 1 : 6); ++ks) {
         if (U16) {
           const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
                          w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),
@@ -573,8 +592,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       // last k-step (16 wide, slot order): g4 = 0 (budget, shares, 1, col 200); 1, 2 window columns; 3 pads
       s4v X6, Xn6;
+      const float bud_t = e_b;   // the tile's budget / shares (the env-state registers rotate below)
+      const int sh_t = e_sh;
+      auto feat_tail = [&]() {
       if (g4 == 0) {
-        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, fx(lastw));
+        X6 = pk4(feat_budget(bud_t, p.inv_b0, FEAT), feat_shares(sh_t, last, p.inv_b0, FEAT), 1.0f, fx(lastw));
         Xn6 = zero_s4();   // completed after the env step
       } else if (g4 < 3) {
         if (U16) {
@@ -591,11 +613,14 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         X6 = zero_s4();
         Xn6 = zero_s4();
       }
+      };
+      if (!FIL) feat_tail();
       const int pos = e_pos, sh0 = e_sh, ep0 = e_ep;
       const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
       // rotate the prefetched env state; load the one after next
       e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep; e_sc = n_sc;
-      WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
+      if (!FIL) { WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6); }
+      else { WS_PIN(X[0]); WS_PIN(Xn[0]); }
       WS_SB();
       WS_STAMP(1);
       // (after the features: a store or load issued before them would hold their window wait)
@@ -632,6 +657,10 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
         for (int j = 0; j < 48; ++j) {
           const int ks = j >> 3, i = j & 7;
+          if (FIL && rep == 0 && i == 0) {   // the next k-step's operands, in this k-step's VALU slots
+            if (ks < 5) feat_ks(ks + 1);
+            else feat_tail();
+          }
           a1[i] = mfma32(A[j % NB1], X[ks], a1[i]);
           a1n[i] = mfma32(A[j % NB1], Xn[ks], a1n[i]);
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
@@ -640,7 +669,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
             A[jn % NB1] = lds_ld8(w0b + (jn & 7) * 16 * KX + 32 * (jn >> 3));
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           }
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU (the Philox draw) between MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x002, FIL ? WS_FILV : 2, 0);   // VALU (Philox, features) between MFMAs
         }
         }
         WS_PIN(u1); WS_PIN(u2);   // (else the draw sinks into the env-step branch)
