@@ -48,13 +48,6 @@
 #ifndef WS_PD1
 #define WS_PD1 8        // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs (10: 0.5 % slower, 12: 1 %)
 #endif
-#ifndef WS_FIL
-#define WS_FIL 0        // U16: window features of k-steps 1..5 and the tail built inside layer 1 (VALU slots between
-                        // its MFMAs) instead of before it
-#endif
-#ifndef WS_FILV
-#define WS_FILV 4       // WS_FIL: VALU instructions the schedule places between two MFMA pairs of layer 1
-#endif
 #ifndef WS_NOPHIL
 #define WS_NOPHIL 0     // timing build csrc/ab/qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
 #endif
@@ -559,7 +552,9 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto lo16f = [](unsigned v) { return (float)(v & 0xFFFFu); };
       auto hi16f = [](unsigned v) { return (float)(v >> 16); };
       s8v X[6], Xn[6];
-      constexpr bool FIL = U16 && WS_FIL;
+      // (round 6: building k-steps 1..5 and the tail inside layer 1's VALU slots instead ties: 0.578-0.582 vs
+      // 0.577-0.597 ms on one box; 4 or 8 VALU per MFMA pair spill)
+      constexpr bool FIL = false;
       auto feat_ks = [&](int ks) {   // U16: the k-step's B operands of x and x' from its 5 raw dwords
           const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
                          w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),

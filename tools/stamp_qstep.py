@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--waves", type=int, default=8, help="64-env-chunk kernel: 4 or 8 waves")
     ap.add_argument("--kernel", default="auto", help="engine.step_kernel: auto | wide | narrow | ws")
     ap.add_argument("--ws-dvariant", default="", help="ws: data-wave stamps build suffix ('' = stamps, gskipst)")
+    ap.add_argument("--bank16", default="auto", help="ws: engine.bank16 (auto: u16 tick windows; off: fp32 windows)")
     a = ap.parse_args()
     if a.kernel == "ws":
         return ws_stamps(a)
@@ -100,6 +101,7 @@ def ws_stamps(a):
 
     cfg = preset_config("flagship")
     cfg.engine.step_kernel = "ws"
+    cfg.engine.bank16 = a.bank16
     dev = torch.device("cuda", 0)
     eng = VectorEngine(cfg, device=dev, envs=a.envs)
     eng.run(3)
@@ -126,7 +128,7 @@ def ws_stamps(a):
              "epsilon-greedy + env step", "Q(x'): layer-1 tail, layer 2, output (8 + 32 + 4 MFMA) + next prices issued",
              "TD + state write-back", "dZ2 (8 MFMA 16x16x16 + packed mask)", "dZ2, dQ -> slot, publish"]
     lines = [f"# ws step kernel: data wave 0 of workgroup 0 ({a.envs} envs, grid {eng.grid}, {nmy} tiles per data "
-             f"wave; s_memtime ticks; build {a.ws_dvariant or 'stamps'})\n", "| phase | ticks/tile | % |", "|---|---|---|"]
+             f"wave; s_memtime ticks; build {a.ws_dvariant or 'stamps'}; windows {'u16 ticks' if eng.ticks is not None else 'fp32'})\n", "| phase | ticks/tile | % |", "|---|---|---|"]
     tot = 0.0
     rows = []
     for ph in range(11):
