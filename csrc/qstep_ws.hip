@@ -552,22 +552,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto lo16f = [](unsigned v) { return (float)(v & 0xFFFFu); };
       auto hi16f = [](unsigned v) { return (float)(v >> 16); };
       s8v X[6], Xn[6];
-      // (round 6: building k-steps 1..5 and the tail inside layer 1's VALU slots instead ties: 0.578-0.582 vs
-      // 0.577-0.597 ms on one box; 4 or 8 VALU per MFMA pair spill)
-      constexpr bool FIL = false;
-      auto feat_ks = [&](int ks) {   // U16: the k-step's B operands of x and x' from its 5 raw dwords
-          const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
-                         w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),
-                         w2 = __builtin_amdgcn_alignbyte(ta[ks].w, ta[ks].z, shb),
-                         w3 = __builtin_amdgcn_alignbyte(tb[ks], ta[ks].w, shb),
-                         w4 = __builtin_amdgcn_alignbyte(0u, tb[ks], shb);
-          const float f0 = lo16f(w0), f1 = hi16f(w0), f2 = lo16f(w1), f3 = hi16f(w1), f4 = lo16f(w2),
-                      f5 = hi16f(w2), f6 = lo16f(w3), f7 = hi16f(w3), f8 = lo16f(w4);
-          X[ks] = cat8(pk4(fx(f0), fx(f1), fx(f2), fx(f3)), pk4(fx(f4), fx(f5), fx(f6), fx(f7)));
-          Xn[ks] = cat8(pk4(fxn(f1), fxn(f2), fxn(f3), fxn(f4)), pk4(fxn(f5), fxn(f6), fxn(f7), fxn(f8)));
-      };
 #pragma unroll
-      for (int ks = 0; ks < (FIL ? 1 : 6); ++ks) {
+      for (int ks = 0; ks < 6; ++ks) {
         if (U16) {
           const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
                          w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),
@@ -587,11 +573,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       }
       // last k-step (16 wide, slot order): g4 = 0 (budget, shares, 1, col 200); 1, 2 window columns; 3 pads
       s4v X6, Xn6;
-      const float bud_t = e_b;   // the tile's budget / shares (the env-state registers rotate below)
-      const int sh_t = e_sh;
-      auto feat_tail = [&]() {
       if (g4 == 0) {
-        X6 = pk4(feat_budget(bud_t, p.inv_b0, FEAT), feat_shares(sh_t, last, p.inv_b0, FEAT), 1.0f, fx(lastw));
+        X6 = pk4(feat_budget(e_b, p.inv_b0, FEAT), feat_shares(e_sh, last, p.inv_b0, FEAT), 1.0f, fx(lastw));
         Xn6 = zero_s4();   // completed after the env step
       } else if (g4 < 3) {
         if (U16) {
@@ -608,14 +591,11 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
         X6 = zero_s4();
         Xn6 = zero_s4();
       }
-      };
-      if (!FIL) feat_tail();
       const int pos = e_pos, sh0 = e_sh, ep0 = e_ep;
       const float bud0 = e_b, vprev = e_val, rs0 = e_rs;
       // rotate the prefetched env state; load the one after next
       e_pos = n_pos; e_b = n_b; e_sh = n_sh; e_val = n_val; e_rs = n_rs; e_ep = n_ep; e_sc = n_sc;
-      if (!FIL) { WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6); }
-      else { WS_PIN(X[0]); WS_PIN(Xn[0]); }
+      WS_PIN(X[5]); WS_PIN(Xn[5]); WS_PIN(X6);
       WS_SB();
       WS_STAMP(1);
       // (after the features: a store or load issued before them would hold their window wait)
@@ -652,10 +632,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
 #pragma unroll
         for (int j = 0; j < 48; ++j) {
           const int ks = j >> 3, i = j & 7;
-          if (FIL && rep == 0 && i == 0) {   // the next k-step's operands, in this k-step's VALU slots
-            if (ks < 5) feat_ks(ks + 1);
-            else feat_tail();
-          }
           a1[i] = mfma32(A[j % NB1], X[ks], a1[i]);
           a1n[i] = mfma32(A[j % NB1], Xn[ks], a1n[i]);
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
@@ -664,7 +640,7 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
             A[jn % NB1] = lds_ld8(w0b + (jn & 7) * 16 * KX + 32 * (jn >> 3));
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           }
-          __builtin_amdgcn_sched_group_barrier(0x002, FIL ? WS_FILV : 2, 0);   // VALU (Philox, features) between MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU (the Philox draw) between MFMAs
         }
         }
         WS_PIN(u1); WS_PIN(u2);   // (else the draw sinks into the env-step branch)
