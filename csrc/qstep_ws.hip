@@ -32,8 +32,6 @@
 // 208 = 6 k-steps of 32 + one of 16), 64-env chunks (one 16-env tile per data wave), static chunk
 // schedule.  Numerics: bf16 operands, fp32 accumulation, the rounding points of qstep_wide.hip; fp32
 // summation order differs (bias added first, k order pi inside MFMAs, per-16-env gradient sums).
-#include <type_traits>
-
 #include "qstep.h"
 
 #ifndef WS_STAMPS
@@ -49,13 +47,6 @@
 #endif
 #ifndef WS_PD1
 #define WS_PD1 8        // data waves: layer-1 W0 fragment pairs read ahead of their MFMAs (10: 0.5 % slower, 12: 1 %)
-#endif
-#ifndef WS_PAR
-#define WS_PAR 0        // U16: window features from the raw ticks by static word selects when the tile's envs share
-                        // their window parity (lock-step envs: every tile), v_alignbyte only for mixed tiles
-#endif
-#ifndef WS_DPRIO
-#define WS_DPRIO 0      // data waves at s_setprio WS_DPRIO through the tile loop (0: no priorities)
 #endif
 #ifndef WS_NOPHIL
 #define WS_NOPHIL 0     // timing build csrc/ab/qstep_ws_nophil.hip: no Philox draw (constant u1, u2; wrong results)
@@ -405,7 +396,6 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
   if (wave < ND) {
     // ================================================================ DATA WAVE
     const int d = wave;
-    if (WS_DPRIO > 0) __builtin_amdgcn_s_setprio(WS_DPRIO);   // the critical chain's wave first on its SIMD
     float st_reward = 0.f, st_loss = 0.f, st_explore = 0.f, st_done = 0.f, st_fsum = 0.f, st_fsq = 0.f,
           st_qslot = 0.f;
     const float b2v[3] = {sB2[0], sB2[1], sB2[2]};
@@ -562,37 +552,8 @@ __global__ void __launch_bounds__(NT, 1) qstep_ws_kernel(QStepParams p) {
       auto lo16f = [](unsigned v) { return (float)(v & 0xFFFFu); };
       auto hi16f = [](unsigned v) { return (float)(v >> 16); };
       s8v X[6], Xn[6];
-      // U16 with every env of the tile at the same window parity (WS_PAR): word i of the k-step's 5 dwords
-      // (ta.x .. ta.w, tb) is tick i - SH, converted by a static SDWA word select -- no v_alignbyte
-      auto feat_par = [&](auto shc) {
-        constexpr int SH = decltype(shc)::value;
-#pragma unroll
-        for (int ks = 0; ks < 6; ++ks) {
-          const unsigned dw[5] = {ta[ks].x, ta[ks].y, ta[ks].z, ta[ks].w, tb[ks]};
-          float f[9];
-#pragma unroll
-          for (int i = 0; i < 9; ++i) {
-            const int w = i + SH;
-            f[i] = (w & 1) ? hi16f(dw[w >> 1]) : lo16f(dw[w >> 1]);
-          }
-          X[ks] = cat8(pk4(fx(f[0]), fx(f[1]), fx(f[2]), fx(f[3])), pk4(fx(f[4]), fx(f[5]), fx(f[6]), fx(f[7])));
-          Xn[ks] = cat8(pk4(fxn(f[1]), fxn(f[2]), fxn(f[3]), fxn(f[4])), pk4(fxn(f[5]), fxn(f[6]), fxn(f[7]), fxn(f[8])));
-        }
-      };
-      bool par_done = false;
-      if (U16 && WS_PAR) {
-        const unsigned long long odd = __builtin_amdgcn_ballot_w64(shb != 0u);
-        if (odd == 0ull) {
-          feat_par(std::integral_constant<int, 0>());
-          par_done = true;
-        } else if (odd == ~0ull) {
-          feat_par(std::integral_constant<int, 1>());
-          par_done = true;
-        }
-      }
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
-        if (par_done) break;
         if (U16) {
           const unsigned w0 = __builtin_amdgcn_alignbyte(ta[ks].y, ta[ks].x, shb),
                          w1 = __builtin_amdgcn_alignbyte(ta[ks].z, ta[ks].y, shb),
