@@ -38,6 +38,40 @@ METRIC = "env steps/sec (whole node) + episode return, 2x128 MLP Q-net at 1/2/4/
 REFERENCE_FLOOR = 58.0  # derived minimum throughput of the reference app; not a published number
 
 
+STABLE_RAMP = 500.0   # exploit ramp of the stabilised learner over the bench's ~281 training steps (r6 sweep)
+
+
+def learner_knobs_on(cfg) -> bool:
+    a = cfg.agent
+    return bool(a.target_every or a.double_dqn or a.reward_scale != 1.0 or a.ramp_mode != "position")
+
+
+def stable_learner_eval(args, dev, rank, world, group, train_steps):
+    """Train preset flagship_stable (target net refreshed every 1,000 steps + Double DQN + reward scale 100 + gamma
+    0.99, exploit ramp STABLE_RAMP) on the same banks for ``train_steps`` steps, then one greedy frozen episode per
+    env: the learner that beats a random policy's median on this bank (profiles/r6_learner_breakdown.md)."""
+    from sharetrade.config import preset_config
+    from sharetrade.trainer import benchkit
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config("flagship_stable")
+    cfg.engine.envs_per_rank = args.envs
+    cfg.agent.ramp = STABLE_RAMP
+    eng = VectorEngine(cfg, device=dev, rank=rank, world_size=world, group=group)
+    eng.sync_params_from(0)
+    benchkit.prepare_steps(eng, not args.no_graph, rank, world, group, prime_reps=8 if world > 1 else 16,
+                           fixed_prime=True)
+    if train_steps > eng.step_count:
+        eng.run(train_steps - eng.step_count)
+    eng.synchronize()
+    g = benchkit.greedy_episode_returns(eng, world, group)
+    res = {"preset": "flagship_stable", "ramp": STABLE_RAMP, "train_steps": eng.step_count,
+           "greedy_mean": round(g["mean"], 4), "greedy_std": round(g["std"], 4), "greedy_median": round(g["median"], 4)}
+    del eng
+    torch.cuda.empty_cache()
+    return res
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +112,9 @@ def main() -> int:
     ap.add_argument("--double-dqn", action="store_true", help="learning knob: Double DQN (needs --target-every)")
     ap.add_argument("--reward-scale", type=float, default=1.0, help="learning knob: reward multiplier in the TD target")
     ap.add_argument("--ramp-mode", default="position", help="learning knob: exploit ramp over 'position' | 'global'")
+    ap.add_argument("--no-stable-eval", action="store_true",
+                    help="skip the untimed evaluation of the stabilised learner (preset flagship_stable: target net + "
+                         "Double DQN, trained for the same number of steps on the same banks)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,6 +264,17 @@ def main() -> int:
     if world > 1:
         peaks = [torch.zeros_like(peak) for _ in range(world)]
         torch.distributed.all_gather(peaks, peak)
+    # the stabilised learner (untimed, after everything above): the plain learner's greedy policy chases momentum on
+    # this bank and loses to a uniformly random one on the median (profiles/r6_learner_breakdown.md); Double DQN
+    # with a target network does not.  Same banks, same number of training steps, then the same greedy episode.
+    stable = None
+    if episodes is not None and not args.no_stable_eval and not learner_knobs_on(cfg):
+        try:
+            stable = stable_learner_eval(args, dev, rank, world, group, eng.step_count)
+        except Exception as e:  # noqa: BLE001 -- the timed measurement above stands
+            if world > 1:
+                raise
+            stable = {"error": f"{type(e).__name__}: {str(e).splitlines()[0] if str(e) else ''}"}
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -296,6 +344,11 @@ def main() -> int:
                 er[f"{k}_median"] = round(episodes[k]["median"], 4)
             er["episodes"] = lr_["n"]
             er["complete_frac"] = round(min(episodes[k]["complete_frac"] for k in episodes), 6)
+            if stable is not None:
+                if "error" not in stable:
+                    stable["greedy_median_minus_random_median"] = round(stable["greedy_median"] -
+                                                                        episodes["random"]["median"], 4)
+                er["stable_learner"] = stable
             out["episode_return"] = er
         print(json.dumps(out))
     if world > 1:

@@ -32,3 +32,10 @@ def test_bench_json_contract(native_built):
     assert c["global_batch"] == 8192 and c["parallelism"] == "dp1" and c["seq_len"] == 201
     # value is the whole-job rate implied by ms_per_step
     assert abs(d["value"] - 8192 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
+    # the untimed evaluations: the plain learner's episodes and the stabilised learner's greedy episode
+    er = d["episode_return"]
+    for k in ("greedy_median", "random_median", "buy_hold_median"):
+        assert k in er, k
+    sl = er["stable_learner"]
+    assert "error" not in sl, sl
+    assert sl["preset"] == "flagship_stable" and sl["train_steps"] >= 44 and "greedy_median" in sl
