@@ -203,6 +203,7 @@ def main() -> int:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(args.trace)
     eng.check_kernel_err()   # (untimed) a ws ring-protocol abort in the window would make its gradients invalid
+    trained_steps = eng.step_count   # prime + warm-up + timed: what the evaluated policy has learned from
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     pf1 = eng.current_portfolios().double()
     # per-env return over the window (episode resets inside the window are rare: 5,846-step episodes)
@@ -270,7 +271,7 @@ def main() -> int:
     stable = None
     if episodes is not None and not args.no_stable_eval and not learner_knobs_on(cfg):
         try:
-            stable = stable_learner_eval(args, dev, rank, world, group, eng.step_count)
+            stable = stable_learner_eval(args, dev, rank, world, group, trained_steps)
         except Exception as e:  # noqa: BLE001 -- the timed measurement above stands
             if world > 1:
                 raise

@@ -196,3 +196,42 @@ def test_philox_init_identical_on_host_and_device(native_built):
     a = qn.init_params(layout, cfg.model, seed=5, device="cpu")
     b = qn.init_params(layout, cfg.model, seed=5, device=torch.device("cuda", 0))
     assert a.device.type == "cpu" and torch.equal(a, b.cpu())
+
+
+def _bench_learner(preset, **agent):
+    """The bench's engine (its synthetic bank, 1,835,008 envs) trained exactly as bench.py trains before its
+    evaluation: 256 graph-primed + 5 warm-up + 20 timed steps."""
+    from sharetrade.config import preset_config
+    from sharetrade.trainer import benchkit
+    from sharetrade.trainer.engine import VectorEngine
+
+    cfg = preset_config(preset)
+    cfg.engine.envs_per_rank = 7 << 18
+    for k, v in agent.items():
+        setattr(cfg.agent, k, v)
+    eng = VectorEngine(cfg, device=torch.device("cuda", 0))
+    benchkit.prepare_steps(eng, True, 0, 1, prime_reps=16, fixed_prime=True)
+    eng.run(25)
+    eng.synchronize()
+    assert eng.step_count == 281 and eng.ticks is not None
+    return eng
+
+
+def test_bench_learners_against_random_median(native_built):
+    """VERDICT r5 item 5, pinned at the bench's batch and training length (profiles/r6_learner_breakdown.md):
+    the plain flagship learner's greedy policy ends below a uniformly random policy on the median (it chases
+    momentum on this bank), and the stabilised learner (target network + Double DQN, bench.py's stable_learner
+    evaluation: preset flagship_stable, ramp 500) ends above it."""
+    from sharetrade.trainer import benchkit
+
+    eng = _bench_learner("flagship")
+    plain = benchkit.greedy_episode_returns(eng)
+    rnd = benchkit.full_episode_returns(eng, random_policy=True)
+    del eng
+    torch.cuda.empty_cache()
+    eng = _bench_learner("flagship_stable", ramp=500.0)
+    stable = benchkit.greedy_episode_returns(eng)
+    print(f"[meas] greedy median plain {plain['median']:.1f}, stable {stable['median']:.1f}, random {rnd['median']:.1f}")
+    # measured (round 6): plain -484 .. -502, stable 267 .. 611 over seeds / boxes, random 214 .. 217
+    assert plain["median"] < rnd["median"] - 300
+    assert stable["median"] > rnd["median"] + 25
