@@ -200,7 +200,7 @@ def test_philox_init_identical_on_host_and_device(native_built):
 
 def _bench_learner(preset, **agent):
     """The bench's engine (its synthetic bank, 1,835,008 envs) trained exactly as bench.py trains before its
-    evaluation: 256 graph-primed + 5 warm-up + 20 timed steps."""
+    evaluation: 2 eager + 1 + 16 x 16 graph-primed (bench.py's graph_prime_steps = 259) + 5 warm-up + 20 timed steps."""
     from sharetrade.config import preset_config
     from sharetrade.trainer import benchkit
     from sharetrade.trainer.engine import VectorEngine
@@ -213,7 +213,7 @@ def _bench_learner(preset, **agent):
     benchkit.prepare_steps(eng, True, 0, 1, prime_reps=16, fixed_prime=True)
     eng.run(25)
     eng.synchronize()
-    assert eng.step_count == 281 and eng.ticks is not None
+    assert eng.step_count == 284 and eng.ticks is not None
     return eng
 
 
