@@ -448,7 +448,9 @@ class VectorEngine:
                 t.wimg = native.ptr(self._qt_img)
             self._qtp = t
             # one workgroup per CU (the weight images take 87.5 KB of LDS), grid-stride over 16-env tiles
-            self._qt_variant = int(os.environ.get("SHARETRADE_QT_VARIANT", "1"))
+            # variant 3 (one 16-env tile per wave, 16 waves): 383 vs 393 us for variant 1 on the tick windows, 442
+            # vs 447 on fp32 windows (tools/bench_qtarget.py, profiles/r6_window_u16.md)
+            self._qt_variant = int(os.environ.get("SHARETRADE_QT_VARIANT", "3"))
             tpw, nw = native.QTARGET_VARIANTS[self._qt_variant]
             if self.E % (16 * tpw):
                 raise NotImplementedError(f"target pass: E % {16 * tpw} != 0")
