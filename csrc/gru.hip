@@ -922,7 +922,8 @@ __global__ void __launch_bounds__(RT, 1) gru_act_pair_kernel(GruAct p) {
   auto writeback = [&](auto sl) {
     constexpr int K = decltype(sl)::v;
     if (!valid_[K]) return;
-    const int e0 = e0_[K];
+    int e0 = e0_[K];
+    asm volatile("" : "+s"(e0));   // (the h row addresses recomputed here, not kept from init() across the step loop)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
