@@ -33,10 +33,13 @@ NS = "sharetrade"
 @custom_op(f"{NS}::gemm_nt", mutates_args=())
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor], relu: bool, out_fp32: bool) -> torch.Tensor:
     """``C = A . B^T`` on the bf16 MFMA GEMM (csrc/gemm_bf16.hip): A [M, K], B [N, K] bf16 (K-contiguous),
-    optional fp32 bias [N] and ReLU fused into the epilogue; C bf16 (or fp32 with ``out_fp32``).  Tile choice as
+    optional fp32 bias [N] fused into the epilogue; C bf16 with an optional fused ReLU, or fp32 (``out_fp32``,
+    no ReLU).  Tile choice as
     the engines' (``ops.gemm.auto_tile``); M, N, K must fit whole tiles (K % 64 == 0)."""
     from . import gemm as gm
 
+    if relu and out_fp32:
+        raise ValueError("sharetrade::gemm_nt: the fp32 epilogue has bias (and alpha / accumulate) but no ReLU")
     M, N = A.shape[0], B.shape[0]
     out = torch.empty(M, N, dtype=torch.float32 if out_fp32 else torch.bfloat16, device=A.device)
     gm.gemm_nt(A.contiguous(), B.contiguous(), out, gm.EPI_F32 if out_fp32 else gm.EPI_BF16,

@@ -19,11 +19,13 @@ def test_gemm_nt_op_matches_fp32_reference(native_built):
     A = torch.randn(512, 256, device="cuda", generator=g).bfloat16()
     B = torch.randn(256, 256, device="cuda", generator=g).bfloat16()
     bias = torch.randn(256, device="cuda", generator=g)
-    ref = torch.relu(A.float() @ B.float().t() + bias)
-    out = torch.ops.sharetrade.gemm_nt(A, B, bias, True, True)
-    assert out.dtype == torch.float32 and _rel(out, ref) < 1e-5
-    outb = torch.ops.sharetrade.gemm_nt(A, B, None, False, False)
-    assert outb.dtype == torch.bfloat16 and _rel(outb, A.float() @ B.float().t()) < 1e-2
+    lin = A.float() @ B.float().t() + bias
+    out = torch.ops.sharetrade.gemm_nt(A, B, bias, False, True)      # fp32 epilogue: bias
+    assert out.dtype == torch.float32 and _rel(out, lin) < 1e-5
+    outb = torch.ops.sharetrade.gemm_nt(A, B, bias, True, False)     # bf16 epilogue: bias + ReLU
+    assert outb.dtype == torch.bfloat16 and _rel(outb, torch.relu(lin)) < 1e-2
+    with pytest.raises(Exception, match="ReLU"):
+        torch.ops.sharetrade.gemm_nt(A, B, bias, True, True)
 
 
 def test_qnet_select_op_matches_reference(native_built):
@@ -79,7 +81,7 @@ def test_ops_in_profiler_and_compile(native_built):
     assert any("sharetrade::gemm_nt" in e.name for e in prof.events())
 
     def f(a, b):
-        return torch.ops.sharetrade.gemm_nt(a, b, None, True, True) * 2.0
+        return torch.ops.sharetrade.gemm_nt(a, b, None, False, True) * 2.0
 
     cf = torch.compile(f, backend="eager", fullgraph=True)
     assert torch.allclose(cf(A, B), f(A, B))
