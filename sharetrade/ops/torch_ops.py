@@ -34,8 +34,7 @@ NS = "sharetrade"
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor], relu: bool, out_fp32: bool) -> torch.Tensor:
     """``C = A . B^T`` on the bf16 MFMA GEMM (csrc/gemm_bf16.hip): A [M, K], B [N, K] bf16 (K-contiguous),
     optional fp32 bias [N] fused into the epilogue; C bf16 with an optional fused ReLU, or fp32 (``out_fp32``,
-    no ReLU).  Tile choice as
-    the engines' (``ops.gemm.auto_tile``); M, N, K must fit whole tiles (K % 64 == 0)."""
+    no ReLU).  Tile choice as the engines' (``ops.gemm.auto_tile``); M, N, K must fit whole tiles (K % 64 == 0)."""
     from . import gemm as gm
 
     if relu and out_fp32:
