@@ -383,10 +383,7 @@ ST_DEV void wait_vm_lgkm0() {   // vmcnt = N, lgkmcnt = 0, expcnt not waited on
 ST_DEV void barrier() { asm volatile("s_barrier" ::: "memory"); }
 }  // namespace pp
 
-// LS = 1: every interval's LDS-DMA staging is issued by the group in its L segment only (4 waves, 8 pieces each per
-// interval), so the C segment's wave issues nothing but its 64 MFMAs (LS = 0: both groups stage 4 pieces per interval;
-// an LDS-DMA piece costs the issuing wave ~60 cycles among bare MFMAs: MI355X_MICROARCH.md, per-instruction table)
-template <int EPI, int PRIO = 0, int LS = 0>
+template <int EPI, int PRIO = 0>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
@@ -411,17 +408,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
     if (kt < nk)
       stage_tile<128, 8>(p.B, p.ldb, n0 + 128 * half, kt * GBK, buf + pp::B_OFF + (kt % 3) * pp::BB + half * pp::HT,
                          wave, lane);
-  };
-  // LS: the same pieces staged by the 4 waves of one group (wc = wave within the group)
-  auto stA4 = [&](int half, int kt) {
-    if (kt < nk)
-      stage_tile<128, 4>(p.A, p.lda, m0 + 128 * half, kt * GBK, buf + pp::A_OFF + (kt & 1) * pp::AB + half * pp::HT,
-                         wc, lane);
-  };
-  auto stB4 = [&](int half, int kt) {
-    if (kt < nk)
-      stage_tile<128, 4>(p.B, p.ldb, n0 + 128 * half, kt * GBK, buf + pp::B_OFF + (kt % 3) * pp::BB + half * pp::HT,
-                         wc, lane);
   };
 
   f4v acc[8][4];
@@ -468,53 +454,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
     stB(1, t + 2);
   };
 
-  if constexpr (LS) {
-    // prologue as below (all 8 waves), drained; then in every interval only the group in its L segment stages:
-    // G0 stage_even(t) in interval 2t, G1 stage_odd(t) in interval 2t + 1.  Each group's L interval ends with a
-    // vmcnt that leaves exactly that interval's pieces in flight (the pieces it staged one L interval earlier have
-    // landed: one barrier before their first read), a C interval with lgkmcnt(0) only.
-    stA(0, 0);
-    stB(0, 0);
-    stB(1, 0);
-    stA(1, 0);
-    stB(0, 1);
-    stA(0, 1);
-    stB(1, 1);
-    pp::wait_vm_lgkm0<0>();
-    pp::barrier();
-    auto c_end = [&]() {
-      pp::wait_vm_lgkm0<63>();
-      pp::barrier();
-    };
-    if (wr == 0) {
-      for (int t = 0; t < nk; ++t) {
-        stA4(1, t + 1);              // stage_even(t)
-        stB4(0, t + 2);
-        load(t);                     // interval 2t
-        if (t + 2 < nk) pp::wait_vm_lgkm0<8>(); else if (t + 1 < nk) pp::wait_vm_lgkm0<4>(); else pp::wait_vm_lgkm0<0>();
-        pp::barrier();
-        compute();                   // interval 2t+1
-        c_end();
-      }
-    } else {
-      c_end();                       // interval 0: nothing to multiply yet
-      stA4(0, 2);                    // stage_odd(0)
-      stB4(1, 2);
-      load(0);                       // interval 1
-      if (2 < nk) pp::wait_vm_lgkm0<8>(); else pp::wait_vm_lgkm0<0>();
-      pp::barrier();
-      for (int t = 1; t < nk; ++t) {
-        compute();                   // interval 2t
-        c_end();
-        stA4(0, t + 2);              // stage_odd(t)
-        stB4(1, t + 2);
-        load(t);                     // interval 2t+1
-        if (t + 2 < nk) pp::wait_vm_lgkm0<8>(); else pp::wait_vm_lgkm0<0>();
-        pp::barrier();
-      }
-      compute();                     // interval 2nk
-    }
-  } else {
   // prologue: K-tile 0 whole, then what intervals -2 / -1 would have staged: A1(0) B0(1), A0(1) B1(1)
   stA(0, 0);
   stB(0, 0);
@@ -549,7 +488,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
       odd_end(t);
     }
     compute();                     // interval 2nk
-  }
   }
   pp::wait_vm_lgkm0<0>();
   pp::barrier();   // every wave is done with the K-loop buffers
@@ -604,16 +542,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
   }
 }
 
-template <int EPI, int PRIO = 0, int LS = 0>
+template <int EPI, int PRIO = 0>
 static hipError_t launch_gemm_pp(const GemmArgs& p, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, PRIO, LS>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, pp::LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       pp::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, PRIO, LS>), dim3((p.M / 256) * (p.N / 256)), dim3(pp::NT), pp::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, PRIO>), dim3((p.M / 256) * (p.N / 256)), dim3(pp::NT), pp::LDS_BYTES, s, p);
   return hipGetLastError();
 }
 
@@ -848,14 +786,6 @@ extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipSt
       return hipErrorInvalidValue;
     if (epi == st::EPI_BF16) return st::launch_gemm_w4<st::EPI_BF16>(*p, stream);
     if (epi == st::EPI_F32) return st::launch_gemm_w4<st::EPI_F32>(*p, stream);
-    return hipErrorInvalidValue;
-  }
-  if (tile == 10) {   // 256x256 ping-pong, all staging by the loading group (LS)
-    if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
-    if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)
-      return hipErrorInvalidValue;
-    if (epi == st::EPI_BF16) return st::launch_gemm_pp<st::EPI_BF16, 0, 1>(*p, stream);
-    if (epi == st::EPI_F32) return st::launch_gemm_pp<st::EPI_F32, 0, 1>(*p, stream);
     return hipErrorInvalidValue;
   }
   if (tile == 7 || tile == 8) {   // 256x256 ping-pong (8: with s_setprio); one product per launch,

@@ -13,7 +13,7 @@ from . import native
 EPI_BF16, EPI_RELU_GRAD, EPI_F32 = 0, 1, 2
 # (BM, BN) or (BM, BN, LDS stages) -> st_gemm_nt tile id (csrc/gemm_bf16.hip)
 TILES = {(128, 128): 0, (64, 64): 1, (128, 64): 2, (256, 128): 3, (128, 128, 3): 4, (128, 128, 4): 5,
-         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8, (256, 256, "w4"): 9, (256, 256, "ppl"): 10}
+         (256, 256): 6, (256, 256, "pp"): 7, (256, 256, "ppp"): 8, (256, 256, "w4"): 9}
 # 7: 8-wave ping-pong, 8: the same with s_setprio on the MFMA segments, 9: 4 waves of 128x128 with
 # fragment double buffering; 7-9 are gemm_nt only (no batch / C^T / split-K)
 
@@ -117,7 +117,7 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = EPI_
     """``out = A . B^T`` (+ epilogue).  ``splitk="auto"`` (fp32 epilogue only) splits long-K,
     few-tile products (weight gradients) over extra workgroups with atomic accumulation."""
     t = tile or auto_tile(A.shape[0], B.shape[0], epi, kw)
-    if len(t) == 3 and t[2] in ("pp", "ppp", "w4", "ppl") and kw.get("splitk", 1) == "auto":
+    if len(t) == 3 and t[2] in ("pp", "ppp", "w4") and kw.get("splitk", 1) == "auto":
         kw = dict(kw, splitk=1)
     sk = kw.pop("splitk", 1)
     prezeroed = kw.pop("prezeroed", False)   # split-K output already zeroed by an earlier kernel

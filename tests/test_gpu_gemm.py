@@ -189,7 +189,7 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     ref = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     gemm_nt(A, B, ref, EPI_BF16, tile=(128, 128), bias=bias, relu=True)
     out = torch.empty_like(ref)
-    for t in ((256, 256, "pp"), (256, 256, "w4"), (256, 256, "ppl")):
+    for t in ((256, 256, "pp"), (256, 256, "w4")):
         for _ in range(3):
             out.fill_(7)
             gemm_nt(A, B, out, EPI_BF16, tile=t, bias=bias, relu=True)
@@ -201,10 +201,8 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     o32 = torch.full((M, N), float("nan"), device="cuda")
     gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), bias=bias, alpha=0.5)
     gemm_nt(A, B, o32w, EPI_F32, tile=(256, 256, "w4"), bias=bias, alpha=0.5)
-    o32l = torch.full((M, N), float("nan"), device="cuda")
-    gemm_nt(A, B, o32l, EPI_F32, tile=(256, 256, "ppl"), bias=bias, alpha=0.5)
     torch.cuda.synchronize()
-    assert torch.equal(o32, r32) and torch.equal(o32w, r32) and torch.equal(o32l, r32)
+    assert torch.equal(o32, r32) and torch.equal(o32w, r32)
     gemm_nt(A, B, o32, EPI_F32, tile=(256, 256, "pp"), alpha=0.5, accumulate=True)
     full = 0.5 * (A.float() @ B.float().t())
     torch.cuda.synchronize()

@@ -29,7 +29,7 @@ def main():
     from sharetrade.ops import gemm as gm
 
     dev = torch.device("cuda", 0)
-    tiles = [t for t in gm.TILES if len(t) == 3 and t[2] in ("pp", "ppp", "w4", "ppl")] + [(128, 128)]
+    tiles = [t for t in gm.TILES if len(t) == 3 and t[2] in ("pp", "ppp", "w4")] + [(128, 128)]
     print("| M | N | K | " + " | ".join(str(t) for t in tiles) + " | hipBLASLt |")
     print("|---" * (4 + len(tiles)) + "|")
     for M, N, K in ((16384, 1024, 256), (16384, 1024, 1024), (16384, 1024, 4096), (8192, 8192, 8192),
