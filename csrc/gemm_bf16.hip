@@ -383,7 +383,10 @@ ST_DEV void wait_vm_lgkm0() {   // vmcnt = N, lgkmcnt = 0, expcnt not waited on
 ST_DEV void barrier() { asm volatile("s_barrier" ::: "memory"); }
 }  // namespace pp
 
-template <int EPI, int PRIO = 0>
+// ABL (tools/ubench/gemm_lab.hip ablations only; wrong results by design): 1 no staging in the K-loop,
+// 2 neither staging nor fragment reads (fragments of K-tile 0 reused), 3 no MFMAs.  GROUPED = 0: the
+// round-5 tile order (one tile row per XCD wave), kept for the lab's A/B (profiles/r6_gemm_ablation.md)
+template <int EPI, int PRIO = 0, int ABL = 0, int GROUPED = 1>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   bf16_t* buf = reinterpret_cast<bf16_t*>(gsm);
@@ -396,19 +399,46 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
     const int xcd = bid % 8, q = nwg / 8, r = nwg % 8;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
   }
-  const int m0 = (bid / ntn) * 256, n0 = (bid % ntn) * 256;
+  // tile order within an XCD's range: groups of 8 tile rows walked column by column, so the ~32
+  // workgroups one XCD runs at a time cover an 8 x 4 block of C (12 operand tiles per K-tile through its
+  // L2) instead of one tile row (1 + ntn); the same order as before when ntn <= 4
+  int tm, tn;
+  {
+    const int gsz = 8 * ntn, g = bid / gsz, r = bid % gsz;
+    const int gm = ntm - 8 * g < 8 ? ntm - 8 * g : 8;
+    tm = 8 * g + r % gm;
+    tn = r / gm;
+  }
+  const int m0 = (GROUPED ? tm : bid / ntn) * 256, n0 = (GROUPED ? tn : bid % ntn) * 256;
   const int nk = p.K / GBK;
 
-  auto stA = [&](int half, int kt) {   // A half-tile (rows m0 + 128 half ..) of K-tile kt
-    if (kt < nk)
-      stage_tile<128, 8>(p.A, p.lda, m0 + 128 * half, kt * GBK, buf + pp::A_OFF + (kt & 1) * pp::AB + half * pp::HT,
-                         wave, lane);
+  // Half-tile staging = stage_tile<128, 8>'s pieces (rows 8 wave + lane / 8 and 64 below them, swizzled
+  // chunk (lane & 7) ^ (lane / 8)), addressed as a uniform base (SGPRs: tile row, K-tile, wave) plus ONE
+  // loop-invariant 32-bit lane offset per operand: per-piece 64-bit lane addresses kept group 0's loop 2
+  // VGPRs over the 256 budget, and the spill's reload put a vmcnt(0) -- a drain of the staging -- in
+  // every K-tile.
+  const uint32_t sw8 = (uint32_t)(((lane & 7) ^ (lane >> 3)) << 3);
+  const uint32_t offA = ((uint32_t)(lane >> 3) * (uint32_t)p.lda + sw8) * 2u;
+  const uint32_t offB = ((uint32_t)(lane >> 3) * (uint32_t)p.ldb + sw8) * 2u;
+  auto glds = [&](const bf16_t* base, uint32_t off, bf16_t* lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(reinterpret_cast<const char*>(base) + off),
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
   };
-  auto stB = [&](int half, int kt) {
+  bool in_loop = false;   // ABL 1 / 2: no staging once the K-loop starts
+  auto stAq = [&](int half, int kt, int q) {   // piece q (rows + 64 q) of A half-tile (rows m0 + 128 half ..)
+    if ((ABL == 1 || ABL == 2) && in_loop) return;
     if (kt < nk)
-      stage_tile<128, 8>(p.B, p.ldb, n0 + 128 * half, kt * GBK, buf + pp::B_OFF + (kt % 3) * pp::BB + half * pp::HT,
-                         wave, lane);
+      glds(p.A + (size_t)(m0 + 128 * half + 8 * wave + 64 * q) * p.lda + kt * GBK, offA,
+           buf + pp::A_OFF + (kt & 1) * pp::AB + half * pp::HT + (wave + 8 * q) * 512);
   };
+  auto stBq = [&](int half, int kt, int q) {
+    if ((ABL == 1 || ABL == 2) && in_loop) return;
+    if (kt < nk)
+      glds(p.B + (size_t)(n0 + 128 * half + 8 * wave + 64 * q) * p.ldb + kt * GBK, offB,
+           buf + pp::B_OFF + (kt % 3) * pp::BB + half * pp::HT + (wave + 8 * q) * 512);
+  };
+  auto stA = [&](int half, int kt) { stAq(half, kt, 0); stAq(half, kt, 1); };
+  auto stB = [&](int half, int kt) { stBq(half, kt, 0); stBq(half, kt, 1); };
 
   f4v acc[8][4];
 #pragma unroll
@@ -417,6 +447,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
   s8v fa[8][2], fb[4][2];
   auto load = [&](int kt) {   // L segment: every fragment of K-tile kt this wave multiplies
+    if constexpr (ABL == 2) {
+      if (kt > 0) return;
+    }
     const bf16_t* bA = buf + pp::A_OFF + (kt & 1) * pp::AB + wr * pp::HT;
     const bf16_t* bB = buf + pp::B_OFF + (kt % 3) * pp::BB + (wc >> 1) * pp::HT;
 #pragma unroll
@@ -428,6 +461,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
     }
   };
   auto compute = [&]() {      // C segment: 64 MFMAs, no LDS access
+    if constexpr (ABL == 3) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(fa[i][kk]));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(fb[j][kk]));
+      }
+      return;
+    }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // the MFMA wave first when both can issue
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -464,6 +507,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
   stB(1, 1);
   if (nk > 1) pp::wait_vm_lgkm0<6>(); else pp::wait_vm_lgkm0<0>();
   pp::barrier();
+  in_loop = true;
   if (wr == 0) {
     for (int t = 0; t < nk; ++t) {
       stage_even(t);
@@ -542,16 +586,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p) {
   }
 }
 
-template <int EPI, int PRIO = 0>
+template <int EPI, int PRIO = 0, int ABL = 0, int GROUPED = 1>
 static hipError_t launch_gemm_pp(const GemmArgs& p, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       pp::LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, PRIO, ABL, GROUPED>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, pp::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, PRIO>), dim3((p.M / 256) * (p.N / 256)), dim3(pp::NT), pp::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, PRIO, ABL, GROUPED>), dim3((p.M / 256) * (p.N / 256)), dim3(pp::NT), pp::LDS_BYTES, s, p);
   return hipGetLastError();
 }
 

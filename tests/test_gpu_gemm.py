@@ -189,7 +189,7 @@ def test_gemm_pingpong_matches_128_tile(native_built, M, N, K):
     ref = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     gemm_nt(A, B, ref, EPI_BF16, tile=(128, 128), bias=bias, relu=True)
     out = torch.empty_like(ref)
-    for t in ((256, 256, "pp"), (256, 256, "w4")):
+    for t in ((256, 256, "pp"), (256, 256, "ppp"), (256, 256, "w4")):
         for _ in range(3):
             out.fill_(7)
             gemm_nt(A, B, out, EPI_BF16, tile=t, bias=bias, relu=True)
