@@ -439,6 +439,7 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
       w -= p.lr * (m * c1) / (sqrtf(v * c2) + p.eps);
       S.w[idx] = w;
     }
+    if (S.wb) S.wb[idx] = f2bf(w);   // biases: optional bf16 copy (the library act-step epilogue's operand)
     return w;
   };
   if (S.bias && !S.gT) {

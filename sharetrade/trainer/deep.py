@@ -119,7 +119,8 @@ class DeepDQN:
                  concurrent: bool = True, fused_adam: bool = True, overlap_act: bool = False,
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
-                 fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False):
+                 fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False,
+                 act_gemm: str = "lib"):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -161,6 +162,9 @@ class DeepDQN:
         # act_after_fwd (with overlap_act): fork the act step after the update's forward instead of
         # right after the replay sample
         self.act_after_fwd = bool(act_after_fwd)
+        if act_gemm not in ("own", "lib"):
+            raise ValueError(f"act_gemm must be 'own' or 'lib', not {act_gemm!r}")
+        self.act_gemm = act_gemm
         # early_adam (with overlap_act): Adam waits for the act step's forward only, not its env step
         self.early_adam = bool(early_adam)
         # data parallel (one process per GPU, trainer/runs.py): grad_sync(grad_flat) sums the weight and
@@ -434,25 +438,36 @@ class DeepDQN:
         b.w, b.g, b.m, b.v = (self.b[l].data_ptr(), self.db[l].data_ptr(), self.bm[l].data_ptr(),
                               self.bv[l].data_ptr())
         b.mask = None if bool(self.bmask[l].bool().all()) else self.bmask[l].data_ptr()
-        b.wb, b.wbT, b.gT = None, None, self.GT[l].data_ptr() if reduce else None
+        b.wb, b.wbT, b.gT = self._bscratch(l).data_ptr(), None, self.GT[l].data_ptr() if reduce else None
         b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
         b.blocks = (O + 31) // 32
         return b
 
     def _bscratch(self, l: int) -> torch.Tensor:
+        """bf16 copy of bias l [1, n], rewritten by every Adam step (the operand of the library act-step
+        epilogue, ``act_gemm="lib"``)."""
         if not hasattr(self, "_bias_bf"):
-            self._bias_bf = [torch.zeros(1, self.pdims[k + 1], dtype=torch.bfloat16, device=self.dev)
-                             for k in range(self.L)]
+            self._bias_bf = [self.b[k].detach().to(torch.bfloat16).view(1, -1).clone() for k in range(self.L)]
         return self._bias_bf[l]
 
+    def _refresh_bias_bf(self) -> None:
+        for l in range(self.L):
+            self._bscratch(l).copy_(self.b[l].view(1, -1).to(torch.bfloat16))
+
     # ---------------------------------------------------------------- forward
-    def _forward(self, X, acts, actsT, Wb, bias, Q) -> None:
-        """acts[l+1] = relu(acts[l] . W_l^T + b_l); Q = acts[L-1] . W_{L-1}^T + b_{L-1} (fp32)."""
+    def _forward(self, X, acts, actsT, Wb, bias, Q, lib: bool = False) -> None:
+        """acts[l+1] = relu(acts[l] . W_l^T + b_l); Q = acts[L-1] . W_{L-1}^T + b_{L-1} (fp32).  ``lib``: the
+        hidden layers after the first through hipBLASLt's fused bias + ReLU epilogue (bf16 bias copies; the
+        act step's 16,384 x 1024 -> 1024 layers, where the library's K loop is faster than our ping-pong
+        kernel's: profiles/r6_gemm_ablation.md)."""
         a = X
         for l in range(self.L):
             if l < self.L - 1:
-                gm.gemm_nt(a, Wb[l], acts[l + 1], gm.EPI_BF16, outT=actsT[l + 1] if actsT else None,
-                           bias=bias[l], relu=True)
+                if lib and l > 0:
+                    torch._addmm_activation(self._bscratch(l)[0], a, Wb[l].t(), out=acts[l + 1])
+                else:
+                    gm.gemm_nt(a, Wb[l], acts[l + 1], gm.EPI_BF16, outT=actsT[l + 1] if actsT else None,
+                               bias=bias[l], relu=True)
                 a = acts[l + 1]
             else:
                 gm.gemm_nt(a, Wb[l], Q, gm.EPI_F32, bias=bias[l])
@@ -481,7 +496,7 @@ class DeepDQN:
         ``after_forward()`` runs between the forward (the last reader of the weights) and the env step."""
         sh = native.stream_handle()
         native.check(self.k.st_deep_gather(self._gather_env, sh), "deep_gather(env)")
-        self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe)
+        self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe, lib=self.act_gemm == "lib")
         if after_forward is not None:
             after_forward()
         native.check(self.k.st_deep_env_step(self._env, sh), "deep_env_step")
@@ -624,6 +639,7 @@ class DeepDQN:
         for l in range(self.L):
             self.Wb[l].copy_(self.W[l].to(torch.bfloat16))
             self.WbT[l].copy_(self.W[l].t().contiguous().to(torch.bfloat16))
+        self._refresh_bias_bf()
         self.sync_target()
 
     def sync_target(self) -> None:
@@ -737,6 +753,7 @@ class DeepDQN:
             # the bf16 operand copies are a rounding of the masters (what the Adam kernel writes)
             self.Wb[l].copy_(self.W[l].to(torch.bfloat16))
             self.WbT[l].copy_(self.W[l].t().contiguous().to(torch.bfloat16))
+        self._refresh_bias_bf()
         for k in self._ENV_KEYS:
             getattr(self, k).copy_(d[k].to(self.dev))
         for k, t in self.rp.items():

@@ -189,3 +189,35 @@ def test_replay_gather_writes_x_transposed(native_built, fuse_xt):
     torch.cuda.synchronize()
     assert torch.equal(d.XT, d.X.t().contiguous())
     assert d.X.float().abs().sum() > 0
+
+
+def test_act_gemm_lib_matches_own_and_captures(native_built):
+    """act_gemm="lib": the act step's hidden layers after the first through hipBLASLt's fused bias + ReLU
+    epilogue.  The bf16 bias copies the Adam kernel rewrites equal the rounded fp32 biases after updates; the
+    library forward's Q matches our kernel's to bf16 accuracy (bias rounded to bf16, other summation order);
+    the path captures into the iteration graph."""
+    d = _dqn(act_gemm="lib")
+    for _ in range(6):
+        d.act_step()
+    for _ in range(3):
+        d.update_step()
+    torch.cuda.synchronize()
+    for l in range(d.L):
+        assert torch.equal(d._bscratch(l), d.b[l].view(1, -1).to(torch.bfloat16)), l
+        assert float(d.b[l].abs().sum()) > 0, l   # the biases moved, so the copies were rewritten
+    qs = []
+    for lib in (False, True):
+        acts = [d.Xe] + [t.clone() for t in d.Acte[1:]]
+        q = d.Qe.clone()
+        d._forward(d.Xe, acts, None, d.Wb, d.b, q, lib=lib)
+        qs.append(q[:, : d.n_act].float())
+    torch.cuda.synchronize()
+    own, lib = qs
+    assert float((lib - own).norm() / own.norm()) < 2e-2
+    d.capture()
+    for _ in range(3):
+        d.iteration()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(w).all() for w in d.W)
+    for l in range(d.L):
+        assert torch.equal(d._bscratch(l), d.b[l].view(1, -1).to(torch.bfloat16)), l
