@@ -50,6 +50,8 @@ def main():
                     help="the act step's hidden 1024 -> 1024 layers through hipBLASLt's fused bias + ReLU epilogue "
                          "(default: 0.408 vs 0.417 ms per iteration, profiles/r6_config4_act_lib.md) or on our "
                          "ping-pong kernel")
+    ap.add_argument("--no-fuse-head", action="store_true",
+                    help="TD and the output layer's backward as three launches instead of one")
     ap.add_argument("--no-overlap-act", action="store_true",
                     help="serial act step then update (default: the act step runs beside the update's GEMM chains "
                          "and the update samples the ring before this iteration's inserts; profiles/r2_config4_update_ab.md)")
@@ -72,7 +74,7 @@ def main():
                 concurrent=not a.serial, fused_adam=not a.unfused_adam, overlap_act=not a.no_overlap_act,
                 batched_fwd=not a.unbatched_fwd, dual_bwd=not a.no_dual_bwd, act_inline=a.act_inline,
                 fuse_act=a.fuse_act, fuse_xt=not a.no_fuse_xt, act_after_fwd=not a.act_before_fwd,
-                early_adam=a.early_adam, act_gemm=a.act_gemm)
+                early_adam=a.early_adam, act_gemm=a.act_gemm, fuse_head=not a.no_fuse_head)
     for _ in range(a.warmup):
         d.act_step()
     d.capture()
@@ -112,7 +114,7 @@ def main():
         "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
         "concurrent_update": d.concurrent, "fused_adam": d.fused_adam, "overlap_act": d.overlap_act,
         "batched_fwd": d.batched_fwd, "pingpong_gemm": not a.no_pingpong, "dual_bwd": d.dual_bwd, "act_inline": d.act_inline, "fuse_act": d.fuse_act,
-        "act_gemm": d.act_gemm,
+        "act_gemm": d.act_gemm, "fuse_head": d.fuse_head,
     }
     print(json.dumps(out))
 

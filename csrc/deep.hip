@@ -299,6 +299,136 @@ __global__ void __launch_bounds__(256) deep_td_kernel(DeepTD p) {
   if (p.t && blockIdx.x == 0 && threadIdx.x == 0) p.t[0] += 1ull;
 }
 
+// TD + the output layer's backward in one launch (replaces deep_td_kernel, the G_{L-2} = (dq . W_{L-1}) *
+// (A > 0) GEMM and the dW_{L-1} = dq^T . A split-K GEMM of the update chain).  dq has ONE nonzero per row
+// (coef * diff at the taken action a), so (dq . W)[m][n] = dq[m][a_m] * W[a_m][n]: the product of two bf16
+// values, exact in fp32 -- bit-identical to the GEMM's EPI_RELU_GRAD output -- and dW_{L-1}[a][n] is a sum
+// over the rows that took a.  Block (column block of 256, row block of 64), 256 threads:
+//   threads 0-63: TD of row m0 + t (dq, dqT, loss written by column block 0 only);
+//   thread (rg = t / 32, cc = t % 32): rows m0 + 8 rg .. +7, columns n0 + 8 cc .. +7 -- 16-byte loads of A
+//   and stores of G, G^T through an LDS transpose (8 rows of a column = one 16-byte LDS store), dW partials
+//   reduced over the 8 row groups in LDS, then one fp32 atomic per (action, column) per block (dW prezeroed).
+struct DeepHead {
+  DeepTD td;
+  const bf16_t* A;      // [B, H] last hidden activation (row-major)
+  const bf16_t* W;      // [ldq, H] output weights, bf16 copy
+  bf16_t* G;            // [B, H]
+  bf16_t* GT;           // [H, B]
+  float* dW;            // [ldq, H] fp32, zeroed before the launch
+  int H;
+};
+constexpr int HEAD_MAXA = 4;
+
+__global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
+  __shared__ float s_g[64];
+  __shared__ int s_a[64];
+  __shared__ __attribute__((aligned(16))) bf16_t sT[256][72];
+  __shared__ float red[8][HEAD_MAXA][256];
+  const DeepTD& q = p.td;
+  const int tid = threadIdx.x, m0 = blockIdx.y * 64, n0 = blockIdx.x * 256;
+  const int nact = q.n_actions;
+  if (tid < 64) {
+    const int b = m0 + tid;
+    const float* qt = q.qt + (size_t)b * q.ldq;
+    float mx = qt[0];
+    for (int a = 1; a < nact; ++a) mx = fmaxf(mx, qt[a]);
+    const float y = q.r[b] + q.gamma * (1.0f - q.done[b]) * mx;
+    const int a = q.a[b];
+    const float diff = q.q[(size_t)b * q.ldq + a] - y;
+    const bf16_t dqv = f2bf(q.coef * diff);
+    s_g[tid] = bf2f(dqv);
+    s_a[tid] = a;
+    if (blockIdx.x == 0) {
+      for (int j = 0; j < nact; ++j) {
+        const bf16_t v = (j == a) ? dqv : (bf16_t)0;
+        q.dq[(size_t)b * q.ldq + j] = v;
+        q.dqT[(size_t)j * q.B + b] = v;
+      }
+      const float l = wave_sum(diff * diff);
+      if (tid == 0) {
+        atomicAdd(q.loss, l);
+        if (q.t && blockIdx.y == 0) q.t[0] += 1ull;
+      }
+    }
+  }
+  __syncthreads();
+  const int rg = tid >> 5, cc = tid & 31, n = n0 + 8 * cc;
+  float wv[HEAD_MAXA][8];
+#pragma unroll
+  for (int a = 0; a < HEAD_MAXA; ++a) {
+    if (a < nact) {
+      const uint4 w4 = *reinterpret_cast<const uint4*>(p.W + (size_t)a * p.H + n);
+      const uint32_t u[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        wv[a][2 * k] = bf2f((bf16_t)(u[k] & 0xFFFF));
+        wv[a][2 * k + 1] = bf2f((bf16_t)(u[k] >> 16));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wv[a][k] = 0.f;
+    }
+  }
+  float acc[HEAD_MAXA][8];
+#pragma unroll
+  for (int a = 0; a < HEAD_MAXA; ++a)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[a][k] = 0.f;
+  bf16_t gcol[8][8];   // [column k][row r]
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int ml = 8 * rg + r, m = m0 + ml;
+    const int am = s_a[ml];
+    const float g = s_g[ml];
+    const uint4 x4 = *reinterpret_cast<const uint4*>(p.A + (size_t)m * p.H + n);
+    const uint32_t u[4] = {x4.x, x4.y, x4.z, x4.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bf16_t h[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int c = 2 * k + e;
+        const float av = bf2f((bf16_t)(e ? (u[k] >> 16) : (u[k] & 0xFFFF)));
+        float w = 0.f;
+#pragma unroll
+        for (int a = 0; a < HEAD_MAXA; ++a) {
+          if (a == am) w = wv[a][c];
+          acc[a][c] += (a == am) ? g * av : 0.f;
+        }
+        h[e] = (av > 0.f) ? f2bf(__fadd_rn(__fmul_rn(g, w), 0.f)) : (bf16_t)0;
+        gcol[c][r] = h[e];
+      }
+      o[k] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(p.G + (size_t)m * p.H + n) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (uint32_t)gcol[c][2 * k] | ((uint32_t)gcol[c][2 * k + 1] << 16);
+    *reinterpret_cast<uint4*>(&sT[8 * cc + c][8 * rg]) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+#pragma unroll
+  for (int a = 0; a < HEAD_MAXA; ++a)
+    if (a < nact)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) red[rg][a][8 * cc + c] = acc[a][c];
+  __syncthreads();
+#pragma unroll
+  for (int i = tid; i < 256 * 8; i += 256) {
+    const int nl = i >> 3, ch = i & 7;
+    *reinterpret_cast<uint4*>(p.GT + (size_t)(n0 + nl) * q.B + m0 + 8 * ch) = *reinterpret_cast<const uint4*>(&sT[nl][8 * ch]);
+  }
+  for (int a = 0; a < nact; ++a) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) sacc += red[g][a][tid];
+    atomicAdd(p.dW + (size_t)a * p.H + n0 + tid, sacc);
+  }
+}
+
 // bias gradient: db[o] = sum_b dZT[o][b]  (one workgroup per output row)
 __global__ void __launch_bounds__(256) row_sum_bf16_kernel(const bf16_t* __restrict__ X, int ld, int n, float* out) {
   __shared__ float red[4];
@@ -594,6 +724,14 @@ extern "C" hipError_t st_deep_env_step(const st::DeepEnv* p, hipStream_t s) {
 
 extern "C" hipError_t st_deep_td(const st::DeepTD* p, hipStream_t s) {
   hipLaunchKernelGGL(st::deep_td_kernel, dim3((p->B + 63) / 64), dim3(64), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_deep_head(const st::DeepHead* p, hipStream_t s) {
+  const st::DeepTD& q = p->td;
+  if (q.n_actions < 1 || q.n_actions > st::HEAD_MAXA || q.n_actions > q.ldq || q.B % 64 || p->H % 256 || q.B <= 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::deep_head_kernel, dim3(p->H / 256, q.B / 64), dim3(256), 0, s, *p);
   return hipGetLastError();
 }
 

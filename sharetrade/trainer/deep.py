@@ -67,6 +67,11 @@ class _TD(C.Structure):
                 ("n_actions", C.c_int), ("gamma", C.c_float), ("coef", C.c_float), ("t", C.c_void_p)]
 
 
+class _Head(C.Structure):
+    _fields_ = [("td", _TD), ("A", C.c_void_p), ("W", C.c_void_p), ("G", C.c_void_p), ("GT", C.c_void_p),
+                ("dW", C.c_void_p), ("H", C.c_int)]
+
+
 class _Adam(C.Structure):
     _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("mask", C.c_void_p),
                 ("wb", C.c_void_p), ("wbT", C.c_void_p), ("t", C.c_void_p), ("O", C.c_int), ("I", C.c_int),
@@ -93,6 +98,7 @@ def _bind():
         for fn, args in (("st_deep_gather", [C.POINTER(_Gather), C.c_void_p]),
                          ("st_deep_env_step", [C.POINTER(_Env), C.c_void_p]),
                          ("st_deep_td", [C.POINTER(_TD), C.c_void_p]),
+                         ("st_deep_head", [C.POINTER(_Head), C.c_void_p]),
                          ("st_row_sum_bf16", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
                          ("st_transpose_bf16", [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                 C.c_void_p]),
@@ -120,7 +126,7 @@ class DeepDQN:
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
                  fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False,
-                 act_gemm: str = "lib"):
+                 act_gemm: str = "lib", fuse_head: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -256,6 +262,10 @@ class DeepDQN:
             while tiles * self._q_splitk < 256 and ktiles % (2 * self._q_splitk) == 0 and \
                     ktiles // (2 * self._q_splitk) >= 4:
                 self._q_splitk *= 2
+        # fuse_head: TD + the output layer's backward (G_{L-2}, dW_{L-1}) in one launch (csrc/deep.hip
+        # deep_head_kernel); dW_{L-1} is then accumulated atomically into the zeroed span
+        self.fuse_head = bool(fuse_head) and self.L >= 2 and self.pdims[-2] % 256 == 0 and self.B % 64 == 0 \
+            and 1 <= self.n_act <= 4
         self._dual = [False] * self.L   # layer l's weight gradient in a dual launch with G_{l-1}
         if self.dual_bwd:
             for l in range(1, self.L - 1):
@@ -263,7 +273,8 @@ class DeepDQN:
                 if o % 128 == 0 and i % 128 == 0 and self.B % 128 == 0:
                     self._dw_plan[l] = ("hip", ((128, 128), gm.pick_splitk(o, i, self.B, (128, 128))))
                     self._dual[l] = True
-        sk_layers = [l for l, (k, a) in enumerate(self._dw_plan) if k == "hip" and a[1] > 1]
+        sk_layers = [l for l, (k, a) in enumerate(self._dw_plan) if k == "hip" and (a[1] > 1 or
+                                                                                    (self.fuse_head and l == self.L - 1))]
         self._zero_span = (0, 0)
         if sk_layers:
             lo = sum(sizes[:sk_layers[0]])
@@ -376,6 +387,12 @@ class DeepDQN:
         td.gamma, td.coef = float(cfg.agent.gamma), 2.0 / (self.B * self.world_size)
         td.t = self.t_ctr.data_ptr()   # the update counter advances in the TD kernel
         self._td = td
+        hd = _Head()
+        hd.td = td
+        hd.A, hd.W = self.Act[self.L - 1].data_ptr(), self.Wb[self.L - 1].data_ptr()
+        hd.G, hd.GT = self.G[self.L - 2].data_ptr(), self.GT[self.L - 2].data_ptr()
+        hd.dW, hd.H = self.dW[self.L - 1].data_ptr(), self.pdims[self.L - 1]
+        self._head = hd
         a = cfg.agent
         self._adam = []
         for l in range(self.L):
@@ -563,15 +580,19 @@ class DeepDQN:
             # the act step beside the backward chain (TD, small GEMMs, dual launches) rather than beside
             # the forward's GEMMs, which already fill the chip
             act_fwd_done = self._fork_act(main, act)
-        native.check(k.st_deep_td(self._td, sh), "deep_td")
+        if self.fuse_head:
+            native.check(k.st_deep_head(self._head, sh), "deep_head")
+        else:
+            native.check(k.st_deep_td(self._td, sh), "deep_td")
         for l in reversed(range(self.L)):
-            if self._dual[l]:
+            head = self.fuse_head and l == self.L - 1   # TD launch did G_{L-2} and dW_{L-1}
+            if not head and self._dual[l]:
                 # one launch: G_{l-1} = (G_l . W_l) * (A_l > 0)  and  dW_l = G_l^T . A_l (split-K)
                 _, (_, sk) = self._dw_plan[l]
                 gm.gemm_dual((self.G[l], self.WbT[l], self.G[l - 1], dict(outT=self.GT[l - 1], auxT=actsT[l])),
                              gm.EPI_RELU_GRAD,
                              (self.GT[l], actsT[l], self.dW[l], dict(splitk=sk, prezeroed=sk > 1)), gm.EPI_F32)
-            else:
+            elif not head:
                 if side is not None and not self.dual_bwd:
                     side.wait_stream(main)        # G_l is ready
                     with torch.cuda.stream(side):
@@ -590,7 +611,7 @@ class DeepDQN:
                     self.layer_sync(self.dW[l])
                     if self._bias_multi is None:
                         self.layer_sync(self.db[l])
-            if l > 0 and not self._dual[l]:
+            if l > 0 and not self._dual[l] and not head:
                 # G_{l-1} = (G_l . W_l) * (A_l > 0)
                 gm.gemm_nt(self.G[l], self.WbT[l], self.G[l - 1], gm.EPI_RELU_GRAD, outT=self.GT[l - 1],
                            auxT=actsT[l])

@@ -221,3 +221,28 @@ def test_act_gemm_lib_matches_own_and_captures(native_built):
     assert all(torch.isfinite(w).all() for w in d.W)
     for l in range(d.L):
         assert torch.equal(d._bscratch(l), d.b[l].view(1, -1).to(torch.bfloat16)), l
+
+
+def test_fused_head_matches_td_and_gemms(native_built):
+    """fuse_head: TD + the output layer's backward in one launch (csrc/deep.hip deep_head_kernel) gives the
+    same dq / dq^T, a bit-identical G_{L-2} and G_{L-2}^T (one nonzero product per element, as the
+    EPI_RELU_GRAD GEMM computes it) and dW_{L-1} equal up to fp32 summation order."""
+    res = []
+    for fuse in (True, False):
+        d = _dqn(fuse_head=fuse)
+        for _ in range(8):
+            d.act_step()
+        d.update_step()
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    assert a.fuse_head and not b.fuse_head
+    L = a.L
+    for k in (L - 1, L - 2):
+        assert torch.equal(a.G[k], b.G[k]), k
+        assert torch.equal(a.GT[k], b.GT[k]), k
+    assert float(a.G[L - 2].float().abs().sum()) > 0
+    assert float((a.dW[L - 1] - b.dW[L - 1]).norm() / b.dW[L - 1].norm()) < 1e-5
+    assert abs(float(a.loss) - float(b.loss)) <= 1e-5 * abs(float(b.loss))
+    for wa, wb in zip(a.W, b.W):
+        assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
