@@ -50,6 +50,9 @@ def main():
                     help="the act step's hidden 1024 -> 1024 layers through hipBLASLt's fused bias + ReLU epilogue "
                          "(default: 0.408 vs 0.417 ms per iteration, profiles/r6_config4_act_lib.md) or on our "
                          "ping-pong kernel")
+    ap.add_argument("--iters-per-graph", type=int, default=4,
+                    help="capture k whole iterations into one HIP graph (one launch per k iterations; 4: 0.402-0.405 vs "
+                         "0.405-0.409 ms per iteration at 1, profiles/r6_config4_head.md)")
     ap.add_argument("--no-fuse-head", action="store_true",
                     help="TD and the output layer's backward as three launches instead of one")
     ap.add_argument("--no-overlap-act", action="store_true",
@@ -77,13 +80,17 @@ def main():
                 early_adam=a.early_adam, act_gemm=a.act_gemm, fuse_head=not a.no_fuse_head)
     for _ in range(a.warmup):
         d.act_step()
-    d.capture()
+    k = a.iters_per_graph if a.updates == 1 else 1
+    d.capture(iters_per_graph=k)
     for _ in range(3):
         d.iteration(a.updates)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        d.iteration(a.updates)
+    if k > 1:
+        d.iterations(a.steps)
+    else:
+        for _ in range(a.steps):
+            d.iteration(a.updates)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     # time the two halves separately
@@ -114,7 +121,7 @@ def main():
         "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
         "concurrent_update": d.concurrent, "fused_adam": d.fused_adam, "overlap_act": d.overlap_act,
         "batched_fwd": d.batched_fwd, "pingpong_gemm": not a.no_pingpong, "dual_bwd": d.dual_bwd, "act_inline": d.act_inline, "fuse_act": d.fuse_act,
-        "act_gemm": d.act_gemm, "fuse_head": d.fuse_head,
+        "act_gemm": d.act_gemm, "fuse_head": d.fuse_head, "iters_per_graph": k,
     }
     print(json.dumps(out))
 

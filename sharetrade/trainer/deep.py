@@ -669,8 +669,11 @@ class DeepDQN:
             self.bt[l].copy_(self.b[l])
 
     # ---------------------------------------------------------------- driver
-    def capture(self) -> None:
-        """Capture one act step and one update into HIP graphs (after a warm-up of each)."""
+    def capture(self, iters_per_graph: int = 1) -> None:
+        """Capture one act step and one update into HIP graphs (after a warm-up of each).  With
+        ``iters_per_graph`` k > 1 (overlapped single-update iterations without a host all-reduce) also k whole
+        iterations into one graph, which ``iterations(n)`` replays: one graph launch per k iterations instead
+        of per iteration."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
@@ -696,6 +699,12 @@ class DeepDQN:
                 self._g_iter = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self._g_iter, capture_error_mode=_CAPTURE_MODE):
                     self.update_step(with_act=True)
+                if iters_per_graph > 1:
+                    self._g_iter_k = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._g_iter_k, capture_error_mode=_CAPTURE_MODE):
+                        for _ in range(iters_per_graph):
+                            self.update_step(with_act=True)
+                    self._iter_k = int(iters_per_graph)
         else:
             # data parallel: the gradient all-reduce runs between two graphs (act + gradients | Adam);
             # the collective itself stays outside the capture
@@ -715,6 +724,24 @@ class DeepDQN:
         (self._g_pre_act if with_act else self._g_pre).replay()
         self.grad_sync(self.grad_flat)
         self._g_post.replay()
+
+    def iterations(self, n: int) -> None:
+        """n single-update iterations: whole k-iteration graphs (``capture(iters_per_graph=k)``) where the
+        target-net copy cannot fall inside one (it runs on the host between graphs), single ones otherwise."""
+        k = getattr(self, "_iter_k", 1)
+        g = getattr(self, "_g_iter_k", None)
+        while n > 0:
+            if (g is not None and n >= k and (not self.target_every or
+                                              self.updates // self.target_every == (self.updates + k - 1) // self.target_every)):
+                g.replay()
+                self.env_steps += k
+                self.updates += k
+                if self.target_every and self.updates % self.target_every == 0:
+                    self.sync_target()
+                n -= k
+            else:
+                self.iteration()
+                n -= 1
 
     def iteration(self, updates_per_step: int = 1) -> None:
         if self.overlap_act and updates_per_step >= 1:

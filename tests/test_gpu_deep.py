@@ -246,3 +246,29 @@ def test_fused_head_matches_td_and_gemms(native_built):
     assert abs(float(a.loss) - float(b.loss)) <= 1e-5 * abs(float(b.loss))
     for wa, wb in zip(a.W, b.W):
         assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
+
+
+def test_k_iteration_graph_matches_single_iterations(native_built):
+    """capture(iters_per_graph=4) + iterations(n): 4 whole iterations per graph launch (singles where a
+    target-net copy would fall inside a graph) run the same sequence as n single-iteration replays: identical
+    env state and replay contents, weights within fp32 atomic-order tolerance, same counters."""
+    res = []
+    for k in (4, 1):
+        d = _dqn(dw_gemm="hip", overlap_act=True, target_every=6)
+        for _ in range(6):
+            d.act_step()
+        d.capture(iters_per_graph=k)
+        d.iterations(9)
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    assert a.updates == b.updates == 10 and a.env_steps == b.env_steps
+    assert int(a.t_ctr) == int(b.t_ctr) == 10
+    for k in ("pos", "budget", "shares", "episodes"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    for k in a.rp:
+        assert torch.equal(a.rp[k], b.rp[k]), k
+    for wa, wb in zip(a.W, b.W):
+        assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
+    for wa, wb in zip(a.Wt, b.Wt):
+        assert float((wa.float() - wb.float()).norm() / (wb.float().norm() + 1e-20)) < 1e-4
