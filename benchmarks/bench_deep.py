@@ -84,6 +84,8 @@ def main():
     d.capture(iters_per_graph=k)
     for _ in range(3):
         d.iteration(a.updates)
+    if k > 1:
+        d.iterations(2 * k)   # the multi-iteration graph's first replays upload it to the device
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if k > 1:

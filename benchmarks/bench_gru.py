@@ -25,13 +25,16 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--bars", type=int, default=4096)
     ap.add_argument("--replay", type=int, default=1 << 17)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=4, help="actor launches to pre-fill the replay")
     ap.add_argument("--updates", type=int, default=1)
     ap.add_argument("--grid", type=int, default=0,
                     help="actor workgroups (one per CU): 0 = auto (RecurrentDQN._auto_grid)")
     ap.add_argument("--actor-kernel", default="auto", choices=["auto", "single", "pair"],
                     help="single- or two-chunk actor kernel (auto: two-chunk when seq <= 32)")
+    ap.add_argument("--iters-per-graph", type=int, default=4,
+                    help="capture k (even) whole iterations into one HIP graph (one launch per k iterations; 4: "
+                         "0.583-0.584 vs 0.589-0.591 ms per iteration at 1 over 200 steps, profiles/r6_config5_kgraph.md)")
     ap.add_argument("--no-overlap-act", action="store_true",
                     help="serial actor launch then update (default: the actor runs beside the update after its "
                          "segments are sampled; profiles/r2_config5_overlap.md)")
@@ -49,13 +52,19 @@ def main():
     a.grid = d.grid
     for _ in range(a.warmup):
         d.act()
-    d.capture()
+    k = a.iters_per_graph if a.updates == 1 and not a.no_overlap_act else 1
+    d.capture(iters_per_graph=k)
     for _ in range(2):
         d.iteration(a.updates)
+    if k > 1:
+        d.iterations(2 * k)   # the multi-iteration graph's first replays upload it to the device
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        d.iteration(a.updates)
+    if k > 1:
+        d.iterations(a.steps)
+    else:
+        for _ in range(a.steps):
+            d.iteration(a.updates)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     t1 = time.perf_counter()
@@ -85,7 +94,7 @@ def main():
         "actor_tflops": round(act_flop / t_act / 1e12, 1),
         "update_ms": round(t_upd * 1e3, 4), "update_tflops": round(upd_flop / t_upd / 1e12, 1),
         "episodes": s["episodes"], "episode_return_mean": s["episode_return_mean"],
-        "reward_per_step": s["reward_per_step"], "loss": s["loss"], "overlap_act": d.overlap_act,
+        "reward_per_step": s["reward_per_step"], "loss": s["loss"], "overlap_act": d.overlap_act, "iters_per_graph": k,
         "actor_grid": a.grid, "actor_kernel": d.actor_kernel,
     }
     print(json.dumps(out))

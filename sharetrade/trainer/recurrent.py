@@ -405,9 +405,11 @@ class RecurrentDQN:
         """Whether the overlapped iteration alternates the online sets (not in the split DP capture)."""
         return self.grad_sync is None or self.capture_sync
 
-    def capture(self) -> None:
+    def capture(self, iters_per_graph: int = 1) -> None:
         """Warm up, then capture the actor launch, the learner update and (overlap_act) the whole
-        iteration into HIP graphs -- one of each per online weight set."""
+        iteration into HIP graphs -- one of each per online weight set.  ``iters_per_graph`` k > 1 (even;
+        overlapped, alternating sets, no host all-reduce): also k whole iterations per graph, one per
+        starting set, which ``iterations(n)`` replays."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         flip = self.overlap_act and self._flips()
@@ -440,6 +442,18 @@ class RecurrentDQN:
                     self._g_iters[par] = g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                         self.update(with_act=True, flip=True)
+        self._g_iters_k, self._iter_k = {}, 1
+        if self.overlap_act and self._flips() and iters_per_graph > 1:
+            if iters_per_graph % 2:
+                raise ValueError("iters_per_graph must be even (the online sets alternate)")
+            for par in (0, 1):
+                self._par = par
+                self._g_iters_k[par] = g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                    for _ in range(iters_per_graph):
+                        self.update(with_act=True, flip=True)
+                        self._par ^= 1
+            self._iter_k = int(iters_per_graph)
         self._par = cur
         if not self._flips():
             # data parallel: the gradient all-reduce runs between two graphs (gradients | Adam + re-pack),
@@ -481,6 +495,23 @@ class RecurrentDQN:
         self.updates += 1
         if self.updates % self.target_every == 0:
             self.sync_target()
+
+    def iterations(self, n: int) -> None:
+        """n single-update iterations: whole k-iteration graphs (``capture(iters_per_graph=k)``) where no
+        target-net copy falls inside one (it runs on the host between graphs), single ones otherwise."""
+        k = getattr(self, "_iter_k", 1)
+        gs = getattr(self, "_g_iters_k", {})
+        while n > 0:
+            if gs and n >= k and self.updates // self.target_every == (self.updates + k - 1) // self.target_every:
+                gs[self._par].replay()   # k even: the set alternates back
+                self.launches += k
+                self.updates += k
+                if self.updates % self.target_every == 0:
+                    self.sync_target()
+                n -= k
+            else:
+                self.iteration()
+                n -= 1
 
     def iteration(self, updates: int = 1) -> None:
         if self.overlap_act and updates >= 1:

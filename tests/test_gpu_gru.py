@@ -309,3 +309,28 @@ def test_pair_actor_rejects_long_sequences(native_built):
     with pytest.raises(ValueError):
         _small(S=40, actor_kernel="pair", bars=800)
     assert _small(S=40, bars=800).actor_kernel == "single"
+
+
+def test_k_iteration_graph_matches_single_iterations(native_built):
+    """capture(iters_per_graph=4) + iterations(n): 4 whole overlapped iterations (alternating online sets)
+    per graph launch, singles where a target copy would fall inside one -- the same sequence as single
+    iteration replays: identical replay / env counters, parameters within fp32 atomic-order noise."""
+    res = []
+    for k in (4, 1):
+        d = _small(E=256, S=8, eps=0.9, batch=256, overlap_act=True)
+        d.target_every = 6
+        for _ in range(2):
+            d.act()
+        d.capture(iters_per_graph=k)
+        d.iterations(9)
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    assert a.updates == b.updates == 10 and a.launches == b.launches
+    assert int(a.t_ctr) == int(b.t_ctr) == 10
+    assert a._par == b._par
+    assert torch.equal(a.rctrl, b.rctrl)
+    rel = float((a.flat - b.flat).norm() / (b.flat.norm() + 1e-20))
+    assert rel < 1e-5, rel
+    relt = float((a.tflat - b.tflat).norm() / (b.tflat.norm() + 1e-20))
+    assert relt < 1e-5, relt
