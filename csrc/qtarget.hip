@@ -103,12 +103,9 @@ struct QTargetParams {
 
 // TPW 16-env tiles per wave (each weight fragment read from LDS feeds TPW MFMAs), NWV waves per workgroup (one
 // workgroup per CU: the weight images take 87.5 KB of LDS)
-// PF (TPW 1 only): the next tile's window position is loaded one tile ahead, so a tile's window loads wait for
-// one HBM round trip instead of two (budget / shares load beside the window)
-template <int FEAT, int TPW, int NWV, bool U16 = false, bool PF = false>
+template <int FEAT, int TPW, int NWV, bool U16 = false>
 __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
   static_assert(!U16 || FEAT, "the tick bank serves the relative features only");
-  static_assert(!PF || TPW == 1, "env-state prefetch: one tile per wave");
   constexpr int NW = NWV, NT = 64 * NWV;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* W0 = reinterpret_cast<bf16_t*>(smem + oW0);
@@ -153,12 +150,6 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
   s4v w0t[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w0t[i] = lds_ld4(W0 + (16 * i + l16) * KS + 192 + 4 * g4);
-  int npos = 0;   // PF: window position of the wave's next tile
-  const int* envpos = p.env + ER_POS * E;
-  if constexpr (PF) {
-    const int t0f = (blockIdx.x * NW + w) * TPW;
-    if (t0f < ntiles) npos = envpos[(unsigned)(16 * t0f + l16)];
-  }
   for (int t0 = (blockIdx.x * NW + w) * TPW; t0 < ntiles; t0 += gridDim.x * NW * TPW) {
     // an opaque zero offset per iteration: the weight-fragment LDS reads are loop-invariant, and hoisted out of
     // the loops they would pin ~400 registers (W0 / W1 / W2 fragments) and spill
@@ -173,10 +164,9 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
       const int e = 16 * (t0 + q) + l16;
-      const int pos = PF ? npos : p.env[ER_POS * E + e];
+      const int pos = p.env[ER_POS * E + e];
       const float bud = __int_as_float(p.env[ER_BUDGET * E + e]);
       const int sh = p.env[ER_SHARES * E + e];
-
       const int pc = min(max(pos, 0), p.T - HWIN - 1);
       if (U16) {
         // x' starts at tick pc + 1: per k-step a dwordx4 + a dword from the 4-byte boundary at or below the lane's
@@ -251,10 +241,6 @@ __global__ void __launch_bounds__(64 * NWV, 1) qtarget_kernel(QTargetParams p) {
       }
 #pragma unroll
       for (int q = 0; q < TPW; ++q) a1[q][i] = mfma32z(w0t[i], Xw[q], a1[q][i]);
-    }
-    if constexpr (PF) {   // the next tile's window position, behind this tile's layer 1
-      const int tn = t0 + gridDim.x * NW * TPW;
-      if (tn < ntiles) npos = envpos[(unsigned)(16 * tn + l16)];
     }
 #pragma unroll 1
     for (int a = 0; a < 3; ++a) {
@@ -347,7 +333,7 @@ extern "C" hipError_t st_qtarget_img_map(int* map, int off_w0, int off_w1, int o
 
 
 namespace {
-template <int TPW, int NWV, bool PF = false>
+template <int TPW, int NWV>
 hipError_t launch_qt(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
   using namespace st::qtgt;
   if (p->E % (16 * TPW) != 0) return hipErrorInvalidValue;
@@ -355,20 +341,19 @@ hipError_t launch_qt(const st::qtgt::QTargetParams* p, int grid, hipStream_t str
   const bool u16 = p->ticks != nullptr;
   if (u16 && (!p->feat_mode || p->tscale == nullptr || p->T16 < p->T + 8 || p->T16 % 8)) return hipErrorInvalidValue;
   const int f = u16 ? 2 : (p->feat_mode ? 1 : 0);
-  const void* fn = f == 2 ? (const void*)qtarget_kernel<1, TPW, NWV, true, PF>
-                          : (f ? (const void*)qtarget_kernel<1, TPW, NWV, false, PF>
-                               : (const void*)qtarget_kernel<0, TPW, NWV, false, PF>);
+  const void* fn = f == 2 ? (const void*)qtarget_kernel<1, TPW, NWV, true>
+                          : (f ? (const void*)qtarget_kernel<1, TPW, NWV> : (const void*)qtarget_kernel<0, TPW, NWV>);
   if (!attr[f]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
     attr[f] = true;
   }
   if (f == 2)
-    hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV, true, PF>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
+    hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV, true>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
   else if (f)
-    hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV, false, PF>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
+    hipLaunchKernelGGL((qtarget_kernel<1, TPW, NWV>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
   else
-    hipLaunchKernelGGL((qtarget_kernel<0, TPW, NWV, false, PF>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
+    hipLaunchKernelGGL((qtarget_kernel<0, TPW, NWV>), dim3(grid), dim3(64 * NWV), LDS_BYTES, stream, *p);
   return hipGetLastError();
 }
 }  // namespace
@@ -386,7 +371,6 @@ extern "C" hipError_t st_qtarget_launch_v(const st::qtgt::QTargetParams* p, int 
     case 1: return launch_qt<2, 8>(p, grid, stream);
     case 2: return launch_qt<1, 8>(p, grid, stream);
     case 3: return launch_qt<1, 16>(p, grid, stream);
-    case 4: return launch_qt<1, 16, true>(p, grid, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -51,7 +51,7 @@ class QStepParams(C.Structure):
 
 
 # csrc/qtarget.hip launch variants: (16-env tiles per wave, waves per workgroup)
-QTARGET_VARIANTS = {0: (4, 4), 1: (2, 8), 2: (1, 8), 3: (1, 16), 4: (1, 16)}   # 4: 3 + next window position prefetched
+QTARGET_VARIANTS = {0: (4, 4), 1: (2, 8), 2: (1, 8), 3: (1, 16)}
 
 
 class QTargetParams(C.Structure):
