@@ -173,79 +173,82 @@ struct DeepEnv {
   float* stats;               // [4]: reward sum, explore count, episodes done, final sum (atomics)
 };
 
-// epsilon-greedy + Buy/Sell/Hold transition + replay insert, one thread per env.
-__global__ void __launch_bounds__(256) deep_env_step_kernel(DeepEnv p) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned long long step = p.ctrl[0];
-  float r_ = 0.f, x_ = 0.f;
-  if (e < p.E) {
-    const float* q = p.q + (size_t)e * p.ldq;
-    int greedy = 0;
-    float best = q[0];
-    for (int a = 1; a < p.n_actions; ++a)
-      if (q[a] > best) { best = q[a]; greedy = a; }
-    const int ps = p.pos[e];
-    uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32), c3 = 0u;
-    philox4x32(c0, c1, c2, c3, p.key0, p.key1);
-    const float u1 = u24(c0), u2 = u24(c1);
-    const bool exploit = u1 < fminf(p.eps, (float)ps * p.inv_ramp);
-    int rnd = (int)(u2 * 3.0f);
-    rnd = rnd > 2 ? 2 : rnd;
-    const int a = exploit ? greedy : rnd;
-    const float* pr = p.prices + (size_t)e * p.T + ps;
-    const float vnew = pr[p.H];
-    const float b = p.budget[e], vprev = p.value[e];
-    const int s = p.shares[e];
-    const float bd = p.compat_env ? p.b0 : b;
-    const int sd = p.compat_env ? p.s0 : s;
-    const bool buy = (a == 0) && (bd >= vnew);
-    const bool sell = (a == 1) && (sd > 0);
-    const float b2 = buy ? bd - vnew : (sell ? bd + vnew : bd);
-    const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
-    const float rew = (b2 + (float)s2 * vnew) - (b + (float)s * vprev);
-    const int np = ps + 1;
-    const bool done = np >= p.T - p.H;
-    // replay insert (ring)
-    const unsigned long long slot = (p.rp.ctrl[0] + (unsigned long long)e) % (unsigned long long)p.rp.cap;
-    p.rp.env[slot] = e;
-    p.rp.pos[slot] = ps;
-    p.rp.budget[slot] = b;
-    p.rp.shares[slot] = s;
-    p.rp.action[slot] = a;
-    p.rp.reward[slot] = rew;
-    p.rp.budget2[slot] = b2;
-    p.rp.shares2[slot] = s2;
-    p.rp.done[slot] = done ? 1 : 0;
-    if (done) {
-      const float fin = b2 + (float)s2 * vnew;
-      p.last_final[e] = fin;
-      p.episodes[e] += 1;
-      p.budget[e] = p.b0;
-      p.shares[e] = p.s0;
-      p.value[e] = 0.f;
-      p.pos[e] = 0;
-      atomicAdd(p.stats + 2, 1.f);
-      atomicAdd(p.stats + 3, fin);
-    } else {
-      p.budget[e] = b2;
-      p.shares[e] = s2;
-      p.value[e] = vnew;
-      p.pos[e] = np;
-    }
-    r_ = rew;
-    x_ = exploit ? 0.f : 1.f;
+// epsilon-greedy + Buy/Sell/Hold transition + replay insert of env e (greedy: argmax of its Q row)
+ST_DEV void deep_env_one(const DeepEnv& p, int e, int greedy, unsigned long long step, float& r_, float& x_) {
+  const int ps = p.pos[e];
+  uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(step & 0xFFFFFFFFull), c2 = (uint32_t)(step >> 32), c3 = 0u;
+  philox4x32(c0, c1, c2, c3, p.key0, p.key1);
+  const float u1 = u24(c0), u2 = u24(c1);
+  const bool exploit = u1 < fminf(p.eps, (float)ps * p.inv_ramp);
+  int rnd = (int)(u2 * 3.0f);
+  rnd = rnd > 2 ? 2 : rnd;
+  const int a = exploit ? greedy : rnd;
+  const float* pr = p.prices + (size_t)e * p.T + ps;
+  const float vnew = pr[p.H];
+  const float b = p.budget[e], vprev = p.value[e];
+  const int s = p.shares[e];
+  const float bd = p.compat_env ? p.b0 : b;
+  const int sd = p.compat_env ? p.s0 : s;
+  const bool buy = (a == 0) && (bd >= vnew);
+  const bool sell = (a == 1) && (sd > 0);
+  const float b2 = buy ? bd - vnew : (sell ? bd + vnew : bd);
+  const int s2 = buy ? sd + 1 : (sell ? sd - 1 : sd);
+  const float rew = (b2 + (float)s2 * vnew) - (b + (float)s * vprev);
+  const int np = ps + 1;
+  const bool done = np >= p.T - p.H;
+  // replay insert (ring)
+  const unsigned long long slot = (p.rp.ctrl[0] + (unsigned long long)e) % (unsigned long long)p.rp.cap;
+  p.rp.env[slot] = e;
+  p.rp.pos[slot] = ps;
+  p.rp.budget[slot] = b;
+  p.rp.shares[slot] = s;
+  p.rp.action[slot] = a;
+  p.rp.reward[slot] = rew;
+  p.rp.budget2[slot] = b2;
+  p.rp.shares2[slot] = s2;
+  p.rp.done[slot] = done ? 1 : 0;
+  if (done) {
+    const float fin = b2 + (float)s2 * vnew;
+    p.last_final[e] = fin;
+    p.episodes[e] += 1;
+    p.budget[e] = p.b0;
+    p.shares[e] = p.s0;
+    p.value[e] = 0.f;
+    p.pos[e] = 0;
+    atomicAdd(p.stats + 2, 1.f);
+    atomicAdd(p.stats + 3, fin);
+  } else {
+    p.budget[e] = b2;
+    p.shares[e] = s2;
+    p.value[e] = vnew;
+    p.pos[e] = np;
   }
-  // wave-reduced statistics (all lanes take part)
+  r_ = rew;
+  x_ = exploit ? 0.f : 1.f;
+}
+
+// the launch's statistics (every thread of every block takes part) and, in its last block, the ring cursor /
+// step counter advance (every thread read them before; ctrl[1] counts finished blocks, 0 between launches)
+ST_DEV void deep_env_finish(const DeepEnv& p, unsigned long long step, float r_, float x_) {
+  // block sums first: one pair of stats atomics per block (per-wave atomics on two addresses serialise)
+  __shared__ float red[16][2];
   r_ = wave_sum(r_);
   x_ = wave_sum(x_);
+  const int nw = blockDim.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(p.stats + 0, r_);
-    atomicAdd(p.stats + 1, x_);
+    red[threadIdx.x >> 6][0] = r_;
+    red[threadIdx.x >> 6][1] = x_;
   }
-  // the ring cursor / step counter advance in the launch's last block (every thread read them above, and
-  // the last block to finish runs after all of those reads): no one-thread launch behind the env step.
-  // ctrl[1] counts finished blocks (0 between launches).
   __syncthreads();
+  if (threadIdx.x == 0) {
+    float rs = 0.f, xs = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      rs += red[w][0];
+      xs += red[w][1];
+    }
+    atomicAdd(p.stats + 0, rs);
+    atomicAdd(p.stats + 1, xs);
+  }
   if (threadIdx.x == 0) {
     __threadfence();
     unsigned* done_blocks = reinterpret_cast<unsigned*>(p.ctrl + 1);
@@ -258,6 +261,22 @@ __global__ void __launch_bounds__(256) deep_env_step_kernel(DeepEnv p) {
       __threadfence();
     }
   }
+}
+
+// one thread per env: greedy action from the Q rows the output-layer GEMM wrote
+__global__ void __launch_bounds__(256) deep_env_step_kernel(DeepEnv p) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long step = p.ctrl[0];
+  float r_ = 0.f, x_ = 0.f;
+  if (e < p.E) {
+    const float* q = p.q + (size_t)e * p.ldq;
+    int greedy = 0;
+    float best = q[0];
+    for (int a = 1; a < p.n_actions; ++a)
+      if (q[a] > best) { best = q[a]; greedy = a; }
+    deep_env_one(p, e, greedy, step, r_, x_);
+  }
+  deep_env_finish(p, step, r_, x_);
 }
 
 struct DeepTD {
