@@ -43,9 +43,29 @@ static float host_f(unsigned short h) {
 
 typedef hipError_t (*launch_t)(const st::GemmArgs&, hipStream_t);
 
-int main() {
+int main(int argc, char** argv) {
   const int shapes[][3] = {{16384, 1024, 1024}, {16384, 1024, 4096}, {8192, 8192, 8192}, {4096, 4096, 4096},
                            {8192, 4096, 1024}, {4096, 1024, 1024}};
+  // "pmc V": only variant V at the act step's shape, 20 launches, no checks (one kernel for rocprofv3 --pmc)
+  if (argc > 2 && std::strcmp(argv[1], "pmc") == 0) {
+    const int v = std::atoi(argv[2]);
+    launch_t f[] = {st::launch_gemm_pp<st::EPI_BF16, 0>, st::launch_gemm_pp<st::EPI_BF16, 0, 1>,
+                    st::launch_gemm_pp<st::EPI_BF16, 0, 2>, st::launch_gemm_pp<st::EPI_BF16, 0, 3>};
+    const int M = 16384, N = 1024, K = 1024;
+    bf16_t *A, *B, *C;
+    CK(hipMalloc(&A, (size_t)M * K * 2));
+    CK(hipMalloc(&B, (size_t)N * K * 2));
+    CK(hipMalloc(&C, (size_t)M * N * 2));
+    CK(hipMemset(A, 0x3c, (size_t)M * K * 2));   // 0x3c3c: a small positive bf16 everywhere
+    CK(hipMemset(B, 0x3c, (size_t)N * K * 2));
+    st::GemmArgs a{};
+    a.A = A; a.B = B; a.out = C; a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = K; a.ldo = N;
+    a.relu = 1; a.alpha = 1.f; a.splitk = 1;
+    for (int i = 0; i < 20; ++i) CK(f[v](a, nullptr));
+    CK(hipDeviceSynchronize());
+    std::printf("pmc variant %d done\n", v);
+    return 0;
+  }
   const char* names[] = {"pp", "ppp", "pp-rowmajor", "pp-nostage", "pp-mfma-only", "pp-no-mfma"};
   launch_t fns[] = {st::launch_gemm_pp<st::EPI_BF16, 0>, st::launch_gemm_pp<st::EPI_BF16, 1>,
                     st::launch_gemm_pp<st::EPI_BF16, 0, 0, 0>, st::launch_gemm_pp<st::EPI_BF16, 0, 1>,
