@@ -94,11 +94,31 @@ ST_DEV void gather_row(const DeepGather& g, int row, int lane, float (&xv)[4]) {
   const float last = pr[H - 1], vnew = pr[H];
   const float inv = 1.0f / last, invn = 1.0f / vnew;
   float xnv[4];
+  // the lane's 4 window prices (and the 4 shifted by one for x') as 16-byte loads from 4-byte-aligned
+  // addresses where all 4 are window columns; scalar loads on the boundary lane
+  float wv[4], wnv[4];
+  if (4 * lane + 3 < H) {
+    float4 a4;
+    __builtin_memcpy(&a4, pr + 4 * lane, sizeof(a4));
+    wv[0] = a4.x; wv[1] = a4.y; wv[2] = a4.z; wv[3] = a4.w;
+    if (g.mode == 1) {   // x' window = the same prices shifted by one: one more scalar (pr[4 L + 4] <= pr[H])
+      wnv[0] = a4.y; wnv[1] = a4.z; wnv[2] = a4.w; wnv[3] = pr[4 * lane + 4];
+    } else {
+      wnv[0] = wnv[1] = wnv[2] = wnv[3] = 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 4 * lane + j;
+      wv[j] = pr[k < H ? k : H - 1];
+      wnv[j] = pr[k < H ? k + 1 : H];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = 4 * lane + j;
-    const float w = pr[k < H ? k : H - 1];
-    const float wn = pr[k < H ? k + 1 : H];
+    const float w = wv[j];
+    const float wn = wnv[j];
     float fb = g.feat_mode ? b * g.inv_b0 : b;
     float fs = g.feat_mode ? (float)s * last * g.inv_b0 : (float)s;
     float fb2 = g.feat_mode ? b2 * g.inv_b0 : b2;
