@@ -170,6 +170,8 @@ class DeepDQN:
         self.act_after_fwd = bool(act_after_fwd)
         if act_gemm not in ("own", "lib"):
             raise ValueError(f"act_gemm must be 'own' or 'lib', not {act_gemm!r}")
+        if act_gemm == "lib" and not hasattr(torch, "_addmm_activation"):   # (a private PyTorch op)
+            act_gemm = "own"
         self.act_gemm = act_gemm
         # early_adam (with overlap_act): Adam waits for the act step's forward only, not its env step
         self.early_adam = bool(early_adam)
