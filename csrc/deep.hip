@@ -590,7 +590,6 @@ struct AdamMulti {
 
 __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
   __shared__ __attribute__((aligned(16))) bf16_t tl[64][72];   // 144-byte rows: 16-byte aligned chunks
-  __shared__ float red[32];
   int b = blockIdx.x, si = 0;
   while (si + 1 < p.nseg && b >= p.seg[si].blocks) b -= p.seg[si++].blocks;
   const AdamSeg& S = p.seg[si];
@@ -617,39 +616,25 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
       if (i < S.I) upd((size_t)i, S.g[i]);
     }
   } else if (S.bias) {
-    // 32 entries: wave w reduces rows 8w..8w+7 of gT (nb bf16 each, 16-byte loads)
-    // (the 8 rows advance together: 8 independent 16-byte loads in flight per lane and step)
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i0 = b * 32;
-    float acc[8];
+    // 4 entries per block, one row of gT per wave (nb bf16, 16-byte loads, up to 8 in flight per lane): the
+    // reduction spreads over ~1,000 short blocks instead of 130 long ones (32 rows each), which left a ~9 us tail
+    // behind the weight tiles (tools/bench_adam_bias.py).  Per row the same summation order as before.
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = b * 4 + wave;
+    float acc = 0.f;
+    if (i < S.I) {
+      const bf16_t* row = S.gT + (size_t)i * S.ldg;
+#pragma unroll 8
+      for (int c = 8 * lane; c < S.nb; c += 512) {
+        const uint4 q = *reinterpret_cast<const uint4*>(row + c);
+        const uint32_t u[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int r = 0; r < 8; ++r) acc[r] = 0.f;
-    for (int c = 8 * lane; c < S.nb; c += 512) {
-      uint4 q[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int i = i0 + 8 * wave + r;
-        q[r] = i < S.I ? *reinterpret_cast<const uint4*>(S.gT + (size_t)i * S.ldg + c) : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t u[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc[r] += bf2f((bf16_t)(u[k] & 0xFFFF)) + bf2f((bf16_t)(u[k] >> 16));
+        for (int k = 0; k < 4; ++k) acc += bf2f((bf16_t)(u[k] & 0xFFFF)) + bf2f((bf16_t)(u[k] >> 16));
       }
     }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float t = wave_sum(acc[r]);
-      if (lane == 0) red[8 * wave + r] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x < 32) {
-      const int i = i0 + threadIdx.x;
-      if (i < S.I) {
-        const float g = red[threadIdx.x];
-        S.g[i] = g;
-        if (!p.grads_only) upd((size_t)i, g);
-      }
+    const float g = wave_sum(acc);
+    if (lane == 0 && i < S.I) {
+      S.g[i] = g;
+      if (!p.grads_only) upd((size_t)i, g);
     }
   } else {
     // 64 x 64 tile: thread t owns columns i0 + 4 (t % 16) .. +3 of rows o0 + t / 16 + 16 r (r < 4) --
@@ -730,7 +715,7 @@ extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
   int total = 0;
   for (int i = 0; i < p->nseg; ++i) {
     const st::AdamSeg& g = p->seg[i];
-    const int want = g.bias ? (g.I + 31) / 32 : ((g.I + 63) / 64) * ((g.O + 63) / 64);
+    const int want = g.bias ? (g.gT ? (g.I + 3) / 4 : (g.I + 31) / 32) : ((g.I + 63) / 64) * ((g.O + 63) / 64);
     if (g.blocks != want || (g.bias && g.gT && (g.nb % 8 || g.ldg % 8))) return hipErrorInvalidValue;
     if (!g.bias && (g.I % 4 || g.O % 8)) return hipErrorInvalidValue;   // vector paths of the weight tiles
     if (p->grads_only && !(g.bias && g.gT)) return hipErrorInvalidValue;

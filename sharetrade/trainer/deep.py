@@ -424,7 +424,7 @@ class DeepDQN:
             w.blocks = ((I + 63) // 64) * ((O + 63) // 64)
             b = self._bias_seg(l, reduce=not self._bias_from_db)
             segs += [w, b]
-        # bias segments first: their blocks (32 rows x batch of gradient sums each) are the longest,
+        # bias segments first: their blocks (4 rows x batch of gradient sums each) are the longest,
         # started first they do not form the tail
         segs = [sg for sg in segs if sg.bias] + [sg for sg in segs if not sg.bias]
         if len(segs) > ADAM_MAX_SEG:
@@ -459,7 +459,7 @@ class DeepDQN:
         b.mask = None if bool(self.bmask[l].bool().all()) else self.bmask[l].data_ptr()
         b.wb, b.wbT, b.gT = self._bscratch(l).data_ptr(), None, self.GT[l].data_ptr() if reduce else None
         b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
-        b.blocks = (O + 31) // 32
+        b.blocks = (O + 3) // 4 if reduce else (O + 31) // 32   # (4 rows of G^T / 32 entries per block)
         return b
 
     def _bscratch(self, l: int) -> torch.Tensor:
