@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--iters-per-graph", type=int, default=4,
                     help="capture k whole iterations into one HIP graph (one launch per k iterations; 4: 0.402-0.405 vs "
                          "0.405-0.409 ms per iteration at 1, profiles/r6_config4_head.md)")
+    ap.add_argument("--no-bias-part", action="store_true",
+                    help="Adam reduces the bias gradients from G^T instead of the backward launches' column partials")
     ap.add_argument("--no-fuse-head", action="store_true",
                     help="TD and the output layer's backward as three launches instead of one")
     ap.add_argument("--no-overlap-act", action="store_true",
@@ -77,7 +79,8 @@ def main():
                 concurrent=not a.serial, fused_adam=not a.unfused_adam, overlap_act=not a.no_overlap_act,
                 batched_fwd=not a.unbatched_fwd, dual_bwd=not a.no_dual_bwd, act_inline=a.act_inline,
                 fuse_act=a.fuse_act, fuse_xt=not a.no_fuse_xt, act_after_fwd=not a.act_before_fwd,
-                early_adam=a.early_adam, act_gemm=a.act_gemm, fuse_head=not a.no_fuse_head)
+                early_adam=a.early_adam, act_gemm=a.act_gemm, fuse_head=not a.no_fuse_head,
+                bias_part=not a.no_bias_part)
     for _ in range(a.warmup):
         d.act_step()
     k = a.iters_per_graph if a.updates == 1 else 1
@@ -123,7 +126,7 @@ def main():
         "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
         "concurrent_update": d.concurrent, "fused_adam": d.fused_adam, "overlap_act": d.overlap_act,
         "batched_fwd": d.batched_fwd, "pingpong_gemm": not a.no_pingpong, "dual_bwd": d.dual_bwd, "act_inline": d.act_inline, "fuse_act": d.fuse_act,
-        "act_gemm": d.act_gemm, "fuse_head": d.fuse_head, "iters_per_graph": k,
+        "act_gemm": d.act_gemm, "fuse_head": d.fuse_head, "bias_part": d._bpart[0] is not None, "iters_per_graph": k,
     }
     print(json.dumps(out))
 

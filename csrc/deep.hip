@@ -355,6 +355,8 @@ struct DeepHead {
   bf16_t* GT;           // [H, B]
   float* dW;            // [ldq, H] fp32, zeroed before the launch
   int H;
+  float* gpart;         // optional: column sums of G over each 64-row block [B / 64][ldgp] (bias partials)
+  int ldgp;
 };
 constexpr int HEAD_MAXA = 4;
 
@@ -363,6 +365,7 @@ __global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
   __shared__ int s_a[64];
   __shared__ __attribute__((aligned(16))) bf16_t sT[256][72];
   __shared__ float red[8][HEAD_MAXA][256];
+  __shared__ float gred[8][256];
   const DeepTD& q = p.td;
   const int tid = threadIdx.x, m0 = blockIdx.y * 64, n0 = blockIdx.x * 256;
   const int nact = q.n_actions;
@@ -454,7 +457,22 @@ __global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
     if (a < nact)
 #pragma unroll
       for (int c = 0; c < 8; ++c) red[rg][a][8 * cc + c] = acc[a][c];
+  if (p.gpart) {   // G's column sums over the thread's 8 rows (the stored bf16 values)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float cs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) cs += bf2f(gcol[c][r]);
+      gred[rg][8 * cc + c] = cs;
+    }
+  }
   __syncthreads();
+  if (p.gpart) {
+    float cs = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) cs += gred[g][tid];
+    p.gpart[(size_t)blockIdx.y * p.ldgp + n0 + tid] = cs;
+  }
 #pragma unroll
   for (int i = tid; i < 256 * 8; i += 256) {
     const int nl = i >> 3, ch = i & 7;
@@ -576,7 +594,10 @@ struct AdamSeg {
   int O, I;              // weights: [O][I]; biases: O = 1, I = n
   int ldg, nb;
   int bias;
-  int blocks;            // tiles (weights) or 32-entry blocks (biases)
+  int blocks;            // tiles (weights), 4-row blocks (biases from gT) or 32-entry blocks (biases from g / gP)
+  const float* gP;       // biases, instead of gT: fp32 partial column sums [np][ldp] (the backward GEMM epilogue's /
+                         // the head kernel's), summed over np here -- 1 / 64 of gT's bytes
+  int np, ldp;
 };
 struct AdamMulti {
   AdamSeg seg[ADAM_MAX_SEG];
@@ -610,7 +631,21 @@ __global__ void __launch_bounds__(256) adam_multi_kernel(AdamMulti p) {
     if (S.wb) S.wb[idx] = f2bf(w);   // biases: optional bf16 copy (the library act-step epilogue's operand)
     return w;
   };
-  if (S.bias && !S.gT) {
+  if (S.bias && S.gP) {
+    // 32 entries per block, 8 threads per entry (a stride-8 share of the np partial rows each), combined by
+    // shuffles in a fixed order
+    const int i = b * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
+    float acc = 0.f;
+    if (i < S.I)
+      for (int r = part; r < S.np; r += 8) acc += S.gP[(size_t)r * S.ldp + i];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (part == 0 && i < S.I) {
+      S.g[i] = acc;
+      if (!p.grads_only) upd((size_t)i, acc);
+    }
+  } else if (S.bias && !S.gT) {
     if (threadIdx.x < 32) {
       const int i = b * 32 + threadIdx.x;
       if (i < S.I) upd((size_t)i, S.g[i]);
@@ -715,10 +750,11 @@ extern "C" hipError_t st_adam_multi(const st::AdamMulti* p, hipStream_t s) {
   int total = 0;
   for (int i = 0; i < p->nseg; ++i) {
     const st::AdamSeg& g = p->seg[i];
-    const int want = g.bias ? (g.gT ? (g.I + 3) / 4 : (g.I + 31) / 32) : ((g.I + 63) / 64) * ((g.O + 63) / 64);
+    const int want = g.bias ? ((g.gT && !g.gP) ? (g.I + 3) / 4 : (g.I + 31) / 32) : ((g.I + 63) / 64) * ((g.O + 63) / 64);
+    if (g.bias && g.gP && (g.np < 1 || g.ldp < g.I)) return hipErrorInvalidValue;
     if (g.blocks != want || (g.bias && g.gT && (g.nb % 8 || g.ldg % 8))) return hipErrorInvalidValue;
     if (!g.bias && (g.I % 4 || g.O % 8)) return hipErrorInvalidValue;   // vector paths of the weight tiles
-    if (p->grads_only && !(g.bias && g.gT)) return hipErrorInvalidValue;
+    if (p->grads_only && !(g.bias && (g.gT || g.gP))) return hipErrorInvalidValue;
     total += g.blocks;
   }
   if (total != p->total) return hipErrorInvalidValue;
@@ -753,7 +789,8 @@ extern "C" hipError_t st_deep_td(const st::DeepTD* p, hipStream_t s) {
 
 extern "C" hipError_t st_deep_head(const st::DeepHead* p, hipStream_t s) {
   const st::DeepTD& q = p->td;
-  if (q.n_actions < 1 || q.n_actions > st::HEAD_MAXA || q.n_actions > q.ldq || q.B % 64 || p->H % 256 || q.B <= 0)
+  if (q.n_actions < 1 || q.n_actions > st::HEAD_MAXA || q.n_actions > q.ldq || q.B % 64 || p->H % 256 || q.B <= 0 ||
+      (p->gpart && p->ldgp < p->H))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(st::deep_head_kernel, dim3(p->H / 256, q.B / 64), dim3(256), 0, s, *p);
   return hipGetLastError();

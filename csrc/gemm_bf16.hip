@@ -45,6 +45,11 @@ struct GemmArgs {
   float alpha;
   int splitk;            // EPI_F32 only: K split over splitk workgroups per tile, atomically
                          // added into out (which then holds the prior value / zeros)
+  // EPI_RELU_GRAD (2-stage gemm_body tiles) only, optional: column sums of the bf16 output over each wave's
+  // rows, colpart[(M / WM) rows][ldcp] fp32 with partial row tm * NWM + wm -- the bias gradient's partials
+  // (plain stores, no atomics; the optimizer sums the M / WM rows)
+  float* colpart;
+  int ldcp;
 };
 
 // a group of up to 4 products with one epilogue / tile in one launch (e.g. the online and target
@@ -239,6 +244,9 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
     constexpr int SC = BN + 8, SCT = BM + 8;
     bf16_t* sC = buf;
     bf16_t* sCT = buf + BM * SC;   // (only with G::HAS_T)
+    float csum[G::TN];   // EPI_RELU_GRAD: this lane's column sums over its TM x 4 rows
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) csum[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < G::TM; ++i)
 #pragma unroll
@@ -257,11 +265,25 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
           const s4v h = *reinterpret_cast<const s4v*>(p.auxT + (size_t)(n0 + nl) * p.ldaux + m0 + ml);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (bf2f((bf16_t)h[r]) > 0.f) ? acc[i][j][r] : 0.f;
+          if constexpr (EPI == EPI_RELU_GRAD) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) csum[j] += bf2f(f2bf(v[r]));   // the stored (bf16) values
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) sC[(ml + r) * SC + nl] = f2bf(v[r]);
         if constexpr (G::HAS_T) lds_st4(sCT + nl * SCT + ml, v[0], v[1], v[2], v[3]);
       }
+    if (EPI == EPI_RELU_GRAD && p.colpart) {
+      // the 4 lane groups (rows 4 g4 ..) of each column, then one store per column of the wave's WM rows
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) {
+        float x = csum[j];
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 32);
+        if (g4 == 0) p.colpart[(size_t)(tm * G::NWM + wm) * p.ldcp + n0 + wn * G::WN + 16 * j + l16] = x;
+      }
+    }
     __syncthreads();
     bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
     constexpr int CPR = BN / 8;   // 16-byte chunks per C row
@@ -780,6 +802,7 @@ static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool ha
   if (p->outT && (p->ldoT % 8 || epi == st::EPI_F32)) return false;
   if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return false;
   if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return false;
+  if (p->colpart && (epi != st::EPI_RELU_GRAD || p->ldcp < p->N)) return false;
   return true;
 }
 
@@ -824,6 +847,7 @@ extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::G
 }
 
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
+  if (p->colpart && tile >= 7) return hipErrorInvalidValue;   // column partials: 2-stage gemm_body tiles only
   if (tile == 9) {   // 256x256, 4 waves of 128x128 (bf16 / fp32 epilogues, no C^T, no split-K)
     if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
     if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)

@@ -23,7 +23,7 @@ class GemmArgs(C.Structure):
         ("A", C.c_void_p), ("B", C.c_void_p), ("out", C.c_void_p), ("outT", C.c_void_p), ("bias", C.c_void_p),
         ("auxT", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
         ("ldo", C.c_int), ("ldoT", C.c_int), ("ldaux", C.c_int), ("relu", C.c_int), ("accumulate", C.c_int),
-        ("alpha", C.c_float), ("splitk", C.c_int),
+        ("alpha", C.c_float), ("splitk", C.c_int), ("colpart", C.c_void_p), ("ldcp", C.c_int),
     ]
 
 
@@ -51,7 +51,10 @@ def pick_tile(M: int, N: int) -> tuple:
 
 def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, outT: Optional[torch.Tensor] = None,
               bias: Optional[torch.Tensor] = None, auxT: Optional[torch.Tensor] = None, relu: bool = False,
-              accumulate: bool = False, alpha: float = 1.0, splitk: int = 1) -> GemmArgs:
+              accumulate: bool = False, alpha: float = 1.0, splitk: int = 1,
+              colpart: Optional[torch.Tensor] = None) -> GemmArgs:
+    """``colpart`` (EPI_RELU_GRAD, 128-row 2-stage tiles): fp32 [M / 64, >= N] -- column sums of the bf16 output
+    over each 64-row wave block (the bias gradient's partials)."""
     M, K = A.shape
     N, K2 = B.shape
     if K != K2:
@@ -88,6 +91,10 @@ def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, out
         if (K // 64) % splitk:
             raise ValueError(f"split-K {splitk} does not divide the {K // 64} K-tiles")
     g.splitk = int(splitk)
+    if colpart is not None:
+        if epi != EPI_RELU_GRAD or colpart.dtype != torch.float32 or colpart.stride(1) != 1 or colpart.shape[1] < N:
+            raise ValueError("colpart: EPI_RELU_GRAD, fp32 [M / 64, >= N] row-major")
+        g.colpart, g.ldcp = colpart.data_ptr(), colpart.stride(0)
     return g
 
 

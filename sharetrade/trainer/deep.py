@@ -69,7 +69,7 @@ class _TD(C.Structure):
 
 class _Head(C.Structure):
     _fields_ = [("td", _TD), ("A", C.c_void_p), ("W", C.c_void_p), ("G", C.c_void_p), ("GT", C.c_void_p),
-                ("dW", C.c_void_p), ("H", C.c_int)]
+                ("dW", C.c_void_p), ("H", C.c_int), ("gpart", C.c_void_p), ("ldgp", C.c_int)]
 
 
 class _Adam(C.Structure):
@@ -84,7 +84,8 @@ ADAM_MAX_SEG = 16
 class _AdamSeg(C.Structure):
     _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("mask", C.c_void_p),
                 ("wb", C.c_void_p), ("wbT", C.c_void_p), ("gT", C.c_void_p), ("O", C.c_int), ("I", C.c_int),
-                ("ldg", C.c_int), ("nb", C.c_int), ("bias", C.c_int), ("blocks", C.c_int)]
+                ("ldg", C.c_int), ("nb", C.c_int), ("bias", C.c_int), ("blocks", C.c_int), ("gP", C.c_void_p),
+                ("np", C.c_int), ("ldp", C.c_int)]
 
 
 class _AdamMulti(C.Structure):
@@ -126,7 +127,7 @@ class DeepDQN:
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
                  fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False,
-                 act_gemm: str = "lib", fuse_head: bool = True):
+                 act_gemm: str = "lib", fuse_head: bool = True, bias_part: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -275,6 +276,14 @@ class DeepDQN:
                 if o % 128 == 0 and i % 128 == 0 and self.B % 128 == 0:
                     self._dw_plan[l] = ("hip", ((128, 128), gm.pick_splitk(o, i, self.B, (128, 128))))
                     self._dual[l] = True
+        # bias_part: the hidden layers' bias gradients as fp32 column partials of G over 64-row blocks, written by
+        # the backward launches themselves (the dual GEMMs' EPI_RELU_GRAD epilogue, deep_head_kernel) and summed by
+        # the fused Adam -- instead of Adam re-reading every G^T (8 MB per 1024-wide layer at batch 4096)
+        self._bpart = [None] * self.L
+        if (bias_part and self.fused_adam and self.fuse_head and self.B % 128 == 0 and
+                all(self._dual[l] for l in range(1, self.L - 1))):
+            for l in range(self.L - 1):
+                self._bpart[l] = torch.zeros(self.B // 64, self.pdims[l + 1], device=dev)
         sk_layers = [l for l, (k, a) in enumerate(self._dw_plan) if k == "hip" and (a[1] > 1 or
                                                                                     (self.fuse_head and l == self.L - 1))]
         self._zero_span = (0, 0)
@@ -394,6 +403,8 @@ class DeepDQN:
         hd.A, hd.W = self.Act[self.L - 1].data_ptr(), self.Wb[self.L - 1].data_ptr()
         hd.G, hd.GT = self.G[self.L - 2].data_ptr(), self.GT[self.L - 2].data_ptr()
         hd.dW, hd.H = self.dW[self.L - 1].data_ptr(), self.pdims[self.L - 1]
+        if self._bpart[self.L - 2] is not None:
+            hd.gpart, hd.ldgp = self._bpart[self.L - 2].data_ptr(), self.pdims[self.L - 1]
         self._head = hd
         a = cfg.agent
         self._adam = []
@@ -460,6 +471,9 @@ class DeepDQN:
         b.wb, b.wbT, b.gT = self._bscratch(l).data_ptr(), None, self.GT[l].data_ptr() if reduce else None
         b.O, b.I, b.ldg, b.nb, b.bias = 1, O, self.B, self.B, 1
         b.blocks = (O + 3) // 4 if reduce else (O + 31) // 32   # (4 rows of G^T / 32 entries per block)
+        if reduce and self._bpart[l] is not None:   # the backward launch's column partials instead of G^T
+            b.gT, b.gP, b.np, b.ldp = None, self._bpart[l].data_ptr(), self._bpart[l].shape[0], O
+            b.blocks = (O + 31) // 32
         return b
 
     def _bscratch(self, l: int) -> torch.Tensor:
@@ -591,7 +605,10 @@ class DeepDQN:
             if not head and self._dual[l]:
                 # one launch: G_{l-1} = (G_l . W_l) * (A_l > 0)  and  dW_l = G_l^T . A_l (split-K)
                 _, (_, sk) = self._dw_plan[l]
-                gm.gemm_dual((self.G[l], self.WbT[l], self.G[l - 1], dict(outT=self.GT[l - 1], auxT=actsT[l])),
+                kw0 = dict(outT=self.GT[l - 1], auxT=actsT[l])
+                if self._bpart[l - 1] is not None:
+                    kw0["colpart"] = self._bpart[l - 1]
+                gm.gemm_dual((self.G[l], self.WbT[l], self.G[l - 1], kw0),
                              gm.EPI_RELU_GRAD,
                              (self.GT[l], actsT[l], self.dW[l], dict(splitk=sk, prezeroed=sk > 1)), gm.EPI_F32)
             elif not head:

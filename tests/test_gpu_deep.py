@@ -272,3 +272,27 @@ def test_k_iteration_graph_matches_single_iterations(native_built):
         assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
     for wa, wb in zip(a.Wt, b.Wt):
         assert float((wa.float() - wb.float()).norm() / (wb.float().norm() + 1e-20)) < 1e-4
+
+
+def test_bias_partials_match_gt_reduction(native_built):
+    """bias_part: the hidden layers' bias gradients summed by the fused Adam from the fp32 column partials the
+    backward launches write (dual GEMM epilogue, deep_head_kernel) equal the row sums of G^T it used to read, up
+    to fp32 summation order; the parameters after several updates agree to 1e-5."""
+    res = []
+    for part in (True, False):
+        d = _dqn(bias_part=part)
+        for _ in range(8):
+            d.act_step()
+        for _ in range(3):
+            d.update_step()
+        torch.cuda.synchronize()
+        res.append(d)
+    a, b = res
+    assert all(p is not None for p in a._bpart[: a.L - 1]) and all(p is None for p in b._bpart)
+    for l in range(a.L - 1):
+        ref = b.GT[l].float().sum(dim=1)
+        got = a._bpart[l].sum(dim=0)
+        assert float((got - ref).norm() / (ref.norm() + 1e-20)) < 1e-5, l
+        assert float((a.db[l] - b.db[l]).norm() / (b.db[l].norm() + 1e-20)) < 1e-5, l
+    for pa, pb in zip(a.W + a.b, b.W + b.b):
+        assert float((pa - pb).norm() / (pb.norm() + 1e-20)) < 1e-5
