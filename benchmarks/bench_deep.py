@@ -46,10 +46,10 @@ def main():
                     help="weight gradients on a second stream beside each data-gradient GEMM (fork / join per layer)")
     ap.add_argument("--unbatched-fwd", action="store_true",
                     help="online / target forward as two GEMM chains (two streams) instead of one batched launch per layer")
-    ap.add_argument("--act-gemm", default="lib", choices=("own", "lib"),
+    ap.add_argument("--act-gemm", default="lib", choices=("own", "lib", "lib0"),
                     help="the act step's hidden 1024 -> 1024 layers through hipBLASLt's fused bias + ReLU epilogue "
-                         "(default: 0.408 vs 0.417 ms per iteration, profiles/r6_config4_act_lib.md) or on our "
-                         "ping-pong kernel")
+                         "(lib, default: 0.408 vs 0.417 ms per iteration), also its first layer (lib0: +0.5 %%), or "
+                         "every layer on our GEMMs (own); profiles/r6_config4_act_lib.md")
     ap.add_argument("--iters-per-graph", type=int, default=4,
                     help="capture k whole iterations into one HIP graph (one launch per k iterations; 4: 0.402-0.405 vs "
                          "0.405-0.409 ms per iteration at 1, profiles/r6_config4_head.md)")

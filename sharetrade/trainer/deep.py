@@ -169,9 +169,9 @@ class DeepDQN:
         # act_after_fwd (with overlap_act): fork the act step after the update's forward instead of
         # right after the replay sample
         self.act_after_fwd = bool(act_after_fwd)
-        if act_gemm not in ("own", "lib"):
-            raise ValueError(f"act_gemm must be 'own' or 'lib', not {act_gemm!r}")
-        if act_gemm == "lib" and not hasattr(torch, "_addmm_activation"):   # (a private PyTorch op)
+        if act_gemm not in ("own", "lib", "lib0"):
+            raise ValueError(f"act_gemm must be 'own', 'lib' or 'lib0', not {act_gemm!r}")
+        if act_gemm != "own" and not hasattr(torch, "_addmm_activation"):   # (a private PyTorch op)
             act_gemm = "own"
         self.act_gemm = act_gemm
         # early_adam (with overlap_act): Adam waits for the act step's forward only, not its env step
@@ -488,15 +488,17 @@ class DeepDQN:
             self._bscratch(l).copy_(self.b[l].view(1, -1).to(torch.bfloat16))
 
     # ---------------------------------------------------------------- forward
-    def _forward(self, X, acts, actsT, Wb, bias, Q, lib: bool = False) -> None:
-        """acts[l+1] = relu(acts[l] . W_l^T + b_l); Q = acts[L-1] . W_{L-1}^T + b_{L-1} (fp32).  ``lib``: the
-        hidden layers after the first through hipBLASLt's fused bias + ReLU epilogue (bf16 bias copies; the
-        act step's 16,384 x 1024 -> 1024 layers, where the library's K loop is faster than our ping-pong
-        kernel's: profiles/r6_gemm_ablation.md)."""
+    def _forward(self, X, acts, actsT, Wb, bias, Q, lib: int = -1) -> None:
+        """acts[l+1] = relu(acts[l] . W_l^T + b_l); Q = acts[L-1] . W_{L-1}^T + b_{L-1} (fp32).  ``lib`` >= 0:
+        the hidden layers from that one on through hipBLASLt's fused bias + ReLU epilogue (bf16 bias copies;
+        the act step's 16,384 x 1024 -> 1024 layers, where the library's K loop is faster than our ping-pong
+        kernel's, profiles/r6_gemm_ablation.md).  The act step passes 1 (``act_gemm="lib"``); 0 (``"lib0"``) also
+        takes its 16,384 x 256 -> 1024 first layer, alone 18.7 vs 22.0 us but +0.5 % per iteration beside the
+        update chain (profiles/r6_config4_act_lib.md)."""
         a = X
         for l in range(self.L):
             if l < self.L - 1:
-                if lib and l > 0:
+                if 0 <= lib <= l:
                     torch._addmm_activation(self._bscratch(l)[0], a, Wb[l].t(), out=acts[l + 1])
                 else:
                     gm.gemm_nt(a, Wb[l], acts[l + 1], gm.EPI_BF16, outT=actsT[l + 1] if actsT else None,
@@ -529,7 +531,8 @@ class DeepDQN:
         ``after_forward()`` runs between the forward (the last reader of the weights) and the env step."""
         sh = native.stream_handle()
         native.check(self.k.st_deep_gather(self._gather_env, sh), "deep_gather(env)")
-        self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe, lib=self.act_gemm == "lib")
+        self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe,
+                      lib={"own": -1, "lib": 1, "lib0": 0}[self.act_gemm])
         if after_forward is not None:
             after_forward()
         native.check(self.k.st_deep_env_step(self._env, sh), "deep_env_step")

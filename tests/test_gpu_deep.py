@@ -192,8 +192,8 @@ def test_replay_gather_writes_x_transposed(native_built, fuse_xt):
 
 
 def test_act_gemm_lib_matches_own_and_captures(native_built):
-    """act_gemm="lib": the act step's hidden layers after the first through hipBLASLt's fused bias + ReLU
-    epilogue.  The bf16 bias copies the Adam kernel rewrites equal the rounded fp32 biases after updates; the
+    """act_gemm="lib": the act step's hidden layers through hipBLASLt's fused bias + ReLU epilogue after
+    the first ("lib0": the first too).  The bf16 bias copies the Adam kernel rewrites equal the rounded fp32 biases after updates; the
     library forward's Q matches our kernel's to bf16 accuracy (bias rounded to bf16, other summation order);
     the path captures into the iteration graph."""
     d = _dqn(act_gemm="lib")
@@ -206,14 +206,15 @@ def test_act_gemm_lib_matches_own_and_captures(native_built):
         assert torch.equal(d._bscratch(l), d.b[l].view(1, -1).to(torch.bfloat16)), l
         assert float(d.b[l].abs().sum()) > 0, l   # the biases moved, so the copies were rewritten
     qs = []
-    for lib in (False, True):
+    for lib in (-1, 0, 1):
         acts = [d.Xe] + [t.clone() for t in d.Acte[1:]]
         q = d.Qe.clone()
         d._forward(d.Xe, acts, None, d.Wb, d.b, q, lib=lib)
         qs.append(q[:, : d.n_act].float())
     torch.cuda.synchronize()
-    own, lib = qs
-    assert float((lib - own).norm() / own.norm()) < 2e-2
+    own = qs[0]
+    for lib in qs[1:]:
+        assert float((lib - own).norm() / own.norm()) < 2e-2
     d.capture()
     for _ in range(3):
         d.iteration()
