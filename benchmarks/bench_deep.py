@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--hidden", default="1024,1024,1024,1024")
     ap.add_argument("--replay", type=int, default=1 << 20)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=64, help="timed iterations (a multiple of --iters-per-graph)")
     ap.add_argument("--warmup", type=int, default=64, help="acting steps to pre-fill the replay ring")
     ap.add_argument("--updates", type=int, default=1)
     ap.add_argument("--dw-gemm", default="auto", help="weight-gradient GEMMs: auto | hip (own split-K kernels)")
@@ -50,9 +50,10 @@ def main():
                     help="the act step's hidden 1024 -> 1024 layers through hipBLASLt's fused bias + ReLU epilogue "
                          "(lib, default: 0.408 vs 0.417 ms per iteration), also its first layer (lib0: +0.5 %%), or "
                          "every layer on our GEMMs (own); profiles/r6_config4_act_lib.md")
-    ap.add_argument("--iters-per-graph", type=int, default=4,
+    ap.add_argument("--iters-per-graph", type=int, default=16,
                     help="capture k whole iterations into one HIP graph (one launch per k iterations; 4: 0.402-0.405 vs "
-                         "0.405-0.409 ms per iteration at 1, profiles/r6_config4_head.md)")
+                         "0.405-0.409 ms per iteration at 1, profiles/r6_config4_head.md; 16: 0.381-0.383 vs 0.382-0.385 "
+                         "at 4, profiles/r6_config5_kgraph.md)")
     ap.add_argument("--no-bias-part", action="store_true",
                     help="Adam reduces the bias gradients from G^T instead of the backward launches' column partials")
     ap.add_argument("--no-fuse-head", action="store_true",

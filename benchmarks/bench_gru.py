@@ -25,16 +25,17 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--bars", type=int, default=4096)
     ap.add_argument("--replay", type=int, default=1 << 17)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=128, help="timed iterations (a multiple of --iters-per-graph)")
     ap.add_argument("--warmup", type=int, default=4, help="actor launches to pre-fill the replay")
     ap.add_argument("--updates", type=int, default=1)
     ap.add_argument("--grid", type=int, default=0,
                     help="actor workgroups (one per CU): 0 = auto (RecurrentDQN._auto_grid)")
     ap.add_argument("--actor-kernel", default="auto", choices=["auto", "single", "pair"],
                     help="single- or two-chunk actor kernel (auto: two-chunk when seq <= 32)")
-    ap.add_argument("--iters-per-graph", type=int, default=4,
+    ap.add_argument("--iters-per-graph", type=int, default=16,
                     help="capture k (even) whole iterations into one HIP graph (one launch per k iterations; 4: "
-                         "0.583-0.584 vs 0.589-0.591 ms per iteration at 1 over 200 steps, profiles/r6_config5_kgraph.md)")
+                         "0.583-0.584 vs 0.589-0.591 ms per iteration at 1 over 200 steps; 16: 0.578 vs 0.583-0.584 at "
+                         "4; profiles/r6_config5_kgraph.md)")
     ap.add_argument("--no-overlap-act", action="store_true",
                     help="serial actor launch then update (default: the actor runs beside the update after its "
                          "segments are sampled; profiles/r2_config5_overlap.md)")
