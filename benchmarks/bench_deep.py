@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--hidden", default="1024,1024,1024,1024")
     ap.add_argument("--replay", type=int, default=1 << 20)
-    ap.add_argument("--steps", type=int, default=64, help="timed iterations (a multiple of --iters-per-graph)")
+    ap.add_argument("--steps", type=int, default=128, help="timed iterations (a multiple of --iters-per-graph)")
     ap.add_argument("--warmup", type=int, default=64, help="acting steps to pre-fill the replay ring")
     ap.add_argument("--updates", type=int, default=1)
     ap.add_argument("--dw-gemm", default="auto", help="weight-gradient GEMMs: auto | hip (own split-K kernels)")
