@@ -493,8 +493,8 @@ class DeepDQN:
         the hidden layers from that one on through hipBLASLt's fused bias + ReLU epilogue (bf16 bias copies;
         the act step's 16,384 x 1024 -> 1024 layers, where the library's K loop is faster than our ping-pong
         kernel's, profiles/r6_gemm_ablation.md).  The act step passes 1 (``act_gemm="lib"``); 0 (``"lib0"``) also
-        takes its 16,384 x 256 -> 1024 first layer, alone 18.7 vs 22.0 us but +0.5 % per iteration beside the
-        update chain (profiles/r6_config4_act_lib.md)."""
+        takes its 16,384 x 256 -> 1024 first layer, alone a tie with our ping-pong kernel (18.2-18.7 vs 18.6 us) and
+        +0.5 % per iteration beside the update chain (profiles/r6_config4_act_lib.md)."""
         a = X
         for l in range(self.L):
             if l < self.L - 1:

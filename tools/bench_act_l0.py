@@ -39,6 +39,9 @@ def main():
         o2 = torch.empty_like(o1)
         t = gm.pick_tile(E, N)
         ours = timeit(lambda: gm.gemm_nt(X, W, o1, gm.EPI_BF16, tile=t, bias=b, relu=True))
+        for tt in ((256, 256, "pp"), (256, 128), (128, 128, 3)):
+            us = timeit(lambda: gm.gemm_nt(X, W, o1, gm.EPI_BF16, tile=tt, bias=b, relu=True))
+            print(f"| {E}x{K}->{N} | ours (tile {tt}) {us:.1f} us |", flush=True)
         lib = timeit(lambda: torch._addmm_activation(bb, X, W.t(), out=o2))
         ref = torch.relu(X.float() @ W.float().t() + b)
         e1 = float((o1.float() - ref).abs().max() / ref.abs().max())
