@@ -69,7 +69,8 @@ class _TD(C.Structure):
 
 class _Head(C.Structure):
     _fields_ = [("td", _TD), ("A", C.c_void_p), ("W", C.c_void_p), ("G", C.c_void_p), ("GT", C.c_void_p),
-                ("dW", C.c_void_p), ("H", C.c_int), ("gpart", C.c_void_p), ("ldgp", C.c_int)]
+                ("dW", C.c_void_p), ("H", C.c_int), ("gpart", C.c_void_p), ("ldgp", C.c_int), ("At", C.c_void_p),
+                ("Wt", C.c_void_p), ("bq", C.c_void_p), ("bqt", C.c_void_p)]
 
 
 class _Adam(C.Structure):
@@ -127,7 +128,7 @@ class DeepDQN:
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
                  fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False,
-                 act_gemm: str = "lib", fuse_head: bool = True, bias_part: bool = True):
+                 act_gemm: str = "lib", fuse_head: bool = True, bias_part: bool = True, head_qfwd: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -269,6 +270,9 @@ class DeepDQN:
         # deep_head_kernel); dW_{L-1} is then accumulated atomically into the zeroed span
         self.fuse_head = bool(fuse_head) and self.L >= 2 and self.pdims[-2] % 256 == 0 and self.B % 64 == 0 \
             and 1 <= self.n_act <= 4
+        # head_qfwd: the output layer's forward (online on x, target on x') inside deep_head_kernel too, instead of
+        # the batched forward's split-K output GEMM launch
+        self.head_qfwd = bool(head_qfwd) and self.fuse_head and self.batched_fwd and self.pdims[-2] <= 1024
         self._dual = [False] * self.L   # layer l's weight gradient in a dual launch with G_{l-1}
         if self.dual_bwd:
             for l in range(1, self.L - 1):
@@ -405,6 +409,9 @@ class DeepDQN:
         hd.dW, hd.H = self.dW[self.L - 1].data_ptr(), self.pdims[self.L - 1]
         if self._bpart[self.L - 2] is not None:
             hd.gpart, hd.ldgp = self._bpart[self.L - 2].data_ptr(), self.pdims[self.L - 1]
+        if self.head_qfwd:
+            hd.At, hd.Wt = self.ActN[self.L - 1].data_ptr(), self.Wt[self.L - 1].data_ptr()
+            hd.bq, hd.bqt = self.b[self.L - 1].data_ptr(), self.bt[self.L - 1].data_ptr()
         self._head = hd
         a = cfg.agent
         self._adam = []
@@ -520,11 +527,13 @@ class DeepDQN:
                 gm.gemm_nt_batched(probs, gm.EPI_BF16, tile=gm.pick_tile(self.B, self.pdims[l + 1]))
             else:
                 sk = self._q_splitk   # few output tiles, long K: split (outputs zeroed by the replay gather)
-                probs = [(acts[l], self.Wb[l], self.Q, dict(bias=self.b[l], splitk=sk, prezeroed=True)),
-                         (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l], splitk=sk, prezeroed=True))]
+                probs = [] if self.head_qfwd else [   # (head_qfwd: Q, Qt come from deep_head_kernel)
+                    (acts[l], self.Wb[l], self.Q, dict(bias=self.b[l], splitk=sk, prezeroed=True)),
+                    (actsN[l], self.Wt[l], self.Qt, dict(bias=self.bt[l], splitk=sk, prezeroed=True))]
                 if actsE is not None:
                     probs.append((actsE[l], self.Wb[l], self.Qe, dict(bias=self.b[l])))
-                gm.gemm_nt_batched(probs, gm.EPI_F32, tile=gm.pick_tile(self.B, ACT_PAD))
+                if probs:
+                    gm.gemm_nt_batched(probs, gm.EPI_F32, tile=gm.pick_tile(self.B, ACT_PAD))
 
     def act_step(self, after_forward=None) -> None:
         """One env step of all E envs: gather -> Q forward -> select/transition/replay insert.

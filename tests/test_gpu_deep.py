@@ -230,7 +230,7 @@ def test_fused_head_matches_td_and_gemms(native_built):
     EPI_RELU_GRAD GEMM computes it) and dW_{L-1} equal up to fp32 summation order."""
     res = []
     for fuse in (True, False):
-        d = _dqn(fuse_head=fuse)
+        d = _dqn(fuse_head=fuse, head_qfwd=False)   # (Q, Qt from the same output GEMM in both)
         for _ in range(8):
             d.act_step()
         d.update_step()
@@ -247,6 +247,40 @@ def test_fused_head_matches_td_and_gemms(native_built):
     assert abs(float(a.loss) - float(b.loss)) <= 1e-5 * abs(float(b.loss))
     for wa, wb in zip(a.W, b.W):
         assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-5
+
+
+def test_head_output_forward_matches_output_gemm(native_built):
+    """head_qfwd: deep_head_kernel also computes the output layer's forward (Q on x, Q_target on x') of its rows
+    instead of reading the batched forward's split-K output GEMM.  Q and Qt match the GEMM's and the fp32
+    reference to fp32 summation order; dq / G_{L-2} agree except where a 1-ulp change of the fp32 TD error
+    crosses a bf16 rounding boundary; the trajectory stays within bf16 accuracy over captured iterations."""
+    res = []
+    for qf in (True, False):
+        d = _dqn(head_qfwd=qf, overlap_act=True)
+        assert d.head_qfwd == qf
+        for _ in range(8):
+            d.act_step()
+        w0, b0 = d.Wb[d.L - 1].clone(), d.b[d.L - 1].clone()   # (the update's Adam moves them)
+        d.update_step()
+        torch.cuda.synchronize()
+        q1 = (d.Q[:, : d.n_act].clone(), d.Qt[:, : d.n_act].clone(), d.G[d.L - 2].clone(), d.dW[d.L - 1].clone())
+        # fp32 reference of the output layer on this update's activations
+        ref = (d.Act[d.L - 1].float() @ w0.float().t() + b0.view(1, -1))[:, : d.n_act]
+        reft = (d.ActN[d.L - 1].float() @ d.Wt[d.L - 1].float().t() + d.bt[d.L - 1].view(1, -1))[:, : d.n_act]
+        torch.cuda.synchronize()
+        assert torch.allclose(q1[0], ref, rtol=1e-4, atol=1e-4) and torch.allclose(q1[1], reft, rtol=1e-4, atol=1e-4)
+        d.capture(iters_per_graph=2)
+        d.iterations(6)
+        torch.cuda.synchronize()
+        res.append((d, q1))
+    (a, qa), (b, qb) = res
+    assert torch.allclose(qa[0], qb[0], rtol=1e-5, atol=1e-5) and torch.allclose(qa[1], qb[1], rtol=1e-5, atol=1e-5)
+    neq = (qa[2] != qb[2]).float().mean().item()
+    assert neq < 0.02, neq
+    assert float((qa[2].float() - qb[2].float()).norm() / qb[2].float().norm()) < 1e-2
+    assert float((qa[3] - qb[3]).norm() / qb[3].norm()) < 1e-2
+    for wa, wb in zip(a.W, b.W):
+        assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-3
 
 
 def test_k_iteration_graph_matches_single_iterations(native_built):
