@@ -347,10 +347,9 @@ __global__ void __launch_bounds__(256) deep_td_kernel(DeepTD p) {
 //   thread (rg = t / 32, cc = t % 32): rows m0 + 8 rg .. +7, columns n0 + 8 cc .. +7 -- 16-byte loads of A
 //   and stores of G, G^T through an LDS transpose (8 rows of a column = one 16-byte LDS store), dW partials
 //   reduced over the 8 row groups in LDS, then one fp32 atomic per (action, column) per block (dW prezeroed).
-// With ``At`` set the block also computes the output layer's forward of its 64 rows, Q(x) = A . W^T + b and
-// Q_target(x') = At . Wt^T + bt (the n_actions real columns; fp32 sums of bf16 products in a fixed order, the
-// same in every column block of the row block), instead of reading Q / Qt from the batched forward's split-K
-// output GEMM: that launch leaves the update chain.  Column block 0 writes the rows to q / qt.
+// With ``qp`` set the output layer's forward comes from the batched forward's last hidden-layer launch: its
+// epilogue leaves fp32 partial head sums per row and 64-column group (GemmArgs::qpart), summed here in a fixed
+// order + bias -- Q(x) and Q_target(x') without an output-layer launch.  Column block 0 writes them to q / qt.
 struct DeepHead {
   DeepTD td;
   const bf16_t* A;      // [B, H] last hidden activation (row-major)
@@ -361,14 +360,13 @@ struct DeepHead {
   int H;
   float* gpart;         // optional: column sums of G over each 64-row block [B / 64][ldgp] (bias partials)
   int ldgp;
-  const bf16_t* At;     // optional [B, H]: the target net's last hidden activation on x' -> Q, Qt computed here
-  const bf16_t* Wt;     // [ldq, H] target output weights, bf16
+  const float* qp;      // optional: Q(x) partials [nqp][B][4] from the last hidden layer's GEMM epilogue (qpart)
+  const float* qpt;     // the same for Q_target(x')
+  int nqp;
   const float* bq;      // [>= n_actions] online output bias
   const float* bqt;     // [>= n_actions] target output bias
 };
 constexpr int HEAD_MAXA = 4;
-constexpr int HEAD_QMAXH = 1024;
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));   // the in-kernel output forward stages both nets' output rows in LDS
 
 __global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
   __shared__ float s_g[64];
@@ -376,11 +374,10 @@ __global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
   __shared__ __attribute__((aligned(16))) bf16_t sT[256][72];
   __shared__ float red[8][HEAD_MAXA][256];
   __shared__ float gred[8][256];
-  __shared__ uint4 sWq[2][HEAD_MAXA][HEAD_QMAXH / 8];
   __shared__ float s_q[2][64][HEAD_MAXA];
   const DeepTD& q = p.td;
   // 1-D grid, XCD-aware: workgroup L runs on XCD L % 8, and the nx column blocks of a row block share an XCD
-  // (its L2 holds the row block's A / At rows once for all of them); plain row-major order when ny % 8 != 0
+  // (its L2 holds the row block's A rows once for all of them); plain row-major order when ny % 8 != 0
   const int nx = p.H / 256, ny = p.td.B / 64, L = blockIdx.x;
   int bx, by;
   if (ny % 8 == 0) {
@@ -393,66 +390,24 @@ __global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
   }
   const int tid = threadIdx.x, m0 = by * 64, n0 = bx * 256;
   const int nact = q.n_actions;
-  if (p.At) {
-    // output rows of both nets -> LDS (16-byte units; rows a >= n_actions zero)
-    const int hc = p.H / 8;
-    for (int i = tid; i < 2 * HEAD_MAXA * hc; i += 256) {
-      const int net = i / (HEAD_MAXA * hc), a = (i / hc) % HEAD_MAXA, c = i % hc;
-      sWq[net][a][c] = a < nact ? *reinterpret_cast<const uint4*>((net ? p.Wt : p.W) + (size_t)a * p.H + 8 * c)
-                                : make_uint4(0u, 0u, 0u, 0u);
+  if (p.qp) {
+    // Q(x), Q_target(x') of the block's rows from the last hidden layer's epilogue partials (fixed order)
+    const int rl = tid >> 2, a = tid & 3;
+    float v0 = 0.f, v1 = 0.f;
+#pragma unroll 16
+    for (int part = 0; part < p.nqp; ++part) {
+      v0 += p.qp[((size_t)part * q.B + m0 + rl) * 4 + a];
+      v1 += p.qpt[((size_t)part * q.B + m0 + rl) * 4 + a];
     }
-    __syncthreads();
-    // 4 lanes per row (16 rows per wave), lane q4 takes the 16-byte units q4, q4 + 4, ...
-    const int rl = 16 * (tid >> 6) + ((tid & 63) >> 2), q4 = tid & 3;
-    float sq[2][HEAD_MAXA];
-#pragma unroll
-    for (int net = 0; net < 2; ++net) {
-#pragma unroll
-      for (int a = 0; a < HEAD_MAXA; ++a) sq[net][a] = 0.f;
-      const bf16_t* Ar = (net ? p.At : p.A) + (size_t)(m0 + rl) * p.H;
-      // every load of the row share issued before the first use (latency-bound otherwise: one HBM round trip
-      // per few units), 32 units per batch (the whole share at H = 1024)
-      for (int c0 = 0; c0 < hc; c0 += 128) {
-        uint4 xs[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          const int c = c0 + q4 + 4 * i;
-          xs[i] = c < hc ? *reinterpret_cast<const uint4*>(Ar + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          const int c = c0 + q4 + 4 * i;
-          if (c >= hc) break;
-          const uint32_t u[4] = {xs[i].x, xs[i].y, xs[i].z, xs[i].w};
-#pragma unroll
-          for (int a = 0; a < HEAD_MAXA; ++a) {
-            if (a >= nact) break;
-            const uint4 w4 = sWq[net][a][c];
-            const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
-            // packed bf16 pairs straight into v_dot2c_f32_bf16 (no unpacking: one wave per SIMD here, so the
-            // VALU issue count is the time)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              sq[net][a] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, u[k]),
-                                                           __builtin_bit_cast(bf16x2_t, w[k]), sq[net][a], false);
-          }
-        }
-      }
+    if (a < nact) {
+      s_q[0][rl][a] = v0 + p.bq[a];
+      s_q[1][rl][a] = v1 + p.bqt[a];
     }
-#pragma unroll
-    for (int net = 0; net < 2; ++net)
-#pragma unroll
-      for (int a = 0; a < HEAD_MAXA; ++a) {
-        float v = sq[net][a];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        if (q4 == 0 && a < nact) s_q[net][rl][a] = v + (net ? p.bqt[a] : p.bq[a]);
-      }
     __syncthreads();
   }
   if (tid < 64) {
     const int b = m0 + tid;
-    const bool qf = p.At != nullptr;
+    const bool qf = p.qp != nullptr;
     const float* qt = q.qt + (size_t)b * q.ldq;
     float mx = qf ? s_q[1][tid][0] : qt[0];
     for (int a = 1; a < nact; ++a) mx = fmaxf(mx, qf ? s_q[1][tid][a] : qt[a]);
@@ -879,7 +834,7 @@ extern "C" hipError_t st_deep_head(const st::DeepHead* p, hipStream_t s) {
   if (q.n_actions < 1 || q.n_actions > st::HEAD_MAXA || q.n_actions > q.ldq || q.B % 64 || p->H % 256 || q.B <= 0 ||
       (p->gpart && p->ldgp < p->H))
     return hipErrorInvalidValue;
-  if (p->At && (p->H > st::HEAD_QMAXH || !p->Wt || !p->bq || !p->bqt)) return hipErrorInvalidValue;
+  if (p->qp && (!p->qpt || p->nqp < 1 || !p->bq || !p->bqt)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(st::deep_head_kernel, dim3((p->H / 256) * (q.B / 64)), dim3(256), 0, s, *p);
   return hipGetLastError();
 }

@@ -30,6 +30,8 @@ enum GemmEpi : int {
   EPI_BF16 = 0,      // out = act(alpha*acc + bias) as bf16 [M][N] (+ optional outT [N][M])
   EPI_RELU_GRAD = 1, // out = acc * (auxT[n][m] > 0) as bf16 [M][N] (+ outT)
   EPI_F32 = 2,       // out = alpha*acc (+ bias[n]) (+ out if accumulate) as fp32 [M][N]
+  EPI_BF16_QH = 3,   // (internal) EPI_BF16 with the qpart head: its own instantiation, so the plain bf16
+                     // epilogue keeps its registers (the launcher picks it when a problem sets qpart)
 };
 
 struct GemmArgs {
@@ -50,6 +52,13 @@ struct GemmArgs {
   // (plain stores, no atomics; the optimizer sums the M / WM rows)
   float* colpart;
   int ldcp;
+  // EPI_BF16 (2-stage gemm_body tiles) only, optional: the next layer's output head folded into this epilogue --
+  // per row m and head row a < nq, the fp32 sum over each wave's WN columns of the stored (bf16) value times
+  // qw[a][n]: qpart[(part * M + m) * 4 + a], part = n / WN (N / WN parts, plain stores; the consumer sums the
+  // parts in a fixed order).  The update's Q(x) / Q_target(x') head without an output-layer launch.
+  const bf16_t* qw;      // [nq][ldqw] bf16 head rows
+  float* qpart;
+  int ldqw, nq;
 };
 
 // a group of up to 4 products with one epilogue / tile in one launch (e.g. the online and target
@@ -116,6 +125,17 @@ ST_DEV void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// one reduce-scatter step of the qpart head sums (see gemm_body's epilogue): lanes l and l ^ H swap halves
+template <int H>
+ST_DEV void qh_step(float* x, int l16) {
+  const bool up = (l16 & H) != 0;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const float keep = up ? x[k + H] : x[k], send = up ? x[k] : x[k + H];
+    x[k] = keep + __shfl_xor(send, H);
+  }
+}
+
 // workgroups of one problem: tiles x K-splits
 template <int BM, int BN>
 ST_DEV int gemm_blocks(const GemmArgs& p) {
@@ -146,6 +166,16 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
   for (int i = 0; i < G::TM; ++i)
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) acc[i][j] = zero4();
+  // EPI_BF16 head (qpart): qw[a][this lane's column of j] (0 for a >= nq), loaded under the K loop
+  const bool qh = EPI == EPI_BF16_QH && p.qpart != nullptr;
+  float qwv[G::TN][4];
+  if (qh) {
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        qwv[j][a] = a < p.nq ? bf2f(p.qw[(size_t)a * p.ldqw + n0 + wn * G::WN + 16 * j + l16]) : 0.f;
+  }
 
   const int nk = p.K / GBK / nsplit;
   const int kb = ks * nk * GBK;
@@ -248,18 +278,31 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
 #pragma unroll
     for (int j = 0; j < G::TN; ++j) csum[j] = 0.f;
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i)
+    for (int i = 0; i < G::TM; ++i) {
+      float qs[4][4];   // [r][a]: this lane's head sums of rows 16 i + 4 g4 + r over its TN columns
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) qs[r][a] = 0.f;
 #pragma unroll
       for (int j = 0; j < G::TN; ++j) {
         const int nl = wn * G::WN + 16 * j + l16;          // local col
         const int ml = wm * G::WM + 16 * i + 4 * g4;       // local row of r = 0
         float v[4];
-        if constexpr (EPI == EPI_BF16) {
+        if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_QH) {
           const float bb = p.bias ? p.bias[n0 + nl] : 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float x = p.alpha * acc[i][j][r] + bb;
             v[r] = p.relu ? fmaxf(x, 0.f) : x;
+          }
+          if (qh) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float hv = bf2f(f2bf(v[r]));   // the stored value
+#pragma unroll
+              for (int a = 0; a < 4; ++a) qs[r][a] = fmaf(hv, qwv[j][a], qs[r][a]);
+            }
           }
         } else {  // EPI_RELU_GRAD: mask by the forward activation (read from its transposed copy)
           const s4v h = *reinterpret_cast<const s4v*>(p.auxT + (size_t)(n0 + nl) * p.ldaux + m0 + ml);
@@ -274,6 +317,22 @@ ST_DEV void gemm_body(const GemmArgs& p, int bid, char* gsm) {
         for (int r = 0; r < 4; ++r) sC[(ml + r) * SC + nl] = f2bf(v[r]);
         if constexpr (G::HAS_T) lds_st4(sCT + nl * SCT + ml, v[0], v[1], v[2], v[3]);
       }
+      if (qh) {
+        // sum the 16 values k = 4 r + a over the 16 lanes of the row group (its 16 columns per j) by a
+        // reduce-scatter: at each step a lane keeps the half of its values selected by one bit of l16 and adds the
+        // partner's copy of it (8 + 4 + 2 + 1 shuffles instead of 64); lane l16 ends with the sum of k = l16
+        float x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = qs[k >> 2][k & 3];
+        qh_step<8>(x, l16);   // (one template step each: constant indices, so x stays in registers)
+        qh_step<4>(x, l16);
+        qh_step<2>(x, l16);
+        qh_step<1>(x, l16);
+        const int part = (n0 + wn * G::WN) / G::WN;
+        const int m = m0 + wm * G::WM + 16 * i + 4 * g4 + (l16 >> 2);
+        p.qpart[((size_t)part * p.M + m) * 4 + (l16 & 3)] = x[0];
+      }
+    }
     if (EPI == EPI_RELU_GRAD && p.colpart) {
       // the 4 lane groups (rows 4 g4 ..) of each column, then one store per column of the wave's WM rows
 #pragma unroll
@@ -803,6 +862,8 @@ static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool ha
   if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return false;
   if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return false;
   if (p->colpart && (epi != st::EPI_RELU_GRAD || p->ldcp < p->N)) return false;
+  if (p->qpart && (epi != st::EPI_BF16 || !p->qw || p->nq < 1 || p->nq > 4 || p->ldqw < p->N || p->splitk > 1))
+    return false;
   return true;
 }
 
@@ -813,16 +874,20 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
   const int bn = (tile == 1 || tile == 2) ? 64 : (tile == 6 ? 256 : 128);
   st::GemmBatch b;
   b.n = n;
+  bool qh = false;
   for (int i = 0; i < n; ++i) {
     const st::GemmArgs* p = ps + i;
     if (!gemm_args_ok(p, epi, bm, bn, tile != 6)) return hipErrorInvalidValue;
     b.a[i] = *p;
+    qh = qh || p->qpart;
   }
+  if (qh) epi = st::EPI_BF16_QH;   // (gemm_args_ok: qpart only with EPI_BF16)
 #define ST_G(BM_, BN_, S_)                                                               \
   switch (epi) {                                                                         \
     case 0: return st::launch_gemm<BM_, BN_, 0, S_>(b, stream);                          \
     case 1: return st::launch_gemm<BM_, BN_, 1, S_>(b, stream);                          \
     case 2: return st::launch_gemm<BM_, BN_, 2, S_>(b, stream);                          \
+    case 3: return st::launch_gemm<BM_, BN_, 3, S_>(b, stream);                          \
     default: return hipErrorInvalidValue;                                                \
   }
   if (tile == 0) { ST_G(128, 128, 2) }
@@ -847,7 +912,7 @@ extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::G
 }
 
 extern "C" hipError_t st_gemm_nt(const st::GemmArgs* p, int epi, int tile, hipStream_t stream) {
-  if (p->colpart && tile >= 7) return hipErrorInvalidValue;   // column partials: 2-stage gemm_body tiles only
+  if ((p->colpart || p->qpart) && tile >= 7) return hipErrorInvalidValue;   // 2-stage gemm_body tiles only
   if (tile == 9) {   // 256x256, 4 waves of 128x128 (bf16 / fp32 epilogues, no C^T, no split-K)
     if (p->M % 256 || p->N % 256 || p->K % st::GBK || p->M <= 0 || p->N <= 0 || p->K <= 0) return hipErrorInvalidValue;
     if (p->lda % 8 || p->ldb % 8 || (epi != st::EPI_F32 && p->ldo % 8) || p->outT || p->splitk > 1)

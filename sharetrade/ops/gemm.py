@@ -24,6 +24,7 @@ class GemmArgs(C.Structure):
         ("auxT", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
         ("ldo", C.c_int), ("ldoT", C.c_int), ("ldaux", C.c_int), ("relu", C.c_int), ("accumulate", C.c_int),
         ("alpha", C.c_float), ("splitk", C.c_int), ("colpart", C.c_void_p), ("ldcp", C.c_int),
+        ("qw", C.c_void_p), ("qpart", C.c_void_p), ("ldqw", C.c_int), ("nq", C.c_int),
     ]
 
 
@@ -52,9 +53,11 @@ def pick_tile(M: int, N: int) -> tuple:
 def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, outT: Optional[torch.Tensor] = None,
               bias: Optional[torch.Tensor] = None, auxT: Optional[torch.Tensor] = None, relu: bool = False,
               accumulate: bool = False, alpha: float = 1.0, splitk: int = 1,
-              colpart: Optional[torch.Tensor] = None) -> GemmArgs:
+              colpart: Optional[torch.Tensor] = None, qhead=None) -> GemmArgs:
     """``colpart`` (EPI_RELU_GRAD, 128-row 2-stage tiles): fp32 [M / 64, >= N] -- column sums of the bf16 output
-    over each 64-row wave block (the bias gradient's partials)."""
+    over each 64-row wave block (the bias gradient's partials).  ``qhead = (W, qpart)`` (EPI_BF16, 2-stage tiles):
+    the next layer's head rows W bf16 [nq <= 4, >= N] folded into the epilogue -- qpart fp32 [N / WN, M, 4] gets
+    per row the sums of output x W[a] over each wave's WN = BN / 2 columns (csrc/gemm_bf16.hip GemmArgs::qpart)."""
     M, K = A.shape
     N, K2 = B.shape
     if K != K2:
@@ -95,6 +98,13 @@ def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, out
         if epi != EPI_RELU_GRAD or colpart.dtype != torch.float32 or colpart.stride(1) != 1 or colpart.shape[1] < N:
             raise ValueError("colpart: EPI_RELU_GRAD, fp32 [M / 64, >= N] row-major")
         g.colpart, g.ldcp = colpart.data_ptr(), colpart.stride(0)
+    if qhead is not None:
+        qw, qp = qhead
+        if (epi != EPI_BF16 or qw.dtype != torch.bfloat16 or qw.stride(1) != 1 or not 1 <= qw.shape[0] <= 4 or
+                qw.shape[1] < N or qp.dtype != torch.float32 or not qp.is_contiguous() or qp.dim() != 3 or
+                qp.shape[1] != M or qp.shape[2] != 4 or splitk > 1):
+            raise ValueError("qhead: EPI_BF16, W bf16 [<= 4, >= N], qpart fp32 contiguous [N / WN, M, 4], no split-K")
+        g.qw, g.qpart, g.ldqw, g.nq = qw.data_ptr(), qp.data_ptr(), qw.stride(0), qw.shape[0]
     return g
 
 

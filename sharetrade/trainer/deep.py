@@ -69,8 +69,8 @@ class _TD(C.Structure):
 
 class _Head(C.Structure):
     _fields_ = [("td", _TD), ("A", C.c_void_p), ("W", C.c_void_p), ("G", C.c_void_p), ("GT", C.c_void_p),
-                ("dW", C.c_void_p), ("H", C.c_int), ("gpart", C.c_void_p), ("ldgp", C.c_int), ("At", C.c_void_p),
-                ("Wt", C.c_void_p), ("bq", C.c_void_p), ("bqt", C.c_void_p)]
+                ("dW", C.c_void_p), ("H", C.c_int), ("gpart", C.c_void_p), ("ldgp", C.c_int), ("qp", C.c_void_p),
+                ("qpt", C.c_void_p), ("nqp", C.c_int), ("bq", C.c_void_p), ("bqt", C.c_void_p)]
 
 
 class _Adam(C.Structure):
@@ -270,9 +270,14 @@ class DeepDQN:
         # deep_head_kernel); dW_{L-1} is then accumulated atomically into the zeroed span
         self.fuse_head = bool(fuse_head) and self.L >= 2 and self.pdims[-2] % 256 == 0 and self.B % 64 == 0 \
             and 1 <= self.n_act <= 4
-        # head_qfwd: the output layer's forward (online on x, target on x') inside deep_head_kernel too, instead of
-        # the batched forward's split-K output GEMM launch
-        self.head_qfwd = bool(head_qfwd) and self.fuse_head and self.batched_fwd and self.pdims[-2] <= 1024
+        # head_qfwd: the output layer's forward (online on x, target on x') folded into the last hidden layer's
+        # batched launch (per-row partial head sums in its epilogue, GemmArgs::qpart) and summed by deep_head_kernel,
+        # instead of a split-K output GEMM launch
+        self.head_qfwd = bool(head_qfwd) and self.fuse_head and self.batched_fwd
+        self._qpart = None
+        if self.head_qfwd:   # [online, target][N / WN parts][B][4], WN = the forward tile's per-wave width
+            wn = gm.pick_tile(self.B, self.pdims[-2])[1] // 2
+            self._qpart = torch.zeros(2, self.pdims[-2] // wn, self.B, 4, device=dev)
         self._dual = [False] * self.L   # layer l's weight gradient in a dual launch with G_{l-1}
         if self.dual_bwd:
             for l in range(1, self.L - 1):
@@ -410,7 +415,7 @@ class DeepDQN:
         if self._bpart[self.L - 2] is not None:
             hd.gpart, hd.ldgp = self._bpart[self.L - 2].data_ptr(), self.pdims[self.L - 1]
         if self.head_qfwd:
-            hd.At, hd.Wt = self.ActN[self.L - 1].data_ptr(), self.Wt[self.L - 1].data_ptr()
+            hd.qp, hd.qpt, hd.nqp = self._qpart[0].data_ptr(), self._qpart[1].data_ptr(), self._qpart.shape[1]
             hd.bq, hd.bqt = self.b[self.L - 1].data_ptr(), self.bt[self.L - 1].data_ptr()
         self._head = hd
         a = cfg.agent
@@ -520,8 +525,11 @@ class DeepDQN:
         weights, no transposed copy) is a third product of the same launches."""
         for l in range(self.L):
             if l < self.L - 1:
-                probs = [(acts[l], self.Wb[l], acts[l + 1], dict(outT=actsT[l + 1], bias=self.b[l], relu=True)),
-                         (actsN[l], self.Wt[l], actsN[l + 1], dict(bias=self.bt[l], relu=True))]
+                qh = self.head_qfwd and l == self.L - 2   # the output head folded into this launch's epilogue
+                qa = (self.Wb[l + 1][: self.n_act], self._qpart[0]) if qh else None
+                qb = (self.Wt[l + 1][: self.n_act], self._qpart[1]) if qh else None
+                probs = [(acts[l], self.Wb[l], acts[l + 1], dict(outT=actsT[l + 1], bias=self.b[l], relu=True, qhead=qa)),
+                         (actsN[l], self.Wt[l], actsN[l + 1], dict(bias=self.bt[l], relu=True, qhead=qb))]
                 if actsE is not None:
                     probs.append((actsE[l], self.Wb[l], actsE[l + 1], dict(bias=self.b[l], relu=True)))
                 gm.gemm_nt_batched(probs, gm.EPI_BF16, tile=gm.pick_tile(self.B, self.pdims[l + 1]))

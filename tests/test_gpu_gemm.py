@@ -46,6 +46,42 @@ def test_gemm_bf16_bias_relu_and_transposed_out(native_built, tile):
     assert torch.equal(outT, out.t().contiguous())
 
 
+@pytest.mark.parametrize("tile", [(128, 128), (64, 64), (128, 64), (256, 128), (128, 128, 3)])
+def test_gemm_bf16_qhead_partials(native_built, tile):
+    """qhead: the next layer's head (nq <= 4 rows) folded into the bf16 epilogue -- the per-row partial sums over
+    each wave's BN / 2 columns add up to the stored bf16 output times the head rows (fp32 reference); the output
+    itself is unchanged; two problems of one batched launch write their own partials."""
+    from sharetrade.ops.gemm import EPI_BF16, gemm_nt, gemm_nt_batched
+
+    M, N, K = 512, 256, 320
+    A, B = _bf((M, K), 13), _bf((N, K), 14)
+    bias = torch.randn(N, device="cuda")
+    Wq = _bf((3, N), 15, 0.1)
+    wn = tile[1] // 2
+    qp = torch.full((N // wn, M, 4), float("nan"), device="cuda")
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    out0 = torch.empty_like(out)
+    gemm_nt(A, B, out0, EPI_BF16, tile=tile, bias=bias, relu=True)
+    gemm_nt(A, B, out, EPI_BF16, tile=tile, bias=bias, relu=True, qhead=(Wq, qp))
+    torch.cuda.synchronize()
+    assert torch.equal(out, out0)
+    ref = out.float() @ Wq.float().t()
+    got = qp.sum(0)
+    assert torch.allclose(got[:, :3], ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
+    assert float(got[:, 3].abs().max()) == 0.0
+    if len(tile) == 2:
+        A2 = _bf((M, K), 16)
+        qp2 = torch.zeros_like(qp)
+        out2 = torch.empty_like(out)
+        qp.zero_()
+        gemm_nt_batched([(A, B, out, dict(bias=bias, relu=True, qhead=(Wq, qp))),
+                         (A2, B, out2, dict(bias=bias, relu=True, qhead=(Wq, qp2)))], EPI_BF16, tile=tile)
+        torch.cuda.synchronize()
+        assert torch.allclose(qp.sum(0)[:, :3], ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
+        ref2 = out2.float() @ Wq.float().t()
+        assert torch.allclose(qp2.sum(0)[:, :3], ref2, rtol=1e-4, atol=1e-4 * float(ref2.abs().max()))
+
+
 @pytest.mark.parametrize("tile", [(64, 64), (256, 128), (128, 128, 4)])
 def test_gemm_relu_grad_epilogue(native_built, tile):
     from sharetrade.ops.gemm import EPI_RELU_GRAD, gemm_nt
