@@ -48,6 +48,8 @@ def main():
                     help="online / target forward as two GEMM chains (two streams) instead of one batched launch per layer")
     ap.add_argument("--no-head-qfwd", action="store_true",
                     help="the update's output-layer forward as a split-K GEMM launch instead of inside deep_head_kernel")
+    ap.add_argument("--no-act-qhead", action="store_true",
+                    help="the act step's output layer as the 64-wide padded fp32 GEMM instead of csrc/deep.hip qhead_kernel")
     ap.add_argument("--act-gemm", default="lib", choices=("own", "lib", "lib0"),
                     help="the act step's hidden 1024 -> 1024 layers through hipBLASLt's fused bias + ReLU epilogue "
                          "(lib, default: 0.408 vs 0.417 ms per iteration), also its first layer (lib0: +0.5 %%), or "
@@ -82,7 +84,7 @@ def main():
                 concurrent=not a.serial, fused_adam=not a.unfused_adam, overlap_act=not a.no_overlap_act,
                 batched_fwd=not a.unbatched_fwd, dual_bwd=not a.no_dual_bwd, act_inline=a.act_inline,
                 fuse_act=a.fuse_act, fuse_xt=not a.no_fuse_xt, act_after_fwd=not a.act_before_fwd,
-                early_adam=a.early_adam, act_gemm=a.act_gemm, head_qfwd=not a.no_head_qfwd, fuse_head=not a.no_fuse_head,
+                early_adam=a.early_adam, act_gemm=a.act_gemm, head_qfwd=not a.no_head_qfwd, act_qhead=not a.no_act_qhead, fuse_head=not a.no_fuse_head,
                 bias_part=not a.no_bias_part)
     for _ in range(a.warmup):
         d.act_step()
@@ -129,7 +131,7 @@ def main():
         "mean_loss": s["loss_sum"] / max(1, s["updates"]) / a.batch,
         "concurrent_update": d.concurrent, "fused_adam": d.fused_adam, "overlap_act": d.overlap_act,
         "batched_fwd": d.batched_fwd, "pingpong_gemm": not a.no_pingpong, "dual_bwd": d.dual_bwd, "act_inline": d.act_inline, "fuse_act": d.fuse_act,
-        "act_gemm": d.act_gemm, "head_qfwd": d.head_qfwd, "fuse_head": d.fuse_head, "bias_part": d._bpart[0] is not None, "iters_per_graph": k,
+        "act_gemm": d.act_gemm, "head_qfwd": d.head_qfwd, "act_qhead": d.act_qhead, "fuse_head": d.fuse_head, "bias_part": d._bpart[0] is not None, "iters_per_graph": k,
     }
     print(json.dumps(out))
 

@@ -528,6 +528,61 @@ __global__ void __launch_bounds__(256) deep_head_kernel(DeepHead p) {
   }
 }
 
+// Output layer of the act step: Q[r][a] = A[r] . W[a] + bias[a] for the n_actions (<= 4) real rows of W -- a few
+// outputs per 2 KB row, so no GEMM tile: 16 lanes per row, each with its 8 (H = 1024) 16-byte units of the row in
+// flight at once, packed bf16 pairs into v_dot2c_f32_bf16 against W staged in LDS, a butterfly over the 16 lanes
+// (fixed order).  Replaces the 64-wide padded EPI_F32 GEMM launch (13.3 us at 16,384 x 1024).
+struct QHead {
+  const bf16_t* A;      // [R][lda] bf16
+  const bf16_t* W;      // [>= nact][ldw] bf16
+  const float* bias;    // [>= nact]
+  float* Q;             // [R][ldq] fp32: columns < nact written
+  int R, H, lda, ldw, ldq, nact;
+};
+constexpr int QHEAD_MAXH = 1024;
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+__global__ void __launch_bounds__(256) qhead_kernel(QHead p) {
+  __shared__ uint4 sW[HEAD_MAXA][QHEAD_MAXH / 8];
+  const int tid = threadIdx.x, l16 = tid & 15, r = blockIdx.x * 16 + (tid >> 4), hc = p.H / 8;
+  uint4 xs[QHEAD_MAXH / 128];
+  const bf16_t* Ar = p.A + (size_t)r * p.lda;
+#pragma unroll
+  for (int i = 0; i < QHEAD_MAXH / 128; ++i) {   // issued before the W staging barrier
+    const int c = l16 + 16 * i;
+    xs[i] = c < hc ? *reinterpret_cast<const uint4*>(Ar + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int i = tid; i < p.nact * hc; i += 256)
+    sW[i / hc][i % hc] = *reinterpret_cast<const uint4*>(p.W + (size_t)(i / hc) * p.ldw + 8 * (i % hc));
+  __syncthreads();
+  float acc[HEAD_MAXA] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < QHEAD_MAXH / 128; ++i) {
+    const int c = l16 + 16 * i;
+    if (c >= hc) break;
+    const uint32_t u[4] = {xs[i].x, xs[i].y, xs[i].z, xs[i].w};
+#pragma unroll
+    for (int a = 0; a < HEAD_MAXA; ++a) {
+      if (a >= p.nact) break;
+      const uint4 w4 = sW[a][c];
+      const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        acc[a] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, u[k]), __builtin_bit_cast(bf16x2_t, w[k]),
+                                                 acc[a], false);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < HEAD_MAXA; ++a) {
+    float v = acc[a];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    if (l16 == 0 && a < p.nact) p.Q[(size_t)r * p.ldq + a] = v + p.bias[a];
+  }
+}
+
 // bias gradient: db[o] = sum_b dZT[o][b]  (one workgroup per output row)
 __global__ void __launch_bounds__(256) row_sum_bf16_kernel(const bf16_t* __restrict__ X, int ld, int n, float* out) {
   __shared__ float red[4];
@@ -821,6 +876,14 @@ extern "C" hipError_t st_deep_gather(const st::DeepGather* g, hipStream_t s) {
 
 extern "C" hipError_t st_deep_env_step(const st::DeepEnv* p, hipStream_t s) {
   hipLaunchKernelGGL(st::deep_env_step_kernel, dim3((p->E + 255) / 256), dim3(256), 0, s, *p);   // (advances too)
+  return hipGetLastError();
+}
+
+extern "C" hipError_t st_qhead(const st::QHead* p, hipStream_t s) {
+  if (p->R % 16 || p->R <= 0 || p->H % 8 || p->H <= 0 || p->H > st::QHEAD_MAXH || p->nact < 1 || p->nact > st::HEAD_MAXA ||
+      p->lda % 8 || p->ldw % 8 || p->ldw < p->H || p->lda < p->H || p->ldq < p->nact || !p->A || !p->W || !p->bias || !p->Q)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(st::qhead_kernel, dim3(p->R / 16), dim3(256), 0, s, *p);
   return hipGetLastError();
 }
 

@@ -73,6 +73,11 @@ class _Head(C.Structure):
                 ("qpt", C.c_void_p), ("nqp", C.c_int), ("bq", C.c_void_p), ("bqt", C.c_void_p)]
 
 
+class _QHead(C.Structure):
+    _fields_ = [("A", C.c_void_p), ("W", C.c_void_p), ("bias", C.c_void_p), ("Q", C.c_void_p), ("R", C.c_int),
+                ("H", C.c_int), ("lda", C.c_int), ("ldw", C.c_int), ("ldq", C.c_int), ("nact", C.c_int)]
+
+
 class _Adam(C.Structure):
     _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("mask", C.c_void_p),
                 ("wb", C.c_void_p), ("wbT", C.c_void_p), ("t", C.c_void_p), ("O", C.c_int), ("I", C.c_int),
@@ -101,6 +106,7 @@ def _bind():
                          ("st_deep_env_step", [C.POINTER(_Env), C.c_void_p]),
                          ("st_deep_td", [C.POINTER(_TD), C.c_void_p]),
                          ("st_deep_head", [C.POINTER(_Head), C.c_void_p]),
+                         ("st_qhead", [C.POINTER(_QHead), C.c_void_p]),
                          ("st_row_sum_bf16", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
                          ("st_transpose_bf16", [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                 C.c_void_p]),
@@ -128,7 +134,8 @@ class DeepDQN:
                  batched_fwd: bool = True, dual_bwd: bool = True, act_inline: bool = False,
                  fuse_act: bool = False, world_size: int = 1, grad_sync=None, bank_seed: int = 0,
                  fuse_xt: bool = True, act_after_fwd: bool = True, early_adam: bool = False,
-                 act_gemm: str = "lib", fuse_head: bool = True, bias_part: bool = True, head_qfwd: bool = True):
+                 act_gemm: str = "lib", fuse_head: bool = True, bias_part: bool = True, head_qfwd: bool = True,
+                 act_qhead: bool = True):
         if device.type != "cuda":
             raise ValueError("DeepDQN runs on the GPU (MFMA GEMMs)")
         self.cfg, self.dev = cfg, device
@@ -274,6 +281,10 @@ class DeepDQN:
         # batched launch (per-row partial head sums in its epilogue, GemmArgs::qpart) and summed by deep_head_kernel,
         # instead of a split-K output GEMM launch
         self.head_qfwd = bool(head_qfwd) and self.fuse_head and self.batched_fwd
+        # act_qhead: the act step's output layer (E x H -> n_actions) on csrc/deep.hip qhead_kernel (16 lanes per
+        # row, packed bf16 dot products) instead of the 64-wide padded EPI_F32 GEMM
+        self.act_qhead = bool(act_qhead) and self.pdims[-2] <= 1024 and self.pdims[-2] % 8 == 0 and \
+            self.E % 16 == 0 and 1 <= self.n_act <= 4
         self._qpart = None
         if self.head_qfwd:   # [online, target][N / WN parts][B][4], WN = the forward tile's per-wave width
             wn = gm.pick_tile(self.B, self.pdims[-2])[1] // 2
@@ -500,7 +511,7 @@ class DeepDQN:
             self._bscratch(l).copy_(self.b[l].view(1, -1).to(torch.bfloat16))
 
     # ---------------------------------------------------------------- forward
-    def _forward(self, X, acts, actsT, Wb, bias, Q, lib: int = -1) -> None:
+    def _forward(self, X, acts, actsT, Wb, bias, Q, lib: int = -1, qhead: bool = False) -> None:
         """acts[l+1] = relu(acts[l] . W_l^T + b_l); Q = acts[L-1] . W_{L-1}^T + b_{L-1} (fp32).  ``lib`` >= 0:
         the hidden layers from that one on through hipBLASLt's fused bias + ReLU epilogue (bf16 bias copies;
         the act step's 16,384 x 1024 -> 1024 layers, where the library's K loop is faster than our ping-pong
@@ -516,6 +527,12 @@ class DeepDQN:
                     gm.gemm_nt(a, Wb[l], acts[l + 1], gm.EPI_BF16, outT=actsT[l + 1] if actsT else None,
                                bias=bias[l], relu=True)
                 a = acts[l + 1]
+            elif qhead:   # (act_qhead)
+                qh = _QHead()
+                qh.A, qh.W, qh.bias, qh.Q = a.data_ptr(), Wb[l].data_ptr(), bias[l].data_ptr(), Q.data_ptr()
+                qh.R, qh.H, qh.lda, qh.ldw, qh.ldq, qh.nact = a.shape[0], a.shape[1], a.stride(0), Wb[l].stride(0), \
+                    Q.stride(0), self.n_act
+                native.check(self.k.st_qhead(qh, native.stream_handle()), "qhead")
             else:
                 gm.gemm_nt(a, Wb[l], Q, gm.EPI_F32, bias=bias[l])
 
@@ -549,7 +566,7 @@ class DeepDQN:
         sh = native.stream_handle()
         native.check(self.k.st_deep_gather(self._gather_env, sh), "deep_gather(env)")
         self._forward(self.Xe, self.Acte, None, self.Wb, self.b, self.Qe,
-                      lib={"own": -1, "lib": 1, "lib0": 0}[self.act_gemm])
+                      lib={"own": -1, "lib": 1, "lib0": 0}[self.act_gemm], qhead=self.act_qhead)
         if after_forward is not None:
             after_forward()
         native.check(self.k.st_deep_env_step(self._env, sh), "deep_env_step")

@@ -283,6 +283,35 @@ def test_head_output_forward_matches_output_gemm(native_built):
         assert float((wa - wb).norm() / (wb.norm() + 1e-20)) < 1e-3
 
 
+def test_act_qhead_matches_output_gemm(native_built):
+    """act_qhead: the act step's output layer on qhead_kernel (16 lanes per row, packed bf16 dot products) gives
+    the padded fp32 GEMM's Q to fp32 summation order and the fp32 reference to 1e-5; only the n_actions columns
+    are written; the act step captures with it."""
+    d = _dqn(act_qhead=True, overlap_act=True)
+    assert d.act_qhead
+    for _ in range(5):
+        d.act_step()
+    torch.cuda.synchronize()
+    qs = []
+    for qh in (True, False):
+        acts = [d.Xe] + [t.clone() for t in d.Acte[1:]]
+        q = torch.full_like(d.Qe, 7.0)
+        d._forward(d.Xe, acts, None, d.Wb, d.b, q, lib=1, qhead=qh)
+        qs.append(q)
+    torch.cuda.synchronize()
+    a, b = qs
+    n = d.n_act
+    assert torch.allclose(a[:, :n], b[:, :n], rtol=1e-5, atol=1e-5)
+    assert bool((a[:, n:] == 7.0).all())
+    H = d.Acte[d.L - 1]
+    ref = H.float() @ d.Wb[d.L - 1][:n].float().t() + d.b[d.L - 1].view(-1)[:n]
+    assert torch.allclose(a[:, :n], ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+    d.capture(iters_per_graph=2)
+    d.iterations(4)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(w).all() for w in d.W)
+
+
 def test_k_iteration_graph_matches_single_iterations(native_built):
     """capture(iters_per_graph=4) + iterations(n): 4 whole iterations per graph launch (singles where a
     target-net copy would fall inside a graph) run the same sequence as n single-iteration replays: identical
