@@ -397,7 +397,9 @@ class DeepDQN:
         gr.zero0 = self._dW_flat.data_ptr() + 4 * z0 if zn else None
         gr.zero0_n = zn
         # the batched output layer accumulates Q / Q_t over K splits: zeroed here as well
-        gr.zero1, gr.zero1_n = (self._Qpair.data_ptr(), self._Qpair.numel()) if self._q_splitk > 1 else (None, 0)
+        # (not with head_qfwd: the head kernel writes Q / Q_t with plain stores)
+        gr.zero1, gr.zero1_n = ((self._Qpair.data_ptr(), self._Qpair.numel()) if self._q_splitk > 1 and not self.head_qfwd
+                                else (None, 0))
         gr.XT, gr.ldxt = (self.XT.data_ptr(), self.B) if self.fuse_xt else (None, 0)
         self._gather_rp = gr
         ev = _Env()
