@@ -59,6 +59,7 @@ struct GemmArgs {
   const bf16_t* qw;      // [nq][ldqw] bf16 head rows
   float* qpart;
   int ldqw, nq;
+  int nqp;               // parts qpart holds (checked: N / WN of the launch's tile)
 };
 
 // a group of up to 4 products with one epilogue / tile in one launch (e.g. the online and target
@@ -862,7 +863,8 @@ static bool gemm_args_ok(const st::GemmArgs* p, int epi, int bm, int bn, bool ha
   if (epi == st::EPI_RELU_GRAD && (!p->auxT || p->ldaux % 4)) return false;
   if (p->splitk > 1 && (epi != st::EPI_F32 || (p->K / st::GBK) % p->splitk)) return false;
   if (p->colpart && (epi != st::EPI_RELU_GRAD || p->ldcp < p->N)) return false;
-  if (p->qpart && (epi != st::EPI_BF16 || !p->qw || p->nq < 1 || p->nq > 4 || p->ldqw < p->N || p->splitk > 1))
+  if (p->qpart && (epi != st::EPI_BF16 || !p->qw || p->nq < 1 || p->nq > 4 || p->ldqw < p->N || p->splitk > 1 ||
+                   p->nqp != p->N / (bn / 2)))   // (every gemm_body tile has 2 wave columns: WN = BN / 2)
     return false;
   return true;
 }

@@ -24,7 +24,7 @@ class GemmArgs(C.Structure):
         ("auxT", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("lda", C.c_int), ("ldb", C.c_int),
         ("ldo", C.c_int), ("ldoT", C.c_int), ("ldaux", C.c_int), ("relu", C.c_int), ("accumulate", C.c_int),
         ("alpha", C.c_float), ("splitk", C.c_int), ("colpart", C.c_void_p), ("ldcp", C.c_int),
-        ("qw", C.c_void_p), ("qpart", C.c_void_p), ("ldqw", C.c_int), ("nq", C.c_int),
+        ("qw", C.c_void_p), ("qpart", C.c_void_p), ("ldqw", C.c_int), ("nq", C.c_int), ("nqp", C.c_int),
     ]
 
 
@@ -104,7 +104,7 @@ def make_args(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int, out
                 qw.shape[1] < N or qp.dtype != torch.float32 or not qp.is_contiguous() or qp.dim() != 3 or
                 qp.shape[1] != M or qp.shape[2] != 4 or splitk > 1):
             raise ValueError("qhead: EPI_BF16, W bf16 [<= 4, >= N], qpart fp32 contiguous [N / WN, M, 4], no split-K")
-        g.qw, g.qpart, g.ldqw, g.nq = qw.data_ptr(), qp.data_ptr(), qw.stride(0), qw.shape[0]
+        g.qw, g.qpart, g.ldqw, g.nq, g.nqp = qw.data_ptr(), qp.data_ptr(), qw.stride(0), qw.shape[0], qp.shape[0]
     return g
 
 

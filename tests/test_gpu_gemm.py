@@ -69,6 +69,8 @@ def test_gemm_bf16_qhead_partials(native_built, tile):
     got = qp.sum(0)
     assert torch.allclose(got[:, :3], ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
     assert float(got[:, 3].abs().max()) == 0.0
+    with pytest.raises(RuntimeError):   # a partial buffer of the wrong part count is refused, not overrun
+        gemm_nt(A, B, out, EPI_BF16, tile=tile, bias=bias, relu=True, qhead=(Wq, qp[:1].contiguous()))
     if len(tile) == 2:
         A2 = _bf((M, K), 16)
         qp2 = torch.zeros_like(qp)
