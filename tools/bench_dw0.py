@@ -47,3 +47,30 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def lib():
+    """hipBLASLt with bf16 operands and an fp32 output (torch.mm(..., out_dtype=torch.float32)) at the same shape."""
+    dev = torch.device("cuda", 0)
+    O, I, B = 1024, 256, 4096
+    A = (torch.randn(O, B, device=dev) * 0.01).to(torch.bfloat16)
+    X = torch.rand(I, B, device=dev).to(torch.bfloat16)
+    ref = A.float() @ X.float().t()
+
+    def run():
+        return torch.mm(A, X.t(), out_dtype=torch.float32)
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(50):
+        out = run()
+    b.record()
+    torch.cuda.synchronize()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    print(f"| hipBLASLt mm, fp32 out | - | - | {a.elapsed_time(b) / 50 * 1e3:.1f} us | {err:.1e} |", flush=True)
+
+
+if __name__ == "__main__" and "--lib" in sys.argv:
+    lib()
