@@ -43,3 +43,29 @@ def test_batched_and_dual_reject_bad_shapes_before_launch():
         gm.gemm_dual(ok, gm.EPI_BF16, (_t(64, 128), _t(256, 128), _t(64, 256, dtype=torch.float32), {}), gm.EPI_F32)
     with pytest.raises(ValueError):   # split-K needs the fp32 epilogue
         gm.make_args(A, B, _t(256, 256), gm.EPI_BF16, splitk=2)
+
+
+def test_epilogue_side_outputs_are_validated_before_launch():
+    """colpart (bias-gradient column partials) and qhead (the next layer's head folded into the bf16 epilogue) are
+    refused on the host when their epilogue, dtype or shape does not fit; a fitting qhead fills the ABI fields the
+    kernel checks against the tile (csrc/gemm_bf16.hip gemm_args_ok)."""
+    A, B = _t(256, 128), _t(256, 128)
+    out16, out32 = _t(256, 256), _t(256, 256, dtype=torch.float32)
+    with pytest.raises(ValueError):   # column partials only with the relu-grad epilogue
+        gm.make_args(A, B, out16, gm.EPI_BF16, colpart=_t(4, 256, dtype=torch.float32))
+    with pytest.raises(ValueError):   # too narrow
+        gm.make_args(A, B, out16, gm.EPI_RELU_GRAD, auxT=_t(256, 256), colpart=_t(4, 128, dtype=torch.float32))
+    qw = _t(3, 256)
+    qp = _t(4, 256, 4, dtype=torch.float32)
+    with pytest.raises(ValueError):   # the head rides on the bf16 epilogue only
+        gm.make_args(A, B, out32, gm.EPI_F32, qhead=(qw, qp))
+    with pytest.raises(ValueError):   # at most 4 head rows
+        gm.make_args(A, B, out16, gm.EPI_BF16, qhead=(_t(5, 256), qp))
+    with pytest.raises(ValueError):   # partials must be fp32 [parts, M, 4]
+        gm.make_args(A, B, out16, gm.EPI_BF16, qhead=(qw, _t(4, 256, 3, dtype=torch.float32)))
+    with pytest.raises(ValueError):   # head rows shorter than N
+        gm.make_args(A, B, out16, gm.EPI_BF16, qhead=(_t(3, 128), qp))
+    g = gm.make_args(A, B, out16, gm.EPI_BF16, qhead=(qw, qp))
+    assert (g.nq, g.nqp, g.ldqw) == (3, 4, 256) and g.qpart == qp.data_ptr() and g.qw == qw.data_ptr()
+    plain = gm.make_args(A, B, out16, gm.EPI_BF16)
+    assert not plain.qpart and not plain.colpart and plain.nqp == 0
