@@ -879,6 +879,16 @@ extern "C" hipError_t st_deep_env_step(const st::DeepEnv* p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_deep_abi(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::Replay), (int)sizeof(st::DeepGather), (int)sizeof(st::DeepEnv), (int)sizeof(st::DeepTD),
+                    (int)sizeof(st::DeepHead), (int)sizeof(st::QHead), (int)sizeof(st::AdamLayer),
+                    (int)sizeof(st::AdamSeg), (int)sizeof(st::AdamMulti)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}
+
 extern "C" hipError_t st_qhead(const st::QHead* p, hipStream_t s) {
   if (p->R % 16 || p->R <= 0 || p->H % 8 || p->H <= 0 || p->H > st::QHEAD_MAXH || p->nact < 1 || p->nact > st::HEAD_MAXA ||
       p->lda % 8 || p->ldw % 8 || p->ldw < p->H || p->lda < p->H || p->ldq < p->nact || !p->A || !p->W || !p->bias || !p->Q)

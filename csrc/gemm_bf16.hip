@@ -905,6 +905,13 @@ extern "C" hipError_t st_gemm_nt_batched(const st::GemmArgs* ps, int n, int epi,
 
 // two products of any shapes / epilogues on 128x128 tiles in one launch (epi pairs: relu-grad + f32,
 // f32 + f32, bf16 + f32)
+// struct sizes of this file's launch ABI, for the host mirror's check (tests/test_abi.py; no HIP call)
+extern "C" int st_gemm_abi(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::GemmArgs), (int)sizeof(st::GemmBatch)};
+  for (int i = 0; i < n && i < 2; ++i) out[i] = sz[i];
+  return 2;
+}
+
 extern "C" hipError_t st_gemm_dual(const st::GemmArgs* a0, int epi0, const st::GemmArgs* a1, int epi1, hipStream_t stream) {
   if (!gemm_args_ok(a0, epi0, 128, 128, true) || !gemm_args_ok(a1, epi1, 128, 128, true)) return hipErrorInvalidValue;
   if (epi0 == st::EPI_RELU_GRAD && epi1 == st::EPI_F32) return st::launch_dual<1, 2>(*a0, *a1, stream);
