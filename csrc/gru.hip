@@ -1082,3 +1082,11 @@ extern "C" hipError_t st_mx_probe(const void* a, const void* b, const int* sa, c
                      (f4v*)d);
   return hipGetLastError();
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_gru(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::MinuteBars), (int)sizeof(st::GruPack), (int)sizeof(st::GruAct)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}

@@ -702,3 +702,11 @@ extern "C" hipError_t st_gru_grad_fixup(const float* ext, int ldx, float* dwhh, 
   hipLaunchKernelGGL(st::gru_grad_fixup_kernel, dim3(st::RG), dim3(256), 0, s, ext, ldx, dwhh, dbhh, dwih, dbih);
   return hipGetLastError();
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_gru_learn(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::GruGather), (int)sizeof(st::GruNetW), (int)sizeof(st::GruSeqFwd), (int)sizeof(st::GruTD), (int)sizeof(st::GruSeqBwd)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}

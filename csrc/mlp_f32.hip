@@ -438,3 +438,11 @@ extern "C" hipError_t st_f32_advance(unsigned long long* ctrl, hipStream_t strea
   hipLaunchKernelGGL(st::f32_advance_kernel, dim3(1), dim3(1), 0, stream, ctrl);
   return hipGetLastError();
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_mlp_f32(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::F32Net), (int)sizeof(st::F32Rows), (int)sizeof(st::F32Optim)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}

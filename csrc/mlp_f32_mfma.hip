@@ -725,3 +725,11 @@ extern "C" long long st_f32b_colsum_part_floats(int E, int N) {
   const bool vec = N % 4 == 0 && N <= 256;
   return vec ? 32ll * 256 : (long long)((E + 255) / 256) * N;
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_mlp_f32_mfma(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::GemmF32), (int)sizeof(st::Fwd2F32), (int)sizeof(st::F32Batch)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}

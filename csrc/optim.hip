@@ -230,3 +230,11 @@ extern "C" hipError_t st_to_bf16(const float* in, bf16_t* out, int n, hipStream_
   hipLaunchKernelGGL(st::to_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, n);
   return hipGetLastError();
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_optim(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::OptimParams)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}

@@ -346,3 +346,11 @@ extern "C" hipError_t st_qserve_launch(const st::serve::ServeParams* p, int grid
     hipLaunchKernelGGL(qserve_kernel<false>, dim3(grid), dim3(NT), LDS_BYTES, stream, *p);
   return hipGetLastError();
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_qserve(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::serve::ServeParams)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}

@@ -38,7 +38,10 @@ constexpr int OUTP = 16;    // padded action dimension
 constexpr int SQ = OUTP + 8;
 constexpr int NSTAT = 8;
 
-struct QStepParams {
+// The launch parameters of this kernel: the leading fields of st::QStepParams (csrc/qstep.h) up to td_clip, in the
+// same order -- the host passes its one QStepParams mirror (sharetrade/ops/native.py) to st_qstep_launch, and this
+// kernel reads the prefix (pinned by tests/test_abi.py).  Its own name: one definition per struct in the library.
+struct FusedStepParams {
   const float* prices;      // [E, T] env-major
   const float* prices4;     // [4][E][T4] shifted replicas (series.hip: replicate4)
   // env state + per-step outputs as ONE struct-of-arrays buffer [ENV_ROWS][E] of 4-byte
@@ -63,7 +66,7 @@ struct QStepParams {
   float td_clip;               // > 0: TD error clamped to [-td_clip, td_clip] (Huber loss)
 };
 
-// rows of QStepParams::env
+// rows of FusedStepParams::env
 enum EnvRow : int { ER_POS = 0, ER_BUDGET, ER_SHARES, ER_VALUE, ER_RET_SUM, ER_EPISODES, ER_LAST_FINAL,
                     ER_ACTION, ER_REWARD, ENV_ROWS };
 #define ENV_I(R, e) (p.env[(size_t)(R) * p.E + (e)])
@@ -232,7 +235,7 @@ ST_DEV void bwd_data(const bf16_t* sWT, const bf16_t* sDZ, const bf16_t* sAct, b
 }
 
 template <int INP, int H1P, int H2P, int FEAT>
-__global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
+__global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(FusedStepParams p) {
   using G = Geo<INP, H1P, H2P>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* sbf = reinterpret_cast<bf16_t*>(smem);
@@ -619,7 +622,7 @@ __global__ void __launch_bounds__(NT, 2) qstep_fused_kernel(QStepParams p) {
 }
 
 template <int INP, int H1P, int H2P, int FEAT>
-static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
+static hipError_t launch_f(const FusedStepParams& p, int grid, hipStream_t stream) {
   using G = Geo<INP, H1P, H2P>;
   static bool attr = false;
   if (!attr) {
@@ -633,7 +636,7 @@ static hipError_t launch_f(const QStepParams& p, int grid, hipStream_t stream) {
 }
 
 template <int INP, int H1P, int H2P>
-static hipError_t launch_t(const QStepParams& p, int grid, hipStream_t stream) {
+static hipError_t launch_t(const FusedStepParams& p, int grid, hipStream_t stream) {
   return p.feat_mode ? launch_f<INP, H1P, H2P, 1>(p, grid, stream) : launch_f<INP, H1P, H2P, 0>(p, grid, stream);
 }
 
@@ -644,8 +647,16 @@ extern "C" int st_qstep_lds_bytes(int inp, int h1p, int h2p) {
   return -1;
 }
 
-extern "C" hipError_t st_qstep_launch(const st::QStepParams* p, int inp, int h1p, int h2p, int grid,
+extern "C" hipError_t st_qstep_launch(const st::FusedStepParams* p, int inp, int h1p, int h2p, int grid,
                                       hipStream_t stream) {
   if (inp == 224 && h1p == 128 && h2p == 128) return st::launch_t<224, 128, 128>(*p, grid, stream);
   return hipErrorInvalidValue;
+}
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_qstep_fused(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::FusedStepParams)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
 }

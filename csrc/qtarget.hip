@@ -377,3 +377,11 @@ extern "C" hipError_t st_qtarget_launch_v(const st::qtgt::QTargetParams* p, int 
 extern "C" hipError_t st_qtarget_launch(const st::qtgt::QTargetParams* p, int grid, hipStream_t stream) {
   return st_qtarget_launch_v(p, grid, 1, stream);
 }
+
+// struct sizes of this file's launch ABI, for the host mirrors' check (tests/test_abi.py; no HIP call)
+extern "C" int st_abi_qtarget(int* out, int n) {
+  const int sz[] = {(int)sizeof(st::QStepParams), (int)sizeof(st::qtgt::QTargetParams)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}
