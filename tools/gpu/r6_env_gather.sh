@@ -1,5 +1,6 @@
 #!/bin/bash
 # config 4: the act step env gather forked at the update start (early_env_gather) vs with its forward; tests, stats, A/B x3
+# (historical record: the variant this A/B measured was removed afterwards, so its flag no longer exists)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/egath

@@ -1,5 +1,6 @@
 #!/bin/bash
 # config 4: the hidden layers' Adam on its own stream (split_adam, new default) vs one launch at the join, A/B x3
+# (historical record: the variant this A/B measured was removed afterwards, so its flag no longer exists)
 set -o pipefail
 O=gpurun_out/splitadam
 mkdir -p $O
